@@ -1,0 +1,177 @@
+/* =====================================================================================
+ * pfx.h -- C-ABI of the MI355X-native (gfx950) feature-extraction path.
+ *
+ * This is the drop-in boundary that replaces the PCL 1.7 calls srv/pcl_feature_extraction
+ * makes on its hot path.  Plain pointers and sizes, no torch or PCL
+ * types.  Every entry point returns 0 on success; on failure a nonzero pfx_status and the
+ * message is available from pfx_last_error(ctx).  PCL's own error behaviour (initCompute
+ * failure -> PCL_ERROR + empty output; per-point failure -> NaN fill) is mapped by the C++
+ * facade (include/pfx_pcl.hpp) onto these codes.
+ *
+ * Two families:
+ *   pfx_*      host pointers in / host pointers out (synchronous, H2D/D2H inside)
+ *   pfx_*_dev  device pointers in / device pointers out, stream-ordered on the ctx stream
+ * Arrays are structure-of-arrays float32 (x, y, z / nx, ny, nz), indexed by the caller's
+ * point index, exactly the order of PointCloud<T>::points.
+ *
+ * Replaced reference interfaces (file:line in /root/reference):
+ *   pfx_normals*        <- Tools::estimateNormals -> NormalEstimationOMP<PointXYZRGB,Normal>
+ *                          ::compute  (include/pcl_feature_extraction/tools.h:22-32)
+ *   pfx_fpfh*           <- FPFHEstimation<PointXYZRGB,Normal,FPFHSignature33>::compute via
+ *                          Features<T>::compute (features.h:175-196, evaluation.cpp:593-612)
+ *   pfx_shot*           <- SHOTEstimationOMP<PointXYZRGB,Normal,SHOT352>::compute
+ *                          (features.h:175-196, evaluation.cpp:766-785)
+ *   pfx_range_image_planar* <- RangeImagePlanar::createFromPointCloudWithFixedSize
+ *                          (keypoints.h:212-216, tools.h:61-77)
+ *   pfx_narf_keypoints* <- RangeImageBorderExtractor + NarfKeypoint::compute
+ *                          (keypoints.h:219-224)
+ *   pfx_radius_search*  <- search::KdTree<PointXYZRGB>::radiusSearch (features.h:192,
+ *                          tools.h:29; FLANN order: (d^2, index) ascending, strict d^2 < r^2)
+ * ===================================================================================== */
+#ifndef PFX_H_
+#define PFX_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct pfx_ctx pfx_ctx;
+typedef int32_t pfx_status;
+
+enum {
+  PFX_OK = 0,
+  PFX_ERR_INVALID = 1,     /* bad argument (null pointer, negative size, radius <= 0, ...) */
+  PFX_ERR_DEVICE = 2,      /* HIP runtime error (message from hipGetErrorString)            */
+  PFX_ERR_CAPACITY = 3,    /* caller buffer too small (required size in the out count)      */
+  PFX_ERR_UNSUPPORTED = 4  /* parameter combination the path does not implement             */
+};
+
+/* NarfKeypoint::Parameters + RangeImageBorderExtractor::Parameters (PCL 1.7 defaults; the
+ * reference sets only support_size = 0.2f, keypoints.h:223). */
+typedef struct pfx_narf_params {
+  float support_size;                            /* -1 (must be set > 0)   */
+  int32_t max_no_of_interest_points;             /* -1 = unlimited          */
+  float min_distance_between_interest_points;    /* 0.25 (x support_size)   */
+  float optimal_distance_to_high_surface_change; /* 0.25                    */
+  float min_interest_value;                      /* 0.45                    */
+  float min_surface_change_score;                /* 0.2                     */
+  int32_t do_non_maximum_suppression;            /* 1                       */
+  int32_t calculate_sparse_interest_image;       /* 1 (same keypoints) */
+  int32_t no_of_polynomial_approximations_per_point; /* 0 (only 0 supported) */
+  int32_t add_points_on_straight_edges;          /* 0 (only 0 supported)    */
+  /* RangeImageBorderExtractor::Parameters */
+  int32_t pixel_radius_borders;                  /* 3   */
+  int32_t pixel_radius_plane_extraction;         /* 2   */
+  int32_t pixel_radius_border_direction;         /* 2   */
+  float minimum_border_probability;              /* 0.8 */
+  int32_t pixel_radius_principal_curvature;      /* 2   */
+} pfx_narf_params;
+
+/* RangeImagePlanar::createFromPointCloudWithFixedSize arguments */
+typedef struct pfx_camera {
+  int32_t width, height;          /* 640, 480 (keypoints.h:204)     */
+  float center_x, center_y;       /* 320, 240 (keypoints.h:205)     */
+  float focal_length_x, focal_length_y; /* 525, 525 (keypoints.h:206, both fx) */
+  float sensor_pose[16];          /* row-major 4x4 Affine3f (sensor_origin_ * orientation_) */
+  int32_t coordinate_frame;       /* 0 = CAMERA_FRAME, 1 = LASER_FRAME */
+  float noise_level;              /* 0 */
+  float min_range;                /* 0 */
+} pfx_camera;
+
+void pfx_narf_params_default(pfx_narf_params* p);
+/* The reference's NARF setup (keypoints.h:203-223) with an identity pose */
+void pfx_camera_default(pfx_camera* c);
+
+/* ---- context ---------------------------------------------------------------------- */
+pfx_status pfx_ctx_create(int device, pfx_ctx** out);
+void pfx_ctx_destroy(pfx_ctx* ctx);
+const char* pfx_last_error(const pfx_ctx* ctx);
+/* Use an external hipStream_t (e.g. torch.cuda.current_stream().cuda_stream); NULL restores
+ * the ctx-owned stream. */
+pfx_status pfx_ctx_set_stream(pfx_ctx* ctx, void* hip_stream);
+void* pfx_ctx_get_stream(pfx_ctx* ctx);
+pfx_status pfx_ctx_synchronize(pfx_ctx* ctx);
+/* Per-kernel HIP-event timing on the ctx stream (for bench.py's live roofline). */
+pfx_status pfx_ctx_set_timing(pfx_ctx* ctx, int enable);
+pfx_status pfx_ctx_reset_timing(pfx_ctx* ctx);
+/* Accumulated device time and launch count of the kernel `name`; syncs the stream. */
+pfx_status pfx_ctx_kernel_time(pfx_ctx* ctx, const char* name, double* total_ms,
+                               int64_t* launches);
+/* Count of neighbours gathered by the last normals call (sum over queries of |N_r(q)|) --
+ * the per-launch unit count for the neighbour-gather roofline. */
+pfx_status pfx_ctx_last_stats(pfx_ctx* ctx, const char* what, int64_t* value);
+
+/* ---- radius search (FLANN semantics) ---------------------------------------------- */
+/* counts[nq] = |{p : d2(q,p) < (float)(r*r)}|; if idx != NULL also the first `cap`
+ * neighbours of each query in (d2, index) order, row-major with row stride `cap`. */
+pfx_status pfx_radius_search(pfx_ctx* ctx, const float* x, const float* y, const float* z,
+                             int64_t n, const float* qx, const float* qy, const float* qz,
+                             int64_t nq, double radius, int64_t* counts, int32_t* idx,
+                             float* d2, int64_t cap);
+
+/* ---- normals: NormalEstimationOMP (input == surface) ------------------------------- */
+pfx_status pfx_normals(pfx_ctx* ctx, const float* x, const float* y, const float* z, int64_t n,
+                       double radius, const float viewpoint[3], float* nx, float* ny, float* nz,
+                       float* curvature);
+pfx_status pfx_normals_dev(pfx_ctx* ctx, const float* d_x, const float* d_y, const float* d_z,
+                           int64_t n, double radius, const float viewpoint[3], float* d_nx,
+                           float* d_ny, float* d_nz, float* d_curvature);
+
+/* ---- FPFH-33: FPFHEstimation (surface + normals, queries = input cloud) ------------- */
+/* same_as_surface != 0 selects PCL's "input_ == surface_ && indices == all" branch (queries
+ * must then be the surface itself).  out: nq x 33 row-major (FPFHSignature33::histogram). */
+pfx_status pfx_fpfh(pfx_ctx* ctx, const float* sx, const float* sy, const float* sz,
+                    const float* snx, const float* sny, const float* snz, int64_t n_surface,
+                    const float* qx, const float* qy, const float* qz, int64_t nq,
+                    int same_as_surface, double radius, float* out);
+pfx_status pfx_fpfh_dev(pfx_ctx* ctx, const float* d_sx, const float* d_sy, const float* d_sz,
+                        const float* d_snx, const float* d_sny, const float* d_snz,
+                        int64_t n_surface, const float* d_qx, const float* d_qy,
+                        const float* d_qz, int64_t nq, int same_as_surface, double radius,
+                        float* d_out);
+
+/* ---- SHOT-352: SHOTEstimationOMP + SHOTLocalReferenceFrameEstimation ---------------- */
+/* desc: nq x 352, rf: nq x 9 (x_axis, y_axis, z_axis) -- SHOT352::{descriptor, rf}. */
+pfx_status pfx_shot(pfx_ctx* ctx, const float* sx, const float* sy, const float* sz,
+                    const float* snx, const float* sny, const float* snz, int64_t n_surface,
+                    const float* qx, const float* qy, const float* qz, int64_t nq,
+                    double radius, float* desc, float* rf);
+pfx_status pfx_shot_dev(pfx_ctx* ctx, const float* d_sx, const float* d_sy, const float* d_sz,
+                        const float* d_snx, const float* d_sny, const float* d_snz,
+                        int64_t n_surface, const float* d_qx, const float* d_qy,
+                        const float* d_qz, int64_t nq, double radius, float* d_desc,
+                        float* d_rf);
+
+/* ---- range image + NARF keypoints ---------------------------------------------------- */
+/* out_points: width*height x 4 floats {x, y, z, range} (PointWithRange); unobserved pixels
+ * are {NaN, NaN, NaN, -inf}. */
+pfx_status pfx_range_image_planar(pfx_ctx* ctx, const float* x, const float* y, const float* z,
+                                  int64_t n, const pfx_camera* cam, float* out_points);
+/* Keypoint pixel indices (y*width + x), ascending, as NarfKeypoint::compute returns them in
+ * PointCloud<int>.  *n_out = number of keypoints; PFX_ERR_CAPACITY if it exceeds cap. */
+pfx_status pfx_narf_keypoints(pfx_ctx* ctx, const float* x, const float* y, const float* z,
+                              int64_t n, const pfx_camera* cam, const pfx_narf_params* params,
+                              int32_t* out, int64_t cap, int64_t* n_out);
+pfx_status pfx_narf_keypoints_dev(pfx_ctx* ctx, const float* d_x, const float* d_y,
+                                  const float* d_z, int64_t n, const pfx_camera* cam,
+                                  const pfx_narf_params* params, int32_t* out, int64_t cap,
+                                  int64_t* n_out);
+/* Debug/parity access to the NARF intermediates of the last pfx_narf_keypoints* call
+ * (host buffers of width*height elements):  "interest" (float), "surface_change" (float),
+ * "border_traits" (uint32 bitset, PCL BorderTrait order), "range" (float).            */
+pfx_status pfx_narf_debug_image(pfx_ctx* ctx, const char* which, void* out, int64_t count);
+
+/* ---- the reference's keypoint -> cloud mapping (keypoints.h:227-229) ----------------- */
+/* k_xyz[i] = cloud[idx[i]] for 0 <= idx[i] < n (the reference indexes the cloud with pixel
+ * indices; out-of-range indices are an out-of-bounds read there and are skipped here).
+ * Returns the number of points written to d_kx/d_ky/d_kz. */
+pfx_status pfx_gather_points_dev(pfx_ctx* ctx, const float* d_x, const float* d_y,
+                                 const float* d_z, int64_t n, const int32_t* idx, int64_t k,
+                                 float* d_kx, float* d_ky, float* d_kz, int64_t* n_out);
+
+#ifdef __cplusplus
+} /* extern "C" */
+#endif
+#endif /* PFX_H_ */

@@ -1,0 +1,202 @@
+"""Python front-end of libpfx (host numpy arrays or torch device tensors).
+
+Every call goes through the HIP C-ABI (include/pfx.h); nothing here computes features on the
+CPU.  ``Context`` owns one ``pfx_ctx`` (one HIP stream) on one device.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from . import _native as N
+
+
+def _f32(a):
+    return np.ascontiguousarray(a, dtype=np.float32)
+
+
+def _ptr(a):
+    if a is None:
+        return None
+    if isinstance(a, np.ndarray):
+        return a.ctypes.data_as(ctypes.c_void_p)
+    return ctypes.c_void_p(a.data_ptr())  # torch tensor (device pointer)
+
+
+def narf_params(support_size=0.2, **kw) -> N.NarfParams:
+    p = N.NarfParams()
+    N.lib().pfx_narf_params_default(ctypes.byref(p))
+    p.support_size = support_size
+    for k, v in kw.items():
+        setattr(p, k, v)
+    return p
+
+
+def camera(**kw) -> N.Camera:
+    c = N.Camera()
+    N.lib().pfx_camera_default(ctypes.byref(c))
+    for k, v in kw.items():
+        if k == "sensor_pose":
+            for i, e in enumerate(np.asarray(v, dtype=np.float32).reshape(16)):
+                c.sensor_pose[i] = float(e)
+        else:
+            setattr(c, k, v)
+    return c
+
+
+class Context:
+    def __init__(self, device: int = 0):
+        self._lib = N.lib()
+        h = ctypes.c_void_p()
+        code = self._lib.pfx_ctx_create(device, ctypes.byref(h))
+        if code != 0:
+            raise N.PfxError(code, f"pfx_ctx_create(device={device}) failed")
+        self.h = h
+        self.device = device
+
+    def close(self):
+        if getattr(self, "h", None):
+            self._lib.pfx_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def _check(self, code):
+        if code != 0:
+            raise N.PfxError(code, self._lib.pfx_last_error(self.h).decode())
+
+    # ---- plumbing ------------------------------------------------------------------
+    def set_stream(self, stream_handle):
+        self._check(self._lib.pfx_ctx_set_stream(self.h, ctypes.c_void_p(stream_handle)))
+
+    def synchronize(self):
+        self._check(self._lib.pfx_ctx_synchronize(self.h))
+
+    def set_timing(self, enable=True):
+        self._check(self._lib.pfx_ctx_set_timing(self.h, 1 if enable else 0))
+
+    def reset_timing(self):
+        self._check(self._lib.pfx_ctx_reset_timing(self.h))
+
+    def kernel_time(self, name):
+        ms = ctypes.c_double()
+        n = ctypes.c_int64()
+        self._check(self._lib.pfx_ctx_kernel_time(self.h, name.encode(), ctypes.byref(ms), ctypes.byref(n)))
+        return ms.value, n.value
+
+    def stat(self, name):
+        v = ctypes.c_int64()
+        self._check(self._lib.pfx_ctx_last_stats(self.h, name.encode(), ctypes.byref(v)))
+        return v.value
+
+    # ---- host-array entry points ---------------------------------------------------
+    def radius_search(self, x, y, z, qx, qy, qz, r, cap=0):
+        x, y, z, qx, qy, qz = map(_f32, (x, y, z, qx, qy, qz))
+        nq = len(qx)
+        counts = np.zeros(nq, dtype=np.int64)
+        idx = d2 = None
+        if cap:
+            idx = np.full((nq, cap), -1, dtype=np.int32)
+            d2 = np.full((nq, cap), np.nan, dtype=np.float32)
+        self._check(self._lib.pfx_radius_search(self.h, _ptr(x), _ptr(y), _ptr(z), len(x), _ptr(qx), _ptr(qy),
+                                                _ptr(qz), nq, float(r), _ptr(counts), _ptr(idx), _ptr(d2),
+                                                int(cap)))
+        return counts, idx, d2
+
+    def normals(self, x, y, z, r, viewpoint=(0.0, 0.0, 0.0)):
+        x, y, z = map(_f32, (x, y, z))
+        n = len(x)
+        out = np.empty((4, n), dtype=np.float32)
+        vp = _f32(viewpoint)
+        self._check(self._lib.pfx_normals(self.h, _ptr(x), _ptr(y), _ptr(z), n, float(r), _ptr(vp), _ptr(out[0]),
+                                          _ptr(out[1]), _ptr(out[2]), _ptr(out[3])))
+        return out[0], out[1], out[2], out[3]
+
+    def fpfh(self, sx, sy, sz, nx, ny, nz, qx, qy, qz, r, same_as_surface=False):
+        sx, sy, sz, nx, ny, nz = map(_f32, (sx, sy, sz, nx, ny, nz))
+        if same_as_surface:
+            qx, qy, qz = sx, sy, sz
+        qx, qy, qz = map(_f32, (qx, qy, qz))
+        nq = len(qx)
+        out = np.empty((nq, 33), dtype=np.float32)
+        self._check(self._lib.pfx_fpfh(self.h, _ptr(sx), _ptr(sy), _ptr(sz), _ptr(nx), _ptr(ny), _ptr(nz), len(sx),
+                                       _ptr(qx), _ptr(qy), _ptr(qz), nq, 1 if same_as_surface else 0, float(r),
+                                       _ptr(out)))
+        return out
+
+    def shot(self, sx, sy, sz, nx, ny, nz, qx, qy, qz, r):
+        sx, sy, sz, nx, ny, nz, qx, qy, qz = map(_f32, (sx, sy, sz, nx, ny, nz, qx, qy, qz))
+        nq = len(qx)
+        desc = np.empty((nq, 352), dtype=np.float32)
+        rf = np.empty((nq, 9), dtype=np.float32)
+        self._check(self._lib.pfx_shot(self.h, _ptr(sx), _ptr(sy), _ptr(sz), _ptr(nx), _ptr(ny), _ptr(nz), len(sx),
+                                       _ptr(qx), _ptr(qy), _ptr(qz), nq, float(r), _ptr(desc), _ptr(rf)))
+        return desc, rf
+
+    def range_image_planar(self, x, y, z, cam=None):
+        cam = cam or camera()
+        x, y, z = map(_f32, (x, y, z))
+        out = np.empty((cam.height, cam.width, 4), dtype=np.float32)
+        self._check(self._lib.pfx_range_image_planar(self.h, _ptr(x), _ptr(y), _ptr(z), len(x), ctypes.byref(cam),
+                                                     _ptr(out)))
+        return out
+
+    def narf_keypoints(self, x, y, z, params=None, cam=None, cap=1 << 20):
+        cam = cam or camera()
+        params = params or narf_params()
+        x, y, z = map(_f32, (x, y, z))
+        out = np.empty(cap, dtype=np.int32)
+        nout = ctypes.c_int64()
+        self._check(self._lib.pfx_narf_keypoints(self.h, _ptr(x), _ptr(y), _ptr(z), len(x), ctypes.byref(cam),
+                                                 ctypes.byref(params), _ptr(out), cap, ctypes.byref(nout)))
+        return out[: nout.value].copy()
+
+    def narf_debug_image(self, which, width=640, height=480):
+        dt = np.uint32 if which == "border_traits" else np.float32
+        out = np.empty(width * height, dtype=dt)
+        self._check(self._lib.pfx_narf_debug_image(self.h, which.encode(), _ptr(out), out.size))
+        return out.reshape(height, width)
+
+    # ---- device (torch tensor) entry points, stream-ordered on the ctx stream ---------
+    def normals_dev(self, x, y, z, r, nx, ny, nz, curv, viewpoint=(0.0, 0.0, 0.0)):
+        vp = _f32(viewpoint)
+        self._check(self._lib.pfx_normals_dev(self.h, _ptr(x), _ptr(y), _ptr(z), x.numel(), float(r), _ptr(vp),
+                                              _ptr(nx), _ptr(ny), _ptr(nz), _ptr(curv)))
+
+    def fpfh_dev(self, sx, sy, sz, nx, ny, nz, qx, qy, qz, r, out, same_as_surface=False):
+        self._check(self._lib.pfx_fpfh_dev(self.h, _ptr(sx), _ptr(sy), _ptr(sz), _ptr(nx), _ptr(ny), _ptr(nz),
+                                           sx.numel(), _ptr(qx), _ptr(qy), _ptr(qz), qx.numel(),
+                                           1 if same_as_surface else 0, float(r), _ptr(out)))
+
+    def shot_dev(self, sx, sy, sz, nx, ny, nz, qx, qy, qz, r, desc, rf):
+        self._check(self._lib.pfx_shot_dev(self.h, _ptr(sx), _ptr(sy), _ptr(sz), _ptr(nx), _ptr(ny), _ptr(nz),
+                                           sx.numel(), _ptr(qx), _ptr(qy), _ptr(qz), qx.numel(), float(r),
+                                           _ptr(desc), _ptr(rf)))
+
+    def narf_keypoints_dev(self, x, y, z, params=None, cam=None, cap=1 << 20):
+        cam = cam or camera()
+        params = params or narf_params()
+        out = np.empty(cap, dtype=np.int32)
+        nout = ctypes.c_int64()
+        self._check(self._lib.pfx_narf_keypoints_dev(self.h, _ptr(x), _ptr(y), _ptr(z), x.numel(),
+                                                     ctypes.byref(cam), ctypes.byref(params), _ptr(out), cap,
+                                                     ctypes.byref(nout)))
+        return out[: nout.value].copy()
+
+    def gather_points_dev(self, x, y, z, idx_np, kx, ky, kz):
+        idx = np.ascontiguousarray(idx_np, dtype=np.int32)
+        nout = ctypes.c_int64()
+        self._check(self._lib.pfx_gather_points_dev(self.h, _ptr(x), _ptr(y), _ptr(z), x.numel(), _ptr(idx),
+                                                    len(idx), _ptr(kx), _ptr(ky), _ptr(kz), ctypes.byref(nout)))
+        return nout.value

@@ -1,0 +1,413 @@
+// pfx_api.hip -- the extern "C" boundary (include/pfx.h).  Host-pointer entry points stage
+// through ctx-owned device buffers and call the stream-ordered *_dev implementations.
+#include <cstring>
+
+#include "pfx_internal.h"
+
+using pfx::Error;
+
+#define PFX_API_BEGIN try {
+#define PFX_API_END(ctx)                                            \
+  }                                                                 \
+  catch (const pfx::Error& e) {                                     \
+    if (ctx) (ctx)->last_error = e.what();                          \
+    return e.code;                                                  \
+  }                                                                 \
+  catch (const std::exception& e) {                                 \
+    if (ctx) (ctx)->last_error = e.what();                          \
+    return PFX_ERR_DEVICE;                                          \
+  }                                                                 \
+  return PFX_OK;
+
+namespace {
+
+void harvest_timing(pfx_ctx* ctx) {
+  if (ctx->timer.pending.empty()) return;
+  PFX_HIP(hipStreamSynchronize(ctx->stream));
+  for (auto& p : ctx->timer.pending) {
+    float ms = 0.f;
+    PFX_HIP(hipEventElapsedTime(&ms, p.a, p.b));
+    auto& acc = ctx->timer.acc[p.name];
+    acc.first += ms;
+    acc.second += 1;
+    ctx->timer.pool.push_back(p.a);
+    ctx->timer.pool.push_back(p.b);
+  }
+  ctx->timer.pending.clear();
+}
+
+float* stage_in(pfx_ctx* ctx, const char* name, const float* host, int64_t count) {
+  float* d = ctx->buf(name).as<float>(count > 0 ? count : 1);
+  if (count > 0) PFX_HIP(hipMemcpyAsync(d, host, sizeof(float) * count, hipMemcpyHostToDevice, ctx->stream));
+  return d;
+}
+
+void check_ctx(pfx_ctx* ctx) {
+  if (!ctx) throw Error(PFX_ERR_INVALID, "null pfx_ctx");
+  PFX_HIP(hipSetDevice(ctx->device));
+}
+
+}  // namespace
+
+extern "C" {
+
+void pfx_narf_params_default(pfx_narf_params* p) {
+  if (!p) return;
+  p->support_size = -1.0f;
+  p->max_no_of_interest_points = -1;
+  p->min_distance_between_interest_points = 0.25f;
+  p->optimal_distance_to_high_surface_change = 0.25f;
+  p->min_interest_value = 0.45f;
+  p->min_surface_change_score = 0.2f;
+  p->do_non_maximum_suppression = 1;
+  p->calculate_sparse_interest_image = 1;
+  p->no_of_polynomial_approximations_per_point = 0;
+  p->add_points_on_straight_edges = 0;
+  p->pixel_radius_borders = 3;
+  p->pixel_radius_plane_extraction = 2;
+  p->pixel_radius_border_direction = 2;
+  p->minimum_border_probability = 0.8f;
+  p->pixel_radius_principal_curvature = 2;
+}
+
+void pfx_camera_default(pfx_camera* c) {
+  if (!c) return;
+  c->width = 640;
+  c->height = 480;
+  c->center_x = 640.0f / 2.0f;
+  c->center_y = 480.0f / 2.0f;
+  c->focal_length_x = 525.0f;
+  c->focal_length_y = 525.0f;
+  for (int i = 0; i < 16; ++i) c->sensor_pose[i] = (i % 5 == 0) ? 1.0f : 0.0f;
+  c->coordinate_frame = 0;
+  c->noise_level = 0.0f;
+  c->min_range = 0.0f;
+}
+
+pfx_status pfx_ctx_create(int device, pfx_ctx** out) {
+  if (!out) return PFX_ERR_INVALID;
+  *out = nullptr;
+  pfx_ctx* ctx = nullptr;
+  try {
+    int count = 0;
+    hipError_t e = hipGetDeviceCount(&count);
+    if (e != hipSuccess || count == 0)
+      throw Error(PFX_ERR_DEVICE, std::string("no HIP device available: ") + hipGetErrorString(e));
+    if (device < 0 || device >= count) throw Error(PFX_ERR_INVALID, "device ordinal out of range");
+    ctx = new pfx_ctx();
+    ctx->device = device;
+    PFX_HIP(hipSetDevice(device));
+    PFX_HIP(hipStreamCreateWithFlags(&ctx->own_stream, hipStreamNonBlocking));
+    ctx->stream = ctx->own_stream;
+    *out = ctx;
+    return PFX_OK;
+  } catch (const Error& e) {
+    delete ctx;
+    return e.code;
+  }
+}
+
+void pfx_ctx_destroy(pfx_ctx* ctx) {
+  if (!ctx) return;
+  (void)hipSetDevice(ctx->device);
+  (void)hipStreamSynchronize(ctx->stream);
+  pfx::narf_release(ctx);
+  ctx->grid_a.release();
+  ctx->grid_b.release();
+  for (auto& kv : ctx->bufs) kv.second.release();
+  for (auto& p : ctx->timer.pending) { (void)hipEventDestroy(p.a); (void)hipEventDestroy(p.b); }
+  for (auto e : ctx->timer.pool) (void)hipEventDestroy(e);
+  if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);
+  delete ctx;
+}
+
+const char* pfx_last_error(const pfx_ctx* ctx) { return ctx ? ctx->last_error.c_str() : "null pfx_ctx"; }
+
+pfx_status pfx_ctx_set_stream(pfx_ctx* ctx, void* hip_stream) {
+  PFX_API_BEGIN
+  check_ctx(ctx);
+  harvest_timing(ctx);
+  ctx->stream = hip_stream ? static_cast<hipStream_t>(hip_stream) : ctx->own_stream;
+  PFX_API_END(ctx)
+}
+
+void* pfx_ctx_get_stream(pfx_ctx* ctx) { return ctx ? (void*)ctx->stream : nullptr; }
+
+pfx_status pfx_ctx_synchronize(pfx_ctx* ctx) {
+  PFX_API_BEGIN
+  check_ctx(ctx);
+  PFX_HIP(hipStreamSynchronize(ctx->stream));
+  PFX_API_END(ctx)
+}
+
+pfx_status pfx_ctx_set_timing(pfx_ctx* ctx, int enable) {
+  PFX_API_BEGIN
+  check_ctx(ctx);
+  harvest_timing(ctx);
+  ctx->timer.enabled = enable != 0;
+  PFX_API_END(ctx)
+}
+
+pfx_status pfx_ctx_reset_timing(pfx_ctx* ctx) {
+  PFX_API_BEGIN
+  check_ctx(ctx);
+  harvest_timing(ctx);
+  ctx->timer.acc.clear();
+  PFX_API_END(ctx)
+}
+
+pfx_status pfx_ctx_kernel_time(pfx_ctx* ctx, const char* name, double* total_ms, int64_t* launches) {
+  PFX_API_BEGIN
+  check_ctx(ctx);
+  if (!name || !total_ms || !launches) throw Error(PFX_ERR_INVALID, "null argument");
+  harvest_timing(ctx);
+  auto it = ctx->timer.acc.find(name);
+  *total_ms = it == ctx->timer.acc.end() ? 0.0 : it->second.first;
+  *launches = it == ctx->timer.acc.end() ? 0 : it->second.second;
+  PFX_API_END(ctx)
+}
+
+pfx_status pfx_ctx_last_stats(pfx_ctx* ctx, const char* what, int64_t* value) {
+  PFX_API_BEGIN
+  if (!ctx || !what || !value) throw Error(PFX_ERR_INVALID, "null argument");
+  auto it = ctx->stats.find(what);
+  if (it == ctx->stats.end()) throw Error(PFX_ERR_INVALID, std::string("unknown stat ") + what);
+  *value = it->second;
+  PFX_API_END(ctx)
+}
+
+pfx_status pfx_radius_search(pfx_ctx* ctx, const float* x, const float* y, const float* z, int64_t n,
+                             const float* qx, const float* qy, const float* qz, int64_t nq, double radius,
+                             int64_t* counts, int32_t* idx, float* d2, int64_t cap) {
+  PFX_API_BEGIN
+  check_ctx(ctx);
+  if (n < 0 || nq < 0 || (n && (!x || !y || !z)) || (nq && (!qx || !qy || !qz || !counts)))
+    throw Error(PFX_ERR_INVALID, "radius_search: invalid arguments");
+  if (idx && (cap <= 0 || !d2)) throw Error(PFX_ERR_INVALID, "radius_search: idx needs cap > 0 and d2");
+  float* dx = stage_in(ctx, "in_x", x, n);
+  float* dy = stage_in(ctx, "in_y", y, n);
+  float* dz = stage_in(ctx, "in_z", z, n);
+  float* dqx = stage_in(ctx, "in_qx", qx, nq);
+  float* dqy = stage_in(ctx, "in_qy", qy, nq);
+  float* dqz = stage_in(ctx, "in_qz", qz, nq);
+  int64_t* dc = ctx->buf("out_counts").as<int64_t>(nq + 1);
+  int32_t* di = idx ? ctx->buf("out_idx").as<int32_t>(nq * cap + 1) : nullptr;
+  float* dd = idx ? ctx->buf("out_d2").as<float>(nq * cap + 1) : nullptr;
+  pfx::radius_search_dev(ctx, dx, dy, dz, n, dqx, dqy, dqz, nq, radius, dc, di, dd, cap);
+  if (nq) PFX_HIP(hipMemcpyAsync(counts, dc, sizeof(int64_t) * nq, hipMemcpyDeviceToHost, ctx->stream));
+  if (idx && nq) {
+    PFX_HIP(hipMemcpyAsync(idx, di, sizeof(int32_t) * nq * cap, hipMemcpyDeviceToHost, ctx->stream));
+    PFX_HIP(hipMemcpyAsync(d2, dd, sizeof(float) * nq * cap, hipMemcpyDeviceToHost, ctx->stream));
+  }
+  PFX_HIP(hipStreamSynchronize(ctx->stream));
+  PFX_API_END(ctx)
+}
+
+pfx_status pfx_normals_dev(pfx_ctx* ctx, const float* d_x, const float* d_y, const float* d_z, int64_t n,
+                           double radius, const float viewpoint[3], float* d_nx, float* d_ny, float* d_nz,
+                           float* d_curvature) {
+  PFX_API_BEGIN
+  check_ctx(ctx);
+  if (n < 0 || (n && (!d_x || !d_y || !d_z || !d_nx || !d_ny || !d_nz || !d_curvature)))
+    throw Error(PFX_ERR_INVALID, "normals: invalid arguments");
+  const float vp0[3] = {0.f, 0.f, 0.f};
+  pfx::normals_dev(ctx, d_x, d_y, d_z, n, radius, viewpoint ? viewpoint : vp0, d_nx, d_ny, d_nz, d_curvature);
+  PFX_API_END(ctx)
+}
+
+pfx_status pfx_normals(pfx_ctx* ctx, const float* x, const float* y, const float* z, int64_t n, double radius,
+                       const float viewpoint[3], float* nx, float* ny, float* nz, float* curvature) {
+  PFX_API_BEGIN
+  check_ctx(ctx);
+  if (n < 0 || (n && (!x || !y || !z || !nx || !ny || !nz || !curvature)))
+    throw Error(PFX_ERR_INVALID, "normals: invalid arguments");
+  float* dx = stage_in(ctx, "in_x", x, n);
+  float* dy = stage_in(ctx, "in_y", y, n);
+  float* dz = stage_in(ctx, "in_z", z, n);
+  float* out = ctx->buf("out_normals").as<float>(4 * n + 4);
+  const float vp0[3] = {0.f, 0.f, 0.f};
+  pfx::normals_dev(ctx, dx, dy, dz, n, radius, viewpoint ? viewpoint : vp0, out, out + n, out + 2 * n, out + 3 * n);
+  if (n) {
+    PFX_HIP(hipMemcpyAsync(nx, out, sizeof(float) * n, hipMemcpyDeviceToHost, ctx->stream));
+    PFX_HIP(hipMemcpyAsync(ny, out + n, sizeof(float) * n, hipMemcpyDeviceToHost, ctx->stream));
+    PFX_HIP(hipMemcpyAsync(nz, out + 2 * n, sizeof(float) * n, hipMemcpyDeviceToHost, ctx->stream));
+    PFX_HIP(hipMemcpyAsync(curvature, out + 3 * n, sizeof(float) * n, hipMemcpyDeviceToHost, ctx->stream));
+  }
+  PFX_HIP(hipStreamSynchronize(ctx->stream));
+  PFX_API_END(ctx)
+}
+
+pfx_status pfx_fpfh_dev(pfx_ctx* ctx, const float* d_sx, const float* d_sy, const float* d_sz,
+                        const float* d_snx, const float* d_sny, const float* d_snz, int64_t n_surface,
+                        const float* d_qx, const float* d_qy, const float* d_qz, int64_t nq,
+                        int same_as_surface, double radius, float* d_out) {
+  PFX_API_BEGIN
+  check_ctx(ctx);
+  if (n_surface < 0 || nq < 0 || (nq && !d_out) ||
+      (n_surface && (!d_sx || !d_sy || !d_sz || !d_snx || !d_sny || !d_snz)) ||
+      (nq && (!d_qx || !d_qy || !d_qz)))
+    throw Error(PFX_ERR_INVALID, "fpfh: invalid arguments");
+  if (same_as_surface && nq != n_surface)
+    throw Error(PFX_ERR_INVALID, "fpfh: same_as_surface requires nq == n_surface");
+  pfx::fpfh_dev(ctx, d_sx, d_sy, d_sz, d_snx, d_sny, d_snz, n_surface, d_qx, d_qy, d_qz, nq, same_as_surface,
+                radius, d_out);
+  PFX_API_END(ctx)
+}
+
+pfx_status pfx_fpfh(pfx_ctx* ctx, const float* sx, const float* sy, const float* sz, const float* snx,
+                    const float* sny, const float* snz, int64_t n_surface, const float* qx, const float* qy,
+                    const float* qz, int64_t nq, int same_as_surface, double radius, float* out) {
+  PFX_API_BEGIN
+  check_ctx(ctx);
+  if (n_surface < 0 || nq < 0 || (nq && !out)) throw Error(PFX_ERR_INVALID, "fpfh: invalid arguments");
+  if (same_as_surface && nq != n_surface)
+    throw Error(PFX_ERR_INVALID, "fpfh: same_as_surface requires nq == n_surface");
+  float* dsx = stage_in(ctx, "in_x", sx, n_surface);
+  float* dsy = stage_in(ctx, "in_y", sy, n_surface);
+  float* dsz = stage_in(ctx, "in_z", sz, n_surface);
+  float* dnx = stage_in(ctx, "in_nx", snx, n_surface);
+  float* dny = stage_in(ctx, "in_ny", sny, n_surface);
+  float* dnz = stage_in(ctx, "in_nz", snz, n_surface);
+  float *dqx = dsx, *dqy = dsy, *dqz = dsz;
+  if (!same_as_surface) {
+    dqx = stage_in(ctx, "in_qx", qx, nq);
+    dqy = stage_in(ctx, "in_qy", qy, nq);
+    dqz = stage_in(ctx, "in_qz", qz, nq);
+  }
+  float* dout = ctx->buf("out_fpfh").as<float>(nq * 33 + 1);
+  pfx::fpfh_dev(ctx, dsx, dsy, dsz, dnx, dny, dnz, n_surface, dqx, dqy, dqz, nq, same_as_surface, radius, dout);
+  if (nq) PFX_HIP(hipMemcpyAsync(out, dout, sizeof(float) * nq * 33, hipMemcpyDeviceToHost, ctx->stream));
+  PFX_HIP(hipStreamSynchronize(ctx->stream));
+  PFX_API_END(ctx)
+}
+
+pfx_status pfx_shot_dev(pfx_ctx* ctx, const float* d_sx, const float* d_sy, const float* d_sz,
+                        const float* d_snx, const float* d_sny, const float* d_snz, int64_t n_surface,
+                        const float* d_qx, const float* d_qy, const float* d_qz, int64_t nq, double radius,
+                        float* d_desc, float* d_rf) {
+  PFX_API_BEGIN
+  check_ctx(ctx);
+  if (n_surface < 0 || nq < 0 || (nq && (!d_desc || !d_rf || !d_qx || !d_qy || !d_qz)))
+    throw Error(PFX_ERR_INVALID, "shot: invalid arguments");
+  pfx::shot_dev(ctx, d_sx, d_sy, d_sz, d_snx, d_sny, d_snz, n_surface, d_qx, d_qy, d_qz, nq, radius, d_desc, d_rf);
+  PFX_API_END(ctx)
+}
+
+pfx_status pfx_shot(pfx_ctx* ctx, const float* sx, const float* sy, const float* sz, const float* snx,
+                    const float* sny, const float* snz, int64_t n_surface, const float* qx, const float* qy,
+                    const float* qz, int64_t nq, double radius, float* desc, float* rf) {
+  PFX_API_BEGIN
+  check_ctx(ctx);
+  if (n_surface < 0 || nq < 0 || (nq && (!desc || !rf))) throw Error(PFX_ERR_INVALID, "shot: invalid arguments");
+  float* dsx = stage_in(ctx, "in_x", sx, n_surface);
+  float* dsy = stage_in(ctx, "in_y", sy, n_surface);
+  float* dsz = stage_in(ctx, "in_z", sz, n_surface);
+  float* dnx = stage_in(ctx, "in_nx", snx, n_surface);
+  float* dny = stage_in(ctx, "in_ny", sny, n_surface);
+  float* dnz = stage_in(ctx, "in_nz", snz, n_surface);
+  float* dqx = stage_in(ctx, "in_qx", qx, nq);
+  float* dqy = stage_in(ctx, "in_qy", qy, nq);
+  float* dqz = stage_in(ctx, "in_qz", qz, nq);
+  float* ddesc = ctx->buf("out_shot").as<float>(nq * 352 + 1);
+  float* drf = ctx->buf("out_rf").as<float>(nq * 9 + 1);
+  pfx::shot_dev(ctx, dsx, dsy, dsz, dnx, dny, dnz, n_surface, dqx, dqy, dqz, nq, radius, ddesc, drf);
+  if (nq) {
+    PFX_HIP(hipMemcpyAsync(desc, ddesc, sizeof(float) * nq * 352, hipMemcpyDeviceToHost, ctx->stream));
+    PFX_HIP(hipMemcpyAsync(rf, drf, sizeof(float) * nq * 9, hipMemcpyDeviceToHost, ctx->stream));
+  }
+  PFX_HIP(hipStreamSynchronize(ctx->stream));
+  PFX_API_END(ctx)
+}
+
+pfx_status pfx_range_image_planar(pfx_ctx* ctx, const float* x, const float* y, const float* z, int64_t n,
+                                  const pfx_camera* cam, float* out_points) {
+  PFX_API_BEGIN
+  check_ctx(ctx);
+  if (!cam || !out_points || n < 0 || cam->width <= 0 || cam->height <= 0)
+    throw Error(PFX_ERR_INVALID, "range_image: invalid arguments");
+  float* dx = stage_in(ctx, "in_x", x, n);
+  float* dy = stage_in(ctx, "in_y", y, n);
+  float* dz = stage_in(ctx, "in_z", z, n);
+  int64_t npx = (int64_t)cam->width * cam->height;
+  float4* d = ctx->buf("out_ri").as<float4>(npx);
+  pfx::range_image_dev(ctx, dx, dy, dz, n, *cam, d);
+  PFX_HIP(hipMemcpyAsync(out_points, d, sizeof(float4) * npx, hipMemcpyDeviceToHost, ctx->stream));
+  PFX_HIP(hipStreamSynchronize(ctx->stream));
+  PFX_API_END(ctx)
+}
+
+pfx_status pfx_narf_keypoints_dev(pfx_ctx* ctx, const float* d_x, const float* d_y, const float* d_z, int64_t n,
+                                  const pfx_camera* cam, const pfx_narf_params* params, int32_t* out, int64_t cap,
+                                  int64_t* n_out) {
+  PFX_API_BEGIN
+  check_ctx(ctx);
+  if (!cam || !params || !n_out || n < 0 || (cap > 0 && !out))
+    throw Error(PFX_ERR_INVALID, "narf: invalid arguments");
+  std::vector<int32_t> kp;
+  pfx::narf_dev(ctx, d_x, d_y, d_z, n, *cam, *params, kp);
+  *n_out = (int64_t)kp.size();
+  if ((int64_t)kp.size() > cap) throw Error(PFX_ERR_CAPACITY, "narf: output capacity too small");
+  if (!kp.empty()) std::memcpy(out, kp.data(), sizeof(int32_t) * kp.size());
+  PFX_API_END(ctx)
+}
+
+pfx_status pfx_narf_keypoints(pfx_ctx* ctx, const float* x, const float* y, const float* z, int64_t n,
+                              const pfx_camera* cam, const pfx_narf_params* params, int32_t* out, int64_t cap,
+                              int64_t* n_out) {
+  PFX_API_BEGIN
+  check_ctx(ctx);
+  if (n < 0) throw Error(PFX_ERR_INVALID, "narf: invalid arguments");
+  float* dx = stage_in(ctx, "in_x", x, n);
+  float* dy = stage_in(ctx, "in_y", y, n);
+  float* dz = stage_in(ctx, "in_z", z, n);
+  pfx_status s = pfx_narf_keypoints_dev(ctx, dx, dy, dz, n, cam, params, out, cap, n_out);
+  if (s != PFX_OK) return s;
+  PFX_API_END(ctx)
+}
+
+pfx_status pfx_narf_debug_image(pfx_ctx* ctx, const char* which, void* out, int64_t count) {
+  PFX_API_BEGIN
+  check_ctx(ctx);
+  if (!which || !out) throw Error(PFX_ERR_INVALID, "narf_debug: null argument");
+  pfx::narf_debug(ctx, which, out, count);
+  PFX_API_END(ctx)
+}
+
+}  // extern "C"
+
+// ---- keypoints.h:227-229: cloud_keypoints->points.push_back(cloud->points[keypoints[i]]) ----
+namespace {
+__global__ void k_gather_points(const float* __restrict__ x, const float* __restrict__ y, const float* __restrict__ z,
+                                int64_t n, const int32_t* __restrict__ idx, int64_t k, float* __restrict__ kx,
+                                float* __restrict__ ky, float* __restrict__ kz) {
+  int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (i >= k) return;
+  int32_t p = idx[i];
+  kx[i] = x[p];
+  ky[i] = y[p];
+  kz[i] = z[p];
+}
+}  // namespace
+
+extern "C" pfx_status pfx_gather_points_dev(pfx_ctx* ctx, const float* d_x, const float* d_y, const float* d_z,
+                                            int64_t n, const int32_t* idx, int64_t k, float* d_kx, float* d_ky,
+                                            float* d_kz, int64_t* n_out) {
+  PFX_API_BEGIN
+  check_ctx(ctx);
+  if (!n_out || k < 0 || (k && !idx)) throw Error(PFX_ERR_INVALID, "gather_points: invalid arguments");
+  // the reference reads cloud->points[pixel_index] unchecked (out of bounds when the index is
+  // >= cloud size); the guarded mapping keeps only in-range indices, in order
+  std::vector<int32_t> keep;
+  keep.reserve((size_t)k);
+  for (int64_t i = 0; i < k; ++i)
+    if (idx[i] >= 0 && idx[i] < n) keep.push_back(idx[i]);
+  *n_out = (int64_t)keep.size();
+  if (keep.empty()) return PFX_OK;
+  int32_t* d_idx = ctx->buf("gather_idx").as<int32_t>(keep.size());
+  PFX_HIP(hipMemcpyAsync(d_idx, keep.data(), sizeof(int32_t) * keep.size(), hipMemcpyHostToDevice, ctx->stream));
+  k_gather_points<<<(unsigned)pfx::ceil_div((int64_t)keep.size(), 256), 256, 0, ctx->stream>>>(
+      d_x, d_y, d_z, n, d_idx, (int64_t)keep.size(), d_kx, d_ky, d_kz);
+  pfx::check_launch("k_gather_points");
+  PFX_HIP(hipStreamSynchronize(ctx->stream));  // `keep` is pageable host memory
+  PFX_API_END(ctx)
+}

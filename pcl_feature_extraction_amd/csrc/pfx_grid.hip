@@ -1,0 +1,182 @@
+// pfx_grid.hip -- uniform-grid spatial index (replaces the FLANN kd-tree that
+// search::KdTree<PointXYZRGB> builds at features.h:192 / tools.h:29).
+//
+// Layout in HBM (all SoA, 4-byte elements):
+//   sx/sy/sz[n]     point coordinates sorted by linear cell key  (coalesced run reads)
+//   perm[n]         sorted position -> caller point index         (FLANN tie-break key)
+//   cell_start[C+1] exclusive prefix of per-cell counts, C = nx*ny*nz <= 2^26
+// Cells are >= r (r*(1+1e-6)), so the radius ball of a query lies in its 3x3x3 cell block;
+// with row-major keys (x, y, z) the block is 9 contiguous runs of 3 z-cells.
+// Non-finite points get key C and sort behind every cell (never a neighbour, as PCL's
+// kd-tree skips them).
+#include <cstring>
+#include <rocprim/rocprim.hpp>
+
+#include "pfx_internal.h"
+
+namespace pfx {
+namespace {
+
+__device__ __forceinline__ uint32_t f2ord(float f) {
+  uint32_t u = __float_as_uint(f);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__host__ __device__ __forceinline__ float ord2f(uint32_t u) {
+  uint32_t b = (u & 0x80000000u) ? (u & 0x7fffffffu) : ~u;
+  float f;
+  memcpy(&f, &b, 4);
+  return f;
+}
+
+__global__ void __launch_bounds__(256) k_bbox(const float* __restrict__ x, const float* __restrict__ y,
+                                              const float* __restrict__ z, int64_t n,
+                                              uint32_t* __restrict__ mm) {
+  float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    float p[3] = {x[i], y[i], z[i]};
+    if (!(isfinite(p[0]) && isfinite(p[1]) && isfinite(p[2]))) continue;
+#pragma unroll
+    for (int d = 0; d < 3; ++d) { lo[d] = fminf(lo[d], p[d]); hi[d] = fmaxf(hi[d], p[d]); }
+  }
+#pragma unroll
+  for (int d = 0; d < 3; ++d) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      lo[d] = fminf(lo[d], __shfl_xor(lo[d], off));
+      hi[d] = fmaxf(hi[d], __shfl_xor(hi[d], off));
+    }
+  }
+  if ((threadIdx.x & 63) == 0) {
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+      if (lo[d] <= hi[d]) {
+        atomicMin(&mm[d], f2ord(lo[d]));
+        atomicMax(&mm[3 + d], f2ord(hi[d]));
+      }
+    }
+  }
+}
+
+__global__ void __launch_bounds__(256) k_cell_keys(const float* __restrict__ x, const float* __restrict__ y,
+                                                   const float* __restrict__ z, int64_t n, double inv,
+                                                   double ox, double oy, double oz, int32_t nx, int32_t ny,
+                                                   int32_t nz, uint32_t* __restrict__ keys,
+                                                   uint32_t* __restrict__ vals,
+                                                   uint32_t* __restrict__ counts) {
+  int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  float px = x[i], py = y[i], pz = z[i];
+  uint32_t key = (uint32_t)((int64_t)nx * ny * nz);
+  if (isfinite(px) && isfinite(py) && isfinite(pz)) {
+    int64_t ix = (int64_t)floor(((double)px - ox) * inv);
+    int64_t iy = (int64_t)floor(((double)py - oy) * inv);
+    int64_t iz = (int64_t)floor(((double)pz - oz) * inv);
+    ix = ix < 0 ? 0 : (ix >= nx ? nx - 1 : ix);
+    iy = iy < 0 ? 0 : (iy >= ny ? ny - 1 : iy);
+    iz = iz < 0 ? 0 : (iz >= nz ? nz - 1 : iz);
+    key = (uint32_t)((ix * ny + iy) * nz + iz);
+  }
+  keys[i] = key;
+  vals[i] = (uint32_t)i;
+  atomicAdd(&counts[key], 1u);
+}
+
+__global__ void __launch_bounds__(256) k_gather_sorted(const float* __restrict__ x, const float* __restrict__ y,
+                                                       const float* __restrict__ z, int64_t n,
+                                                       const uint32_t* __restrict__ perm,
+                                                       float* __restrict__ sx, float* __restrict__ sy,
+                                                       float* __restrict__ sz) {
+  int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t p = perm[i];
+  sx[i] = x[p];
+  sy[i] = y[p];
+  sz[i] = z[p];
+}
+
+}  // namespace
+
+void build_grid(pfx_ctx* ctx, Grid& g, const float* d_x, const float* d_y, const float* d_z,
+                int64_t n, double radius) {
+  PFX_CHECK(n >= 0 && n < (int64_t(1) << 31), "point count must be in [0, 2^31)");
+  PFX_CHECK(radius > 0.0, "radius must be > 0");
+  hipStream_t st = ctx->stream;
+  g.n = n;
+  g.ux = d_x; g.uy = d_y; g.uz = d_z;
+  uint32_t* mm = g.b_minmax.as<uint32_t>(6);
+  uint32_t init[6] = {0xffffffffu, 0xffffffffu, 0xffffffffu, 0u, 0u, 0u};
+  PFX_HIP(hipMemcpyAsync(mm, init, sizeof(init), hipMemcpyHostToDevice, st));
+  if (n > 0) {
+    TimeScope ts(ctx, "grid_bbox");
+    int blocks = (int)std::min<int64_t>(ceil_div(n, 256), 2048);
+    k_bbox<<<blocks, 256, 0, st>>>(d_x, d_y, d_z, n, mm);
+    check_launch("k_bbox");
+  }
+  uint32_t host_mm[6];
+  PFX_HIP(hipMemcpyAsync(host_mm, mm, sizeof(host_mm), hipMemcpyDeviceToHost, st));
+  PFX_HIP(hipStreamSynchronize(st));
+  double lo[3] = {0, 0, 0}, hi[3] = {0, 0, 0};
+  bool any = host_mm[0] != 0xffffffffu && host_mm[3] != 0u;
+  for (int d = 0; d < 3 && any; ++d) { lo[d] = ord2f(host_mm[d]); hi[d] = ord2f(host_mm[3 + d]); }
+  double cell = radius * (1.0 + 1e-6);
+  const double max_cells = double(1 << 26);
+  int64_t dims[3];
+  for (int it = 0; it < 64; ++it) {
+    for (int d = 0; d < 3; ++d) dims[d] = (int64_t)std::floor((hi[d] - lo[d]) / cell) + 1;
+    double total = double(dims[0]) * double(dims[1]) * double(dims[2]);
+    if (total <= max_cells) break;
+    cell *= std::cbrt(total / max_cells) * 1.01;
+  }
+  g.cell = (float)cell;
+  g.inv = (float)(1.0 / cell);
+  g.ox = (float)lo[0]; g.oy = (float)lo[1]; g.oz = (float)lo[2];
+  g.nx = (int32_t)dims[0]; g.ny = (int32_t)dims[1]; g.nz = (int32_t)dims[2];
+  g.ncells = dims[0] * dims[1] * dims[2];
+  // exact double parameters used by both builder and queries
+  const double inv = 1.0 / cell;
+  g.inv = (float)inv;
+  const int64_t C = g.ncells;
+
+  int bits = 1;
+  while ((int64_t(1) << bits) <= C) ++bits;
+  // size every scratch buffer before the first launch (no realloc behind pending work)
+  size_t sort_bytes = 0, scan_bytes = 0;
+  PFX_HIP(rocprim::radix_sort_pairs(nullptr, sort_bytes, (uint32_t*)nullptr, (uint32_t*)nullptr,
+                                    (uint32_t*)nullptr, (uint32_t*)nullptr, (size_t)std::max<int64_t>(n, 1),
+                                    0, bits, st));
+  PFX_HIP(rocprim::exclusive_scan(nullptr, scan_bytes, (uint32_t*)nullptr, (uint32_t*)nullptr, 0u,
+                                  (size_t)(C + 2), rocprim::plus<uint32_t>(), st));
+  void* tmp = g.b_tmp.get(std::max(sort_bytes, scan_bytes) + 16);
+  uint32_t* keys = g.b_keys.as<uint32_t>(n + 1);
+  uint32_t* keys2 = g.b_keys2.as<uint32_t>(std::max<int64_t>(n + 1, C + 2));
+  uint32_t* vals = g.b_vals.as<uint32_t>(n + 1);
+  g.perm = g.b_perm.as<int32_t>(n + 1);
+  g.sx = g.b_sx.as<float>(n + 1);
+  g.sy = g.b_sy.as<float>(n + 1);
+  g.sz = g.b_sz.as<float>(n + 1);
+  g.cell_start = g.b_start.as<int32_t>(C + 2);
+  g.dinv = inv;
+  g.dox = lo[0]; g.doy = lo[1]; g.doz = lo[2];
+  uint32_t* counts = keys2;  // per-cell histogram (keys2 is free until the sort)
+  {
+    TimeScope ts(ctx, "grid_build");
+    PFX_HIP(hipMemsetAsync(counts, 0, sizeof(uint32_t) * (C + 2), st));
+    if (n > 0) {
+      k_cell_keys<<<(unsigned)ceil_div(n, 256), 256, 0, st>>>(d_x, d_y, d_z, n, inv, lo[0], lo[1], lo[2],
+                                                              g.nx, g.ny, g.nz, keys, vals, counts);
+      check_launch("k_cell_keys");
+    }
+    PFX_HIP(rocprim::exclusive_scan(tmp, scan_bytes, counts, reinterpret_cast<uint32_t*>(g.cell_start),
+                                    0u, (size_t)(C + 2), rocprim::plus<uint32_t>(), st));
+    if (n > 0) {
+      PFX_HIP(rocprim::radix_sort_pairs(tmp, sort_bytes, keys, keys2, vals,
+                                        reinterpret_cast<uint32_t*>(g.perm), (size_t)n, 0, bits, st));
+      k_gather_sorted<<<(unsigned)ceil_div(n, 256), 256, 0, st>>>(
+          d_x, d_y, d_z, n, reinterpret_cast<uint32_t*>(g.perm), g.sx, g.sy, g.sz);
+      check_launch("k_gather_sorted");
+    }
+  }
+}
+
+}  // namespace pfx

@@ -1,0 +1,170 @@
+// pfx_internal.h -- host-side context, error and workspace plumbing of libpfx (HIP, gfx950).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <map>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/pfx.h"
+
+namespace pfx {
+
+struct Error : std::runtime_error {
+  pfx_status code;
+  Error(pfx_status c, const std::string& m) : std::runtime_error(m), code(c) {}
+};
+
+#define PFX_HIP(expr)                                                                   \
+  do {                                                                                  \
+    hipError_t _e = (expr);                                                             \
+    if (_e != hipSuccess)                                                               \
+      throw ::pfx::Error(PFX_ERR_DEVICE, std::string(#expr) + ": " + hipGetErrorString(_e)); \
+  } while (0)
+
+#define PFX_CHECK(cond, msg)                                                \
+  do {                                                                      \
+    if (!(cond)) throw ::pfx::Error(PFX_ERR_INVALID, std::string(msg));     \
+  } while (0)
+
+// Device scratch that only grows (one per purpose, reused across calls; no hipMalloc inside
+// a steady-state call once sizes have been seen).
+struct DevBuf {
+  void* ptr = nullptr;
+  size_t bytes = 0;
+  void* get(size_t need) {
+    if (need > bytes) {
+      if (ptr) PFX_HIP(hipFree(ptr));
+      size_t nb = need + need / 4 + 256;
+      PFX_HIP(hipMalloc(&ptr, nb));
+      bytes = nb;
+    }
+    return ptr;
+  }
+  template <class T> T* as(size_t count) { return static_cast<T*>(get(count * sizeof(T))); }
+  void release() { if (ptr) (void)hipFree(ptr); ptr = nullptr; bytes = 0; }
+};
+
+struct KernelTimer {
+  struct Pending { hipEvent_t a, b; std::string name; };
+  bool enabled = false;
+  std::vector<Pending> pending;
+  std::vector<hipEvent_t> pool;
+  std::map<std::string, std::pair<double, int64_t> > acc;
+  hipEvent_t take() {
+    if (!pool.empty()) { hipEvent_t e = pool.back(); pool.pop_back(); return e; }
+    hipEvent_t e;
+    PFX_HIP(hipEventCreate(&e));
+    return e;
+  }
+};
+
+// Uniform-grid spatial index over a point set (see pfx_grid.hip).
+struct Grid {
+  int64_t n = 0;
+  float cell = 0.f, inv = 0.f, ox = 0.f, oy = 0.f, oz = 0.f;
+  double dinv = 0.0, dox = 0.0, doy = 0.0, doz = 0.0;  // exact cell mapping (builder == queries)
+  int32_t nx = 0, ny = 0, nz = 0;
+  int64_t ncells = 0;
+  // device arrays
+  float *sx = nullptr, *sy = nullptr, *sz = nullptr;  // sorted-by-cell SoA coordinates
+  const float *ux = nullptr, *uy = nullptr, *uz = nullptr;  // the caller's arrays (not owned)
+  int32_t* perm = nullptr;                            // sorted position -> caller index
+  int32_t* cell_start = nullptr;                      // ncells + 1 prefix (by linear cell key)
+  DevBuf b_sx, b_sy, b_sz, b_perm, b_start, b_keys, b_keys2, b_vals, b_tmp, b_minmax;
+  void release() {
+    b_sx.release(); b_sy.release(); b_sz.release(); b_perm.release(); b_start.release();
+    b_keys.release(); b_keys2.release(); b_vals.release(); b_tmp.release(); b_minmax.release();
+  }
+};
+
+// Per-query view of a grid handed to kernels by value.
+struct GridView {
+  const float *sx, *sy, *sz;
+  const float *ux, *uy, *uz;  // caller-order (unsorted) coordinates, indexed by perm values
+  const int32_t* perm;
+  const int32_t* cell_start;
+  double inv, ox, oy, oz;
+  int32_t nx, ny, nz;
+};
+
+struct NarfState;  // pfx_narf.hip
+
+}  // namespace pfx
+
+struct pfx_ctx {
+  int device = 0;
+  hipStream_t own_stream = nullptr;
+  hipStream_t stream = nullptr;
+  std::string last_error;
+  pfx::KernelTimer timer;
+  std::map<std::string, int64_t> stats;
+  pfx::Grid grid_a, grid_b;          // normal-radius grid, feature-radius grid
+  std::map<std::string, pfx::DevBuf> bufs;  // named scratch
+  pfx::NarfState* narf = nullptr;
+  pfx::DevBuf& buf(const char* name) { return bufs[name]; }
+};
+
+namespace pfx {
+
+// RAII timing scope around kernel launches on ctx->stream
+struct TimeScope {
+  pfx_ctx* ctx;
+  hipEvent_t a = nullptr, b = nullptr;
+  const char* name;
+  TimeScope(pfx_ctx* c, const char* n) : ctx(c), name(n) {
+    if (ctx->timer.enabled) {
+      a = ctx->timer.take();
+      b = ctx->timer.take();
+      PFX_HIP(hipEventRecord(a, ctx->stream));
+    }
+  }
+  ~TimeScope() {
+    if (a) {
+      (void)hipEventRecord(b, ctx->stream);
+      ctx->timer.pending.push_back(KernelTimer::Pending{a, b, std::string(name)});
+    }
+  }
+};
+
+inline void check_launch(const char* what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess)
+    throw Error(PFX_ERR_DEVICE, std::string("launch ") + what + ": " + hipGetErrorString(e));
+}
+
+inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+// grid building (pfx_grid.hip)
+void build_grid(pfx_ctx* ctx, Grid& g, const float* d_x, const float* d_y, const float* d_z,
+                int64_t n, double radius);
+inline GridView view(const Grid& g) {
+  GridView v;
+  v.sx = g.sx; v.sy = g.sy; v.sz = g.sz; v.perm = g.perm; v.cell_start = g.cell_start;
+  v.ux = g.ux; v.uy = g.uy; v.uz = g.uz;
+  v.inv = g.dinv; v.ox = g.dox; v.oy = g.doy; v.oz = g.doz; v.nx = g.nx; v.ny = g.ny; v.nz = g.nz;
+  return v;
+}
+
+// implemented in pfx_normals.hip / pfx_fpfh.hip / pfx_shot.hip / pfx_narf.hip
+void normals_dev(pfx_ctx* ctx, const float* x, const float* y, const float* z, int64_t n,
+                 double r, const float vp[3], float* nx, float* ny, float* nz, float* curv);
+void radius_search_dev(pfx_ctx* ctx, const float* x, const float* y, const float* z, int64_t n,
+                       const float* qx, const float* qy, const float* qz, int64_t nq, double r,
+                       int64_t* d_counts, int32_t* d_idx, float* d_d2, int64_t cap);
+void fpfh_dev(pfx_ctx* ctx, const float* sx, const float* sy, const float* sz, const float* snx,
+              const float* sny, const float* snz, int64_t ns, const float* qx, const float* qy,
+              const float* qz, int64_t nq, int same, double r, float* out);
+void shot_dev(pfx_ctx* ctx, const float* sx, const float* sy, const float* sz, const float* snx,
+              const float* sny, const float* snz, int64_t ns, const float* qx, const float* qy,
+              const float* qz, int64_t nq, double r, float* desc, float* rf);
+void range_image_dev(pfx_ctx* ctx, const float* x, const float* y, const float* z, int64_t n,
+                     const pfx_camera& cam, float4* d_points);
+int64_t narf_dev(pfx_ctx* ctx, const float* x, const float* y, const float* z, int64_t n,
+                 const pfx_camera& cam, const pfx_narf_params& p, std::vector<int32_t>& out);
+void narf_debug(pfx_ctx* ctx, const std::string& which, void* out, int64_t count);
+void narf_release(pfx_ctx* ctx);
+
+}  // namespace pfx

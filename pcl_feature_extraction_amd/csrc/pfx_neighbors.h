@@ -1,0 +1,140 @@
+// pfx_neighbors.h -- device-side radius search on the uniform grid (pfx_grid.hip), producing
+// FLANN's result: every p with ((0+dx^2)+dy^2)+dz^2 < (float)(r*r), dx = q - p,
+// ordered by the 64-bit key (float_bits(d2) << 32) | caller_index  ==  (d2, index) ascending.
+#pragma once
+#include "pfx_device_math.h"
+#include "pfx_internal.h"
+
+namespace pfx {
+
+__device__ __forceinline__ uint64_t nb_key(float d2, int32_t idx) {
+  return ((uint64_t)__float_as_uint(d2) << 32) | (uint32_t)idx;
+}
+__device__ __forceinline__ float key_d2(uint64_t k) { return __uint_as_float((uint32_t)(k >> 32)); }
+__device__ __forceinline__ int32_t key_idx(uint64_t k) { return (int32_t)(uint32_t)(k & 0xffffffffu); }
+
+__device__ __forceinline__ uint64_t lanemask_lt() {
+  const int lane = threadIdx.x & 63;
+  return lane == 0 ? 0ull : (~0ull >> (64 - lane));
+}
+
+// XCD-aware block remap: blocks b and b+8 share an XCD (observed round-robin placement);
+// give each XCD a contiguous slice of the (spatially sorted) work so its L2 sees one region.
+__device__ __forceinline__ int64_t xcd_block(int64_t b, int64_t nblocks) {
+  if (nblocks < 8 || (nblocks & 7)) return b;
+  return (b & 7) * (nblocks >> 3) + (b >> 3);
+}
+
+// The 9 candidate runs (3 contiguous z-cells each) of the 3x3x3 block around a query.
+struct Runs {
+  int32_t start[9];
+  int32_t pref[10];  // exclusive prefix of run lengths, pref[9] = total candidates
+};
+
+__device__ __forceinline__ void query_runs(const GridView& g, float qx, float qy, float qz, Runs& R) {
+  int64_t cx = (int64_t)floor(((double)qx - g.ox) * g.inv);
+  int64_t cy = (int64_t)floor(((double)qy - g.oy) * g.inv);
+  int64_t cz = (int64_t)floor(((double)qz - g.oz) * g.inv);
+  bool finite = isfinite(qx) && isfinite(qy) && isfinite(qz);
+  cx = cx < -2 ? -2 : (cx > g.nx + 1 ? g.nx + 1 : cx);
+  cy = cy < -2 ? -2 : (cy > g.ny + 1 ? g.ny + 1 : cy);
+  cz = cz < -2 ? -2 : (cz > g.nz + 1 ? g.nz + 1 : cz);
+  int64_t z0 = cz - 1 < 0 ? 0 : cz - 1;
+  int64_t z1 = cz + 1 >= g.nz ? g.nz - 1 : cz + 1;
+  int32_t acc = 0;
+#pragma unroll
+  for (int r = 0; r < 9; ++r) {
+    int64_t ix = cx + (r / 3) - 1, iy = cy + (r % 3) - 1;
+    int32_t s = 0, len = 0;
+    if (finite && ix >= 0 && ix < g.nx && iy >= 0 && iy < g.ny && z0 <= z1) {
+      int64_t base = (ix * g.ny + iy) * g.nz;
+      s = g.cell_start[base + z0];
+      len = g.cell_start[base + z1 + 1] - s;
+    }
+    R.start[r] = s;
+    R.pref[r] = acc;
+    acc += len;
+  }
+  R.pref[9] = acc;
+}
+
+__device__ __forceinline__ int32_t run_pos(const Runs& R, int32_t t) {
+  int32_t p = R.start[0] + t;
+#pragma unroll
+  for (int r = 1; r < 9; ++r)
+    if (t >= R.pref[r]) p = R.start[r] + (t - R.pref[r]);
+  return p;
+}
+
+// Gather the neighbours of q into keys[0..min(k,cap)) (unsorted); returns k (may exceed cap).
+// Executed by every thread of the block (nthreads = blockDim.x, a multiple of 64); uses
+// `s_count` (LDS int) for the cross-wave compaction cursor.
+__device__ __forceinline__ int gather_keys(const GridView& g, float qx, float qy, float qz, float rr,
+                                           uint64_t* keys, int cap, int* s_count) {
+  Runs R;
+  query_runs(g, qx, qy, qz, R);
+  const int tid = threadIdx.x, nth = blockDim.x;
+  if (tid == 0) *s_count = 0;
+  __syncthreads();
+  const int32_t T = R.pref[9];
+  for (int32_t t0 = 0; t0 < T; t0 += nth) {
+    int32_t t = t0 + tid;
+    bool hit = false;
+    uint64_t key = 0;
+    if (t < T) {
+      int32_t p = run_pos(R, t);
+      float d2 = flann_d2(qx, qy, qz, g.sx[p], g.sy[p], g.sz[p]);
+      hit = d2 < rr;
+      if (hit) key = nb_key(d2, g.perm[p]);
+    }
+    uint64_t m = __ballot(hit);
+    int base = 0;
+    if ((tid & 63) == 0 && m) base = atomicAdd(s_count, __popcll(m));
+    base = __shfl(base, 0);
+    if (hit) {
+      int pos = base + __popcll(m & lanemask_lt());
+      if (pos < cap) keys[pos] = key;
+    }
+  }
+  __syncthreads();
+  int k = *s_count;
+  __syncthreads();  // every thread has read the cursor before the next call resets it
+  return k;
+}
+
+// In-place ascending bitonic sort of keys[0..P), P a power of two >= 2 (pad with ~0ull).
+__device__ __forceinline__ void bitonic_sort(uint64_t* keys, int P) {
+  const int tid = threadIdx.x, nth = blockDim.x;
+  for (int size = 2; size <= P; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int i = tid; i < (P >> 1); i += nth) {
+        int lo = ((i / stride) * stride << 1) + (i & (stride - 1));
+        int hi = lo + stride;
+        bool asc = (lo & size) == 0;
+        uint64_t a = keys[lo], b = keys[hi];
+        if ((a > b) == asc) { keys[lo] = b; keys[hi] = a; }
+      }
+      __syncthreads();
+    }
+  }
+}
+
+__device__ __forceinline__ int next_pow2(int k) {
+  int P = 2;
+  while (P < k) P <<= 1;
+  return P;
+}
+
+// gather + pad + sort; returns k.  keys must hold cap entries (cap a power of two).
+__device__ __forceinline__ int sorted_neighbors(const GridView& g, float qx, float qy, float qz,
+                                                float rr, uint64_t* keys, int cap, int* s_count) {
+  int k = gather_keys(g, qx, qy, qz, rr, keys, cap, s_count);
+  if (k > cap) return k;
+  int P = next_pow2(k);
+  for (int i = k + threadIdx.x; i < P; i += blockDim.x) keys[i] = ~0ull;
+  __syncthreads();
+  bitonic_sort(keys, P);
+  return k;
+}
+
+}  // namespace pfx
