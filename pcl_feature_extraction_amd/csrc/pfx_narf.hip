@@ -1,15 +1,939 @@
-// pfx_narf.hip -- RangeImagePlanar + RangeImageBorderExtractor + NarfKeypoint (placeholder)
+// pfx_narf.hip -- NARF keypoints on the planar range image (keypoints.h:199-231) on gfx950:
+//   RangeImagePlanar::createFromPointCloudWithFixedSize      k_ri_*
+//   RangeImageBorderExtractor                                k_surface .. k_scs
+//   NarfKeypoint::compute                                    k_interest, k_nms
+// One thread per pixel for the image passes (640x480 = 307,200 px, 16-B/px SoA float4
+// images in HBM), one wave per pixel for the interest region-grow (bitmap + queue in LDS).
+// The only sequential steps -- std::sort of the few hundred NMS survivors and the greedy
+// minimum-distance selection -- run on the host exactly as PCL does.
+//
+// Order-dependent PCL steps and how they are made parallel without changing results:
+//   * z-buffer: with noise_level 0 the result is min(direct hits) else min(fills):
+//     two atomicMin images on the float bits (ranges > 0 order like uints).
+//   * shadow borders are updated in place in raster order: the R/B passes only read the
+//     not-yet-updated L/T scores, the L/T passes read the final R/B scores -> two phases.
+//   * border traits are set-only -> atomicOr.
+//   * interest region-grow: the accepted set is the 8-connected component of p, histogram
+//     max / negative min are order-free -> level-parallel BFS.
+#include <algorithm>
+#include <cstring>
+
+#include "pfx_device_math.h"
 #include "pfx_internal.h"
+
 namespace pfx {
-void range_image_dev(pfx_ctx*, const float*, const float*, const float*, int64_t, const pfx_camera&, float4*) {
-  throw Error(PFX_ERR_UNSUPPORTED, "range image: not implemented yet");
+
+enum {
+  T_OBSTACLE_BORDER = 0, T_SHADOW_BORDER, T_VEIL_POINT, T_SHADOW_BORDER_TOP, T_SHADOW_BORDER_RIGHT,
+  T_SHADOW_BORDER_BOTTOM, T_SHADOW_BORDER_LEFT, T_OBSTACLE_BORDER_TOP, T_OBSTACLE_BORDER_RIGHT,
+  T_OBSTACLE_BORDER_BOTTOM, T_OBSTACLE_BORDER_LEFT, T_VEIL_POINT_TOP, T_VEIL_POINT_RIGHT,
+  T_VEIL_POINT_BOTTOM, T_VEIL_POINT_LEFT
+};
+#define TB(t) (1u << (t))
+
+struct NarfState {
+  int w = 0, h = 0;
+  DevBuf direct, fill, pts, surf, svalid, sL, sR, sT, sB, uL, uR, uT, uB, shadow, traits, rawdir, dir, scs, scd,
+      interest, cand, counters;
+  std::vector<float> h_interest, h_scs, h_range;
+  std::vector<uint32_t> h_traits;
+  bool have_debug = false;
+  void release() {
+    DevBuf* all[] = {&direct, &fill, &pts, &surf, &svalid, &sL, &sR, &sT, &sB, &uL, &uR, &uT, &uB, &shadow,
+                     &traits, &rawdir, &dir, &scs, &scd, &interest, &cand, &counters};
+    for (auto* b : all) b->release();
+  }
+};
+
+namespace {
+
+struct Aff { float m[12]; };  // row-major 3x4 [R | t]
+
+struct Img {
+  int w, h;
+  float cx, cy, fx, fy, fxr, fyr;
+  Aff to_world, to_ri;
+};
+
+__device__ __forceinline__ f3 aff_apply(const Aff& a, f3 p) {
+  return mk3(a.m[3] + (a.m[0] * p.x + a.m[1] * p.y + a.m[2] * p.z),
+             a.m[7] + (a.m[4] * p.x + a.m[5] * p.y + a.m[6] * p.z),
+             a.m[11] + (a.m[8] * p.x + a.m[9] * p.y + a.m[10] * p.z));
 }
-int64_t narf_dev(pfx_ctx*, const float*, const float*, const float*, int64_t, const pfx_camera&,
-                 const pfx_narf_params&, std::vector<int32_t>&) {
-  throw Error(PFX_ERR_UNSUPPORTED, "narf: not implemented yet");
+
+__device__ __forceinline__ bool in_image(const Img& I, int x, int y) { return x >= 0 && x < I.w && y >= 0 && y < I.h; }
+
+__device__ __forceinline__ f3 calc3d(const Img& I, float ix, float iy, float range) {
+  float dx = (ix + 0.0f - I.cx) * I.fxr, dy = (iy + 0.0f - I.cy) * I.fyr;
+  f3 p;
+  p.z = range / (sqrtf(dx * dx + dy * dy + 1));
+  p.x = dx * p.z;
+  p.y = dy * p.z;
+  return aff_apply(I.to_world, p);
 }
-void narf_debug(pfx_ctx*, const std::string&, void*, int64_t) {
-  throw Error(PFX_ERR_UNSUPPORTED, "narf: not implemented yet");
+
+__device__ __forceinline__ void image_point(const Img& I, f3 pt, float& ix, float& iy, float& range) {
+  f3 t = aff_apply(I.to_ri, pt);
+  if (t.z <= 0) { ix = iy = range = -1.0f; return; }
+  range = sqrtf(sqn3(t));
+  ix = I.cx + I.fx * t.x / t.z - 0.0f;
+  iy = I.cy + I.fy * t.y / t.z - 0.0f;
 }
-void narf_release(pfx_ctx*) {}
+
+__device__ __forceinline__ float sq_dist(float4 a, float4 b) {  // diff = b - a
+  float dx = b.x - a.x, dy = b.y - a.y, dz = b.z - a.z;
+  return dx * dx + dy * dy + dz * dz;
+}
+
+__device__ __forceinline__ float4 get_point(const Img& I, const float4* __restrict__ P, int x, int y) {
+  if (!in_image(I, x, y)) return make_float4(__builtin_nanf(""), __builtin_nanf(""), __builtin_nanf(""), -INFINITY);
+  return P[y * I.w + x];
+}
+__device__ __forceinline__ bool is_valid(const Img& I, const float4* __restrict__ P, int x, int y) {
+  return in_image(I, x, y) && isfinite(P[y * I.w + x].w);
+}
+
+// ---- range image ---------------------------------------------------------------------------
+__global__ void k_ri_init(uint32_t* __restrict__ direct, uint32_t* __restrict__ fill, int n) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) { direct[i] = 0xffffffffu; fill[i] = 0xffffffffu; }
+}
+
+__global__ void k_ri_project(Img I, const float* __restrict__ X, const float* __restrict__ Y, const float* __restrict__ Z,
+                             int64_t n, float min_range, uint32_t* __restrict__ direct, uint32_t* __restrict__ fill) {
+  int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  float px = X[i], py = Y[i], pz = Z[i];
+  if (!(isfinite(px) && isfinite(py) && isfinite(pz))) return;
+  float xr, yr, rng;
+  image_point(I, mk3(px, py, pz), xr, yr, rng);
+  int x = (int)rintf(xr), y = (int)rintf(yr);
+  if (rng < min_range || !in_image(I, x, y)) return;
+  int fx0 = (int)floorf(xr), fy0 = (int)floorf(yr), cx0 = (int)ceilf(xr), cy0 = (int)ceilf(yr);
+  int nxs[4] = {fx0, fx0, cx0, cx0}, nys[4] = {fy0, cy0, fy0, cy0};
+  uint32_t rb = __float_as_uint(rng);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    if (nxs[k] == x && nys[k] == y) continue;
+    if (!in_image(I, nxs[k], nys[k])) continue;
+    atomicMin(&fill[nys[k] * I.w + nxs[k]], rb);
+  }
+  atomicMin(&direct[y * I.w + x], rb);
+}
+
+__global__ void k_ri_finalize(Img I, const uint32_t* __restrict__ direct, const uint32_t* __restrict__ fill,
+                              float4* __restrict__ P) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= I.w * I.h) return;
+  uint32_t d = direct[i], f = fill[i];
+  float r = d != 0xffffffffu ? __uint_as_float(d) : (f != 0xffffffffu ? __uint_as_float(f) : -INFINITY);
+  float4 o = make_float4(__builtin_nanf(""), __builtin_nanf(""), __builtin_nanf(""), r);
+  if (!isinf(r)) {
+    int y = i / I.w, x = i - y * I.w;
+    f3 q = calc3d(I, (float)x, (float)y, r);
+    o.x = q.x; o.y = q.y; o.z = q.z;
+  }
+  P[i] = o;
+}
+
+// ---- VectorAverage3f -------------------------------------------------------------------------
+struct VecAvg {
+  int n;
+  float acc_w;
+  f3 mean;
+  float c00, c01, c02, c11, c12, c22;
+  __device__ void init() { n = 0; acc_w = 0.f; mean = mk3(0, 0, 0); c00 = c01 = c02 = c11 = c12 = c22 = 0.f; }
+  __device__ void add(f3 s) {
+    ++n;
+    acc_w += 1.0f;
+    float alpha = 1.0f / acc_w;
+    f3 d = sub3(s, mean);
+    mean = add3(mean, mk3(alpha * d.x, alpha * d.y, alpha * d.z));
+    float om = 1.0f - alpha;
+    c00 = om * (c00 + alpha * (d.x * d.x));
+    c01 = om * (c01 + alpha * (d.x * d.y));
+    c02 = om * (c02 + alpha * (d.x * d.z));
+    c11 = om * (c11 + alpha * (d.y * d.y));
+    c12 = om * (c12 + alpha * (d.y * d.z));
+    c22 = om * (c22 + alpha * (d.z * d.z));
+  }
+  __device__ void pca(float ev[3], f3 evec[3]) const {
+    Sym3 m;
+    m.a00 = c00; m.a01 = c01; m.a02 = c02;
+    m.a10 = c01; m.a11 = c11; m.a12 = c12;
+    m.a20 = c02; m.a21 = c12; m.a22 = c22;
+    eigen33_full(m, evec, ev);
+  }
+};
+
+// RangeImage::getSurfaceInformation (no-jumps part), radius/step from the border parameters
+__global__ void k_surface(Img I, const float4* __restrict__ P, int radius, int step, int no_of_closest,
+                          float4* __restrict__ surf, uint8_t* __restrict__ svalid) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= I.w * I.h) return;
+  svalid[i] = 0;
+  int y = i / I.w, x = i - y * I.w;
+  float4 point = P[i];
+  if (!isfinite(point.w)) return;
+  float nd[25];
+  float4 np[25];
+  int cnt = 0;
+  for (int y2 = y - radius; y2 <= y + radius; y2 += step)
+    for (int x2 = x - radius; x2 <= x + radius; x2 += step) {
+      if (!is_valid(I, P, x2, y2) || cnt >= 25) continue;
+      float4 q = P[y2 * I.w + x2];
+      float d = sq_dist(point, q);
+      int j = cnt++;
+      while (j > 0 && d < nd[j - 1]) { nd[j] = nd[j - 1]; np[j] = np[j - 1]; --j; }
+      nd[j] = d;
+      np[j] = q;
+    }
+  int k = cnt < no_of_closest ? cnt : no_of_closest;
+  float maxd2 = nd[k - 1];
+  float lim = maxd2 * 4.0f;
+  VecAvg va;
+  va.init();
+  for (int j = 0; j < cnt; ++j) {
+    if (nd[j] > lim) break;
+    va.add(mk3(np[j].x, np[j].y, np[j].z));
+  }
+  if (va.n < 3) return;
+  float ev[3];
+  f3 evec[3];
+  va.pca(ev, evec);
+  f3 normal = evec[0];
+  f3 sensor = mk3(I.to_world.m[3], I.to_world.m[7], I.to_world.m[11]);
+  f3 view = normalized3(sub3(sensor, mk3(point.x, point.y, point.z)));
+  if (dot3(normal, view) < 0.0f) normal = scale3(normal, -1.0f);
+  surf[i] = make_float4(normal.x, normal.y, normal.z, maxd2);
+  svalid[i] = 1;
+}
+
+__device__ __forceinline__ float4 point_avg(const Img& I, const float4* __restrict__ P, int x, int y, int dx, int dy,
+                                            int no_of_points) {
+  float ws = 1.0f;
+  float4 a = get_point(I, P, x, y);
+  if (isinf(a.w)) {
+    if (a.w > 0.0f) return a;
+    ws = 0.0f;
+    a = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  int x2 = x, y2 = y;
+  for (int s = 1; s < no_of_points; ++s) {
+    x2 += dx; y2 += dy;
+    if (!is_valid(I, P, x2, y2)) continue;
+    float4 p = P[y2 * I.w + x2];
+    a.x += p.x; a.y += p.y; a.z += p.z; a.w += p.w;
+    ws += 1.0f;
+  }
+  if (ws <= 0.0f) return make_float4(__builtin_nanf(""), __builtin_nanf(""), __builtin_nanf(""), -INFINITY);
+  float nf = 1.0f / ws;
+  a.x *= nf; a.y *= nf; a.z *= nf; a.w *= nf;
+  return a;
+}
+
+__device__ __forceinline__ float dist_change_score(const Img& I, const float4* __restrict__ P, float maxd2, int x,
+                                                   int y, int ox, int oy, int pixel_radius) {
+  float4 point = get_point(I, P, x, y);
+  float4 nb = point_avg(I, P, x + ox, y + oy, ox, oy, pixel_radius);
+  if (isinf(nb.w)) return nb.w < 0.0f ? 0.0f : 1.0f;
+  float nd2 = sq_dist(nb, point);
+  if (nd2 <= maxd2) return 0.0f;
+  float ret = 1.0f - sqrtf(maxd2 / nd2);
+  if (nb.w < point.w) ret = -ret;
+  return ret;
+}
+
+__global__ void k_border_scores(Img I, const float4* __restrict__ P, const float4* __restrict__ surf,
+                                const uint8_t* __restrict__ svalid, int prb, float* __restrict__ sL,
+                                float* __restrict__ sR, float* __restrict__ sT, float* __restrict__ sB) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= I.w * I.h) return;
+  float l = 0.f, r = 0.f, t = 0.f, b = 0.f;
+  if (svalid[i]) {
+    int y = i / I.w, x = i - y * I.w;
+    float maxd2 = surf[i].w;
+    l = dist_change_score(I, P, maxd2, x, y, -1, 0, prb);
+    r = dist_change_score(I, P, maxd2, x, y, 1, 0, prb);
+    t = dist_change_score(I, P, maxd2, x, y, 0, -1, prb);
+    b = dist_change_score(I, P, maxd2, x, y, 0, 1, prb);
+  }
+  sL[i] = l; sR[i] = r; sT[i] = t; sB[i] = b;
+}
+
+__device__ __forceinline__ float updated_score(const Img& I, const float* __restrict__ s, int x, int y, float minp) {
+  const float bonus = 0.5f;
+  float b = s[y * I.w + x];
+  if (b + bonus * (1.0f - b) < minp) return b;
+  float avg = 0.0f, ws = 0.0f;
+  for (int y2 = y - 1; y2 <= y + 1; ++y2)
+    for (int x2 = x - 1; x2 <= x + 1; ++x2) {
+      if (!in_image(I, x2, y2) || (x2 == x && y2 == y)) continue;
+      avg += s[y2 * I.w + x2];
+      ws += 1.0f;
+    }
+  avg /= ws;
+  if (avg * b < 0.0f) return b;
+  return b + bonus * avg * (1.0f - fabsf(b));
+}
+
+__global__ void k_update_scores(Img I, float minp, const float* __restrict__ iL, const float* __restrict__ iR,
+                                const float* __restrict__ iT, const float* __restrict__ iB, float* __restrict__ oL,
+                                float* __restrict__ oR, float* __restrict__ oT, float* __restrict__ oB) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= I.w * I.h) return;
+  int y = i / I.w, x = i - y * I.w;
+  oL[i] = updated_score(I, iL, x, y, minp);
+  oR[i] = updated_score(I, iR, x, y, minp);
+  oT[i] = updated_score(I, iT, x, y, minp);
+  oB[i] = updated_score(I, iB, x, y, minp);
+}
+
+__device__ __forceinline__ bool is_max_range(const Img& I, const float4* __restrict__ P, int x, int y) {
+  if (!in_image(I, x, y)) return false;
+  float r = P[y * I.w + x].w;
+  return isinf(r) && r > 0;
+}
+
+// changeScoreAccordingToShadowBorderValue; returns new score, sets sidx (-1 if none)
+__device__ __forceinline__ float shadow_pass(const Img& I, const float4* __restrict__ P, int x, int y, int ox, int oy,
+                                             float b, const float* __restrict__ other, int prb, float minp, int& sidx) {
+  sidx = -1;
+  if (b < minp) return b;
+  if (b == 1.0f && is_max_range(I, P, x + ox, y + oy)) { sidx = (y + oy) * I.w + x + ox; return b; }
+  float best = 0.0f;
+  for (int d = 1; d <= prb; ++d) {
+    int nx = x + d * ox, ny = y + d * oy;
+    if (!in_image(I, nx, ny)) continue;
+    float s = other[ny * I.w + nx];
+    if (s < best) { sidx = ny * I.w + nx; best = s; }
+  }
+  if (sidx >= 0) {
+    b *= fmaxf(0.9f, 1 - pow3f_cr(1 + best));
+    if (b >= minp) return b;
+  }
+  sidx = -1;
+  return 0.0f;
+}
+
+// phase 1: R and B passes (read the not-yet-updated L / T scores)
+__global__ void k_shadow_rb(Img I, const float4* __restrict__ P, int prb, float minp, const float* __restrict__ sL,
+                            float* __restrict__ sR, const float* __restrict__ sT, float* __restrict__ sB,
+                            int4* __restrict__ sh) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= I.w * I.h) return;
+  int y = i / I.w, x = i - y * I.w;
+  int a, c;
+  sR[i] = shadow_pass(I, P, x, y, 1, 0, sR[i], sL, prb, minp, a);
+  sB[i] = shadow_pass(I, P, x, y, 0, 1, sB[i], sT, prb, minp, c);
+  int4 s = sh[i];
+  s.y = a;  // right
+  s.w = c;  // bottom
+  sh[i] = s;
+}
+
+// phase 2: L and T passes (read the final R / B scores)
+__global__ void k_shadow_lt(Img I, const float4* __restrict__ P, int prb, float minp, float* __restrict__ sL,
+                            const float* __restrict__ sR, float* __restrict__ sT, const float* __restrict__ sB,
+                            int4* __restrict__ sh) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= I.w * I.h) return;
+  int y = i / I.w, x = i - y * I.w;
+  int a, c;
+  sL[i] = shadow_pass(I, P, x, y, -1, 0, sL[i], sR, prb, minp, a);
+  sT[i] = shadow_pass(I, P, x, y, 0, -1, sT[i], sB, prb, minp, c);
+  int4 s = sh[i];
+  s.x = a;  // left
+  s.z = c;  // top
+  sh[i] = s;
+}
+
+__device__ __forceinline__ bool check_max(const Img& I, const float* __restrict__ s, int x, int y, int ox, int oy,
+                                          int sidx, int prb) {
+  float b = s[y * I.w + x];
+  int nx = x - ox, ny = y - oy;
+  if (in_image(I, nx, ny) && s[ny * I.w + nx] > b) return false;
+  for (int d = 1; d <= prb; ++d) {
+    nx = x + d * ox; ny = y + d * oy;
+    if (!in_image(I, nx, ny)) continue;
+    int ni = ny * I.w + nx;
+    if (ni == sidx) return true;
+    if (s[ni] > b) return false;
+  }
+  return true;
+}
+
+__global__ void k_classify(Img I, int prb, const float* __restrict__ sL, const float* __restrict__ sR,
+                           const float* __restrict__ sT, const float* __restrict__ sB, const int4* __restrict__ sh,
+                           uint32_t* __restrict__ traits) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= I.w * I.h) return;
+  int4 s = sh[i];
+  if (s.x < 0 && s.y < 0 && s.z < 0 && s.w < 0) return;
+  int y = i / I.w, x = i - y * I.w;
+  const int w = I.w;
+  uint32_t own = 0;
+  if (s.x >= 0 && check_max(I, sL, x, y, -1, 0, s.x, prb)) {
+    own |= TB(T_OBSTACLE_BORDER) | TB(T_OBSTACLE_BORDER_LEFT);
+    atomicOr(&traits[s.x], TB(T_SHADOW_BORDER) | TB(T_SHADOW_BORDER_RIGHT));
+    int sx = s.x % w;
+    for (int i3 = y * w + sx + 1; i3 < i; ++i3) atomicOr(&traits[i3], TB(T_VEIL_POINT) | TB(T_VEIL_POINT_RIGHT));
+  }
+  if (s.y >= 0 && check_max(I, sR, x, y, 1, 0, s.y, prb)) {
+    own |= TB(T_OBSTACLE_BORDER) | TB(T_OBSTACLE_BORDER_RIGHT);
+    atomicOr(&traits[s.y], TB(T_SHADOW_BORDER) | TB(T_SHADOW_BORDER_LEFT));
+    int sx = s.y % w, sy = s.y / w;
+    for (int i3 = i + 1; i3 < sy * w + sx; ++i3) atomicOr(&traits[i3], TB(T_VEIL_POINT) | TB(T_VEIL_POINT_LEFT));
+  }
+  if (s.z >= 0 && check_max(I, sT, x, y, 0, -1, s.z, prb)) {
+    own |= TB(T_OBSTACLE_BORDER) | TB(T_OBSTACLE_BORDER_TOP);
+    atomicOr(&traits[s.z], TB(T_SHADOW_BORDER) | TB(T_SHADOW_BORDER_BOTTOM));
+    int sy = s.z / w;
+    for (int i3 = (sy + 1) * w + x; i3 < i; i3 += w) atomicOr(&traits[i3], TB(T_VEIL_POINT) | TB(T_VEIL_POINT_BOTTOM));
+  }
+  if (s.w >= 0 && check_max(I, sB, x, y, 0, 1, s.w, prb)) {
+    own |= TB(T_OBSTACLE_BORDER) | TB(T_OBSTACLE_BORDER_BOTTOM);
+    atomicOr(&traits[s.w], TB(T_SHADOW_BORDER) | TB(T_SHADOW_BORDER_TOP));
+    int sy = s.w / w;
+    for (int i3 = i + w; i3 < sy * w + x; i3 += w) atomicOr(&traits[i3], TB(T_VEIL_POINT) | TB(T_VEIL_POINT_TOP));
+  }
+  if (own) atomicOr(&traits[i], own);
+}
+
+// get3dDirection for obstacle borders; rawdir.w = 1 if valid
+__global__ void k_border_dir_raw(Img I, const float4* __restrict__ P, const float4* __restrict__ surf,
+                                 const uint8_t* __restrict__ svalid, const uint32_t* __restrict__ traits,
+                                 float4* __restrict__ rawdir) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= I.w * I.h) return;
+  uint32_t bt = traits[i];
+  float4 out = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (bt & TB(T_OBSTACLE_BORDER)) {
+    int dx = 0, dy = 0;
+    if (bt & TB(T_OBSTACLE_BORDER_LEFT)) --dx;
+    if (bt & TB(T_OBSTACLE_BORDER_RIGHT)) ++dx;
+    if (bt & TB(T_OBSTACLE_BORDER_TOP)) --dy;
+    if (bt & TB(T_OBSTACLE_BORDER_BOTTOM)) ++dy;
+    if (dx != 0 || dy != 0) {
+      int y = i / I.w, x = i - y * I.w;
+      float4 point = P[i];
+      f3 pt = mk3(point.x, point.y, point.z);
+      f3 nbp = calc3d(I, (float)(x + dx), (float)(y + dy), point.w);
+      f3 d;
+      if (svalid[i]) {
+        float4 s = surf[i];
+        f3 nrm = mk3(s.x, s.y, s.z);
+        float k = dot3(sub3(nbp, pt), nrm);
+        f3 proj = sub3(nbp, scale3(nrm, k));
+        d = sub3(proj, pt);
+      } else {
+        d = sub3(nbp, pt);
+      }
+      d = normalized3(d);
+      out = make_float4(d.x, d.y, d.z, 1.0f);
+    }
+  }
+  rawdir[i] = out;
+}
+
+__global__ void k_border_dir_avg(Img I, const float4* __restrict__ P, const float4* __restrict__ surf,
+                                 const float4* __restrict__ rawdir, int radius, float min_cos, float thr,
+                                 float4* __restrict__ dir) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= I.w * I.h) return;
+  float4 r0 = rawdir[i];
+  float4 out = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (r0.w != 0.0f) {
+    int y = i / I.w, x = i - y * I.w;
+    f3 base = mk3(r0.x, r0.y, r0.z);
+    f3 avg = base;
+    float ws = 1.0f;
+    float maxd2 = surf[i].w;
+    int y0 = max(0, y - radius), y1 = min(y + radius, I.h - 1);
+    int x0 = max(0, x - radius), x1 = min(x + radius, I.w - 1);
+    for (int y2 = y0; y2 <= y1; ++y2)
+      for (int x2 = x0; x2 <= x1; ++x2) {
+        int i2 = y2 * I.w + x2;
+        float4 r2 = rawdir[i2];
+        if (r2.w == 0.0f || i2 == i) continue;
+        f3 nb = mk3(r2.x, r2.y, r2.z);
+        if (dot3(nb, base) < min_cos) continue;
+        float between = dist_change_score(I, P, maxd2, x, y, x2 - x, y2 - y, 1);
+        if (fabsf(between) >= thr) continue;
+        avg = add3(avg, nb);
+        ws += 1.0f;
+      }
+    if ((int)rintf(ws) >= radius + 1) {
+      f3 d = normalized3(avg);
+      out = make_float4(d.x, d.y, d.z, 1.0f);
+    }
+  }
+  dir[i] = out;
+}
+
+__global__ void k_surface_change(Img I, const float4* __restrict__ P, const float4* __restrict__ surf,
+                                 const uint8_t* __restrict__ svalid, const uint32_t* __restrict__ traits,
+                                 const float4* __restrict__ dir, int radius, float* __restrict__ scs,
+                                 float4* __restrict__ scd) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= I.w * I.h) return;
+  float score = 0.0f;
+  f3 d = mk3(0.f, 0.f, 0.f);
+  const uint32_t skip = TB(T_VEIL_POINT) | TB(T_SHADOW_BORDER);
+  if (!(traits[i] & skip)) {
+    float4 bd = dir[i];
+    if (bd.w != 0.0f) {
+      score = 1.0f;
+      d = mk3(bd.x, bd.y, bd.z);
+    } else if (svalid[i]) {
+      int y = i / I.w, x = i - y * I.w;
+      VecAvg va;
+      va.init();
+      bool beam[9];
+      for (int step = 1; step <= radius; ++step) {
+        int bi = 0;
+        for (int y2 = y - step; y2 <= y + step; y2 += step)
+          for (int x2 = x - step; x2 <= x + step; x2 += step) {
+            int b = bi++;
+            if (step == 1) {
+              beam[b] = !(x2 == x && y2 == y);
+            } else if (!beam[b]) {
+              continue;
+            }
+            if (!is_valid(I, P, x2, y2)) continue;
+            int i2 = y2 * I.w + x2;
+            if (traits[i2] & skip) { beam[b] = false; continue; }
+            if (!svalid[i2]) continue;
+            float4 s2 = surf[i2];
+            va.add(mk3(s2.x, s2.y, s2.z));
+          }
+      }
+      if (va.n >= 3) {
+        float ev[3];
+        f3 evec[3];
+        va.pca(ev, evec);
+        float mag = sqrtf(ev[2]);
+        if (isfinite(mag)) {
+          score = mag;
+          d = evec[2];
+        }
+      }
+    }
+  }
+  scs[i] = score;
+  scd[i] = make_float4(d.x, d.y, d.z, 0.0f);
+}
+
+// ---- NARF interest image: one wave (64-thread block) per pixel ------------------------------
+constexpr int kBitmapWords = 9600;  // 640*480 bits: the whole image (window clears only)
+constexpr int kQueue = 4096;        // ring buffer of pending pixels
+
+__device__ __forceinline__ float norm_angle(float a) {
+  const float pi = 3.14159265358979323846f;
+  return a >= 0 ? fmodf(a + pi, 2.0f * pi) - pi : -(fmodf(pi - a, 2.0f * pi) - pi);
+}
+
+struct InterestParams {
+  float radius_squared, radius_reciprocal, min_scs, opt_dist, d90, d180;
+  double R;  // search radius for the window bound
+};
+
+__global__ void __launch_bounds__(64) k_interest(Img I, const float4* __restrict__ P, const uint32_t* __restrict__ traits,
+                                                 const float* __restrict__ scs, const float4* __restrict__ scd,
+                                                 InterestParams ip, float* __restrict__ interest,
+                                                 int* __restrict__ err) {
+  __shared__ uint32_t bitmap[kBitmapWords];
+  __shared__ int queue[kQueue];
+  __shared__ unsigned hist[18];
+  __shared__ unsigned neg_bits;
+  __shared__ int s_tail;
+  const int lane = threadIdx.x;
+  const int npx = I.w * I.h;
+  const uint32_t skip = TB(T_SHADOW_BORDER) | TB(T_VEIL_POINT);
+  // bitmap starts clear; every block clears exactly the words it set before moving on
+  for (int k = lane; k < kBitmapWords; k += 64) bitmap[k] = 0u;
+  __syncthreads();
+  for (int index = blockIdx.x; index < npx; index += gridDim.x) {
+    const float4 point = P[index];
+    if (!isfinite(point.w) || (traits[index] & skip)) {
+      if (lane == 0) interest[index] = 0.0f;
+      continue;
+    }
+    const int y = index / I.w, x = index - y * I.w;
+    // rotation to the viewer frame: getTransFromUnitVectorsZY(view, (0,-1,0))
+    const f3 sensor = mk3(I.to_world.m[3], I.to_world.m[7], I.to_world.m[11]);
+    const f3 view = normalized3(sub3(mk3(point.x, point.y, point.z), sensor));
+    const f3 tmp0 = normalized3(cross3(mk3(0.0f, -1.0f, 0.0f), view));
+    const f3 tmp1 = normalized3(cross3(view, tmp0));
+    const f3 tmp2 = normalized3(view);
+    if (lane < 18) hist[lane] = 0u;
+    if (lane == 0) {
+      neg_bits = __float_as_uint(1.0f);
+      queue[0] = index;
+      s_tail = 1;
+      bitmap[index >> 5] |= 1u << (index & 31);
+    }
+    __syncthreads();
+    int head = 0;
+    int ymin = y, ymax = y;  // rows touched (for the clear)
+    while (true) {
+      const int tail = s_tail;
+      if (head >= tail) break;
+      const int take = min(tail - head, 64);
+      if (lane < take) {
+        const int index2 = queue[(head + lane) & (kQueue - 1)];
+        const int y2 = index2 / I.w, x2 = index2 - y2 * I.w;
+        const float4 point2 = P[index2];
+        bool ok = isfinite(point2.w) && !(traits[index2] & skip);
+        const float pd = (float)max(abs(x2 - x), abs(y2 - y));
+        const float d2 = sq_dist(point, point2);
+        if (ok && pd > 2.0f && d2 > ip.radius_squared) ok = false;
+        if (ok) {
+          for (int y3 = max(0, y2 - 1); y3 <= min(I.h - 1, y2 + 1); ++y3)
+            for (int x3 = max(0, x2 - 1); x3 <= min(I.w - 1, x2 + 1); ++x3) {
+              int index3 = y3 * I.w + x3;
+              uint32_t bitm = 1u << (index3 & 31);
+              uint32_t old = atomicOr(&bitmap[index3 >> 5], bitm);
+              if (!(old & bitm)) {
+                int slot = atomicAdd(&s_tail, 1);
+                queue[slot & (kQueue - 1)] = index3;
+                ymin = min(ymin, y3);
+                ymax = max(ymax, y3);
+              }
+            }
+          const float sc = scs[index2];
+          if (sc >= ip.min_scs) {
+            const float4 dv = scd[index2];
+            const f3 dir = mk3(dv.x, dv.y, dv.z);
+            const float distance = sqrtf(d2);
+            const float df = ip.radius_reciprocal * distance;
+            float neg = 1.0f - 0.5f * sc * fmaxf(1.0f - df / ip.opt_dist, 0.0f);
+            neg = neg * neg;
+            const float pos = (pd < 2.0f) ? sc : sc * (1.0f - df);
+            const f3 rot = mk3(0.0f + dot3(tmp0, dir), 0.0f + dot3(tmp1, dir), 0.0f + dot3(tmp2, dir));
+            const float nrm = sqrtf(rot.x * rot.x + rot.y * rot.y);
+            const float dvx = rot.x / nrm;
+            const float angle = 0.5f * norm_angle(2.0f * acosf_cr(dvx));
+            const float cellf = floorf((angle + ip.d90) / ip.d180 * 18);
+            int cell;
+            if (!(cellf == cellf)) cell = 0;
+            else cell = min(17, (int)rintf(cellf));
+            if (cell < 0) cell = 0;
+            if (pos > 0.0f) atomicMax(&hist[cell], __float_as_uint(pos));
+            if (neg < 1.0f) atomicMin(&neg_bits, __float_as_uint(neg));
+          }
+        }
+      }
+      head += take;
+      __syncthreads();
+      if (s_tail - head > kQueue) {
+        if (lane == 0) atomicExch(err, 1);
+        break;
+      }
+    }
+    __syncthreads();
+    if (lane == 0) {
+      float h[18];
+      for (int c = 0; c < 18; ++c) h[c] = __uint_as_float(hist[c]);
+      float acv = 0.0f;
+      for (int c1 = 0; c1 < 17; ++c1) {
+        if (h[c1] == 0.0f) continue;
+        for (int c2 = c1 + 1; c2 < 18; ++c2) {
+          if (h[c2] == 0.0f) continue;
+          float nd = 2.0f * (float)(c2 - c1) / (float)18;
+          nd = (nd <= 1.0f ? nd : 2.0f - nd);
+          float v = h[c1] * h[c2] * nd;
+          acv = (v < acv) ? acv : v;
+        }
+      }
+      acv = sqrtf(acv);
+      interest[index] = __uint_as_float(neg_bits) * acv;
+    }
+    // clear the touched rows of the bitmap
+    int r0 = ymin, r1 = ymax;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      r0 = min(r0, __shfl_xor(r0, off));
+      r1 = max(r1, __shfl_xor(r1, off));
+    }
+    const int w0 = (r0 * I.w) >> 5, w1 = ((r1 + 1) * I.w + 31) >> 5;
+    for (int k = w0 + lane; k < w1 && k < kBitmapWords; k += 64) bitmap[k] = 0u;
+    __syncthreads();
+  }
+}
+
+__global__ void k_nms(Img I, const float* __restrict__ interest, float min_interest, int nms,
+                      int* __restrict__ cand, int* __restrict__ ncand) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= I.w * I.h) return;
+  float iv = interest[i];
+  if (iv < min_interest) return;
+  int y = i / I.w, x = i - y * I.w;
+  bool is_max = true;
+  for (int y2 = y - 1; y2 <= y + 1 && is_max && nms; ++y2)
+    for (int x2 = x - 1; x2 <= x + 1; ++x2) {
+      if (!in_image(I, x2, y2)) continue;
+      if (interest[y2 * I.w + x2] <= iv) continue;
+      is_max = false;
+      break;
+    }
+  if (!is_max) return;
+  cand[atomicAdd(ncand, 1)] = i;
+}
+
+__global__ void k_gather_cand(const int* __restrict__ cand, int nc, const float4* __restrict__ P,
+                              const float* __restrict__ interest, float4* __restrict__ out) {
+  int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= nc) return;
+  int i = cand[k];
+  float4 p = P[i];
+  out[k] = make_float4(p.x, p.y, p.z, interest[i]);
+}
+
+__global__ void k_valid_bits(const float4* __restrict__ P, int npx, uint32_t* __restrict__ bits) {
+  int wd = blockIdx.x * blockDim.x + threadIdx.x;
+  if (wd * 32 >= npx) return;
+  uint32_t v = 0;
+  for (int b = 0; b < 32; ++b) {
+    int i = wd * 32 + b;
+    if (i < npx && isfinite(P[i].w)) v |= 1u << b;
+  }
+  bits[wd] = v;
+}
+
+struct HostInterestPoint { float x, y, z, strength; };
+bool host_better(const HostInterestPoint& a, const HostInterestPoint& b) { return a.strength > b.strength; }
+
+Img make_img(const pfx_camera& c) {
+  Img I;
+  I.w = c.width; I.h = c.height;
+  I.cx = c.center_x; I.cy = c.center_y; I.fx = c.focal_length_x; I.fy = c.focal_length_y;
+  I.fxr = 1 / c.focal_length_x; I.fyr = 1 / c.focal_length_y;
+  float F[4][4] = {{1, 0, 0, 0}, {0, 1, 0, 0}, {0, 0, 1, 0}, {0, 0, 0, 1}};
+  if (c.coordinate_frame == 1) {
+    float L[4][4] = {{0, 0, 1, 0}, {-1, 0, 0, 0}, {0, -1, 0, 0}, {0, 0, 0, 1}};
+    std::memcpy(F, L, sizeof(F));
+  }
+  float W[4][4];
+  for (int i = 0; i < 4; ++i)
+    for (int j = 0; j < 4; ++j)
+      W[i][j] = ((c.sensor_pose[i * 4 + 0] * F[0][j] + c.sensor_pose[i * 4 + 1] * F[1][j]) +
+                 c.sensor_pose[i * 4 + 2] * F[2][j]) + c.sensor_pose[i * 4 + 3] * F[3][j];
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 4; ++j) I.to_world.m[i * 4 + j] = W[i][j];
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) I.to_ri.m[i * 4 + j] = W[j][i];
+  for (int i = 0; i < 3; ++i)
+    I.to_ri.m[i * 4 + 3] = -(I.to_ri.m[i * 4 + 0] * W[0][3] + I.to_ri.m[i * 4 + 1] * W[1][3] +
+                             I.to_ri.m[i * 4 + 2] * W[2][3]);
+  return I;
+}
+
+// host mirror of image_point (same float operation order)
+void host_image_point(const Img& I, float px, float py, float pz, float& ix, float& iy) {
+  const float* a = I.to_ri.m;
+  float tx = a[3] + (a[0] * px + a[1] * py + a[2] * pz);
+  float ty = a[7] + (a[4] * px + a[5] * py + a[6] * pz);
+  float tz = a[11] + (a[8] * px + a[9] * py + a[10] * pz);
+  if (tz <= 0) { ix = iy = -1.0f; return; }
+  ix = I.cx + I.fx * tx / tz - 0.0f;
+  iy = I.cy + I.fy * ty / tz - 0.0f;
+}
+
+NarfState& state(pfx_ctx* ctx) {
+  if (!ctx->narf) ctx->narf = new NarfState();
+  return *ctx->narf;
+}
+
+inline unsigned nblk(int64_t n, int b = 256) { return (unsigned)((n + b - 1) / b); }
+
+}  // namespace
+
+void range_image_dev(pfx_ctx* ctx, const float* x, const float* y, const float* z, int64_t n, const pfx_camera& cam,
+                     float4* d_points) {
+  PFX_CHECK(cam.width > 0 && cam.height > 0 && (int64_t)cam.width * cam.height < (int64_t(1) << 30),
+            "range image: bad image size");
+  if (cam.noise_level != 0.0f)
+    throw Error(PFX_ERR_UNSUPPORTED, "range image: noise_level != 0 (running-average z-buffer) not supported");
+  NarfState& S = state(ctx);
+  hipStream_t st = ctx->stream;
+  Img I = make_img(cam);
+  const int npx = I.w * I.h;
+  uint32_t* direct = S.direct.as<uint32_t>(npx);
+  uint32_t* fill = S.fill.as<uint32_t>(npx);
+  TimeScope ts(ctx, "range_image");
+  k_ri_init<<<nblk(npx), 256, 0, st>>>(direct, fill, npx);
+  if (n > 0) k_ri_project<<<nblk(n), 256, 0, st>>>(I, x, y, z, n, cam.min_range, direct, fill);
+  k_ri_finalize<<<nblk(npx), 256, 0, st>>>(I, direct, fill, d_points);
+  check_launch("range image");
+}
+
+int64_t narf_dev(pfx_ctx* ctx, const float* x, const float* y, const float* z, int64_t n, const pfx_camera& cam,
+                 const pfx_narf_params& p, std::vector<int32_t>& out) {
+  PFX_CHECK(p.support_size > 0.0f, "narf: support_size must be > 0");
+  if (p.no_of_polynomial_approximations_per_point != 0 || p.add_points_on_straight_edges != 0)
+    throw Error(PFX_ERR_UNSUPPORTED, "narf: polynomial refinement / straight-edge points not supported");
+  PFX_CHECK(p.pixel_radius_plane_extraction >= 0 && p.pixel_radius_plane_extraction <= 4,
+            "narf: pixel_radius_plane_extraction must be in [0, 4]");
+  NarfState& S = state(ctx);
+  hipStream_t st = ctx->stream;
+  Img I = make_img(cam);
+  S.w = I.w;
+  S.h = I.h;
+  const int npx = I.w * I.h;
+  PFX_CHECK(npx <= kBitmapWords * 32, "narf: image larger than 640x480 pixels is not supported");
+  float4* P = S.pts.as<float4>(npx);
+  range_image_dev(ctx, x, y, z, n, cam, P);
+  float4* surf = S.surf.as<float4>(npx);
+  uint8_t* svalid = S.svalid.as<uint8_t>(npx);
+  float *sL = S.sL.as<float>(npx), *sR = S.sR.as<float>(npx), *sT = S.sT.as<float>(npx), *sB = S.sB.as<float>(npx);
+  float *uL = S.uL.as<float>(npx), *uR = S.uR.as<float>(npx), *uT = S.uT.as<float>(npx), *uB = S.uB.as<float>(npx);
+  int4* sh = S.shadow.as<int4>(npx);
+  uint32_t* traits = S.traits.as<uint32_t>(npx);
+  float4* rawdir = S.rawdir.as<float4>(npx);
+  float4* dir = S.dir.as<float4>(npx);
+  float* scs = S.scs.as<float>(npx);
+  float4* scd = S.scd.as<float4>(npx);
+  float* interest = S.interest.as<float>(npx);
+  int* cand = S.cand.as<int>(npx);
+  int* counters = S.counters.as<int>(4);
+  {
+    TimeScope ts(ctx, "narf_border");
+    const int step = (p.pixel_radius_plane_extraction / 2) + 1;
+    const int nn = (int)std::pow((double)(p.pixel_radius_plane_extraction / step + 1), 2.0);
+    k_surface<<<nblk(npx), 256, 0, st>>>(I, P, p.pixel_radius_plane_extraction, step, nn, surf, svalid);
+    k_border_scores<<<nblk(npx), 256, 0, st>>>(I, P, surf, svalid, p.pixel_radius_borders, sL, sR, sT, sB);
+    k_update_scores<<<nblk(npx), 256, 0, st>>>(I, p.minimum_border_probability, sL, sR, sT, sB, uL, uR, uT, uB);
+    PFX_HIP(hipMemsetAsync(sh, 0xff, sizeof(int4) * npx, st));
+    PFX_HIP(hipMemsetAsync(traits, 0, sizeof(uint32_t) * npx, st));
+    k_shadow_rb<<<nblk(npx), 256, 0, st>>>(I, P, p.pixel_radius_borders, p.minimum_border_probability, uL, uR, uT,
+                                           uB, sh);
+    k_shadow_lt<<<nblk(npx), 256, 0, st>>>(I, P, p.pixel_radius_borders, p.minimum_border_probability, uL, uR, uT,
+                                           uB, sh);
+    k_classify<<<nblk(npx), 256, 0, st>>>(I, p.pixel_radius_borders, uL, uR, uT, uB, sh, traits);
+    k_border_dir_raw<<<nblk(npx), 256, 0, st>>>(I, P, surf, svalid, traits, rawdir);
+    const float deg = 0.017453292519943295769236907684886127134428718885417f;
+    const float min_cos = (float)std::cos((double)(120.0f * deg));
+    const float thr = 0.95f * p.minimum_border_probability;
+    k_border_dir_avg<<<nblk(npx), 256, 0, st>>>(I, P, surf, rawdir, p.pixel_radius_border_direction, min_cos, thr,
+                                                dir);
+    k_surface_change<<<nblk(npx), 256, 0, st>>>(I, P, surf, svalid, traits, dir, p.pixel_radius_principal_curvature,
+                                                scs, scd);
+    check_launch("narf border extraction");
+  }
+  InterestParams ip;
+  const float search_radius = 0.5f * p.support_size;
+  ip.radius_squared = search_radius * search_radius;
+  ip.radius_reciprocal = 1.0f / search_radius;
+  ip.min_scs = p.min_surface_change_score;
+  ip.opt_dist = p.optimal_distance_to_high_surface_change;
+  const float deg = 0.017453292519943295769236907684886127134428718885417f;
+  ip.d90 = 90.0f * deg;
+  ip.d180 = 180.0f * deg;
+  ip.R = search_radius;
+  PFX_HIP(hipMemsetAsync(counters, 0, 4 * sizeof(int), st));
+  {
+    TimeScope ts(ctx, "narf_interest");
+    k_interest<<<256 * 8, 64, 0, st>>>(I, P, traits, scs, scd, ip, interest, counters + 1);
+    check_launch("k_interest");
+  }
+  {
+    TimeScope ts(ctx, "narf_nms");
+    k_nms<<<nblk(npx), 256, 0, st>>>(I, interest, p.min_interest_value, p.do_non_maximum_suppression, cand, counters);
+    check_launch("k_nms");
+  }
+  int h_cnt[4];
+  PFX_HIP(hipMemcpyAsync(h_cnt, counters, sizeof(h_cnt), hipMemcpyDeviceToHost, st));
+  PFX_HIP(hipStreamSynchronize(st));
+  if (h_cnt[1] != 0) throw Error(PFX_ERR_CAPACITY, "narf: interest region-grow queue overflow");
+  const int nc = h_cnt[0];
+  // NMS survivors (point + strength) and the image's validity bits go to the host in one copy
+  const int nwords = (npx + 31) / 32;
+  float4* cpts = S.rawdir.as<float4>(npx);  // rawdir is dead after k_border_dir_avg: reuse
+  uint32_t* vbits = reinterpret_cast<uint32_t*>(S.sL.as<float>(npx));  // sL is dead after the update
+  {
+    TimeScope ts(ctx, "narf_gather");
+    if (nc > 0) k_gather_cand<<<nblk(nc), 256, 0, st>>>(cand, nc, P, interest, cpts);
+    k_valid_bits<<<nblk(nwords), 256, 0, st>>>(P, npx, vbits);
+    check_launch("k_gather_cand");
+  }
+  std::vector<float4> h_pts(nc);
+  std::vector<uint32_t> h_valid(nwords);
+  if (nc > 0) PFX_HIP(hipMemcpyAsync(h_pts.data(), cpts, sizeof(float4) * nc, hipMemcpyDeviceToHost, st));
+  PFX_HIP(hipMemcpyAsync(h_valid.data(), vbits, sizeof(uint32_t) * nwords, hipMemcpyDeviceToHost, st));
+  PFX_HIP(hipStreamSynchronize(st));
+  // k_gather_cand wrote (x, y, z, strength) plus the pixel index in the sort key: restore raster order
+  std::vector<std::pair<int, float4>> ordered(nc);
+  std::vector<int> h_cand(nc);
+  if (nc > 0) PFX_HIP(hipMemcpy(h_cand.data(), cand, sizeof(int) * nc, hipMemcpyDeviceToHost));
+  for (int k = 0; k < nc; ++k) ordered[k] = std::make_pair(h_cand[k], h_pts[k]);
+  std::sort(ordered.begin(), ordered.end(),
+            [](const std::pair<int, float4>& a, const std::pair<int, float4>& b) { return a.first < b.first; });
+  std::vector<HostInterestPoint> tmp(nc);
+  for (int k = 0; k < nc; ++k) {
+    const float4& q = ordered[k].second;
+    tmp[k] = HostInterestPoint{q.x, q.y, q.z, q.w};
+  }
+  std::sort(tmp.begin(), tmp.end(), host_better);
+  const float md = p.min_distance_between_interest_points * p.support_size;
+  const float min_d2 = md * md;
+  std::vector<HostInterestPoint> accepted;
+  std::vector<int> marked;
+  for (size_t k = 0; k < tmp.size(); ++k) {
+    if (p.max_no_of_interest_points > 0 && (int)accepted.size() >= p.max_no_of_interest_points) break;
+    const HostInterestPoint& a = tmp[k];
+    bool too_close = false;
+    for (const HostInterestPoint& b : accepted) {
+      float dx = a.x - b.x, dy = a.y - b.y, dz = a.z - b.z;
+      if (dx * dx + dy * dy + dz * dz < min_d2) { too_close = true; break; }
+    }
+    if (too_close) continue;
+    accepted.push_back(a);
+    float ixr, iyr;
+    host_image_point(I, a.x, a.y, a.z, ixr, iyr);
+    int ix = (int)std::lrint(ixr), iy = (int)std::lrint(iyr);
+    if (ix >= 0 && ix < I.w && iy >= 0 && iy < I.h) {
+      const int pix = iy * I.w + ix;
+      if (h_valid[pix >> 5] & (1u << (pix & 31))) marked.push_back(pix);
+    }
+  }
+  std::sort(marked.begin(), marked.end());
+  marked.erase(std::unique(marked.begin(), marked.end()), marked.end());
+  out.assign(marked.begin(), marked.end());
+  S.have_debug = true;
+  ctx->stats["narf_candidates"] = nc;
+  ctx->stats["narf_keypoints"] = (int64_t)out.size();
+  return (int64_t)out.size();
+}
+
+void narf_debug(pfx_ctx* ctx, const std::string& which, void* out, int64_t count) {
+  if (!ctx->narf || !ctx->narf->have_debug) throw Error(PFX_ERR_INVALID, "narf_debug: no NARF run yet");
+  NarfState& S = *ctx->narf;
+  const int64_t npx = (int64_t)S.w * S.h;
+  if (count < npx) throw Error(PFX_ERR_CAPACITY, "narf_debug: buffer smaller than width*height");
+  PFX_HIP(hipStreamSynchronize(ctx->stream));
+  if (which == "interest") {
+    PFX_HIP(hipMemcpy(out, S.interest.ptr, sizeof(float) * npx, hipMemcpyDeviceToHost));
+  } else if (which == "surface_change") {
+    PFX_HIP(hipMemcpy(out, S.scs.ptr, sizeof(float) * npx, hipMemcpyDeviceToHost));
+  } else if (which == "border_traits") {
+    PFX_HIP(hipMemcpy(out, S.traits.ptr, sizeof(uint32_t) * npx, hipMemcpyDeviceToHost));
+  } else if (which == "range") {
+    std::vector<float4> pts(npx);
+    PFX_HIP(hipMemcpy(pts.data(), S.pts.ptr, sizeof(float4) * npx, hipMemcpyDeviceToHost));
+    float* o = static_cast<float*>(out);
+    for (int64_t i = 0; i < npx; ++i) o[i] = pts[i].w;
+  } else {
+    throw Error(PFX_ERR_INVALID, "narf_debug: unknown image " + which);
+  }
+}
+
+void narf_release(pfx_ctx* ctx) {
+  if (ctx->narf) {
+    ctx->narf->release();
+    delete ctx->narf;
+    ctx->narf = nullptr;
+  }
+}
+
 }  // namespace pfx

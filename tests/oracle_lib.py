@@ -79,3 +79,61 @@ def fpfh(sx, sy, sz, nx, ny, nz, qx, qy, qz, r, same_as_surface=False, threads=0
                    _p(qz), _i64(nq), ctypes.c_int(1 if same_as_surface else 0),
                    ctypes.c_double(r), _p(out), ctypes.c_int(threads))
     return out
+
+
+CAM_DEFAULT = dict(width=640, height=480, center_x=320.0, center_y=240.0, focal_length_x=525.0,
+                   focal_length_y=525.0, sensor_pose=np.eye(4, dtype=np.float32), coordinate_frame=0,
+                   noise_level=0.0, min_range=0.0)
+NARF_DEFAULT = dict(support_size=0.2, max_no_of_interest_points=-1, min_distance_between_interest_points=0.25,
+                    optimal_distance_to_high_surface_change=0.25, min_interest_value=0.45,
+                    min_surface_change_score=0.2, do_non_maximum_suppression=1, calculate_sparse_interest_image=1,
+                    no_of_polynomial_approximations_per_point=0, add_points_on_straight_edges=0,
+                    pixel_radius_borders=3, pixel_radius_plane_extraction=2, pixel_radius_border_direction=2,
+                    minimum_border_probability=0.8, pixel_radius_principal_curvature=2)
+_NARF_ORDER = list(NARF_DEFAULT)
+
+
+def _cam(cam):
+    c = dict(CAM_DEFAULT)
+    c.update(cam or {})
+    pose = np.ascontiguousarray(np.asarray(c["sensor_pose"], np.float32).reshape(16))
+    return c, pose
+
+
+def range_image_planar(x, y, z, cam=None):
+    x, y, z = map(_f32, (x, y, z))
+    c, pose = _cam(cam)
+    out = np.empty((c["height"], c["width"], 4), dtype=np.float32)
+    lib().orc_range_image_planar(_p(x), _p(y), _p(z), _i64(len(x)), ctypes.c_int(c["width"]),
+                                 ctypes.c_int(c["height"]), ctypes.c_float(c["center_x"]),
+                                 ctypes.c_float(c["center_y"]), ctypes.c_float(c["focal_length_x"]),
+                                 ctypes.c_float(c["focal_length_y"]), _p(pose), ctypes.c_int(c["coordinate_frame"]),
+                                 ctypes.c_float(c["noise_level"]), ctypes.c_float(c["min_range"]), _p(out))
+    return out
+
+
+def narf_keypoints(x, y, z, params=None, cam=None, debug=False, threads=0):
+    x, y, z = map(_f32, (x, y, z))
+    c, pose = _cam(cam)
+    p = dict(NARF_DEFAULT)
+    p.update(params or {})
+    pv = np.array([float(p[k]) for k in _NARF_ORDER], dtype=np.float32)
+    cap = c["width"] * c["height"]
+    out = np.empty(cap, dtype=np.int32)
+    nout = ctypes.c_int64()
+    npx = c["width"] * c["height"]
+    dbg_i = np.empty(npx, np.float32) if debug else None
+    dbg_s = np.empty(npx, np.float32) if debug else None
+    dbg_t = np.empty(npx, np.uint32) if debug else None
+    lib().orc_narf_keypoints(_p(x), _p(y), _p(z), _i64(len(x)), ctypes.c_int(c["width"]), ctypes.c_int(c["height"]),
+                             ctypes.c_float(c["center_x"]), ctypes.c_float(c["center_y"]),
+                             ctypes.c_float(c["focal_length_x"]), ctypes.c_float(c["focal_length_y"]), _p(pose),
+                             ctypes.c_int(c["coordinate_frame"]), ctypes.c_float(c["noise_level"]),
+                             ctypes.c_float(c["min_range"]), _p(pv), _p(out, _i32p), _i64(cap), ctypes.byref(nout),
+                             _p(dbg_i), _p(dbg_s), _p(dbg_t, ctypes.POINTER(ctypes.c_uint32)), ctypes.c_int(threads))
+    kp = out[: nout.value].copy()
+    if debug:
+        h, w = c["height"], c["width"]
+        return kp, dict(interest=dbg_i.reshape(h, w), surface_change=dbg_s.reshape(h, w),
+                        border_traits=dbg_t.reshape(h, w))
+    return kp

@@ -1,0 +1,70 @@
+"""GPU parity of the NARF keypoint branch (keypoints.h:199-231) against the CPU restatement.
+
+Bar: range image, border traits, surface-change scores, the interest image and the keypoint
+pixel indices are all bit-exact (the index list is what NarfKeypoint::compute returns).
+Parity vs real PCL is unpinned (oracle/or_narf.cpp header).
+"""
+import os
+
+import numpy as np
+import pytest
+
+import oracle_lib as O
+from pcl_feature_extraction_amd.pcd import read_pcd
+
+pytestmark = pytest.mark.gpu
+
+CLOUDS = ["indoor_source", "indoor_target", "underwater_source", "underwater_target"]
+
+
+def _cloud(name):
+    c = read_pcd(os.path.join(os.path.dirname(__file__), "golden", "clouds", name + ".pcd"))
+    return c.x, c.y, c.z
+
+
+def _same(a, b):
+    a = np.asarray(a, np.float32).ravel()
+    b = np.asarray(b, np.float32).ravel()
+    na, nb = np.isnan(a), np.isnan(b)
+    if not np.array_equal(na, nb):
+        return False
+    return np.array_equal(a[~na].view(np.uint32), b[~nb].view(np.uint32))
+
+
+@pytest.mark.parametrize("name", CLOUDS)
+def test_range_image_bit_exact(ctx, name):
+    x, y, z = _cloud(name)
+    g = ctx.range_image_planar(x, y, z)
+    o = O.range_image_planar(x, y, z)
+    assert _same(g, o)
+
+
+@pytest.mark.parametrize("name", CLOUDS)
+def test_narf_keypoints_bit_exact(ctx, name):
+    x, y, z = _cloud(name)
+    kp = ctx.narf_keypoints(x, y, z)
+    okp, dbg = O.narf_keypoints(x, y, z, debug=True)
+    traits = ctx.narf_debug_image("border_traits")
+    scs = ctx.narf_debug_image("surface_change")
+    interest = ctx.narf_debug_image("interest")
+    assert np.array_equal(traits, dbg["border_traits"]), "border traits differ"
+    assert _same(scs, dbg["surface_change"]), "surface change scores differ"
+    assert _same(interest, dbg["interest"]), "interest image differs"
+    assert np.array_equal(kp, okp)
+    assert len(kp) > 0
+    assert np.all(np.diff(kp) > 0)  # ascending pixel indices
+
+
+def test_narf_empty_cloud(ctx):
+    e = np.zeros(0, np.float32)
+    assert len(ctx.narf_keypoints(e, e, e)) == 0
+
+
+def test_narf_points_behind_camera_ignored(ctx):
+    x, y, z = _cloud("underwater_source")
+    # mirror half the cloud behind the sensor: it must not change the image
+    xb = np.concatenate([x, x[:5000]])
+    yb = np.concatenate([y, y[:5000]])
+    zb = np.concatenate([z, -z[:5000]])
+    assert _same(ctx.range_image_planar(xb, yb, zb), O.range_image_planar(x, y, z))
+    assert np.array_equal(ctx.narf_keypoints(xb, yb, zb), O.narf_keypoints(x, y, z))
