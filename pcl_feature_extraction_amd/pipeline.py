@@ -1,0 +1,58 @@
+"""The reference's NARF + FPFH descriptor path as one device-resident pass.
+
+Mirrors, for one scan, what src/evaluation.cpp does for the (Narf, FPFH) pair:
+  Keypoints("Narf").compute(cloud, kps)        keypoints.h:199-231
+      RangeImagePlanar 640x480 -> NarfKeypoint(support 0.2) -> pixel indices
+      kps = cloud->points[pixel_index]          keypoints.h:227-229 (index quirk, guarded)
+  Features<FPFHSignature33>(FPFHEstimation, 0.08, 0.05).compute(cloud, kps, desc)
+      Tools::estimateNormals(cloud, r = 0.05)   features.h:187, tools.h:22-32
+      FPFH(surface = cloud, input = kps, r = 0.08)   features.h:188-195
+All arrays stay in HBM (torch tensors as device memory); the C-ABI calls are stream-ordered on
+the ctx stream.  Nothing here computes on the CPU except NARF's greedy selection inside libpfx.
+"""
+from __future__ import annotations
+
+import dataclasses
+
+import numpy as np
+
+from .api import Context, camera, narf_params
+
+
+@dataclasses.dataclass
+class ScanBuffers:
+    x: object
+    y: object
+    z: object
+    nx: object
+    ny: object
+    nz: object
+    curv: object
+    kx: object
+    ky: object
+    kz: object
+    desc: object
+
+
+def alloc(torch, n: int, device, max_keypoints: int = 1 << 16) -> ScanBuffers:
+    f = dict(dtype=torch.float32, device=device)
+    e = lambda m: torch.empty(m, **f)  # noqa: E731
+    return ScanBuffers(e(n), e(n), e(n), e(n), e(n), e(n), e(n), e(max_keypoints), e(max_keypoints),
+                       e(max_keypoints), torch.empty((max_keypoints, 33), **f))
+
+
+def narf_fpfh(ctx: Context, b: ScanBuffers, normal_radius: float = 0.05, feat_radius: float = 0.08,
+              params=None, cam=None):
+    """Returns (keypoint pixel indices (np.int32), number of descriptor rows K)."""
+    kp = ctx.narf_keypoints_dev(b.x, b.y, b.z, params or narf_params(support_size=0.2), cam or camera())
+    k = ctx.gather_points_dev(b.x, b.y, b.z, kp, b.kx, b.ky, b.kz)
+    ctx.normals_dev(b.x, b.y, b.z, normal_radius, b.nx, b.ny, b.nz, b.curv)
+    if k > 0:
+        ctx.fpfh_dev(b.x, b.y, b.z, b.nx, b.ny, b.nz, b.kx[:k], b.ky[:k], b.kz[:k], feat_radius, b.desc[:k])
+    return kp, k
+
+
+def keypoint_rows(kp: np.ndarray, n: int) -> np.ndarray:
+    """Cloud indices the descriptors belong to (keypoints.h:229 uses pixel index as cloud index)."""
+    kp = np.asarray(kp)
+    return kp[(kp >= 0) & (kp < n)]

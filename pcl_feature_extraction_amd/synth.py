@@ -4,8 +4,9 @@
   (u, v) in [0,640) x [0,480) (f = 525, c = (320, 240), the reference's NARF camera,
   keypoints.h:203-207) onto a piecewise room (floor, back wall, side wall, 3 boxes, 1 sphere)
   spanning z in [1, 4]*s, with Gaussian noise along the ray (sigma = 1.5 mm) and
-  s = sqrt(N / 1e5), so the surface density -- and the mean radius-0.05 neighbour count --
-  does not change with N (k(0.05) ~ 230 as on data/indoor).
+  s = 0.58 sqrt(N / 1e5) (SURVEY's sqrt(N/1e5) times a calibration factor for this scene), so
+  the surface density -- and the mean radius-0.05 neighbour count -- does not change with N
+  (k(0.05) ~ 230 as on data/indoor).
 * ``synth_seabed(N, seed)`` -- a camera looking down at a height field
   z = D + 0.08 fbm(x, y) (5 octaves), D chosen for the data/underwater density
   (k(0.05) ~ 400, k(0.08) ~ 930).
@@ -67,9 +68,12 @@ def _finish(rng, d, t, n, sigma=0.0015):
     return x, y, z, rgb
 
 
-def synth_room(n: int, seed: int = 1):
+ROOM_SCALE = 0.58  # calibrated: mean radius-0.05 neighbour count ~ 230 (data/indoor: 233)
+
+
+def synth_room(n: int, seed: int = 1, scale: float = ROOM_SCALE):
     rng = np.random.default_rng(seed)
-    s = float(np.sqrt(n / 1e5))
+    s = scale * float(np.sqrt(n / 1e5))
     dx, dy = _rays(rng, n)
     d = (dx, dy, np.ones(n))
     ts = [
