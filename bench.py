@@ -112,6 +112,21 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     nrm_ms, nrm_launches = ctx.kernel_time("normals")
+    if os.environ.get("PFX_BENCH_VERBOSE"):
+        names = ["grid_bbox", "grid_build", "normals_tiles", "normals", "normals_medium", "normals_overflow",
+                 "range_image", "narf_border", "narf_interest", "narf_nms", "narf_gather", "fpfh_mark",
+                 "fpfh_spfh", "fpfh_weight", "fpfh_weight_big"]
+        rep = {nm: round(ctx.kernel_time(nm)[0] / args.steps, 3) for nm in names}
+        print("per-step kernel ms:", json.dumps(rep), file=sys.stderr, flush=True)
+        stats = {}
+        for nm in ["normals_neighbors", "normals_tiles_sparse", "normals_tiles_dense", "normals_medium",
+                   "normals_overflow", "fpfh_spfh_points", "narf_candidates", "narf_keypoints",
+                   "narf_interest_fullimage"]:
+            try:
+                stats[nm] = ctx.stat(nm)
+            except Exception:
+                pass
+        print("stats:", json.dumps(stats), file=sys.stderr, flush=True)
     ctx.set_timing(False)
     neighbors = ctx.stat("normals_neighbors")
     if world > 1:

@@ -47,12 +47,21 @@ __global__ void __launch_bounds__(256) k_bbox(const float* __restrict__ x, const
       hi[d] = fmaxf(hi[d], __shfl_xor(hi[d], off));
     }
   }
+  __shared__ float s_lo[3][4], s_hi[3][4];
+  const int wv = threadIdx.x >> 6;
   if ((threadIdx.x & 63) == 0) {
 #pragma unroll
+    for (int d = 0; d < 3; ++d) { s_lo[d][wv] = lo[d]; s_hi[d][wv] = hi[d]; }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {  // one atomic per block and bound
+#pragma unroll
     for (int d = 0; d < 3; ++d) {
-      if (lo[d] <= hi[d]) {
-        atomicMin(&mm[d], f2ord(lo[d]));
-        atomicMax(&mm[3 + d], f2ord(hi[d]));
+      float l = fminf(fminf(s_lo[d][0], s_lo[d][1]), fminf(s_lo[d][2], s_lo[d][3]));
+      float h = fmaxf(fmaxf(s_hi[d][0], s_hi[d][1]), fmaxf(s_hi[d][2], s_hi[d][3]));
+      if (l <= h) {
+        atomicMin(&mm[d], f2ord(l));
+        atomicMax(&mm[3 + d], f2ord(h));
       }
     }
   }
@@ -152,6 +161,7 @@ void build_grid(pfx_ctx* ctx, Grid& g, const float* d_x, const float* d_y, const
   uint32_t* keys2 = g.b_keys2.as<uint32_t>(std::max<int64_t>(n + 1, C + 2));
   uint32_t* vals = g.b_vals.as<uint32_t>(n + 1);
   g.perm = g.b_perm.as<int32_t>(n + 1);
+  g.skeys = keys2;  // radix-sort output: cell key per sorted position
   g.sx = g.b_sx.as<float>(n + 1);
   g.sy = g.b_sy.as<float>(n + 1);
   g.sz = g.b_sz.as<float>(n + 1);

@@ -73,6 +73,7 @@ struct Grid {
   const float *ux = nullptr, *uy = nullptr, *uz = nullptr;  // the caller's arrays (not owned)
   int32_t* perm = nullptr;                            // sorted position -> caller index
   int32_t* cell_start = nullptr;                      // ncells + 1 prefix (by linear cell key)
+  const uint32_t* skeys = nullptr;                    // cell key of each sorted position
   DevBuf b_sx, b_sy, b_sz, b_perm, b_start, b_keys, b_keys2, b_vals, b_tmp, b_minmax;
   void release() {
     b_sx.release(); b_sy.release(); b_sz.release(); b_perm.release(); b_start.release();

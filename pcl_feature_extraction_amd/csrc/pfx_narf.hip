@@ -525,8 +525,15 @@ __global__ void k_surface_change(Img I, const float4* __restrict__ P, const floa
 }
 
 // ---- NARF interest image: one wave (64-thread block) per pixel ------------------------------
-constexpr int kBitmapWords = 9600;  // 640*480 bits: the whole image (window clears only)
-constexpr int kQueue = 4096;        // ring buffer of pending pixels
+// The region grow of pixel p can only accept pixels whose 3D point lies within R of p (or within
+// 2 px), so it stays inside a window whose half-size follows from the pinhole projection:
+//   |du| <= fx R (tz + |tx|) / ((tz - R) tz)   (t = p in the range-image frame, tz > R).
+// The touched bitmap covers that window (+3 px margin) in LDS; pixels whose window exceeds the
+// LDS budget (very close to the sensor) go to the full-image variant.  A pixel touched outside
+// its window raises the error flag (the bound is a checked invariant, not an assumption).
+constexpr int kWinWords = 2048;     // 65,536-pixel window (e.g. 256 x 256)
+constexpr int kFullWords = 9600;    // 640 x 480 bits
+constexpr int kQueue = 2048;        // ring buffer of pending pixels
 
 __device__ __forceinline__ float norm_angle(float a) {
   const float pi = 3.14159265358979323846f;
@@ -538,28 +545,49 @@ struct InterestParams {
   double R;  // search radius for the window bound
 };
 
+template <int WORDS, bool FULL>
 __global__ void __launch_bounds__(64) k_interest(Img I, const float4* __restrict__ P, const uint32_t* __restrict__ traits,
                                                  const float* __restrict__ scs, const float4* __restrict__ scd,
-                                                 InterestParams ip, float* __restrict__ interest,
-                                                 int* __restrict__ err) {
-  __shared__ uint32_t bitmap[kBitmapWords];
+                                                 InterestParams ip, const int* __restrict__ list, int nlist,
+                                                 float* __restrict__ interest, int* __restrict__ fallback,
+                                                 int* __restrict__ n_fallback, int* __restrict__ err) {
+  __shared__ uint32_t bitmap[WORDS];
   __shared__ int queue[kQueue];
   __shared__ unsigned hist[18];
   __shared__ unsigned neg_bits;
   __shared__ int s_tail;
   const int lane = threadIdx.x;
-  const int npx = I.w * I.h;
+  const int npx = FULL ? nlist : I.w * I.h;
   const uint32_t skip = TB(T_SHADOW_BORDER) | TB(T_VEIL_POINT);
-  // bitmap starts clear; every block clears exactly the words it set before moving on
-  for (int k = lane; k < kBitmapWords; k += 64) bitmap[k] = 0u;
-  __syncthreads();
-  for (int index = blockIdx.x; index < npx; index += gridDim.x) {
+  for (int it = blockIdx.x; it < npx; it += gridDim.x) {
+    const int index = FULL ? list[it] : it;
     const float4 point = P[index];
     if (!isfinite(point.w) || (traits[index] & skip)) {
       if (lane == 0) interest[index] = 0.0f;
       continue;
     }
     const int y = index / I.w, x = index - y * I.w;
+    int x0 = 0, y0 = 0, ww = I.w, wh = I.h;
+    if (!FULL) {
+      const f3 t = aff_apply(I.to_ri, mk3(point.x, point.y, point.z));
+      const double tz = t.z, R = ip.R;
+      bool whole = !(tz > 1.02 * R);
+      if (!whole) {
+        const double den = (tz - R) * tz;
+        const double wx = (double)I.fx * R * (tz + fabs((double)t.x)) / den * 1.01 + 3.0;
+        const double wy = (double)I.fy * R * (tz + fabs((double)t.y)) / den * 1.01 + 3.0;
+        const int hx = wx > 1e6 ? 1000000 : (int)ceil(wx), hy = wy > 1e6 ? 1000000 : (int)ceil(wy);
+        x0 = max(0, x - hx); y0 = max(0, y - hy);
+        ww = min(I.w - 1, x + hx) - x0 + 1;
+        wh = min(I.h - 1, y + hy) - y0 + 1;
+      }
+      if ((int64_t)ww * wh > (int64_t)WORDS * 32) {
+        if (lane == 0) fallback[atomicAdd(n_fallback, 1)] = index;
+        continue;
+      }
+    }
+    const int nwords = (ww * wh + 31) >> 5;
+    for (int k = lane; k < nwords; k += 64) bitmap[k] = 0u;
     // rotation to the viewer frame: getTransFromUnitVectorsZY(view, (0,-1,0))
     const f3 sensor = mk3(I.to_world.m[3], I.to_world.m[7], I.to_world.m[11]);
     const f3 view = normalized3(sub3(mk3(point.x, point.y, point.z), sensor));
@@ -567,15 +595,16 @@ __global__ void __launch_bounds__(64) k_interest(Img I, const float4* __restrict
     const f3 tmp1 = normalized3(cross3(view, tmp0));
     const f3 tmp2 = normalized3(view);
     if (lane < 18) hist[lane] = 0u;
+    __syncthreads();
     if (lane == 0) {
       neg_bits = __float_as_uint(1.0f);
       queue[0] = index;
       s_tail = 1;
-      bitmap[index >> 5] |= 1u << (index & 31);
+      const int lb = (y - y0) * ww + (x - x0);
+      bitmap[lb >> 5] |= 1u << (lb & 31);
     }
     __syncthreads();
     int head = 0;
-    int ymin = y, ymax = y;  // rows touched (for the clear)
     while (true) {
       const int tail = s_tail;
       if (head >= tail) break;
@@ -591,14 +620,14 @@ __global__ void __launch_bounds__(64) k_interest(Img I, const float4* __restrict
         if (ok) {
           for (int y3 = max(0, y2 - 1); y3 <= min(I.h - 1, y2 + 1); ++y3)
             for (int x3 = max(0, x2 - 1); x3 <= min(I.w - 1, x2 + 1); ++x3) {
-              int index3 = y3 * I.w + x3;
-              uint32_t bitm = 1u << (index3 & 31);
-              uint32_t old = atomicOr(&bitmap[index3 >> 5], bitm);
+              const int lx = x3 - x0, ly = y3 - y0;
+              if (lx < 0 || lx >= ww || ly < 0 || ly >= wh) { atomicOr(err, 2); continue; }
+              const int lb = ly * ww + lx;
+              const uint32_t bitm = 1u << (lb & 31);
+              const uint32_t old = atomicOr(&bitmap[lb >> 5], bitm);
               if (!(old & bitm)) {
-                int slot = atomicAdd(&s_tail, 1);
-                queue[slot & (kQueue - 1)] = index3;
-                ymin = min(ymin, y3);
-                ymax = max(ymax, y3);
+                const int slot = atomicAdd(&s_tail, 1);
+                queue[slot & (kQueue - 1)] = y3 * I.w + x3;
               }
             }
           const float sc = scs[index2];
@@ -627,7 +656,7 @@ __global__ void __launch_bounds__(64) k_interest(Img I, const float4* __restrict
       head += take;
       __syncthreads();
       if (s_tail - head > kQueue) {
-        if (lane == 0) atomicExch(err, 1);
+        if (lane == 0) atomicOr(err, 1);
         break;
       }
     }
@@ -649,15 +678,6 @@ __global__ void __launch_bounds__(64) k_interest(Img I, const float4* __restrict
       acv = sqrtf(acv);
       interest[index] = __uint_as_float(neg_bits) * acv;
     }
-    // clear the touched rows of the bitmap
-    int r0 = ymin, r1 = ymax;
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-      r0 = min(r0, __shfl_xor(r0, off));
-      r1 = max(r1, __shfl_xor(r1, off));
-    }
-    const int w0 = (r0 * I.w) >> 5, w1 = ((r1 + 1) * I.w + 31) >> 5;
-    for (int k = w0 + lane; k < w1 && k < kBitmapWords; k += 64) bitmap[k] = 0u;
     __syncthreads();
   }
 }
@@ -781,7 +801,7 @@ int64_t narf_dev(pfx_ctx* ctx, const float* x, const float* y, const float* z, i
   S.w = I.w;
   S.h = I.h;
   const int npx = I.w * I.h;
-  PFX_CHECK(npx <= kBitmapWords * 32, "narf: image larger than 640x480 pixels is not supported");
+  PFX_CHECK(npx <= kFullWords * 32, "narf: image larger than 640x480 pixels is not supported");
   float4* P = S.pts.as<float4>(npx);
   range_image_dev(ctx, x, y, z, n, cam, P);
   float4* surf = S.surf.as<float4>(npx);
@@ -834,8 +854,18 @@ int64_t narf_dev(pfx_ctx* ctx, const float* x, const float* y, const float* z, i
   PFX_HIP(hipMemsetAsync(counters, 0, 4 * sizeof(int), st));
   {
     TimeScope ts(ctx, "narf_interest");
-    k_interest<<<256 * 8, 64, 0, st>>>(I, P, traits, scs, scd, ip, interest, counters + 1);
+    k_interest<kWinWords, false><<<256 * 10, 64, 0, st>>>(I, P, traits, scs, scd, ip, nullptr, 0, interest,
+                                                           cand, counters + 2, counters + 1);
     check_launch("k_interest");
+    int nfb = 0;
+    PFX_HIP(hipMemcpyAsync(&nfb, counters + 2, sizeof(int), hipMemcpyDeviceToHost, st));
+    PFX_HIP(hipStreamSynchronize(st));
+    ctx->stats["narf_interest_fullimage"] = nfb;
+    if (nfb > 0) {
+      k_interest<kFullWords, true><<<std::min(nfb, 256 * 3), 64, 0, st>>>(I, P, traits, scs, scd, ip, cand, nfb,
+                                                                          interest, nullptr, nullptr, counters + 1);
+      check_launch("k_interest_full");
+    }
   }
   {
     TimeScope ts(ctx, "narf_nms");
@@ -845,7 +875,8 @@ int64_t narf_dev(pfx_ctx* ctx, const float* x, const float* y, const float* z, i
   int h_cnt[4];
   PFX_HIP(hipMemcpyAsync(h_cnt, counters, sizeof(h_cnt), hipMemcpyDeviceToHost, st));
   PFX_HIP(hipStreamSynchronize(st));
-  if (h_cnt[1] != 0) throw Error(PFX_ERR_CAPACITY, "narf: interest region-grow queue overflow");
+  if (h_cnt[1] & 1) throw Error(PFX_ERR_CAPACITY, "narf: interest region-grow queue overflow");
+  if (h_cnt[1] & 2) throw Error(PFX_ERR_DEVICE, "narf: interest region left its window bound (internal error)");
   const int nc = h_cnt[0];
   // NMS survivors (point + strength) and the image's validity bits go to the host in one copy
   const int nwords = (npx + 31) / 32;

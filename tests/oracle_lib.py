@@ -137,3 +137,13 @@ def narf_keypoints(x, y, z, params=None, cam=None, debug=False, threads=0):
         return kp, dict(interest=dbg_i.reshape(h, w), surface_change=dbg_s.reshape(h, w),
                         border_traits=dbg_t.reshape(h, w))
     return kp
+
+
+def shot(sx, sy, sz, nx, ny, nz, qx, qy, qz, r, threads=0):
+    sx, sy, sz, nx, ny, nz, qx, qy, qz = map(_f32, (sx, sy, sz, nx, ny, nz, qx, qy, qz))
+    nq = len(qx)
+    desc = np.empty((nq, 352), dtype=np.float32)
+    rf = np.empty((nq, 9), dtype=np.float32)
+    lib().orc_shot(_p(sx), _p(sy), _p(sz), _p(nx), _p(ny), _p(nz), _i64(len(sx)), _p(qx), _p(qy), _p(qz), _i64(nq),
+                   ctypes.c_double(r), _p(desc), _p(rf), ctypes.c_int(threads))
+    return desc, rf
