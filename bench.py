@@ -113,14 +113,14 @@ def main():
     elapsed = time.perf_counter() - t0
     nrm_ms, nrm_launches = ctx.kernel_time("normals")
     if os.environ.get("PFX_BENCH_VERBOSE"):
-        names = ["grid_bbox", "grid_build", "normals_tiles", "normals", "normals_medium", "normals_overflow",
+        names = ["grid_bbox", "grid_build", "normals", "normals_tiles", "normals_lists", "normals_chain",
                  "range_image", "narf_border", "narf_interest", "narf_nms", "narf_gather", "fpfh_mark",
                  "fpfh_spfh", "fpfh_weight", "fpfh_weight_big"]
         rep = {nm: round(ctx.kernel_time(nm)[0] / args.steps, 3) for nm in names}
         print("per-step kernel ms:", json.dumps(rep), file=sys.stderr, flush=True)
         stats = {}
-        for nm in ["normals_neighbors", "normals_tiles_sparse", "normals_tiles_dense", "normals_medium",
-                   "normals_overflow", "fpfh_spfh_points", "narf_candidates", "narf_keypoints",
+        for nm in ["normals_neighbors", "normals_queries", "normals_tiles_sparse", "normals_tiles_dense",
+                   "normals_single", "fpfh_spfh_points", "narf_candidates", "narf_keypoints",
                    "narf_interest_fullimage"]:
             try:
                 stats[nm] = ctx.stat(nm)

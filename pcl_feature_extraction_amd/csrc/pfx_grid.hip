@@ -95,13 +95,15 @@ __global__ void __launch_bounds__(256) k_gather_sorted(const float* __restrict__
                                                        const float* __restrict__ z, int64_t n,
                                                        const uint32_t* __restrict__ perm,
                                                        float* __restrict__ sx, float* __restrict__ sy,
-                                                       float* __restrict__ sz) {
+                                                       float* __restrict__ sz, float4* __restrict__ sp) {
   int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   if (i >= n) return;
   uint32_t p = perm[i];
-  sx[i] = x[p];
-  sy[i] = y[p];
-  sz[i] = z[p];
+  const float a = x[p], b = y[p], c = z[p];
+  sx[i] = a;
+  sy[i] = b;
+  sz[i] = c;
+  sp[i] = make_float4(a, b, c, 0.0f);
 }
 
 }  // namespace
@@ -165,6 +167,7 @@ void build_grid(pfx_ctx* ctx, Grid& g, const float* d_x, const float* d_y, const
   g.sx = g.b_sx.as<float>(n + 1);
   g.sy = g.b_sy.as<float>(n + 1);
   g.sz = g.b_sz.as<float>(n + 1);
+  g.sp = g.b_sp.as<float4>(n + 1);
   g.cell_start = g.b_start.as<int32_t>(C + 2);
   g.dinv = inv;
   g.dox = lo[0]; g.doy = lo[1]; g.doz = lo[2];
@@ -183,7 +186,7 @@ void build_grid(pfx_ctx* ctx, Grid& g, const float* d_x, const float* d_y, const
       PFX_HIP(rocprim::radix_sort_pairs(tmp, sort_bytes, keys, keys2, vals,
                                         reinterpret_cast<uint32_t*>(g.perm), (size_t)n, 0, bits, st));
       k_gather_sorted<<<(unsigned)ceil_div(n, 256), 256, 0, st>>>(
-          d_x, d_y, d_z, n, reinterpret_cast<uint32_t*>(g.perm), g.sx, g.sy, g.sz);
+          d_x, d_y, d_z, n, reinterpret_cast<uint32_t*>(g.perm), g.sx, g.sy, g.sz, g.sp);
       check_launch("k_gather_sorted");
     }
   }

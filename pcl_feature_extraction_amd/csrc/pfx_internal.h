@@ -70,13 +70,14 @@ struct Grid {
   int64_t ncells = 0;
   // device arrays
   float *sx = nullptr, *sy = nullptr, *sz = nullptr;  // sorted-by-cell SoA coordinates
+  float4* sp = nullptr;                               // the same, packed (x, y, z, 0)
   const float *ux = nullptr, *uy = nullptr, *uz = nullptr;  // the caller's arrays (not owned)
   int32_t* perm = nullptr;                            // sorted position -> caller index
   int32_t* cell_start = nullptr;                      // ncells + 1 prefix (by linear cell key)
   const uint32_t* skeys = nullptr;                    // cell key of each sorted position
-  DevBuf b_sx, b_sy, b_sz, b_perm, b_start, b_keys, b_keys2, b_vals, b_tmp, b_minmax;
+  DevBuf b_sx, b_sy, b_sz, b_sp, b_perm, b_start, b_keys, b_keys2, b_vals, b_tmp, b_minmax;
   void release() {
-    b_sx.release(); b_sy.release(); b_sz.release(); b_perm.release(); b_start.release();
+    b_sx.release(); b_sy.release(); b_sz.release(); b_sp.release(); b_perm.release(); b_start.release();
     b_keys.release(); b_keys2.release(); b_vals.release(); b_tmp.release(); b_minmax.release();
   }
 };
@@ -84,6 +85,7 @@ struct Grid {
 // Per-query view of a grid handed to kernels by value.
 struct GridView {
   const float *sx, *sy, *sz;
+  const float4* sp;
   const float *ux, *uy, *uz;  // caller-order (unsorted) coordinates, indexed by perm values
   const int32_t* perm;
   const int32_t* cell_start;
@@ -114,8 +116,8 @@ namespace pfx {
 struct TimeScope {
   pfx_ctx* ctx;
   hipEvent_t a = nullptr, b = nullptr;
-  const char* name;
-  TimeScope(pfx_ctx* c, const char* n) : ctx(c), name(n) {
+  std::string name;
+  TimeScope(pfx_ctx* c, std::string n) : ctx(c), name(std::move(n)) {
     if (ctx->timer.enabled) {
       a = ctx->timer.take();
       b = ctx->timer.take();
@@ -125,7 +127,7 @@ struct TimeScope {
   ~TimeScope() {
     if (a) {
       (void)hipEventRecord(b, ctx->stream);
-      ctx->timer.pending.push_back(KernelTimer::Pending{a, b, std::string(name)});
+      ctx->timer.pending.push_back(KernelTimer::Pending{a, b, name});
     }
   }
 };
@@ -143,7 +145,7 @@ void build_grid(pfx_ctx* ctx, Grid& g, const float* d_x, const float* d_y, const
                 int64_t n, double radius);
 inline GridView view(const Grid& g) {
   GridView v;
-  v.sx = g.sx; v.sy = g.sy; v.sz = g.sz; v.perm = g.perm; v.cell_start = g.cell_start;
+  v.sx = g.sx; v.sy = g.sy; v.sz = g.sz; v.sp = g.sp; v.perm = g.perm; v.cell_start = g.cell_start;
   v.ux = g.ux; v.uy = g.uy; v.uz = g.uz;
   v.inv = g.dinv; v.ox = g.dox; v.oy = g.doy; v.oz = g.doz; v.nx = g.nx; v.ny = g.ny; v.nz = g.nz;
   return v;

@@ -1,0 +1,548 @@
+// pfx_nblist.hip -- radius-neighbour lists of grid points in FLANN order (see pfx_nblist.h).
+//
+// Tiles: up to 16 consecutive queries of one grid cell share the 3x3x3 candidate block (9
+// contiguous runs of the cell-sorted SoA copy), staged once in LDS.  Each wave owns 4 of the
+// tile's queries: it streams the candidates from LDS and keeps hits as u16 candidate indices
+// (wave-uniform cursors, no atomics), then orders each list with a wave-local LDS bucket sort on
+// d2 (exact (d2, caller index) rank inside a bucket).  The tile's lists are written to HBM
+// interleaved (stride 2^lg >= tile size) with one global atomic per tile.
+//   sparse tiles: <= 1280 candidates, <= 512 neighbours per query in LDS  (3 workgroups / CU)
+//   dense tiles:  <= 8000 candidates, <= 1024 neighbours per query in LDS (1 workgroup / CU)
+// Queries of larger blocks and overflowing lists go to k_nb_query (one 256-thread workgroup per
+// query, candidates streamed from L2/HBM, <= 4096 neighbours sorted in LDS); beyond that the
+// same kernel runs with its sort arrays in global scratch (<= 262144 neighbours).
+#include <cstring>
+#include <rocprim/rocprim.hpp>
+
+#include "pfx_nblist.h"
+#include "pfx_neighbors.h"
+
+namespace pfx {
+namespace {
+
+constexpr int kQ = 16;  // tile: consecutive queries of one cell
+constexpr int kTcapSparse = 1280, kTcapDense = 8000;
+constexpr int kCapQuery = 4096, kBucketsQuery = 1024;
+constexpr int kCapHuge = 1 << 18, kBucketsHuge = 4096, kHugeBlocks = 32;
+
+// tile descriptor: first query index (28 bits) | (tile size - 1) << 28
+__device__ __forceinline__ uint32_t tile_pack(int32_t start, int qn) {
+  return (uint32_t)start | ((uint32_t)(qn - 1) << 28);
+}
+__device__ __forceinline__ int32_t tile_start(uint32_t e) { return (int32_t)(e & 0x0fffffffu); }
+__device__ __forceinline__ int tile_qn(uint32_t e) { return (int)(e >> 28) + 1; }
+
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
+__device__ __forceinline__ void cell_runs(const GridView& g, uint32_t key, int r, int32_t& s, int32_t& len) {
+  const int64_t iz = key % g.nz, iy = (key / g.nz) % g.ny, ix = key / ((uint64_t)g.nz * g.ny);
+  const int64_t bx = ix + (r / 3) - 1, by = iy + (r % 3) - 1;
+  const int64_t z0 = iz - 1 < 0 ? 0 : iz - 1, z1 = iz + 1 >= g.nz ? g.nz - 1 : iz + 1;
+  s = 0;
+  len = 0;
+  if (bx >= 0 && bx < g.nx && by >= 0 && by < g.ny) {
+    const int64_t base = (bx * g.ny + by) * g.nz;
+    s = g.cell_start[base + z0];
+    len = g.cell_start[base + z1 + 1] - s;
+  }
+}
+
+__device__ __forceinline__ int block_runs(const GridView& g, uint32_t key, Runs& R) {
+  int acc = 0;
+#pragma unroll
+  for (int r = 0; r < 9; ++r) {
+    int32_t s, len;
+    cell_runs(g, key, r, s, len);
+    R.start[r] = s;
+    R.pref[r] = acc;
+    acc += len;
+  }
+  R.pref[9] = acc;
+  return acc;
+}
+
+__global__ void k_iota(int32_t* __restrict__ out, int64_t n) {
+  int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (i < n) out[i] = (int32_t)i;
+}
+
+__global__ void k_mask_flags(const int32_t* __restrict__ perm, const uint32_t* __restrict__ skeys, int64_t n,
+                             uint64_t ncells, const uint8_t* __restrict__ mask, uint8_t* __restrict__ flags) {
+  int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (i < n) flags[i] = ((uint64_t)skeys[i] < ncells) && mask[perm[i]];
+}
+
+// segment (cell) start of each query position j, as (j if the cell changes at j else 0)
+__global__ void k_seg_marks(const int32_t* __restrict__ qpos, const uint32_t* __restrict__ skeys,
+                            const int64_t* __restrict__ nq_ptr, int32_t* __restrict__ marks) {
+  int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (j >= *nq_ptr) return;
+  marks[j] = (j == 0 || skeys[qpos[j]] != skeys[qpos[j - 1]]) ? (int32_t)j : 0;
+}
+
+__global__ void k_tile_flags(const int32_t* __restrict__ seg, const int64_t* __restrict__ nq_ptr,
+                             uint8_t* __restrict__ flags, int64_t n) {
+  int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (j >= n) return;
+  flags[j] = (j < *nq_ptr) && ((j - seg[j]) % kQ == 0);
+}
+
+// candidate-block class of a tile: sparse, dense, or every query to the per-query path
+__global__ void k_tile_class(GridView g, const int32_t* __restrict__ qpos, const uint32_t* __restrict__ skeys,
+                             const int64_t* __restrict__ nq_ptr, const int32_t* __restrict__ tiles,
+                             const int64_t* __restrict__ ntiles_ptr, uint32_t* __restrict__ sparse,
+                             uint32_t* __restrict__ dense, int32_t* __restrict__ single, int* __restrict__ counts) {
+  const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const int64_t ntiles = *ntiles_ptr;
+  if (t >= ntiles) return;
+  const int32_t start = tiles[t];
+  const int64_t next = (t + 1 < ntiles) ? tiles[t + 1] : *nq_ptr;  // tiles never span cells
+  const int qn = (int)(next - start < kQ ? next - start : kQ);
+  Runs R;
+  const int T = block_runs(g, skeys[qpos[start]], R);
+  if (T <= kTcapSparse) {
+    sparse[atomicAdd(&counts[0], 1)] = tile_pack(start, qn);
+  } else if (T <= kTcapDense) {
+    dense[atomicAdd(&counts[1], 1)] = tile_pack(start, qn);
+  } else {
+    const int h = atomicAdd(&counts[2], qn);
+    for (int j = 0; j < qn; ++j) single[h + j] = start + j;
+  }
+}
+
+struct ListOut {
+  int64_t* off;
+  int32_t* cnt;
+  uint8_t* lg;
+  uint32_t* list;
+  unsigned long long* cursor;  // [0] slots allocated, [1] neighbours
+  unsigned long long cap;
+};
+
+// Wave-local bucket sort of one query's list L[0..k) (u16 candidate indices) into FLANN order.
+// Sd/St: wave-private scratch (k entries), bcount/bpos: wave-private NB buckets.
+template <int NB>
+__device__ __forceinline__ void wave_sort(uint16_t* L, int k, float qx, float qy, float qz, const float* cx,
+                                          const float* cy, const float* cz, float bscale, uint32_t* Sd,
+                                          uint16_t* St, int* bcount, int* bpos, const GridView& g, const Runs& R,
+                                          int lane) {
+  for (int b = lane; b < NB; b += 64) bcount[b] = 0;
+  wave_sync();
+  for (int e = lane; e < k; e += 64) {
+    const int t = L[e];
+    const int b = (int)(flann_d2(qx, qy, qz, cx[t], cy[t], cz[t]) * bscale);
+    atomicAdd(&bcount[b < NB ? b : NB - 1], 1);
+  }
+  wave_sync();
+  {
+    constexpr int PER = NB / 64;
+    int c[PER], s = 0;
+#pragma unroll
+    for (int v = 0; v < PER; ++v) { c[v] = bcount[lane * PER + v]; s += c[v]; }
+    int inc = s;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int x = __shfl_up(inc, o);
+      if (lane >= o) inc += x;
+    }
+    int ex = inc - s;
+#pragma unroll
+    for (int v = 0; v < PER; ++v) { bpos[lane * PER + v] = ex; ex += c[v]; }
+  }
+  wave_sync();
+  for (int e = lane; e < k; e += 64) {
+    const int t = L[e];
+    const float d2 = flann_d2(qx, qy, qz, cx[t], cy[t], cz[t]);
+    int b = (int)(d2 * bscale);
+    b = b < NB ? b : NB - 1;
+    const int slot = atomicAdd(&bpos[b], 1);
+    Sd[slot] = __float_as_uint(d2);  // d2 >= +0: bit order == value order
+    St[slot] = (uint16_t)t;
+  }
+  wave_sync();
+  for (int s = lane; s < k; s += 64) {
+    const uint32_t d = Sd[s];
+    int b = (int)(__uint_as_float(d) * bscale);
+    b = b < NB ? b : NB - 1;
+    const int en = bpos[b], st = en - bcount[b];
+    const int t = St[s];
+    int rank = 0;
+    for (int v = st; v < en; ++v) {
+      const uint32_t dv = Sd[v];
+      if (dv < d) ++rank;
+      else if (dv == d && v != s && g.perm[run_pos(R, St[v])] < g.perm[run_pos(R, t)]) ++rank;
+    }
+    L[st + rank] = (uint16_t)t;
+  }
+  wave_sync();
+}
+
+template <int LCAP, int NB, int TCAP>
+__global__ void __launch_bounds__(256) k_nb_tile(GridView g, const int32_t* __restrict__ qpos,
+                                                 const uint32_t* __restrict__ skeys,
+                                                 const uint32_t* __restrict__ tiles, const int* __restrict__ ntiles_ptr,
+                                                 float rr, float bscale, int sorted, ListOut out,
+                                                 int32_t* __restrict__ single, int* __restrict__ n_single) {
+  constexpr int Q = kQ, QW = Q / 4;  // queries per tile / per wave
+  __shared__ float cx[TCAP], cy[TCAP], cz[TCAP];
+  __shared__ uint16_t lists[Q][LCAP + 2];  // +2: odd dword row stride (no bank conflicts)
+  __shared__ uint32_t sd[4][LCAP];
+  __shared__ uint16_t stt[4][LCAP];
+  __shared__ int bcount[4][NB], bpos[4][NB];
+  __shared__ int s_k[Q];
+  __shared__ unsigned long long s_base;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int ntiles = *ntiles_ptr;
+  const int64_t vb = xcd_block(blockIdx.x, gridDim.x);
+  for (int64_t tile = vb; tile < ntiles; tile += gridDim.x) {
+    const uint32_t te = tiles[tile];
+    const int32_t start = tile_start(te);
+    const int qn = tile_qn(te);
+    Runs R;
+    const int T = block_runs(g, skeys[qpos[start]], R);
+    if (T > TCAP) {  // cannot happen after k_tile_class; keep the kernel safe regardless
+      if (tid < qn) single[atomicAdd(n_single, 1)] = start + tid;
+      continue;
+    }
+    for (int t = tid; t < T; t += 256) {
+      const int32_t pos = run_pos(R, t);
+      cx[t] = g.sx[pos];
+      cy[t] = g.sy[pos];
+      cz[t] = g.sz[pos];
+    }
+    __syncthreads();
+    float qx[QW], qy[QW], qz[QW];
+    int cursor[QW];
+#pragma unroll
+    for (int u = 0; u < QW; ++u) {
+      const int j = wv + 4 * u;
+      cursor[u] = 0;
+      qx[u] = qy[u] = qz[u] = 0.f;
+      if (j < qn) {
+        const float4 c = g.sp[qpos[start + j]];
+        qx[u] = c.x; qy[u] = c.y; qz[u] = c.z;
+      }
+    }
+    for (int t0 = 0; t0 < T; t0 += 64) {
+      const int t = t0 + lane;
+      const bool in = t < T;
+      const float px = in ? cx[t] : 0.f, py = in ? cy[t] : 0.f, pz = in ? cz[t] : 0.f;
+#pragma unroll
+      for (int u = 0; u < QW; ++u) {
+        const int j = wv + 4 * u;
+        const bool hit = in && j < qn && flann_d2(qx[u], qy[u], qz[u], px, py, pz) < rr;
+        const uint64_t m = __ballot(hit);
+        if (hit) {
+          const int slot = cursor[u] + __popcll(m & lanemask_lt());
+          if (slot < LCAP) lists[j][slot] = (uint16_t)t;
+        }
+        cursor[u] += __popcll(m);
+      }
+    }
+    // tile layout in HBM: the lists of the tile's qn queries interleaved with stride 2^lg >= qn
+    // (entry m of query j at base + (m << lg) + j), so lane-per-query consumers read coalesced
+    if (lane == 0) {
+#pragma unroll
+      for (int u = 0; u < QW; ++u)
+        if (wv + 4 * u < qn) s_k[wv + 4 * u] = cursor[u];
+    }
+    __syncthreads();
+    int lg = 0;
+    while ((1 << lg) < qn) ++lg;
+    int maxk = 0;
+    for (int j = 0; j < qn; ++j) {
+      const int k = s_k[j];
+      maxk = (k <= LCAP && k > maxk) ? k : maxk;
+    }
+    if (tid == 0) {
+      s_base = maxk ? atomicAdd(out.cursor, (unsigned long long)maxk << lg) : 0ull;
+      unsigned long long sum = 0;
+      for (int j = 0; j < qn; ++j) sum += s_k[j] <= LCAP ? (unsigned long long)s_k[j] : 0ull;
+      if (sum) atomicAdd(out.cursor + 1, sum);
+    }
+    if (tid < qn) {
+      const int k = s_k[tid];
+      if (k > LCAP) {
+        single[atomicAdd(n_single, 1)] = start + tid;  // the per-query path writes its descriptor
+      } else {
+        out.cnt[start + tid] = k;
+        out.lg[start + tid] = (uint8_t)lg;
+      }
+    }
+    if (sorted) {
+#pragma unroll
+      for (int u = 0; u < QW; ++u) {
+        const int j = wv + 4 * u;
+        const int k = cursor[u];
+        if (j < qn && k <= LCAP && k > 1)  // wave-uniform
+          wave_sort<NB>(lists[j], k, qx[u], qy[u], qz[u], cx, cy, cz, bscale, sd[wv], stt[wv], bcount[wv],
+                        bpos[wv], g, R, lane);
+      }
+    }
+    __syncthreads();
+    const int64_t base = (int64_t)s_base;
+    if (tid < qn && s_k[tid] <= LCAP) out.off[start + tid] = base + tid;
+    // coalesced write of the interleaved block (padding slots are left unwritten)
+    const int total = maxk << lg;
+    if ((unsigned long long)(base + total) <= out.cap) {
+      for (int e = tid; e < total; e += 256) {
+        const int m = e >> lg, j = e & ((1 << lg) - 1);
+        if (j < qn) {
+          const int k = s_k[j];
+          if (m < k && k <= LCAP) out.list[base + e] = (uint32_t)run_pos(R, lists[j][m]);
+        }
+      }
+    }
+    __syncthreads();  // LDS is reused by the next tile
+  }
+}
+
+// One 256-thread workgroup per query: candidates streamed from L2/HBM, the list bucket-sorted
+// in LDS (GLOBAL = false) or in a per-workgroup global scratch slice (GLOBAL = true).
+// Lists longer than CAP go to `over` (or raise err when over == nullptr).
+template <int CAP, int NB, bool GLOBAL>
+__global__ void __launch_bounds__(256) k_nb_query(GridView g, const int32_t* __restrict__ qpos,
+                                                  const int32_t* __restrict__ work, const int* __restrict__ n_ptr,
+                                                  float rr, float bscale, int sorted, ListOut out,
+                                                  int32_t* __restrict__ over, int* __restrict__ n_over,
+                                                  int* __restrict__ err, uint32_t* __restrict__ scratch) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+  __shared__ int bcount[NB], bpos[NB];
+  __shared__ int s_count;
+  __shared__ unsigned long long s_base;
+  uint32_t* base_arr = GLOBAL ? scratch + (size_t)blockIdx.x * 4 * CAP : smem;
+  uint32_t* hits = base_arr;        // positions, then the sorted list
+  uint32_t* hd = base_arr + CAP;    // d2 bits of hits
+  uint32_t* sdv = base_arr + 2 * CAP;
+  uint32_t* spv = base_arr + 3 * CAP;
+  const int tid = threadIdx.x;
+  const int count = *n_ptr;
+  for (int w = blockIdx.x; w < count; w += gridDim.x) {
+    const int32_t j = work[w];
+    const int32_t qp = qpos[j];
+    const float4 q = g.sp[qp];
+    Runs R;
+    query_runs(g, q.x, q.y, q.z, R);
+    if (tid == 0) s_count = 0;
+    for (int b = tid; b < NB; b += 256) bcount[b] = 0;
+    __syncthreads();
+    for (int t0 = 0; t0 < R.pref[9]; t0 += 256) {
+      const int t = t0 + tid;
+      bool hit = false;
+      int32_t pos = 0;
+      float d2 = 0.f;
+      if (t < R.pref[9]) {
+        pos = run_pos(R, t);
+        const float4 c = g.sp[pos];
+        d2 = flann_d2(q.x, q.y, q.z, c.x, c.y, c.z);
+        hit = d2 < rr;
+      }
+      const uint64_t m = __ballot(hit);
+      int base = 0;
+      if ((tid & 63) == 0 && m) base = atomicAdd(&s_count, __popcll(m));
+      base = __shfl(base, 0);
+      if (hit) {
+        const int slot = base + __popcll(m & lanemask_lt());
+        if (slot < CAP) {
+          hits[slot] = (uint32_t)pos;
+          hd[slot] = __float_as_uint(d2);
+        }
+      }
+    }
+    __syncthreads();
+    const int k = s_count;
+    if (k > CAP) {
+      if (tid == 0) {
+        if (over) over[atomicAdd(n_over, 1)] = j;
+        else atomicMax(err, k);
+      }
+      __syncthreads();
+      continue;
+    }
+    if (sorted && k > 1) {
+      for (int e = tid; e < k; e += 256) {
+        const int b = (int)(__uint_as_float(hd[e]) * bscale);
+        atomicAdd(&bcount[b < NB ? b : NB - 1], 1);
+      }
+      __syncthreads();
+      if (tid < 64) {  // one wave scans the counts
+        constexpr int PER = NB / 64;
+        int s = 0;
+        for (int v = 0; v < PER; ++v) s += bcount[tid * PER + v];
+        int inc = s;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+          const int x = __shfl_up(inc, o);
+          if (tid >= o) inc += x;
+        }
+        int ex = inc - s;
+        for (int v = 0; v < PER; ++v) { bpos[tid * PER + v] = ex; ex += bcount[tid * PER + v]; }
+      }
+      __syncthreads();
+      for (int e = tid; e < k; e += 256) {
+        const uint32_t d = hd[e];
+        int b = (int)(__uint_as_float(d) * bscale);
+        b = b < NB ? b : NB - 1;
+        const int slot = atomicAdd(&bpos[b], 1);
+        sdv[slot] = d;
+        spv[slot] = hits[e];
+      }
+      __syncthreads();
+      for (int s = tid; s < k; s += 256) {
+        const uint32_t d = sdv[s], p = spv[s];
+        int b = (int)(__uint_as_float(d) * bscale);
+        b = b < NB ? b : NB - 1;
+        const int en = bpos[b], st = en - bcount[b];
+        int rank = 0;
+        for (int v = st; v < en; ++v) {
+          const uint32_t dv = sdv[v];
+          if (dv < d) ++rank;
+          else if (dv == d && v != s && g.perm[spv[v]] < g.perm[p]) ++rank;
+        }
+        hits[st + rank] = p;
+      }
+      __syncthreads();
+    }
+    if (tid == 0) {
+      s_base = k ? atomicAdd(out.cursor, (unsigned long long)k) : 0ull;
+      if (k) atomicAdd(out.cursor + 1, (unsigned long long)k);
+      out.off[j] = (int64_t)s_base;
+      out.cnt[j] = k;
+      out.lg[j] = 0;
+    }
+    __syncthreads();
+    const int64_t off = (int64_t)s_base;
+    if ((unsigned long long)(off + k) <= out.cap)
+      for (int m = tid; m < k; m += 256) out.list[off + m] = hits[m];
+    __syncthreads();
+  }
+}
+
+std::string bname(const char* tag, const char* what) { return std::string(tag) + "_" + what; }
+
+}  // namespace
+
+void build_lists(pfx_ctx* ctx, const Grid& G, const uint8_t* mask, double radius, bool sorted, NbLists& out,
+                 const char* tag) {
+  hipStream_t st = ctx->stream;
+  const int64_t n = G.n;
+  GridView g = view(G);
+  const float rr = (float)(radius * radius);
+  out = NbLists();
+  if (n == 0) return;
+  if (n >= (int64_t(1) << 28))
+    throw Error(PFX_ERR_CAPACITY, std::string(tag) + ": neighbour lists support < 2^28 points");
+  auto B = [&](const char* what) -> DevBuf& { return ctx->bufs[bname(tag, what)]; };
+  int32_t* qpos = B("qpos").as<int32_t>(n);
+  int64_t* d_nq = B("nq").as<int64_t>(1);
+  uint8_t* flags = B("flags").as<uint8_t>(n);
+  int32_t* seg = B("seg").as<int32_t>(n);
+  int32_t* tiles = B("tiles").as<int32_t>(n);
+  int64_t* d_ntiles = B("ntiles").as<int64_t>(1);
+  uint32_t* sparse = B("sparse").as<uint32_t>(n);
+  uint32_t* dense = B("dense").as<uint32_t>(n);
+  int32_t* single = B("single").as<int32_t>(n);
+  int32_t* huge = B("huge").as<int32_t>(n);
+  int64_t* off = B("off").as<int64_t>(n);
+  int32_t* cnt = B("cnt").as<int32_t>(n);
+  uint8_t* lgs = B("lg").as<uint8_t>(n);
+  // counters: 0 sparse tiles, 1 dense tiles, 2 per-query work, 3 huge work, 4 max k over cap,
+  // 6 per-query work queued by the classifier (restored for a rerun)
+  int* counters = B("counters").as<int>(8);
+  unsigned long long* cursor = B("cursor").as<unsigned long long>(2);
+  size_t t1 = 0, t2 = 0, t3 = 0;
+  PFX_HIP(rocprim::select(nullptr, t1, rocprim::counting_iterator<int32_t>(0), flags, qpos, d_nq, (size_t)n, st));
+  PFX_HIP(rocprim::inclusive_scan(nullptr, t2, seg, seg, (size_t)n, rocprim::maximum<int32_t>(), st));
+  PFX_HIP(rocprim::select(nullptr, t3, rocprim::counting_iterator<int32_t>(0), flags, tiles, d_ntiles, (size_t)n,
+                          st));
+  void* tmp = B("tmp").get(std::max(t1, std::max(t2, t3)) + 16);
+  PFX_HIP(hipMemsetAsync(counters, 0, 8 * sizeof(int), st));
+  const unsigned nb = (unsigned)ceil_div(n, 256);
+  {
+    TimeScope ts(ctx, std::string(tag) + "_tiles");
+    if (mask) {
+      k_mask_flags<<<nb, 256, 0, st>>>(G.perm, G.skeys, n, (uint64_t)G.ncells, mask, flags);
+      PFX_HIP(rocprim::select(tmp, t1, rocprim::counting_iterator<int32_t>(0), flags, qpos, d_nq, (size_t)n, st));
+    } else {
+      // every finite point, in cell order: sorted positions [0, cell_start[ncells])
+      k_iota<<<nb, 256, 0, st>>>(qpos, n);
+      PFX_HIP(hipMemcpyAsync(d_nq, G.cell_start + G.ncells, sizeof(int32_t), hipMemcpyDeviceToDevice, st));
+      PFX_HIP(hipMemsetAsync(reinterpret_cast<char*>(d_nq) + 4, 0, 4, st));
+    }
+    k_seg_marks<<<nb, 256, 0, st>>>(qpos, G.skeys, d_nq, seg);
+    PFX_HIP(rocprim::inclusive_scan(tmp, t2, seg, seg, (size_t)n, rocprim::maximum<int32_t>(), st));
+    k_tile_flags<<<nb, 256, 0, st>>>(seg, d_nq, flags, n);
+    PFX_HIP(rocprim::select(tmp, t3, rocprim::counting_iterator<int32_t>(0), flags, tiles, d_ntiles, (size_t)n, st));
+    k_tile_class<<<nb, 256, 0, st>>>(g, qpos, G.skeys, d_nq, tiles, d_ntiles, sparse, dense, single, counters);
+    check_launch("nblist tiles");
+    PFX_HIP(hipMemcpyAsync(counters + 6, counters + 2, sizeof(int), hipMemcpyDeviceToDevice, st));
+  }
+  const size_t lds_q = sizeof(uint32_t) * 4 * kCapQuery;
+  PFX_HIP(hipFuncSetAttribute((const void*)k_nb_query<kCapQuery, kBucketsQuery, false>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_q));
+  DevBuf& lb = B("list");
+  if (!lb.ptr) lb.get(sizeof(uint32_t) * 64 * (size_t)(n + 1));
+  const int isort = sorted ? 1 : 0;
+  for (int attempt = 0; attempt < 2; ++attempt) {
+    ListOut lo{off, cnt, lgs, static_cast<uint32_t*>(lb.ptr), cursor, lb.bytes / sizeof(uint32_t)};
+    PFX_HIP(hipMemsetAsync(cursor, 0, 2 * sizeof(unsigned long long), st));
+    if (attempt) {
+      PFX_HIP(hipMemcpyAsync(counters + 2, counters + 6, sizeof(int), hipMemcpyDeviceToDevice, st));
+      PFX_HIP(hipMemsetAsync(counters + 3, 0, 2 * sizeof(int), st));
+    }
+    int h_cnt[8];
+    {
+      TimeScope ts(ctx, std::string(tag) + "_lists");
+      k_nb_tile<512, 256, kTcapSparse><<<256 * 3 * 4, 256, 0, st>>>(
+          g, qpos, G.skeys, sparse, counters + 0, rr, 256.0f / rr, isort, lo, single, counters + 2);
+      k_nb_tile<1024, 256, kTcapDense><<<256 * 2, 256, 0, st>>>(
+          g, qpos, G.skeys, dense, counters + 1, rr, 256.0f / rr, isort, lo, single, counters + 2);
+      k_nb_query<kCapQuery, kBucketsQuery, false><<<256 * 4, 256, lds_q, st>>>(
+          g, qpos, single, counters + 2, rr, (float)kBucketsQuery / rr, isort, lo, huge, counters + 3,
+          counters + 4, nullptr);
+      check_launch("nblist lists");
+      PFX_HIP(hipMemcpyAsync(h_cnt, counters, sizeof(h_cnt), hipMemcpyDeviceToHost, st));
+      PFX_HIP(hipStreamSynchronize(st));
+      if (h_cnt[3] > 0) {  // very long lists: sort arrays in global scratch
+        uint32_t* scratch = B("scratch").as<uint32_t>((size_t)kHugeBlocks * 4 * kCapHuge);
+        k_nb_query<kCapHuge, kBucketsHuge, true><<<kHugeBlocks, 256, 0, st>>>(
+            g, qpos, huge, counters + 3, rr, (float)kBucketsHuge / rr, isort, lo, nullptr, nullptr, counters + 4,
+            scratch);
+        check_launch("nblist huge lists");
+      }
+    }
+    int64_t h_nq = 0;
+    unsigned long long h_cur[2] = {0, 0};
+    PFX_HIP(hipMemcpyAsync(&h_nq, d_nq, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+    PFX_HIP(hipMemcpyAsync(h_cur, cursor, sizeof(h_cur), hipMemcpyDeviceToHost, st));
+    PFX_HIP(hipMemcpyAsync(h_cnt, counters, sizeof(h_cnt), hipMemcpyDeviceToHost, st));
+    PFX_HIP(hipStreamSynchronize(st));
+    if (h_cnt[4] > 0)
+      throw Error(PFX_ERR_CAPACITY, std::string(tag) + ": a query has " + std::to_string(h_cnt[4]) +
+                                        " neighbours (> " + std::to_string(kCapHuge) + " supported)");
+    if (h_cur[0] > lo.cap) {  // list buffer too small: grow (no copy needed) and rebuild once
+      lb.release();
+      lb.get(sizeof(uint32_t) * (size_t)h_cur[0]);
+      continue;
+    }
+    out.nq = h_nq;
+    out.total = (int64_t)h_cur[1];
+    out.slots = (int64_t)h_cur[0];
+    out.qpos = qpos;
+    out.off = off;
+    out.cnt = cnt;
+    out.lg = lgs;
+    out.list = lo.list;
+    ctx->stats[std::string(tag) + "_tiles_sparse"] = h_cnt[0];
+    ctx->stats[std::string(tag) + "_tiles_dense"] = h_cnt[1];
+    ctx->stats[std::string(tag) + "_single"] = h_cnt[2];
+    ctx->stats[std::string(tag) + "_huge"] = h_cnt[3];
+    return;
+  }
+  throw Error(PFX_ERR_DEVICE, std::string(tag) + ": neighbour-list buffer growth failed");
+}
+
+}  // namespace pfx

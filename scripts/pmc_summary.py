@@ -1,0 +1,43 @@
+#!/usr/bin/env python3
+"""Per-kernel averages of rocprofv3 --pmc passes (scripts/gpu_pmc.sh output directory).
+
+FETCH_SIZE is reported doubled (x2, MI355X_MICROARCH.md: gfx950 tallies 128-B requests at 64 B)."""
+import csv
+import glob
+import sys
+from collections import defaultdict
+
+root = sys.argv[1]
+vals = defaultdict(lambda: defaultdict(list))
+dur = defaultdict(list)
+for f in sorted(glob.glob(f"{root}/p*/**/*counter_collection.csv", recursive=True)):
+    for row in csv.DictReader(open(f)):
+        name = row["Kernel_Name"].replace("pfx::(anonymous namespace)::", "").replace("void ", "")
+        name = name.split("(")[0][:60]
+        vals[name][row["Counter_Name"]].append(float(row["Counter_Value"]))
+        if row["Counter_Name"] in ("SQ_WAVES", "FETCH_SIZE"):
+            dur[name + row["Counter_Name"]].append(int(row["End_Timestamp"]) - int(row["Start_Timestamp"]))
+rows = []
+for k, d in vals.items():
+    avg = {c: sum(v) / len(v) for c, v in d.items()}
+    t = dur.get(k + "SQ_WAVES") or [0]
+    rows.append((sum(t) / len(t) / 1e3, k, avg))
+rows.sort(key=lambda r: -r[0])
+for us, k, a in rows[:20]:
+    print(f"== {k}  ~{us:.1f} us/dispatch (profiled)")
+    if "FETCH_SIZE" in a:
+        a["FETCH_SIZE_x2_MB"] = a.pop("FETCH_SIZE") * 2 / 1024
+    if "WRITE_SIZE" in a:
+        a["WRITE_SIZE_MB"] = a.pop("WRITE_SIZE") / 1024
+    w = a.get("SQ_WAVES", 0) or 1
+    extra = {}
+    for c in ("SQ_INSTS_VALU", "SQ_INSTS_LDS", "SQ_INSTS_VMEM_RD", "SQ_INSTS_SALU"):
+        if c in a:
+            extra[c + "/wave"] = a[c] / w
+    if "SQ_WAVE_CYCLES" in a and a["SQ_WAVE_CYCLES"]:
+        for c in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY"):
+            if c in a:
+                extra[c + "_frac"] = a[c] / a["SQ_WAVE_CYCLES"]
+    if a.get("TCC_HIT_sum", 0) + a.get("TCC_MISS_sum", 0):
+        extra["L2_hit"] = a["TCC_HIT_sum"] / (a["TCC_HIT_sum"] + a["TCC_MISS_sum"])
+    print("   " + "  ".join(f"{c}={v:.4g}" for c, v in sorted({**a, **extra}.items())))

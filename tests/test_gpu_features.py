@@ -90,6 +90,26 @@ def test_normals_edge_cases(ctx):
     assert np.isnan(g[0][:3]).all()
 
 
+def test_normals_every_list_path(ctx):
+    """Densities that route queries through every neighbour-list path (pfx_nblist.hip): sparse
+    and dense tiles, the per-query LDS kernel (k > 1024) and the global-scratch kernel (k > 4096),
+    plus lane-per-query and nine-lanes-per-query chains; duplicates exercise the index tie-break."""
+    rng = np.random.default_rng(23)
+    sparse = np.c_[rng.uniform(0, 1, (4000, 2)), np.full(4000, 1.0)]
+    dense = np.c_[rng.uniform(2, 2.3, (9000, 2)), np.full(9000, 1.0)]          # k ~ 400..800
+    denser = np.c_[rng.uniform(3, 3.1, (9000, 2)), np.full(9000, 1.0)]         # k ~ 1800..7000
+    blob = rng.normal(0, 0.01, (1500, 3)) + [4, 4, 1]                          # k ~ 900..1500
+    huge = np.repeat(rng.normal(0, 0.004, (1700, 3)) + [6, 6, 1], 3, axis=0)  # k = 5100, ties
+    pts = np.concatenate([sparse, dense, denser, blob, huge]).astype(np.float32)
+    x, y, z = pts[:, 0].copy(), pts[:, 1].copy(), pts[:, 2].copy()
+    g = ctx.normals(x, y, z, 0.05)
+    for nm in ["normals_tiles_sparse", "normals_tiles_dense", "normals_single", "normals_huge"]:
+        assert ctx.stat(nm) > 0, nm
+    o = O.normals(x, y, z, 0.05)
+    for a, b in zip(g, o):
+        assert _nan_aware_equal(a, b)
+
+
 def test_normals_empty_and_tiny(ctx):
     e = np.zeros(0, np.float32)
     g = ctx.normals(e, e, e, 0.05)
