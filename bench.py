@@ -115,7 +115,7 @@ def main():
     if os.environ.get("PFX_BENCH_VERBOSE"):
         names = ["grid_bbox", "grid_build", "normals", "normals_tiles", "normals_lists", "normals_chain",
                  "range_image", "narf_border", "narf_interest", "narf_nms", "narf_gather", "fpfh_mark",
-                 "fpfh_spfh", "fpfh_weight", "fpfh_weight_big"]
+                 "fpfh_spfh", "fpfh_weight"]
         rep = {nm: round(ctx.kernel_time(nm)[0] / args.steps, 3) for nm in names}
         print("per-step kernel ms:", json.dumps(rep), file=sys.stderr, flush=True)
         stats = {}

@@ -10,7 +10,8 @@
 //   FPFH(q)  = sum over N(q) in FLANN order, skipping d2 == 0, of SPFH(nbr) / d2 (float per bin,
 //              double per 11-bin block), then each block scaled to 100      k_fpfh_weight
 // SPFH rows are stored by caller index (n_surface x 33 floats, row-major) -- only rows in S
-// are written/read.
+// are written/read.  Neighbour normals are read from a cell-ordered float4 copy (runs of the
+// grid are contiguous), positions/coordinates from the grid's packed copy.
 #include <cstring>
 #include <rocprim/rocprim.hpp>
 
@@ -21,8 +22,8 @@ namespace {
 
 constexpr int kBins = 11;
 constexpr int kDesc = 33;
-constexpr int kCapW = 2048;     // sorted-neighbour capacity of the weighting kernel (LDS)
-constexpr int kCapWBig = 16384; // overflow weighting kernel
+constexpr int kCapW = 16384;  // sorted-neighbour capacity of the weighting kernel (LDS)
+constexpr int kChunkW = 128;  // SPFH rows staged per chunk in the weighting kernel
 
 // PCL 1.7 `acos (fabs (a1)) > acos (fabs (a2))` (double acos, correctly rounded by glibc):
 // acos is strictly decreasing and distinct floats >= 2^-26 map to distinct rounded values, so
@@ -34,14 +35,44 @@ __device__ __forceinline__ bool acos_greater(float a1, float a2) {
   return (H + (L - (double)x1)) > (H + (L - (double)x2));
 }
 
-// pcl::computePairFeatures (features/src/pfh.cpp), Vector4f maps with w = 0
-__device__ __forceinline__ void pair_features(f3 p1, f3 n1, f3 p2, f3 n2, float& f1, float& f2, float& f3o) {
+__device__ __forceinline__ int bin_of(double v) {
+  if (!(v == v)) return 0;  // static_cast<int>(NaN) == INT_MIN on x86 -> clamped to 0
+  double f = floor(v);
+  int h = (f >= 2147483647.0 || f < -2147483648.0) ? (int)0x80000000 : (int)f;
+  return h < 0 ? 0 : (h >= kBins ? kBins - 1 : h);
+}
+
+__device__ __forceinline__ double f1_scaled(double f1) {
+  const float d_pi = 1.0f / (2.0f * 3.14159265358979323846f);
+  return (double)kBins * ((f1 + 3.14159265358979323846) * (double)d_pi);
+}
+
+// bin of f1 = atan2 correctly rounded to float (PCL: atan2f == (float)atan2 in glibc's
+// double-evaluated form).  The float atan2 is within a few ulp (< 1e-5 rad) of it,
+// and the bin map is monotone, so when both ends of that interval fall in one bin the bin is
+// exact; otherwise (a bin edge within 1e-5 rad) the correctly rounded value is computed.
+__device__ __attribute__((noinline)) int bin_f1_exact(float y, float x) {
+  return bin_of(f1_scaled((double)atan2f_cr(y, x)));
+}
+
+__device__ __forceinline__ int bin_f1(float y, float x) {
+  const float f = atan2f(y, x);
+  if (!(f == f)) return 0;  // NaN argument: the exact value is NaN too
+  const int lo = bin_of(f1_scaled((double)f - 1e-5)), hi = bin_of(f1_scaled((double)f + 1e-5));
+  return lo == hi ? lo : bin_f1_exact(y, x);
+}
+
+// pcl::computePairFeatures (features/src/pfh.cpp) + the three bin indices of
+// computePointSPFHSignature; Vector4f maps with w = 0.  Degenerate pairs give f = 0.
+__device__ __forceinline__ void pair_bins(f3 p1, f3 n1, f3 p2, f3 n2, int& h1, int& h2, int& h3) {
   f3 dp = sub3(p2, p1);
-  float f4 = sqrtf(sqn4(dp));
-  if (f4 == 0.0f) { f1 = f2 = f3o = 0.0f; return; }
+  const float f4 = sqrtf(sqn4(dp));
+  const int b_zero_f1 = bin_of(f1_scaled(0.0)), b_zero = bin_of((double)kBins * ((0.0 + 1.0) * 0.5));
+  if (f4 == 0.0f) { h1 = b_zero_f1; h2 = h3 = b_zero; return; }
   f3 n1c = n1, n2c = n2;
-  float angle1 = dot4(n1c, dp) / f4;
-  float angle2 = dot4(n2c, dp) / f4;
+  const float angle1 = dot4(n1c, dp) / f4;
+  const float angle2 = dot4(n2c, dp) / f4;
+  float f3o;
   if (acos_greater(angle1, angle2)) {
     n1c = n2; n2c = n1;
     dp = scale3(dp, -1.0f);
@@ -50,161 +81,222 @@ __device__ __forceinline__ void pair_features(f3 p1, f3 n1, f3 p2, f3 n2, float&
     f3o = angle1;
   }
   f3 v = cross3(dp, n1c);
-  float v_norm = sqrtf(sqn4(v));
-  if (v_norm == 0.0f) { f1 = f2 = f3o = 0.0f; return; }
+  const float v_norm = sqrtf(sqn4(v));
+  if (v_norm == 0.0f) { h1 = b_zero_f1; h2 = h3 = b_zero; return; }
   v = div3(v, v_norm);
-  f3 w = cross3(n1c, v);
-  f2 = dot4(v, n2c);
-  f1 = atan2f_cr(dot4(w, n2c), dot4(n1c, n2c));
+  const f3 w = cross3(n1c, v);
+  const float f2 = dot4(v, n2c);
+  h1 = bin_f1(dot4(w, n2c), dot4(n1c, n2c));
+  h2 = bin_of((double)kBins * (((double)f2 + 1.0) * 0.5));
+  h3 = bin_of((double)kBins * (((double)f3o + 1.0) * 0.5));
 }
 
-__device__ __forceinline__ int bin_of(double v) {
-  if (!(v == v)) return 0;  // static_cast<int>(NaN) == INT_MIN on x86 -> clamped to 0
-  double f = floor(v);
-  int h = (f >= 2147483647.0 || f < -2147483648.0) ? (int)0x80000000 : (int)f;
-  return h < 0 ? 0 : (h >= kBins ? kBins - 1 : h);
+__global__ void k_sorted_normals(const int32_t* __restrict__ perm, int64_t n, const float* __restrict__ nx,
+                                 const float* __restrict__ ny, const float* __restrict__ nz,
+                                 float4* __restrict__ out) {
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int32_t p = perm[i];
+  out[i] = make_float4(nx[p], ny[p], nz[p], 0.0f);
 }
 
+// S membership by sorted position
 __global__ void __launch_bounds__(256) k_fpfh_mark(GridView g, const float* __restrict__ qx,
                                                    const float* __restrict__ qy, const float* __restrict__ qz,
                                                    int64_t nq, float rr, uint8_t* __restrict__ flags) {
   for (int64_t q = blockIdx.x; q < nq; q += gridDim.x) {
     Runs R;
-    float x = qx[q], y = qy[q], z = qz[q];
+    const float x = qx[q], y = qy[q], z = qz[q];
     query_runs(g, x, y, z, R);
     for (int32_t t = threadIdx.x; t < R.pref[9]; t += blockDim.x) {
-      int32_t p = run_pos(R, t);
-      if (flann_d2(x, y, z, g.sx[p], g.sy[p], g.sz[p]) < rr) flags[g.perm[p]] = 1;
+      const int32_t p = run_pos(R, t);
+      const float4 c = g.sp[p];
+      if (flann_d2(x, y, z, c.x, c.y, c.z) < rr) flags[p] = 1;
     }
   }
 }
 
-// one 64-thread block per S point
-__global__ void __launch_bounds__(64) k_fpfh_spfh(GridView g, const float* __restrict__ nxs,
-                                                  const float* __restrict__ nys, const float* __restrict__ nzs,
-                                                  const int32_t* __restrict__ list, int64_t count, float rr,
-                                                  float* __restrict__ spfh) {
-  __shared__ int hist[kDesc];
-  const int lane = threadIdx.x;
-  const float d_pi = 1.0f / (2.0f * 3.14159265358979323846f);
-  const int64_t vb = xcd_block(blockIdx.x, gridDim.x);
-  for (int64_t w = vb; w < count; w += gridDim.x) {
-    const int32_t p = list ? list[w] : (int32_t)w;
-    if (lane < kDesc) hist[lane] = 0;
-    __syncthreads();
-    const f3 pp = mk3(g.ux[p], g.uy[p], g.uz[p]);
-    const f3 pn = mk3(nxs[p], nys[p], nzs[p]);
+__global__ void k_all_finite(const uint32_t* __restrict__ skeys, int64_t n, uint64_t ncells,
+                             uint8_t* __restrict__ flags) {
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (i < n) flags[i] = (uint64_t)skeys[i] < ncells;
+}
+
+// One wave per S point (sorted position): candidates tested in runs, hits other than the point
+// itself compacted into a wave-private LDS queue and evaluated 64 pairs at a time.
+__global__ void __launch_bounds__(256) k_fpfh_spfh(GridView g, const float4* __restrict__ snp,
+                                                   const int32_t* __restrict__ slist,
+                                                   const int64_t* __restrict__ count_ptr, float rr,
+                                                   float* __restrict__ spfh) {
+  __shared__ uint32_t queue[4][128];
+  __shared__ int hist[4][kDesc];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t count = *count_ptr;
+  const int64_t stride = (int64_t)gridDim.x * 4;
+  for (int64_t w = xcd_block(blockIdx.x, gridDim.x) * 4 + wv; w < count; w += stride) {
+    const int32_t s = slist[w];
+    const float4 pc = g.sp[s], pnc = snp[s];
+    const f3 pp = mk3(pc.x, pc.y, pc.z), pn = mk3(pnc.x, pnc.y, pnc.z);
+    if (lane < kDesc) hist[wv][lane] = 0;
     Runs R;
-    query_runs(g, pp.x, pp.y, pp.z, R);
-    int my_k = 0;
-    for (int32_t t = lane; t < R.pref[9]; t += 64) {
-      int32_t s = run_pos(R, t);
-      float d2 = flann_d2(pp.x, pp.y, pp.z, g.sx[s], g.sy[s], g.sz[s]);
-      if (!(d2 < rr)) continue;
-      ++my_k;
-      int32_t q = g.perm[s];
-      if (q == p) continue;
-      float f1, f2, f3v;
-      pair_features(pp, pn, mk3(g.sx[s], g.sy[s], g.sz[s]), mk3(nxs[q], nys[q], nzs[q]), f1, f2, f3v);
-      int h1 = bin_of((double)kBins * (((double)f1 + 3.14159265358979323846) * (double)d_pi));
-      int h2 = bin_of((double)kBins * (((double)f2 + 1.0) * 0.5));
-      int h3 = bin_of((double)kBins * (((double)f3v + 1.0) * 0.5));
-      atomicAdd(&hist[h1], 1);
-      atomicAdd(&hist[kBins + h2], 1);
-      atomicAdd(&hist[2 * kBins + h3], 1);
-    }
-    // wave reduction of the neighbour count
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) my_k += __shfl_xor(my_k, off);
-    __syncthreads();
-    if (lane < kDesc) {
-      const int c = hist[lane];
-      const float incr = 100.0f / (float)(my_k - 1);
-      float v = 0.0f;
-      for (int j = 0; j < c; ++j) v = v + incr;
-      spfh[(int64_t)p * kDesc + lane] = v;
-    }
-    __syncthreads();
-  }
-}
-
-// weighting: one block per query (64 threads: lanes 0..32 own a bin, 33..35 the block sums)
-template <int CAP>
-__device__ __forceinline__ void weight_one(const uint64_t* keys, int k, const float* __restrict__ spfh,
-                                           float* __restrict__ out_row) {
-  const int lane = threadIdx.x;
-  float fh = 0.0f;
-  double sum = 0.0;
-  if (lane < kDesc) {
-    for (int j = 0; j < k; ++j) {
-      uint64_t key = keys[j];
-      float d2 = key_d2(key);
-      if (d2 == 0.0f) continue;
-      float w = 1.0f / d2;
-      float val = spfh[(int64_t)key_idx(key) * kDesc + lane] * w;
-      fh = fh + val;
-    }
-  } else if (lane < kDesc + 3) {
-    const int blk = lane - kDesc;
-    for (int j = 0; j < k; ++j) {
-      uint64_t key = keys[j];
-      float d2 = key_d2(key);
-      if (d2 == 0.0f) continue;
-      float w = 1.0f / d2;
-      const float* row = spfh + (int64_t)key_idx(key) * kDesc + blk * kBins;
-#pragma unroll
-      for (int b = 0; b < kBins; ++b) {
-        float val = row[b] * w;
-        sum = sum + (double)val;
+    query_runs(g, pc.x, pc.y, pc.z, R);
+    int k = 0, qn = 0;
+    auto process = [&](int nvalid) {
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      if (lane < nvalid) {
+        const uint32_t q = queue[wv][lane];
+        const float4 qc = g.sp[q], qnv = snp[q];
+        int h1, h2, h3;
+        pair_bins(pp, pn, mk3(qc.x, qc.y, qc.z), mk3(qnv.x, qnv.y, qnv.z), h1, h2, h3);
+        atomicAdd(&hist[wv][h1], 1);
+        atomicAdd(&hist[wv][kBins + h2], 1);
+        atomicAdd(&hist[wv][2 * kBins + h3], 1);
+      }
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+    };
+    for (int32_t t0 = 0; t0 < R.pref[9]; t0 += 64) {
+      const int32_t t = t0 + lane;
+      bool hit = false;
+      int32_t pos = 0;
+      if (t < R.pref[9]) {
+        pos = run_pos(R, t);
+        const float4 c = g.sp[pos];
+        hit = flann_d2(pc.x, pc.y, pc.z, c.x, c.y, c.z) < rr;
+      }
+      k += __popcll(__ballot(hit));
+      const bool push = hit && pos != s;
+      const uint64_t m = __ballot(push);
+      if (push) queue[wv][qn + __popcll(m & lanemask_lt())] = (uint32_t)pos;
+      qn += __popcll(m);
+      if (qn >= 64) {
+        process(64);
+        const uint32_t rest = (lane + 64 < qn) ? queue[wv][lane + 64] : 0u;
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        if (lane + 64 < qn) queue[wv][lane] = rest;
+        qn -= 64;
       }
     }
-    if (sum != 0.0) sum = 100.0 / sum;
-  }
-  double s0 = __shfl(sum, kDesc + 0), s1 = __shfl(sum, kDesc + 1), s2 = __shfl(sum, kDesc + 2);
-  if (lane < kDesc) {
-    double s = lane < kBins ? s0 : (lane < 2 * kBins ? s1 : s2);
-    out_row[lane] = fh * (float)s;
+    process(qn);
+    if (lane < kDesc) {
+      const int c = hist[wv][lane];
+      const float incr = 100.0f / (float)(k - 1);
+      float v = 0.0f;
+      for (int j = 0; j < c; ++j) v = v + incr;
+      spfh[(int64_t)g.perm[s] * kDesc + lane] = v;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
   }
 }
 
-__global__ void __launch_bounds__(64) k_fpfh_weight(GridView g, const float* __restrict__ qx,
-                                                    const float* __restrict__ qy, const float* __restrict__ qz,
-                                                    int64_t nq, float rr, const float* __restrict__ spfh,
-                                                    float* __restrict__ out, int32_t* __restrict__ overflow,
-                                                    int* __restrict__ n_overflow) {
-  __shared__ uint64_t keys[kCapW];
+// exponent of the least significant set bit of a finite nonzero float; 1000 for non-finite
+__device__ __forceinline__ int lsb_exp(float v) {
+  const uint32_t b = __float_as_uint(v);
+  const int e = (int)((b >> 23) & 0xff);
+  if (e == 255) return 1000;
+  const uint32_t m = (b & 0x7fffffu) | (e ? 0x800000u : 0u);
+  return (e ? e : 1) - 150 + __builtin_ctz(m);
+}
+
+// Weighting: one 256-thread workgroup per query.  The 33 float chains (strict FLANN order)
+// run one per lane over SPFH rows staged in LDS.  The three double block sums are formed in
+// parallel: every value is a non-negative float, so when all of them are multiples of 2^L and
+// the total is below 2^(L+52) every partial sum -- of the sequential loop or of any other order
+// -- is exact and the parallel sum is bit-identical to PCL's loop; otherwise the block sum is
+// recomputed sequentially.
+__global__ void __launch_bounds__(256) k_fpfh_weight(GridView g, const float* __restrict__ qx,
+                                                     const float* __restrict__ qy, const float* __restrict__ qz,
+                                                     int64_t nq, float rr, const float* __restrict__ spfh,
+                                                     float* __restrict__ out, int* __restrict__ err) {
+  extern __shared__ __attribute__((aligned(16))) uint64_t keys[];  // kCapW
+  __shared__ float rows[kChunkW][kDesc + 1];
+  __shared__ float wts[kChunkW];
+  __shared__ double red_s[3][256];
+  __shared__ int red_l[3][256];
   __shared__ int s_count;
-  const int64_t vb = xcd_block(blockIdx.x, gridDim.x);
-  for (int64_t q = vb; q < nq; q += gridDim.x) {
-    int k = sorted_neighbors(g, qx[q], qy[q], qz[q], rr, keys, kCapW, &s_count);
+  __shared__ double s_sum[3];
+  const int tid = threadIdx.x;
+  for (int64_t q = blockIdx.x; q < nq; q += gridDim.x) {
+    const int k = sorted_neighbors(g, qx[q], qy[q], qz[q], rr, keys, kCapW, &s_count);
     if (k > kCapW) {
-      if (threadIdx.x == 0) overflow[atomicAdd(n_overflow, 1)] = (int32_t)q;
+      if (tid == 0) atomicMax(err, k);
       continue;
     }
     if (k == 0) {
-      if (threadIdx.x < kDesc) out[q * kDesc + threadIdx.x] = __builtin_nanf("");
-    } else {
-      weight_one<kCapW>(keys, k, spfh, out + q * kDesc);
-    }
-    __syncthreads();
-  }
-}
-
-__global__ void __launch_bounds__(64) k_fpfh_weight_big(GridView g, const float* __restrict__ qx,
-                                                        const float* __restrict__ qy, const float* __restrict__ qz,
-                                                        const int32_t* __restrict__ list, int count, float rr,
-                                                        const float* __restrict__ spfh, float* __restrict__ out,
-                                                        int* __restrict__ err) {
-  extern __shared__ __attribute__((aligned(16))) uint64_t keys_big[];
-  __shared__ int s_count;
-  for (int w = blockIdx.x; w < count; w += gridDim.x) {
-    const int64_t q = list[w];
-    int k = sorted_neighbors(g, qx[q], qy[q], qz[q], rr, keys_big, kCapWBig, &s_count);
-    if (k > kCapWBig) {
-      if (threadIdx.x == 0) atomicMax(err, k);
+      if (tid < kDesc) out[q * kDesc + tid] = __builtin_nanf("");
+      __syncthreads();
       continue;
     }
-    weight_one<kCapWBig>(keys_big, k, spfh, out + q * kDesc);
+    float fh = 0.0f;
+    double ps0 = 0.0, ps1 = 0.0, ps2 = 0.0;
+    int pl0 = 1 << 20, pl1 = 1 << 20, pl2 = 1 << 20;
+    for (int c0 = 0; c0 < k; c0 += kChunkW) {
+      const int m = min(kChunkW, k - c0);
+      for (int e = tid; e < m * kDesc; e += 256) {
+        const int j = e / kDesc, b = e - j * kDesc;
+        rows[j][b] = spfh[(int64_t)key_idx(keys[c0 + j]) * kDesc + b];
+      }
+      if (tid < m) {
+        const float d2 = key_d2(keys[c0 + tid]);
+        wts[tid] = d2 == 0.0f ? 0.0f : 1.0f / d2;  // 0 marks a skipped neighbour (d2 == 0)
+      }
+      __syncthreads();
+      if (tid < kDesc) {
+        for (int j = 0; j < m; ++j) {
+          const float w = wts[j];
+          if (w != 0.0f) fh = fh + rows[j][tid] * w;
+        }
+      }
+      for (int e = tid; e < m * kDesc; e += 256) {
+        const int j = e / kDesc, b = e - j * kDesc;
+        const float w = wts[j];
+        if (w == 0.0f) continue;
+        const float v = rows[j][b] * w;
+        if (v != 0.0f) {
+          const int l = lsb_exp(v);
+          if (b < kBins) { ps0 += (double)v; pl0 = min(pl0, l); }
+          else if (b < 2 * kBins) { ps1 += (double)v; pl1 = min(pl1, l); }
+          else { ps2 += (double)v; pl2 = min(pl2, l); }
+        }
+      }
+      __syncthreads();
+    }
+    red_s[0][tid] = ps0; red_s[1][tid] = ps1; red_s[2][tid] = ps2;
+    red_l[0][tid] = pl0; red_l[1][tid] = pl1; red_l[2][tid] = pl2;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+      if (tid < o) {
+#pragma unroll
+        for (int blk = 0; blk < 3; ++blk) {
+          red_s[blk][tid] += red_s[blk][tid + o];
+          red_l[blk][tid] = min(red_l[blk][tid], red_l[blk][tid + o]);
+        }
+      }
+      __syncthreads();
+    }
+    if (tid < 3) {
+      const int blk = tid;
+      double sum = red_s[blk][0];
+      const int L = red_l[blk][0];
+      const bool exact = sum == 0.0 || (L < 1000 && sum < ldexp(1.0, L + 52));
+      if (!exact) {  // PCL's sequential double loop
+        sum = 0.0;
+        for (int j = 0; j < k; ++j) {
+          const float d2 = key_d2(keys[j]);
+          if (d2 == 0.0f) continue;
+          const float w = 1.0f / d2;
+          const float* row = spfh + (int64_t)key_idx(keys[j]) * kDesc + blk * kBins;
+          for (int b = 0; b < kBins; ++b) sum = sum + (double)(row[b] * w);
+        }
+      }
+      if (sum != 0.0) sum = 100.0 / sum;
+      s_sum[blk] = sum;
+    }
+    __syncthreads();
+    if (tid < kDesc) out[q * kDesc + tid] = fh * (float)s_sum[tid / kBins];
     __syncthreads();
   }
 }
@@ -225,64 +317,59 @@ void fpfh_dev(pfx_ctx* ctx, const float* sx, const float* sy, const float* sz, c
     return;
   }
   build_grid(ctx, ctx->grid_b, sx, sy, sz, ns, r);
-  GridView g = view(ctx->grid_b);
+  const Grid& G = ctx->grid_b;
+  GridView g = view(G);
   const float rr = (float)(r * r);
   float* spfh = ctx->buf("fpfh_spfh").as<float>(ns * kDesc);
-  int32_t* list = nullptr;
-  int64_t count = ns;
-  if (!same) {
-    uint8_t* flags = ctx->buf("fpfh_flags").as<uint8_t>(ns);
-    list = ctx->buf("fpfh_list").as<int32_t>(ns);
-    int64_t* d_sel = ctx->buf("fpfh_nsel").as<int64_t>(1);
-    size_t tmp_bytes = 0;
-    PFX_HIP(rocprim::select(nullptr, tmp_bytes, rocprim::counting_iterator<int32_t>(0), flags, list, d_sel,
-                            (size_t)ns, st));
-    void* tmp = ctx->buf("fpfh_tmp").get(tmp_bytes + 16);
-    PFX_HIP(hipMemsetAsync(flags, 0, ns, st));
-    {
-      TimeScope ts(ctx, "fpfh_mark");
+  float4* snp = ctx->buf("fpfh_snp").as<float4>(ns);
+  uint8_t* flags = ctx->buf("fpfh_flags").as<uint8_t>(ns);
+  int32_t* slist = ctx->buf("fpfh_list").as<int32_t>(ns);
+  int64_t* d_sel = ctx->buf("fpfh_nsel").as<int64_t>(1);
+  size_t tmp_bytes = 0;
+  PFX_HIP(rocprim::select(nullptr, tmp_bytes, rocprim::counting_iterator<int32_t>(0), flags, slist, d_sel,
+                          (size_t)ns, st));
+  void* tmp = ctx->buf("fpfh_tmp").get(tmp_bytes + 16);
+  const unsigned nb = (unsigned)ceil_div(ns, 256);
+  {
+    TimeScope ts(ctx, "fpfh_mark");
+    k_sorted_normals<<<nb, 256, 0, st>>>(G.perm, ns, snx, sny, snz, snp);
+    if (same) {
+      k_all_finite<<<nb, 256, 0, st>>>(G.skeys, ns, (uint64_t)G.ncells, flags);
+    } else {
+      PFX_HIP(hipMemsetAsync(flags, 0, ns, st));
       k_fpfh_mark<<<(unsigned)std::min<int64_t>(nq, 8192), 256, 0, st>>>(g, qx, qy, qz, nq, rr, flags);
-      check_launch("k_fpfh_mark");
     }
-    PFX_HIP(rocprim::select(tmp, tmp_bytes, rocprim::counting_iterator<int32_t>(0), flags, list, d_sel,
+    check_launch("k_fpfh_mark");
+    PFX_HIP(rocprim::select(tmp, tmp_bytes, rocprim::counting_iterator<int32_t>(0), flags, slist, d_sel,
                             (size_t)ns, st));
-    PFX_HIP(hipMemcpyAsync(&count, d_sel, sizeof(int64_t), hipMemcpyDeviceToHost, st));
-    PFX_HIP(hipStreamSynchronize(st));
   }
-  ctx->stats["fpfh_spfh_points"] = count;
-  if (count > 0) {
+  {
+    // the S count stays on the device: a grid-stride launch sized for the worst case
     TimeScope ts(ctx, "fpfh_spfh");
-    int blocks = (int)std::min<int64_t>(count, 256 * 16);
-    blocks = std::max(8, blocks & ~7);
-    k_fpfh_spfh<<<blocks, 64, 0, st>>>(g, snx, sny, snz, list, count, rr, spfh);
+    const int64_t waves = std::min<int64_t>(ns, 256 * 4 * 8);
+    k_fpfh_spfh<<<(unsigned)std::max<int64_t>(8, ceil_div(waves, 4) & ~7), 256, 0, st>>>(g, snp, slist, d_sel, rr,
+                                                                                          spfh);
     check_launch("k_fpfh_spfh");
   }
-  int* counters = ctx->buf("fpfh_counters").as<int>(4);
-  int32_t* overflow = ctx->buf("fpfh_overflow").as<int32_t>(nq);
-  PFX_HIP(hipMemsetAsync(counters, 0, 4 * sizeof(int), st));
+  int* err = ctx->buf("fpfh_err").as<int>(1);
+  PFX_HIP(hipMemsetAsync(err, 0, sizeof(int), st));
   {
     TimeScope ts(ctx, "fpfh_weight");
-    int blocks = (int)std::min<int64_t>(nq, 256 * 12);
-    blocks = std::max(8, blocks & ~7);
-    k_fpfh_weight<<<blocks, 64, 0, st>>>(g, qx, qy, qz, nq, rr, spfh, out, overflow, counters);
+    const size_t lds = sizeof(uint64_t) * kCapW;
+    PFX_HIP(hipFuncSetAttribute((const void*)k_fpfh_weight, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    const unsigned blocks = (unsigned)std::min<int64_t>(nq, 256 * 8);
+    k_fpfh_weight<<<blocks, 256, lds, st>>>(g, qx, qy, qz, nq, rr, spfh, out, err);
     check_launch("k_fpfh_weight");
   }
-  int h[4];
-  PFX_HIP(hipMemcpyAsync(h, counters, sizeof(h), hipMemcpyDeviceToHost, st));
+  int h[2] = {0, 0};
+  int64_t count = 0;
+  PFX_HIP(hipMemcpyAsync(h, err, sizeof(int), hipMemcpyDeviceToHost, st));
+  PFX_HIP(hipMemcpyAsync(&count, d_sel, sizeof(int64_t), hipMemcpyDeviceToHost, st));
   PFX_HIP(hipStreamSynchronize(st));
-  if (h[0] > 0) {
-    size_t lds = sizeof(uint64_t) * kCapWBig;
-    PFX_HIP(hipFuncSetAttribute((const void*)k_fpfh_weight_big, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    TimeScope ts(ctx, "fpfh_weight_big");
-    k_fpfh_weight_big<<<std::min(h[0], 2048), 64, lds, st>>>(g, qx, qy, qz, overflow, h[0], rr, spfh, out,
-                                                              counters + 1);
-    check_launch("k_fpfh_weight_big");
-    PFX_HIP(hipMemcpyAsync(h, counters, sizeof(h), hipMemcpyDeviceToHost, st));
-    PFX_HIP(hipStreamSynchronize(st));
-    if (h[1] > 0)
-      throw Error(PFX_ERR_CAPACITY, "fpfh: a query has " + std::to_string(h[1]) + " neighbours (> " +
-                                        std::to_string(kCapWBig) + " supported)");
-  }
+  ctx->stats["fpfh_spfh_points"] = count;
+  if (h[0] > 0)
+    throw Error(PFX_ERR_CAPACITY, "fpfh: a query has " + std::to_string(h[0]) + " neighbours (> " +
+                                      std::to_string(kCapW) + " supported)");
 }
 
 }  // namespace pfx
