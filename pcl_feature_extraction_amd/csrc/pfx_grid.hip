@@ -4,7 +4,7 @@
 // Layout in HBM (all SoA, 4-byte elements):
 //   sx/sy/sz[n]     point coordinates sorted by linear cell key  (coalesced run reads)
 //   perm[n]         sorted position -> caller point index         (FLANN tie-break key)
-//   cell_start[C+1] exclusive prefix of per-cell counts, C = nx*ny*nz <= 2^26
+//   cell_start[C+2] first sorted position of each cell (cells in key order), C = nx*ny*nz <= 2^26
 // Cells are >= r (r*(1+1e-6)), so the radius ball of a query lies in its 3x3x3 cell block;
 // with row-major keys (x, y, z) the block is 9 contiguous runs of 3 z-cells.
 // Non-finite points get key C and sort behind every cell (never a neighbour, as PCL's
@@ -71,8 +71,7 @@ __global__ void __launch_bounds__(256) k_cell_keys(const float* __restrict__ x, 
                                                    const float* __restrict__ z, int64_t n, double inv,
                                                    double ox, double oy, double oz, int32_t nx, int32_t ny,
                                                    int32_t nz, uint32_t* __restrict__ keys,
-                                                   uint32_t* __restrict__ vals,
-                                                   uint32_t* __restrict__ counts) {
+                                                   uint32_t* __restrict__ vals) {
   int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   if (i >= n) return;
   float px = x[i], py = y[i], pz = z[i];
@@ -88,7 +87,15 @@ __global__ void __launch_bounds__(256) k_cell_keys(const float* __restrict__ x, 
   }
   keys[i] = key;
   vals[i] = (uint32_t)i;
-  atomicAdd(&counts[key], 1u);
+}
+
+// first sorted position of every occupied cell (cells are then completed by a suffix minimum)
+__global__ void __launch_bounds__(256) k_mark_starts(const uint32_t* __restrict__ skeys, int64_t n,
+                                                     int32_t* __restrict__ cell_start) {
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t k = skeys[i];
+  if (i == 0 || skeys[i - 1] != k) cell_start[k] = (int32_t)i;
 }
 
 __global__ void __launch_bounds__(256) k_gather_sorted(const float* __restrict__ x, const float* __restrict__ y,
@@ -120,7 +127,7 @@ void build_grid(pfx_ctx* ctx, Grid& g, const float* d_x, const float* d_y, const
   PFX_HIP(hipMemcpyAsync(mm, init, sizeof(init), hipMemcpyHostToDevice, st));
   if (n > 0) {
     TimeScope ts(ctx, "grid_bbox");
-    int blocks = (int)std::min<int64_t>(ceil_div(n, 256), 2048);
+    int blocks = (int)std::min<int64_t>(ceil_div(n, 256), 256);  // few blocks: few atomics
     k_bbox<<<blocks, 256, 0, st>>>(d_x, d_y, d_z, n, mm);
     check_launch("k_bbox");
   }
@@ -156,11 +163,11 @@ void build_grid(pfx_ctx* ctx, Grid& g, const float* d_x, const float* d_y, const
   PFX_HIP(rocprim::radix_sort_pairs(nullptr, sort_bytes, (uint32_t*)nullptr, (uint32_t*)nullptr,
                                     (uint32_t*)nullptr, (uint32_t*)nullptr, (size_t)std::max<int64_t>(n, 1),
                                     0, bits, st));
-  PFX_HIP(rocprim::exclusive_scan(nullptr, scan_bytes, (uint32_t*)nullptr, (uint32_t*)nullptr, 0u,
-                                  (size_t)(C + 2), rocprim::plus<uint32_t>(), st));
+  auto rev = rocprim::make_reverse_iterator(static_cast<int32_t*>(nullptr));
+  PFX_HIP(rocprim::inclusive_scan(nullptr, scan_bytes, rev, rev, (size_t)(C + 1), rocprim::minimum<int32_t>(), st));
   void* tmp = g.b_tmp.get(std::max(sort_bytes, scan_bytes) + 16);
   uint32_t* keys = g.b_keys.as<uint32_t>(n + 1);
-  uint32_t* keys2 = g.b_keys2.as<uint32_t>(std::max<int64_t>(n + 1, C + 2));
+  uint32_t* keys2 = g.b_keys2.as<uint32_t>(n + 1);
   uint32_t* vals = g.b_vals.as<uint32_t>(n + 1);
   g.perm = g.b_perm.as<int32_t>(n + 1);
   g.skeys = keys2;  // radix-sort output: cell key per sorted position
@@ -171,20 +178,20 @@ void build_grid(pfx_ctx* ctx, Grid& g, const float* d_x, const float* d_y, const
   g.cell_start = g.b_start.as<int32_t>(C + 2);
   g.dinv = inv;
   g.dox = lo[0]; g.doy = lo[1]; g.doz = lo[2];
-  uint32_t* counts = keys2;  // per-cell histogram (keys2 is free until the sort)
   {
     TimeScope ts(ctx, "grid_build");
-    PFX_HIP(hipMemsetAsync(counts, 0, sizeof(uint32_t) * (C + 2), st));
+    // cell_start[c] = first sorted position with key >= c: mark the first position of every
+    // occupied cell, then a suffix minimum fills the empty cells (no per-point atomics)
+    PFX_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(g.cell_start), (int)n, (size_t)(C + 2), st));
     if (n > 0) {
       k_cell_keys<<<(unsigned)ceil_div(n, 256), 256, 0, st>>>(d_x, d_y, d_z, n, inv, lo[0], lo[1], lo[2],
-                                                              g.nx, g.ny, g.nz, keys, vals, counts);
+                                                              g.nx, g.ny, g.nz, keys, vals);
       check_launch("k_cell_keys");
-    }
-    PFX_HIP(rocprim::exclusive_scan(tmp, scan_bytes, counts, reinterpret_cast<uint32_t*>(g.cell_start),
-                                    0u, (size_t)(C + 2), rocprim::plus<uint32_t>(), st));
-    if (n > 0) {
       PFX_HIP(rocprim::radix_sort_pairs(tmp, sort_bytes, keys, keys2, vals,
                                         reinterpret_cast<uint32_t*>(g.perm), (size_t)n, 0, bits, st));
+      k_mark_starts<<<(unsigned)ceil_div(n, 256), 256, 0, st>>>(keys2, n, g.cell_start);
+      auto r = rocprim::make_reverse_iterator(g.cell_start + C + 1);
+      PFX_HIP(rocprim::inclusive_scan(tmp, scan_bytes, r, r, (size_t)(C + 1), rocprim::minimum<int32_t>(), st));
       k_gather_sorted<<<(unsigned)ceil_div(n, 256), 256, 0, st>>>(
           d_x, d_y, d_z, n, reinterpret_cast<uint32_t*>(g.perm), g.sx, g.sy, g.sz, g.sp);
       check_launch("k_gather_sorted");

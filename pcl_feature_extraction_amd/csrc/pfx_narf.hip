@@ -34,13 +34,13 @@ enum {
 struct NarfState {
   int w = 0, h = 0;
   DevBuf direct, fill, pts, surf, svalid, sL, sR, sT, sB, uL, uR, uT, uB, shadow, traits, rawdir, dir, scs, scd,
-      interest, cand, counters;
+      interest, cand, counters, sat;
   std::vector<float> h_interest, h_scs, h_range;
   std::vector<uint32_t> h_traits;
   bool have_debug = false;
   void release() {
     DevBuf* all[] = {&direct, &fill, &pts, &surf, &svalid, &sL, &sR, &sT, &sB, &uL, &uR, &uT, &uB, &shadow,
-                     &traits, &rawdir, &dir, &scs, &scd, &interest, &cand, &counters};
+                     &traits, &rawdir, &dir, &scs, &scd, &interest, &cand, &counters, &sat};
     for (auto* b : all) b->release();
   }
 };
@@ -540,6 +540,70 @@ __device__ __forceinline__ float norm_angle(float a) {
   return a >= 0 ? fmodf(a + pi, 2.0f * pi) - pi : -(fmodf(pi - a, 2.0f * pi) - pi);
 }
 
+// Row prefix counts of "contributing" pixels (valid, not shadow/veil, scs >= min_scs): a pixel
+// whose region-grow window holds none of them has interest exactly 0 (no histogram entry, no
+// negative score: 1 * sqrt(0)), so it skips the region grow.  rowp is h x (w+1).
+__global__ void k_contrib_rows(Img I, const float4* __restrict__ P, const uint32_t* __restrict__ traits,
+                               const float* __restrict__ scs, float min_scs, int* __restrict__ rowp) {
+  __shared__ int part[1024];
+  const int y = blockIdx.x, tid = threadIdx.x;  // one row per workgroup, w <= 1024
+  const uint32_t skip = TB(T_SHADOW_BORDER) | TB(T_VEIL_POINT);
+  int v = 0;
+  if (tid < I.w) {
+    const int i = y * I.w + tid;
+    v = (isfinite(P[i].w) && !(traits[i] & skip) && scs[i] >= min_scs) ? 1 : 0;
+  }
+  part[tid] = v;
+  __syncthreads();
+  for (int o = 1; o < 1024; o <<= 1) {
+    const int add = tid >= o ? part[tid - o] : 0;
+    __syncthreads();
+    part[tid] += add;
+    __syncthreads();
+  }
+  if (tid < I.w) rowp[y * (I.w + 1) + tid + 1] = part[tid];
+  if (tid == 0) rowp[y * (I.w + 1)] = 0;
+}
+
+// wave-uniform: does the window hold a contributing pixel?
+__device__ __forceinline__ bool window_contributes(const Img& I, const int* __restrict__ rowp, int x0, int y0,
+                                                   int ww, int wh, int lane) {
+  bool any = false;
+  for (int r = lane; r < wh; r += 64) {
+    const int* row = rowp + (y0 + r) * (I.w + 1);
+    any |= row[x0 + ww] != row[x0];
+  }
+  return __ballot(any) != 0;
+}
+
+// histogram cell of the direction angle: 0.5 * normAngle(2 acos(dvx)) (NarfKeypoint,
+// nkdGetDirectionAngle) with acos correctly rounded to float.  The float acosf is within 1e-5 of
+// it; the map is monotone on each side of acos = pi/2 (where normAngle wraps), so equal cells at
+// both ends of the interval (same side) are exact, otherwise the correctly rounded value is used.
+__device__ __forceinline__ int angle_cell_of(float ac, float d90, float d180) {
+  const float angle = 0.5f * norm_angle(2.0f * ac);
+  const float cellf = floorf((angle + d90) / d180 * 18);
+  if (!(cellf == cellf)) return 0;
+  int cell = min(17, (int)rintf(cellf));
+  return cell < 0 ? 0 : cell;
+}
+
+__device__ __attribute__((noinline)) int angle_cell_exact(float dvx, float d90, float d180) {
+  return angle_cell_of(acosf_cr(dvx), d90, d180);
+}
+
+__device__ __forceinline__ int angle_cell(float dvx, float d90, float d180) {
+  const float a = acosf(dvx);
+  if (!(a == a)) return angle_cell_exact(dvx, d90, d180);
+  const float lo = a - 1e-5f, hi = a + 1e-5f;
+  const float half_pi = 1.57079632679489661923f;
+  if ((lo < half_pi) == (hi < half_pi)) {
+    const int cl = angle_cell_of(lo, d90, d180), ch = angle_cell_of(hi, d90, d180);
+    if (cl == ch) return cl;
+  }
+  return angle_cell_exact(dvx, d90, d180);
+}
+
 struct InterestParams {
   float radius_squared, radius_reciprocal, min_scs, opt_dist, d90, d180;
   double R;  // search radius for the window bound
@@ -548,14 +612,14 @@ struct InterestParams {
 template <int WORDS, bool FULL>
 __global__ void __launch_bounds__(64) k_interest(Img I, const float4* __restrict__ P, const uint32_t* __restrict__ traits,
                                                  const float* __restrict__ scs, const float4* __restrict__ scd,
-                                                 InterestParams ip, const int* __restrict__ list, int nlist,
+                                                 const int* __restrict__ sat, InterestParams ip,
+                                                 const int* __restrict__ list, int nlist,
                                                  float* __restrict__ interest, int* __restrict__ fallback,
                                                  int* __restrict__ n_fallback, int* __restrict__ err) {
   __shared__ uint32_t bitmap[WORDS];
   __shared__ int queue[kQueue];
   __shared__ unsigned hist[18];
   __shared__ unsigned neg_bits;
-  __shared__ int s_tail;
   const int lane = threadIdx.x;
   const int npx = FULL ? nlist : I.w * I.h;
   const uint32_t skip = TB(T_SHADOW_BORDER) | TB(T_VEIL_POINT);
@@ -581,10 +645,14 @@ __global__ void __launch_bounds__(64) k_interest(Img I, const float4* __restrict
         ww = min(I.w - 1, x + hx) - x0 + 1;
         wh = min(I.h - 1, y + hy) - y0 + 1;
       }
-      if ((int64_t)ww * wh > (int64_t)WORDS * 32) {
-        if (lane == 0) fallback[atomicAdd(n_fallback, 1)] = index;
-        continue;
-      }
+    }
+    if (!window_contributes(I, sat, x0, y0, ww, wh, lane)) {  // nothing can contribute: interest 0
+      if (lane == 0) interest[index] = 0.0f;
+      continue;
+    }
+    if (!FULL && (int64_t)ww * wh > (int64_t)WORDS * 32) {
+      if (lane == 0) fallback[atomicAdd(n_fallback, 1)] = index;
+      continue;
     }
     const int nwords = (ww * wh + 31) >> 5;
     for (int k = lane; k < nwords; k += 64) bitmap[k] = 0u;
@@ -599,63 +667,70 @@ __global__ void __launch_bounds__(64) k_interest(Img I, const float4* __restrict
     if (lane == 0) {
       neg_bits = __float_as_uint(1.0f);
       queue[0] = index;
-      s_tail = 1;
       const int lb = (y - y0) * ww + (x - x0);
       bitmap[lb >> 5] |= 1u << (lb & 31);
     }
     __syncthreads();
-    int head = 0;
-    while (true) {
-      const int tail = s_tail;
-      if (head >= tail) break;
+    // breadth-first region grow; the queue tail is wave-uniform (one wave per workgroup)
+    int head = 0, tail = 1;
+    while (head < tail) {
       const int take = min(tail - head, 64);
-      if (lane < take) {
-        const int index2 = queue[(head + lane) & (kQueue - 1)];
-        const int y2 = index2 / I.w, x2 = index2 - y2 * I.w;
+      const bool act = lane < take;
+      int index2 = index, x2 = x, y2 = y;
+      bool ok = false;
+      float pd = 0.0f, d2 = 0.0f;
+      if (act) {
+        index2 = queue[(head + lane) & (kQueue - 1)];
+        y2 = index2 / I.w;
+        x2 = index2 - y2 * I.w;
         const float4 point2 = P[index2];
-        bool ok = isfinite(point2.w) && !(traits[index2] & skip);
-        const float pd = (float)max(abs(x2 - x), abs(y2 - y));
-        const float d2 = sq_dist(point, point2);
+        ok = isfinite(point2.w) && !(traits[index2] & skip);
+        pd = (float)max(abs(x2 - x), abs(y2 - y));
+        d2 = sq_dist(point, point2);
         if (ok && pd > 2.0f && d2 > ip.radius_squared) ok = false;
-        if (ok) {
-          for (int y3 = max(0, y2 - 1); y3 <= min(I.h - 1, y2 + 1); ++y3)
-            for (int x3 = max(0, x2 - 1); x3 <= min(I.w - 1, x2 + 1); ++x3) {
-              const int lx = x3 - x0, ly = y3 - y0;
-              if (lx < 0 || lx >= ww || ly < 0 || ly >= wh) { atomicOr(err, 2); continue; }
-              const int lb = ly * ww + lx;
-              const uint32_t bitm = 1u << (lb & 31);
-              const uint32_t old = atomicOr(&bitmap[lb >> 5], bitm);
-              if (!(old & bitm)) {
-                const int slot = atomicAdd(&s_tail, 1);
-                queue[slot & (kQueue - 1)] = y3 * I.w + x3;
-              }
-            }
-          const float sc = scs[index2];
-          if (sc >= ip.min_scs) {
-            const float4 dv = scd[index2];
-            const f3 dir = mk3(dv.x, dv.y, dv.z);
-            const float distance = sqrtf(d2);
-            const float df = ip.radius_reciprocal * distance;
-            float neg = 1.0f - 0.5f * sc * fmaxf(1.0f - df / ip.opt_dist, 0.0f);
-            neg = neg * neg;
-            const float pos = (pd < 2.0f) ? sc : sc * (1.0f - df);
-            const f3 rot = mk3(0.0f + dot3(tmp0, dir), 0.0f + dot3(tmp1, dir), 0.0f + dot3(tmp2, dir));
-            const float nrm = sqrtf(rot.x * rot.x + rot.y * rot.y);
-            const float dvx = rot.x / nrm;
-            const float angle = 0.5f * norm_angle(2.0f * acosf_cr(dvx));
-            const float cellf = floorf((angle + ip.d90) / ip.d180 * 18);
-            int cell;
-            if (!(cellf == cellf)) cell = 0;
-            else cell = min(17, (int)rintf(cellf));
-            if (cell < 0) cell = 0;
-            if (pos > 0.0f) atomicMax(&hist[cell], __float_as_uint(pos));
-            if (neg < 1.0f) atomicMin(&neg_bits, __float_as_uint(neg));
+      }
+      // the 8-neighbourhood of accepted pixels: newly touched pixels are appended with one
+      // ballot per neighbour offset
+#pragma unroll
+      for (int nb = 0; nb < 9; ++nb) {
+        const int x3 = x2 + nb % 3 - 1, y3 = y2 + nb / 3 - 1;
+        bool fresh = false;
+        if (ok && x3 >= 0 && x3 < I.w && y3 >= 0 && y3 < I.h) {
+          const int lx = x3 - x0, ly = y3 - y0;
+          if (lx < 0 || lx >= ww || ly < 0 || ly >= wh) {
+            atomicOr(err, 2);
+          } else {
+            const int lb = ly * ww + lx;
+            const uint32_t bitm = 1u << (lb & 31);
+            if (!(bitmap[lb >> 5] & bitm)) fresh = !(atomicOr(&bitmap[lb >> 5], bitm) & bitm);
           }
+        }
+        const uint64_t m = __ballot(fresh);
+        if (fresh) queue[(tail + __popcll(m & __lanemask_lt())) & (kQueue - 1)] = y3 * I.w + x3;
+        tail += __popcll(m);
+      }
+      if (ok) {
+        const float sc = scs[index2];
+        if (sc >= ip.min_scs) {  // contributions are max / min: order-free
+          const float4 dv = scd[index2];
+          const f3 dir = mk3(dv.x, dv.y, dv.z);
+          const float distance = sqrtf(d2);
+          const float df = ip.radius_reciprocal * distance;
+          float neg = 1.0f - 0.5f * sc * fmaxf(1.0f - df / ip.opt_dist, 0.0f);
+          neg = neg * neg;
+          const float pos = (pd < 2.0f) ? sc : sc * (1.0f - df);
+          const f3 rot = mk3(0.0f + dot3(tmp0, dir), 0.0f + dot3(tmp1, dir), 0.0f + dot3(tmp2, dir));
+          const float nrm = sqrtf(rot.x * rot.x + rot.y * rot.y);
+          const float dvx = rot.x / nrm;
+          const int cell = angle_cell(dvx, ip.d90, ip.d180);
+          if (pos > 0.0f) atomicMax(&hist[cell], __float_as_uint(pos));
+          if (neg < 1.0f) atomicMin(&neg_bits, __float_as_uint(neg));
         }
       }
       head += take;
-      __syncthreads();
-      if (s_tail - head > kQueue) {
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      if (tail - head > kQueue) {
         if (lane == 0) atomicOr(err, 1);
         break;
       }
@@ -801,7 +876,7 @@ int64_t narf_dev(pfx_ctx* ctx, const float* x, const float* y, const float* z, i
   S.w = I.w;
   S.h = I.h;
   const int npx = I.w * I.h;
-  PFX_CHECK(npx <= kFullWords * 32, "narf: image larger than 640x480 pixels is not supported");
+  PFX_CHECK(npx <= kFullWords * 32 && I.w <= 1024, "narf: image larger than 640x480 pixels is not supported");
   float4* P = S.pts.as<float4>(npx);
   range_image_dev(ctx, x, y, z, n, cam, P);
   float4* surf = S.surf.as<float4>(npx);
@@ -852,9 +927,11 @@ int64_t narf_dev(pfx_ctx* ctx, const float* x, const float* y, const float* z, i
   ip.d180 = 180.0f * deg;
   ip.R = search_radius;
   PFX_HIP(hipMemsetAsync(counters, 0, 4 * sizeof(int), st));
+  int* sat = S.sat.as<int>((I.w + 1) * I.h);
   {
     TimeScope ts(ctx, "narf_interest");
-    k_interest<kWinWords, false><<<256 * 10, 64, 0, st>>>(I, P, traits, scs, scd, ip, nullptr, 0, interest,
+    k_contrib_rows<<<I.h, 1024, 0, st>>>(I, P, traits, scs, ip.min_scs, sat);
+    k_interest<kWinWords, false><<<256 * 10, 64, 0, st>>>(I, P, traits, scs, scd, sat, ip, nullptr, 0, interest,
                                                            cand, counters + 2, counters + 1);
     check_launch("k_interest");
     int nfb = 0;
@@ -862,8 +939,9 @@ int64_t narf_dev(pfx_ctx* ctx, const float* x, const float* y, const float* z, i
     PFX_HIP(hipStreamSynchronize(st));
     ctx->stats["narf_interest_fullimage"] = nfb;
     if (nfb > 0) {
-      k_interest<kFullWords, true><<<std::min(nfb, 256 * 3), 64, 0, st>>>(I, P, traits, scs, scd, ip, cand, nfb,
-                                                                          interest, nullptr, nullptr, counters + 1);
+      k_interest<kFullWords, true><<<std::min(nfb, 256 * 3), 64, 0, st>>>(I, P, traits, scs, scd, sat, ip, cand,
+                                                                          nfb, interest, nullptr, nullptr,
+                                                                          counters + 1);
       check_launch("k_interest_full");
     }
   }

@@ -91,25 +91,48 @@ __global__ void k_tile_flags(const int32_t* __restrict__ seg, const int64_t* __r
 }
 
 // candidate-block class of a tile: sparse, dense, or every query to the per-query path
-__global__ void k_tile_class(GridView g, const int32_t* __restrict__ qpos, const uint32_t* __restrict__ skeys,
-                             const int64_t* __restrict__ nq_ptr, const int32_t* __restrict__ tiles,
-                             const int64_t* __restrict__ ntiles_ptr, uint32_t* __restrict__ sparse,
-                             uint32_t* __restrict__ dense, int32_t* __restrict__ single, int* __restrict__ counts) {
+// (list slots reserved with one atomic per wave and class)
+__global__ void __launch_bounds__(256) k_tile_class(GridView g, const int32_t* __restrict__ qpos,
+                                                    const uint32_t* __restrict__ skeys,
+                                                    const int64_t* __restrict__ nq_ptr,
+                                                    const int32_t* __restrict__ tiles,
+                                                    const int64_t* __restrict__ ntiles_ptr,
+                                                    uint32_t* __restrict__ sparse, uint32_t* __restrict__ dense,
+                                                    int32_t* __restrict__ single, int* __restrict__ counts) {
   const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   const int64_t ntiles = *ntiles_ptr;
-  if (t >= ntiles) return;
-  const int32_t start = tiles[t];
-  const int64_t next = (t + 1 < ntiles) ? tiles[t + 1] : *nq_ptr;  // tiles never span cells
-  const int qn = (int)(next - start < kQ ? next - start : kQ);
-  Runs R;
-  const int T = block_runs(g, skeys[qpos[start]], R);
-  if (T <= kTcapSparse) {
-    sparse[atomicAdd(&counts[0], 1)] = tile_pack(start, qn);
-  } else if (T <= kTcapDense) {
-    dense[atomicAdd(&counts[1], 1)] = tile_pack(start, qn);
-  } else {
-    const int h = atomicAdd(&counts[2], qn);
-    for (int j = 0; j < qn; ++j) single[h + j] = start + j;
+  const int lane = threadIdx.x & 63;
+  int cls = -1, qn = 0;
+  int32_t start = 0;
+  if (t < ntiles) {
+    start = tiles[t];
+    const int64_t next = (t + 1 < ntiles) ? tiles[t + 1] : *nq_ptr;  // tiles never span cells
+    qn = (int)(next - start < kQ ? next - start : kQ);
+    Runs R;
+    const int T = block_runs(g, skeys[qpos[start]], R);
+    cls = T <= kTcapSparse ? 0 : (T <= kTcapDense ? 1 : 2);
+  }
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    const uint64_t m = __ballot(cls == c);
+    if (!m) continue;
+    int base = 0;
+    if (lane == __builtin_ctzll(m)) base = atomicAdd(&counts[c], __popcll(m));
+    base = __shfl(base, __builtin_ctzll(m));
+    if (cls == c) (c ? dense : sparse)[base + __popcll(m & lanemask_lt())] = tile_pack(start, qn);
+  }
+  int v = cls == 2 ? qn : 0, inc = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int x = __shfl_up(inc, o);
+    if (lane >= o) inc += x;
+  }
+  const int total = __shfl(inc, 63);
+  if (total) {
+    int base = 0;
+    if (lane == 63) base = atomicAdd(&counts[2], total);
+    base = __shfl(base, 63) + inc - v;
+    for (int j = 0; j < v; ++j) single[base + j] = start + j;
   }
 }
 
