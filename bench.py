@@ -59,6 +59,7 @@ def main():
     import torch.distributed as dist
 
     from pcl_feature_extraction_amd import Context
+    from pcl_feature_extraction_amd.dist import gather_descriptors
     from pcl_feature_extraction_amd.pipeline import alloc, narf_fpfh
     from pcl_feature_extraction_amd.synth import synth_room
 
@@ -80,20 +81,13 @@ def main():
     b.x.copy_(torch.from_numpy(x))
     b.y.copy_(torch.from_numpy(y))
     b.z.copy_(torch.from_numpy(z))
-    gather_buf = None
+    gathered = None
 
     def step():
         kp, k = narf_fpfh(ctx, b)
         if world > 1:
-            nonlocal gather_buf
-            kk = torch.tensor([k], device=dev, dtype=torch.int64)
-            ks = [torch.zeros_like(kk) for _ in range(world)]
-            dist.all_gather(ks, kk)
-            kmax = int(max(int(t.item()) for t in ks))
-            send = torch.zeros((max(kmax, 1), 33), device=dev)
-            send[:k] = b.desc[:k]
-            gather_buf = [torch.empty_like(send) for _ in range(world)]
-            dist.all_gather(gather_buf, send)
+            nonlocal gathered
+            gathered = gather_descriptors(torch, dist, b.desc, k)
         return kp, k
 
     for _ in range(args.warmup):
@@ -111,16 +105,18 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    nrm_ms, nrm_launches = ctx.kernel_time("normals")
+    chain_ms, chain_launches = ctx.kernel_time("normals_chain")
+    stage_ms, stage_launches = ctx.kernel_time("normals")
     if os.environ.get("PFX_BENCH_VERBOSE"):
-        names = ["grid_bbox", "grid_build", "normals", "normals_tiles", "normals_lists", "normals_chain",
+        names = ["grid_bbox", "grid_build", "normals", "normals_tiles", "normals_lists", "normals_lists_sparse",
+                 "normals_lists_dense", "normals_lists_query", "normals_chain", "normals_long",
                  "range_image", "narf_border", "narf_interest", "narf_nms", "narf_gather", "fpfh_mark",
                  "fpfh_spfh", "fpfh_weight"]
         rep = {nm: round(ctx.kernel_time(nm)[0] / args.steps, 3) for nm in names}
         print("per-step kernel ms:", json.dumps(rep), file=sys.stderr, flush=True)
         stats = {}
         for nm in ["normals_neighbors", "normals_queries", "normals_tiles_sparse", "normals_tiles_dense",
-                   "normals_single", "fpfh_spfh_points", "narf_candidates", "narf_keypoints",
+                   "normals_single", "normals_huge", "fpfh_spfh_points", "narf_candidates", "narf_keypoints",
                    "narf_interest_fullimage"]:
             try:
                 stats[nm] = ctx.stat(nm)
@@ -137,11 +133,20 @@ def main():
     if rank == 0:
         ms_per_step = elapsed / args.steps * 1e3
         value = world * N_POINTS * args.steps / elapsed / 1e6
-        # roofline of the dominant neighbour-gather kernel (normals): algorithmic bytes per launch =
-        # sum_q |N_0.05(q)| * 12 B (SoA xyz) + N * 16 B (nx, ny, nz, curvature out)
+        # roofline of the neighbour-gather kernel: k_normals_chain reads every query's
+        # FLANN-ordered neighbour list and gathers the neighbours' coordinates into the ordered
+        # covariance chains.  Algorithmic bytes per launch = sum_q |N_0.05(q)| * 12 B (xyz) +
+        # N * 16 B (normal + curvature out); time = its HIP-event duration on the ctx stream.
         algo_bytes = neighbors * 12 + N_POINTS * 16
-        avg_launch_s = (nrm_ms / max(nrm_launches, 1)) / 1e3
-        achieved = algo_bytes / avg_launch_s / 1e9 if avg_launch_s > 0 else 0.0
+        chain_s = (chain_ms / max(chain_launches, 1)) / 1e3
+        stage_s = (stage_ms / max(stage_launches, 1)) / 1e3
+        achieved = algo_bytes / chain_s / 1e9 if chain_s > 0 else 0.0
+        stage_gbs = algo_bytes / stage_s / 1e9 if stage_s > 0 else 0.0
+        traffic = None
+        pmc = os.path.join(ROOT, "profiles", "pmc_normals_chain.json")
+        if os.path.exists(pmc):  # FETCH_SIZE x2 + WRITE_SIZE of k_normals_chain (scripts/gpu_pmc.sh)
+            with open(pmc) as f:
+                traffic = json.load(f).get("hbm_bytes_per_launch")
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             cb = cpu_baseline(x, y, z)
@@ -169,10 +174,13 @@ def main():
                                    "configs[4] one 1M-pt room scan per GPU + RCCL all_gather of K x 33 descriptors",
                        "points_per_scan": N_POINTS, "keypoints": int(k), "image": "640x480",
                        "parallelism": f"scan-per-gpu x{world}"},
-            "roofline": {"bound": "hbm", "kernel": "k_normals_main", "achieved": round(achieved, 2),
+            "roofline": {"bound": "hbm", "kernel": "k_normals_chain", "achieved": round(achieved, 2),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
-                         "traffic": None, "algorithmic_bytes_per_launch": int(algo_bytes),
-                         "avg_launch_ms": round(avg_launch_s * 1e3, 4), "neighbors_per_launch": int(neighbors)},
+                         "traffic": traffic, "algorithmic_bytes_per_launch": int(algo_bytes),
+                         "avg_launch_ms": round(chain_s * 1e3, 4), "neighbors_per_launch": int(neighbors),
+                         "stage": {"name": "normals: grid + FLANN-ordered lists + chains", "avg_ms":
+                                   round(stage_s * 1e3, 4), "achieved": round(stage_gbs, 2),
+                                   "frac": round(stage_gbs / HBM_PEAK_GBS, 5)}},
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

@@ -519,13 +519,22 @@ void build_lists(pfx_ctx* ctx, const Grid& G, const uint8_t* mask, double radius
     int h_cnt[8];
     {
       TimeScope ts(ctx, std::string(tag) + "_lists");
-      k_nb_tile<512, 256, kTcapSparse><<<256 * 3 * 4, 256, 0, st>>>(
-          g, qpos, G.skeys, sparse, counters + 0, rr, 256.0f / rr, isort, lo, single, counters + 2);
-      k_nb_tile<1024, 256, kTcapDense><<<256 * 2, 256, 0, st>>>(
-          g, qpos, G.skeys, dense, counters + 1, rr, 256.0f / rr, isort, lo, single, counters + 2);
-      k_nb_query<kCapQuery, kBucketsQuery, false><<<256 * 4, 256, lds_q, st>>>(
-          g, qpos, single, counters + 2, rr, (float)kBucketsQuery / rr, isort, lo, huge, counters + 3,
-          counters + 4, nullptr);
+      {
+        TimeScope t1(ctx, std::string(tag) + "_lists_sparse");
+        k_nb_tile<512, 256, kTcapSparse><<<256 * 3 * 4, 256, 0, st>>>(
+            g, qpos, G.skeys, sparse, counters + 0, rr, 256.0f / rr, isort, lo, single, counters + 2);
+      }
+      {
+        TimeScope t2(ctx, std::string(tag) + "_lists_dense");
+        k_nb_tile<1024, 256, kTcapDense><<<256 * 2, 256, 0, st>>>(
+            g, qpos, G.skeys, dense, counters + 1, rr, 256.0f / rr, isort, lo, single, counters + 2);
+      }
+      {
+        TimeScope t3(ctx, std::string(tag) + "_lists_query");
+        k_nb_query<kCapQuery, kBucketsQuery, false><<<256 * 4, 256, lds_q, st>>>(
+            g, qpos, single, counters + 2, rr, (float)kBucketsQuery / rr, isort, lo, huge, counters + 3,
+            counters + 4, nullptr);
+      }
       check_launch("nblist lists");
       PFX_HIP(hipMemcpyAsync(h_cnt, counters, sizeof(h_cnt), hipMemcpyDeviceToHost, st));
       PFX_HIP(hipStreamSynchronize(st));

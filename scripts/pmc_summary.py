@@ -41,3 +41,18 @@ for us, k, a in rows[:20]:
     if a.get("TCC_HIT_sum", 0) + a.get("TCC_MISS_sum", 0):
         extra["L2_hit"] = a["TCC_HIT_sum"] / (a["TCC_HIT_sum"] + a["TCC_MISS_sum"])
     print("   " + "  ".join(f"{c}={v:.4g}" for c, v in sorted({**a, **extra}.items())))
+
+# machine-readable per-launch HBM traffic of one kernel for bench.py's roofline.traffic
+if len(sys.argv) > 3:
+    kernel, dest = sys.argv[2], sys.argv[3]
+    for us, k, a in rows:
+        if k.startswith(kernel):
+            fetch = a.get("FETCH_SIZE_x2_MB", 0.0) * 1024 * 1024
+            write = a.get("WRITE_SIZE_MB", 0.0) * 1024 * 1024
+            import json
+            with open(dest, "w") as f:
+                json.dump({"kernel": kernel, "hbm_bytes_per_launch": int(fetch + write),
+                           "fetch_bytes_x2": int(fetch), "write_bytes": int(write),
+                           "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes, FETCH x2 "
+                                     "(MI355X_MICROARCH.md gfx950 correction)"}, f, indent=1)
+            break
