@@ -8,7 +8,8 @@
 //
 //      *** parity vs real PCL is UNPINNED ***
 //
-//  The restatement is pinned only by analytic known-answer tests (tests/test_oracle_*.py)
+//  The restatement is pinned only by analytic known-answer tests (tests/test_oracle.py) and the regression
+//  fixtures tests/golden/oracle_small.npz
 //  and is the checker the HIP product is compared against.
 //
 //  Floating-point contract (every oracle TU is built with -O2 -ffp-contract=off, x86-64
