@@ -1,8 +1,407 @@
-// pfx_shot.hip -- SHOTEstimationOMP<PointXYZRGB,Normal,SHOT352> (placeholder until implemented)
-#include "pfx_internal.h"
+// pfx_shot.hip -- SHOTEstimationOMP<PointXYZRGB,Normal,SHOT352> (evaluation.cpp:766-785 via
+// Features<T>::compute, features.h:175-196) on gfx950.  SURVEY A.7.
+//
+// One 256-thread workgroup per query:
+//   1. radius neighbours in FLANN order (bitonic sort of (d2, caller index) keys in LDS);
+//   2. SHOTLocalReferenceFrameEstimation::getLocalRF: the weighted double covariance is a set of
+//      strictly ordered double chains (one lane per matrix entry + one for the weight sum) over
+//      LDS-staged neighbour chunks; cyclic Jacobi eigen solver (the oracle's operation
+//      sequence, double); sign disambiguation counts reduced over the block;
+//   3. SHOT: every neighbour's (up to) five interpolated bin updates are computed in parallel and
+//      applied by one wave with LDS float atomics in neighbour order; normalizeHistogram by one
+//      lane (double accumulation, as PCL).
+// The histogram adds are float additions whose order differs from PCL's loop only inside a
+// wave instruction, so descriptors agree with the restatement to float rounding (the
+// north_star bar is 1e-4 L2); the reference frame is bit-exact.
+#include "pfx_neighbors.h"
+
 namespace pfx {
-void shot_dev(pfx_ctx*, const float*, const float*, const float*, const float*, const float*, const float*,
-              int64_t, const float*, const float*, const float*, int64_t, double, float*, float*) {
-  throw Error(PFX_ERR_UNSUPPORTED, "shot: not implemented yet");
+namespace {
+
+constexpr int kCap = 16384;   // sorted-neighbour capacity (LDS keys)
+constexpr int kChunk = 256;   // neighbours staged per chunk
+constexpr int kLen = 352, kBins = 10;
+constexpr double kRad45 = 0.78539816339744830961566084581988;
+constexpr double kRad90 = 1.5707963267948966192313216916398;
+constexpr double kRad135 = 2.3561944901923449288469825374596;
+constexpr double kRadPi78 = 2.7488935718910690836548129603691;
+
+// oracle jacobi3 (or_shot.cpp): same operation sequence
+__device__ void jacobi3(double a[3][3], double evals[3], double V[3][3]) {
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) V[i][j] = (i == j) ? 1.0 : 0.0;
+  for (int sweep = 0; sweep < 50; ++sweep) {
+    const double off = (a[0][1] * a[0][1] + a[0][2] * a[0][2]) + a[1][2] * a[1][2];
+    const double diag = (a[0][0] * a[0][0] + a[1][1] * a[1][1]) + a[2][2] * a[2][2];
+    if (off == 0.0 || off <= 1e-36 * diag) break;
+    for (int pq = 0; pq < 3; ++pq) {
+      const int p = (pq == 2) ? 1 : 0, q = (pq == 0) ? 1 : 2;
+      const double apq = a[p][q];
+      if (apq == 0.0) continue;
+      const double theta = (a[q][q] - a[p][p]) / (2.0 * apq);
+      double t;
+      if (fabs(theta) > 1e150) t = 0.5 / theta;
+      else t = (theta >= 0.0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
+      const double c = 1.0 / sqrt(t * t + 1.0), s = t * c;
+      const double tau = s / (1.0 + c);
+      a[p][p] = a[p][p] - t * apq;
+      a[q][q] = a[q][q] + t * apq;
+      a[p][q] = a[q][p] = 0.0;
+      const int r = 3 - p - q;
+      const double arp = a[r][p], arq = a[r][q];
+      a[r][p] = a[p][r] = arp - s * (arq + tau * arp);
+      a[r][q] = a[q][r] = arq + s * (arp - tau * arq);
+      for (int k = 0; k < 3; ++k) {
+        const double vkp = V[k][p], vkq = V[k][q];
+        V[k][p] = vkp - s * (vkq + tau * vkp);
+        V[k][q] = vkq + s * (vkp - tau * vkq);
+      }
+    }
+  }
+  const double ev[3] = {a[0][0], a[1][1], a[2][2]};
+  int ord[3] = {0, 1, 2};
+  for (int i = 1; i < 3; ++i) {
+    const int v = ord[i];
+    int j = i;
+    while (j > 0 && ev[v] < ev[ord[j - 1]]) { ord[j] = ord[j - 1]; --j; }
+    ord[j] = v;
+  }
+  double Vs[3][3];
+  for (int k = 0; k < 3; ++k) {
+    evals[k] = ev[ord[k]];
+    for (int i = 0; i < 3; ++i) Vs[i][k] = V[i][ord[k]];
+  }
+  for (int i = 0; i < 3; ++i)
+    for (int k = 0; k < 3; ++k) V[i][k] = Vs[i][k];
 }
+
+// the five (bin, value) updates of one neighbour (SHOTEstimation::interpolateSingleChannel with
+// the bin distance of createBinDistanceShape); bin -1 = no update.  Order = PCL's order.
+__device__ __forceinline__ void shot_updates(f3 delta, double distance, double binDist, f3 fx, f3 fy, f3 fz,
+                                             double radius, int bins[5], float vals[5]) {
+  for (int s = 0; s < 5; ++s) bins[s] = -1;
+  const double radius3_4 = (radius * 3) / 4, radius1_4 = radius / 4, radius1_2 = radius / 2;
+  double xIn = dot4(delta, fx), yIn = dot4(delta, fy), zIn = dot4(delta, fz);
+  if (fabs(yIn) < 1E-30) yIn = 0;
+  if (fabs(xIn) < 1E-30) xIn = 0;
+  if (fabs(zIn) < 1E-30) zIn = 0;
+  const int bit4 = ((yIn > 0) || ((yIn == 0.0) && (xIn < 0))) ? 1 : 0;
+  const int bit3 = ((xIn > 0) || ((xIn == 0.0) && (yIn > 0))) ? !bit4 : bit4;
+  int desc_index = ((bit4 << 3) + (bit3 << 2)) << 1;
+  if ((xIn * yIn > 0) || (xIn == 0.0))
+    desc_index += (fabs(xIn) >= fabs(yIn)) ? 0 : 4;
+  else
+    desc_index += (fabs(xIn) > fabs(yIn)) ? 4 : 0;
+  desc_index += zIn > 0 ? 1 : 0;
+  desc_index += (distance > radius1_2) ? 2 : 0;
+  const int step_index = (int)floor(binDist + 0.5);
+  const int volume_index = desc_index * (kBins + 1);
+  binDist -= step_index;
+  double intWeight = (1 - fabs(binDist));
+  if (binDist > 0) {
+    bins[0] = volume_index + ((step_index + 1) % kBins);
+    vals[0] = (float)binDist;
+  } else {
+    bins[0] = volume_index + ((step_index - 1 + kBins) % kBins);
+    vals[0] = -(float)binDist;
+  }
+  if (distance > radius1_2) {
+    const double rd = (distance - radius3_4) / radius1_2;
+    if (distance > radius3_4) {
+      intWeight += 1 - rd;
+    } else {
+      intWeight += 1 + rd;
+      bins[1] = (desc_index - 2) * (kBins + 1) + step_index;
+      vals[1] = -(float)rd;
+    }
+  } else {
+    const double rd = (distance - radius1_4) / radius1_2;
+    if (distance < radius1_4) {
+      intWeight += 1 + rd;
+    } else {
+      intWeight += 1 - rd;
+      bins[1] = (desc_index + 2) * (kBins + 1) + step_index;
+      vals[1] = (float)rd;
+    }
+  }
+  double ic = zIn / distance;
+  if (ic < -1.0) ic = -1.0;
+  if (ic > 1.0) ic = 1.0;
+  const double incl = acos(ic);
+  if (incl > kRad90 || (fabs(incl - kRad90) < 1e-30 && zIn <= 0)) {
+    const double idist = (incl - kRad135) / kRad90;
+    if (incl > kRad135) {
+      intWeight += 1 - idist;
+    } else {
+      intWeight += 1 + idist;
+      bins[2] = (desc_index + 1) * (kBins + 1) + step_index;
+      vals[2] = -(float)idist;
+    }
+  } else {
+    const double idist = (incl - kRad45) / kRad90;
+    if (incl < kRad45) {
+      intWeight += 1 + idist;
+    } else {
+      intWeight += 1 - idist;
+      bins[2] = (desc_index - 1) * (kBins + 1) + step_index;
+      vals[2] = (float)idist;
+    }
+  }
+  if (yIn != 0.0 || xIn != 0.0) {
+    const double azimuth = atan2(yIn, xIn);
+    const int sel = desc_index >> 2;
+    double ad = (azimuth - (-kRadPi78 + kRad45 * sel)) / kRad45;
+    ad = fmax(-0.5, fmin(ad, 0.5));
+    if (ad > 0) {
+      intWeight += 1 - ad;
+      bins[3] = ((desc_index + 4) % 32) * (kBins + 1) + step_index;
+      vals[3] = (float)ad;
+    } else {
+      intWeight += 1 + ad;
+      bins[3] = ((desc_index - 4 + 32) % 32) * (kBins + 1) + step_index;
+      vals[3] = -(float)ad;
+    }
+  }
+  bins[4] = volume_index + step_index;
+  vals[4] = (float)intWeight;
+}
+
+struct ShotLds {
+  union {
+    struct { double v[kChunk][4]; int valid[kChunk]; } lrf;   // (vx, vy, vz, radius - dist)
+    struct { int bin[kChunk][5]; float val[kChunk][5]; } upd;
+  };
+  float hist[kLen];
+  double cov[10];
+  double axes[6];  // v1 (x axis), v3 (z axis)
+  float rf[9];
+  int n_invalid, zero_prefix, plusT, plusN, ok;
+};
+
+__global__ void __launch_bounds__(256) k_shot(GridView g, const float* __restrict__ nx,
+                                              const float* __restrict__ ny, const float* __restrict__ nz,
+                                              const float* __restrict__ qx, const float* __restrict__ qy,
+                                              const float* __restrict__ qz, int64_t nq, double radius,
+                                              float* __restrict__ desc, float* __restrict__ rf_out,
+                                              int* __restrict__ err) {
+  extern __shared__ __attribute__((aligned(16))) uint64_t keys[];  // kCap
+  __shared__ ShotLds S;
+  __shared__ int s_count;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const float rr = (float)(radius * radius);
+  for (int64_t q = blockIdx.x; q < nq; q += gridDim.x) {
+    float* d = desc + q * kLen;
+    float* rfo = rf_out + q * 9;
+    const float cx = qx[q], cy = qy[q], cz = qz[q];
+    if (!(isfinite(cx) && isfinite(cy) && isfinite(cz))) {
+      for (int i = tid; i < kLen; i += 256) d[i] = __builtin_nanf("");
+      if (tid < 9) rfo[tid] = __builtin_nanf("");
+      continue;
+    }
+    const int k = sorted_neighbors(g, cx, cy, cz, rr, keys, kCap, &s_count);
+    if (k > kCap) {
+      if (tid == 0) atomicMax(err, k);
+      continue;
+    }
+    if (tid == 0) { S.n_invalid = 0; S.zero_prefix = 0; S.plusT = 0; S.plusN = 0; }
+    // ---- local reference frame: ordered double covariance ----
+    double acc = 0.0;  // lanes 0..8: cov[a][b], lane 9: weight sum
+    for (int c0 = 0; c0 < k; c0 += kChunk) {
+      const int m = min(kChunk, k - c0);
+      __syncthreads();
+      if (tid < m) {
+        const uint64_t key = keys[c0 + tid];
+        const int32_t p = key_idx(key);
+        const float px = g.ux[p], py = g.uy[p], pz = g.uz[p];
+        const int valid = !(px == cx && py == cy && pz == cz);
+        S.lrf.valid[tid] = valid;
+        S.lrf.v[tid][0] = (double)(px - cx);
+        S.lrf.v[tid][1] = (double)(py - cy);
+        S.lrf.v[tid][2] = (double)(pz - cz);
+        S.lrf.v[tid][3] = radius - sqrt((double)key_d2(key));
+        if (!valid) atomicAdd(&S.n_invalid, 1);
+        if (key_d2(key) == 0.0f) atomicAdd(&S.zero_prefix, 1);
+      }
+      __syncthreads();
+      if (tid < 10) {
+        const int a = tid / 3, b = tid - 3 * (tid / 3);
+        for (int t = 0; t < m; ++t) {
+          if (!S.lrf.valid[t]) continue;
+          const double dist = S.lrf.v[t][3];
+          acc = (tid < 9) ? acc + dist * (S.lrf.v[t][a] * S.lrf.v[t][b]) : acc + dist;
+        }
+      }
+    }
+    if (tid < 10) S.cov[tid] = acc;
+    __syncthreads();
+    const int valid = k - S.n_invalid;
+    if (tid == 0) {
+      S.ok = 0;
+      if (valid >= 5) {
+        double A[3][3], ev[3], V[3][3];
+        const double sum = S.cov[9];
+        for (int a = 0; a < 3; ++a)
+          for (int b = 0; b < 3; ++b) A[a][b] = S.cov[3 * a + b] / sum;
+        jacobi3(A, ev, V);
+        if (isfinite(ev[0]) && isfinite(ev[1]) && isfinite(ev[2])) {
+          S.ok = 1;
+          for (int i = 0; i < 3; ++i) { S.axes[i] = V[i][2]; S.axes[3 + i] = V[i][0]; }
+        }
+      }
+    }
+    __syncthreads();
+    if (!S.ok) {
+      for (int i = tid; i < kLen; i += 256) d[i] = __builtin_nanf("");
+      if (tid < 9) rfo[tid] = __builtin_nanf("");
+      continue;
+    }
+    // sign disambiguation: counts of non-negative projections over the valid neighbours
+    {
+      const double v1x = S.axes[0], v1y = S.axes[1], v1z = S.axes[2];
+      const double v3x = S.axes[3], v3y = S.axes[4], v3z = S.axes[5];
+      int cT = 0, cN = 0;
+      for (int j = tid; j < k; j += 256) {
+        const int32_t p = key_idx(keys[j]);
+        const float px = g.ux[p], py = g.uy[p], pz = g.uz[p];
+        if (px == cx && py == cy && pz == cz) continue;
+        const double vx = (double)(px - cx), vy = (double)(py - cy), vz = (double)(pz - cz);
+        if (((vx * v1x + vy * v1y) + vz * v1z) + 0.0 >= 0) ++cT;
+        if (((vx * v3x + vy * v3y) + vz * v3z) + 0.0 >= 0) ++cN;
+      }
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) { cT += __shfl_xor(cT, o); cN += __shfl_xor(cN, o); }
+      if (lane == 0) { atomicAdd(&S.plusT, cT); atomicAdd(&S.plusN, cN); }
+    }
+    __syncthreads();
+    if (tid == 0) {
+      double ax[2][3] = {{S.axes[0], S.axes[1], S.axes[2]}, {S.axes[3], S.axes[4], S.axes[5]}};
+      const int counts[2] = {S.plusT, S.plusN};
+      // the valid neighbours in order: the d2 == 0 prefix holds every invalid one
+      const int zp = S.zero_prefix;
+      int valid_in_prefix = 0;
+      for (int j = 0; j < zp; ++j) {
+        const int32_t p = key_idx(keys[j]);
+        if (!(g.ux[p] == cx && g.uy[p] == cy && g.uz[p] == cz)) ++valid_in_prefix;
+      }
+      for (int w = 0; w < 2; ++w) {
+        int plus = 2 * counts[w] - valid;
+        if (plus == 0) {
+          const int median = valid / 2;
+          for (int i = -2; i <= 2; ++i) {
+            const int ne = median - i;
+            int j;
+            if (ne < valid_in_prefix) {
+              int seen = -1;
+              for (j = 0; j < zp; ++j) {
+                const int32_t p = key_idx(keys[j]);
+                if (!(g.ux[p] == cx && g.uy[p] == cy && g.uz[p] == cz) && ++seen == ne) break;
+              }
+            } else {
+              j = zp + (ne - valid_in_prefix);
+            }
+            const int32_t p = key_idx(keys[j]);
+            const double vx = (double)(g.ux[p] - cx), vy = (double)(g.uy[p] - cy), vz = (double)(g.uz[p] - cz);
+            if (((vx * ax[w][0] + vy * ax[w][1]) + vz * ax[w][2]) + 0.0 > 0) ++plus;
+          }
+          if (plus < 3)
+            for (int c = 0; c < 3; ++c) ax[w][c] *= -1;
+        } else if (plus < 0) {
+          for (int c = 0; c < 3; ++c) ax[w][c] *= -1;
+        }
+      }
+      const f3 x = mk3((float)ax[0][0], (float)ax[0][1], (float)ax[0][2]);
+      const f3 z = mk3((float)ax[1][0], (float)ax[1][1], (float)ax[1][2]);
+      const f3 y = cross3(z, x);
+      S.rf[0] = x.x; S.rf[1] = x.y; S.rf[2] = x.z;
+      S.rf[3] = y.x; S.rf[4] = y.y; S.rf[5] = y.z;
+      S.rf[6] = z.x; S.rf[7] = z.y; S.rf[8] = z.z;
+    }
+    for (int i = tid; i < kLen; i += 256) S.hist[i] = 0.0f;
+    __syncthreads();
+    const f3 fx = mk3(S.rf[0], S.rf[1], S.rf[2]), fy = mk3(S.rf[3], S.rf[4], S.rf[5]),
+             fz = mk3(S.rf[6], S.rf[7], S.rf[8]);
+    // ---- SHOT histogram ----
+    for (int c0 = 0; c0 < k; c0 += kChunk) {
+      const int m = min(kChunk, k - c0);
+      if (tid < m) {
+        const uint64_t key = keys[c0 + tid];
+        const int32_t p = key_idx(key);
+        int bins[5];
+        float vals[5];
+#pragma unroll
+        for (int s = 0; s < 5; ++s) bins[s] = -1;
+        const float pnx = nx[p], pny = ny[p], pnz = nz[p];
+        const double distance = sqrt((double)key_d2(key));
+        if (isfinite(pnx) && isfinite(pny) && isfinite(pnz) && !(fabs(distance - 0.0) < 1E-15)) {
+          double cosd = dot4(mk3(pnx, pny, pnz), fz);
+          if (cosd > 1.0) cosd = 1.0;
+          if (cosd < -1.0) cosd = -1.0;
+          const double binDist = ((1.0 + cosd) * kBins) / 2;
+          const f3 delta = mk3(g.ux[p] - cx, g.uy[p] - cy, g.uz[p] - cz);
+          shot_updates(delta, distance, binDist, fx, fy, fz, radius, bins, vals);
+        }
+#pragma unroll
+        for (int s = 0; s < 5; ++s) { S.upd.bin[tid][s] = bins[s]; S.upd.val[tid][s] = vals[s]; }
+      }
+      __syncthreads();
+      if (tid < 64) {  // one wave applies the updates in neighbour order
+        for (int t0 = 0; t0 < m; t0 += 64) {
+          const int t = t0 + lane;
+#pragma unroll
+          for (int s = 0; s < 5; ++s) {
+            const int b = t < m ? S.upd.bin[t][s] : -1;
+            if (b >= 0) atomicAdd(&S.hist[b], S.upd.val[t][s]);
+          }
+        }
+      }
+      __syncthreads();
+    }
+    if (tid == 0) {  // normalizeHistogram
+      double acc_norm = 0;
+      for (int j = 0; j < kLen; ++j) acc_norm += S.hist[j] * S.hist[j];
+      S.cov[0] = sqrt(acc_norm);
+    }
+    __syncthreads();
+    const float nrm = (float)S.cov[0];
+    for (int i = tid; i < kLen; i += 256) d[i] = S.hist[i] / nrm;
+    if (tid < 9) rfo[tid] = S.rf[tid];
+    __syncthreads();
+  }
+}
+
+}  // namespace
+
+void shot_dev(pfx_ctx* ctx, const float* sx, const float* sy, const float* sz, const float* snx, const float* sny,
+              const float* snz, int64_t ns, const float* qx, const float* qy, const float* qz, int64_t nq, double r,
+              float* desc, float* rf) {
+  PFX_CHECK(r > 0.0, "shot: radius must be > 0");
+  if (nq == 0) return;
+  hipStream_t st = ctx->stream;
+  if (ns == 0) {
+    std::vector<float> nanv((size_t)nq * kLen, __builtin_nanf(""));
+    PFX_HIP(hipMemcpyAsync(desc, nanv.data(), sizeof(float) * nq * kLen, hipMemcpyHostToDevice, st));
+    PFX_HIP(hipMemcpyAsync(rf, nanv.data(), sizeof(float) * nq * 9, hipMemcpyHostToDevice, st));
+    PFX_HIP(hipStreamSynchronize(st));
+    return;
+  }
+  build_grid(ctx, ctx->grid_b, sx, sy, sz, ns, r);
+  GridView g = view(ctx->grid_b);
+  int* err = ctx->buf("shot_err").as<int>(1);
+  PFX_HIP(hipMemsetAsync(err, 0, sizeof(int), st));
+  {
+    TimeScope ts(ctx, "shot");
+    const size_t lds = sizeof(uint64_t) * kCap;
+    PFX_HIP(hipFuncSetAttribute((const void*)k_shot, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    const unsigned blocks = (unsigned)std::min<int64_t>(nq, 256 * 8);
+    k_shot<<<blocks, 256, lds, st>>>(g, snx, sny, snz, qx, qy, qz, nq, r, desc, rf, err);
+    check_launch("k_shot");
+  }
+  int h = 0;
+  PFX_HIP(hipMemcpyAsync(&h, err, sizeof(int), hipMemcpyDeviceToHost, st));
+  PFX_HIP(hipStreamSynchronize(st));
+  if (h > 0)
+    throw Error(PFX_ERR_CAPACITY, "shot: a query has " + std::to_string(h) + " neighbours (> " +
+                                      std::to_string(kCap) + " supported)");
+}
+
 }  // namespace pfx
