@@ -5,10 +5,14 @@
 One step = the reference's (Narf, FPFH) pass over one scan (pcl_feature_extraction_amd/pipeline.py):
 range image -> border extraction -> NARF interest + NMS + greedy selection -> keypoint mapping ->
 normals of the whole cloud (r = 0.05) -> FPFH at the keypoints (r = 0.08), inputs resident in HBM.
-At N > 1 every rank processes its own scan and the descriptor matrices are gathered to rank 0
-over RCCL (all_gather of the padded K x 33 blocks) inside the step.
+At N > 1 every rank processes its own scan and the descriptor matrices are gathered on every rank
+over RCCL (dist.gather_descriptors: all_gather of the counts and of the padded K x 33 blocks)
+inside the step.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu-baseline]
+`--workload shot` measures configs[3] instead (secondary line): a 1M-point underwater-style
+seabed, normals + SHOT-352 (r = 0.08) at the NARF keypoints and a fixed 10,000-point sample.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload fpfh|shot] [--no-cpu-baseline]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
 """
 from __future__ import annotations
@@ -24,11 +28,21 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 N_POINTS = 1_000_000
+SHOT_SAMPLE = 10_000
+
+VERBOSE_TIMERS = ["grid_bbox", "grid_build", "normals", "normals_tiles", "normals_lists", "normals_lists_sparse",
+                  "normals_lists_dense", "normals_lists_query", "normals_chain", "normals_long", "range_image",
+                  "narf_border", "narf_interest", "narf_nms", "narf_gather", "fpfh_mark", "fpfh_spfh",
+                  "fpfh_weight", "shot"]
+VERBOSE_STATS = ["normals_neighbors", "normals_queries", "normals_tiles_sparse", "normals_tiles_dense",
+                 "normals_single", "normals_huge", "fpfh_spfh_points", "narf_candidates", "narf_keypoints",
+                 "narf_interest_fullimage", "shot_neighbors"]
 
 
-def cpu_baseline(x, y, z):
+def cpu_baseline(x, y, z, workload, sample=None):
     """The CPU restatement (oracle/, test infrastructure) on the same scan, threads as PCL:
-    NARF and FPFH single-threaded (PCL 1.7 defaults, non-OMP FPFHEstimation), normals OpenMP."""
+    NARF and FPFH single-threaded (PCL 1.7 defaults, non-OMP FPFHEstimation), normals and SHOT
+    OpenMP (NormalEstimationOMP / SHOTEstimationOMP)."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import numpy as np
     import oracle_lib as O
@@ -39,11 +53,18 @@ def cpu_baseline(x, y, z):
     nx, ny, nz, _ = O.normals(x, y, z, 0.05, threads=threads)
     t2 = time.perf_counter()
     rows = kp[kp < len(x)]
-    desc = O.fpfh(x, y, z, nx, ny, nz, x[rows], y[rows], z[rows], 0.08, threads=1)
+    if workload == "fpfh":
+        O.fpfh(x, y, z, nx, ny, nz, x[rows], y[rows], z[rows], 0.08, threads=1)
+        feat = "FPFH 1 thread"
+    else:
+        rows = np.r_[rows, sample]
+        O.shot(x, y, z, nx, ny, nz, x[rows], y[rows], z[rows], 0.08, threads=threads)
+        feat = f"SHOT {threads} threads"
     t3 = time.perf_counter()
-    del desc, np
-    return dict(seconds=t3 - t0, narf_s=t1 - t0, normals_s=t2 - t1, fpfh_s=t3 - t2, threads=threads,
-                keypoints=len(kp))
+    return dict(seconds=t3 - t0, threads=threads,
+                sample=(f"the same 1M-point scan through the CPU restatement (oracle/): NARF 1 thread "
+                        f"{t1 - t0:.1f}s, normals {threads} threads {t2 - t1:.1f}s, {feat} {t3 - t2:.1f}s at "
+                        f"{len(rows)} rows; real PCL is not available anywhere in this pipeline"))
 
 
 def main():
@@ -51,6 +72,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--workload", choices=["fpfh", "shot"], default="fpfh")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
@@ -60,8 +82,8 @@ def main():
 
     from pcl_feature_extraction_amd import Context
     from pcl_feature_extraction_amd.dist import gather_descriptors
-    from pcl_feature_extraction_amd.pipeline import alloc, narf_fpfh
-    from pcl_feature_extraction_amd.synth import synth_room
+    from pcl_feature_extraction_amd.pipeline import alloc, alloc_shot, narf_fpfh, narf_shot
+    from pcl_feature_extraction_amd.synth import synth_room, synth_seabed
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -73,22 +95,34 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
 
-    seed = 2 if world == 1 else 100 + rank  # configs[2] (seed 2) / configs[4] (seeds 100..107)
-    x, y, z, _ = synth_room(N_POINTS, seed)
+    shot = args.workload == "shot"
+    if shot:  # configs[3]: seabed seed 3 (per-rank seeds 300 + rank at N > 1)
+        x, y, z, _ = synth_seabed(N_POINTS, 3 if world == 1 else 300 + rank)
+    else:     # configs[2] (seed 2) / configs[4] (seeds 100..107)
+        x, y, z, _ = synth_room(N_POINTS, 2 if world == 1 else 100 + rank)
     ctx = Context(local)
     ctx.set_stream(torch.cuda.current_stream(dev).cuda_stream)
     b = alloc(torch, N_POINTS, dev)
     b.x.copy_(torch.from_numpy(x))
     b.y.copy_(torch.from_numpy(y))
     b.z.copy_(torch.from_numpy(z))
+    sample_np = np.sort(np.random.default_rng(10).choice(N_POINTS, SHOT_SAMPLE, replace=False))
+    if shot:
+        s = alloc_shot(torch, 1 << 16, dev)
+        sample = torch.from_numpy(sample_np.astype(np.int64)).to(dev)
     gathered = None
 
     def step():
-        kp, k = narf_fpfh(ctx, b)
+        nonlocal gathered
+        if shot:
+            rows = narf_shot(ctx, b, s, sample)
+            desc = s.desc
+        else:
+            _, rows = narf_fpfh(ctx, b)
+            desc = b.desc
         if world > 1:
-            nonlocal gathered
-            gathered = gather_descriptors(torch, dist, b.desc, k)
-        return kp, k
+            gathered = gather_descriptors(torch, dist, desc, rows)
+        return rows
 
     for _ in range(args.warmup):
         step()
@@ -100,24 +134,17 @@ def main():
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        kp, k = step()
+        rows = step()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    chain_ms, chain_launches = ctx.kernel_time("normals_chain")
-    stage_ms, stage_launches = ctx.kernel_time("normals")
+    timers = {nm: ctx.kernel_time(nm) for nm in VERBOSE_TIMERS}
     if os.environ.get("PFX_BENCH_VERBOSE"):
-        names = ["grid_bbox", "grid_build", "normals", "normals_tiles", "normals_lists", "normals_lists_sparse",
-                 "normals_lists_dense", "normals_lists_query", "normals_chain", "normals_long",
-                 "range_image", "narf_border", "narf_interest", "narf_nms", "narf_gather", "fpfh_mark",
-                 "fpfh_spfh", "fpfh_weight"]
-        rep = {nm: round(ctx.kernel_time(nm)[0] / args.steps, 3) for nm in names}
+        rep = {nm: round(ms / args.steps, 3) for nm, (ms, _) in timers.items() if ms > 0}
         print("per-step kernel ms:", json.dumps(rep), file=sys.stderr, flush=True)
         stats = {}
-        for nm in ["normals_neighbors", "normals_queries", "normals_tiles_sparse", "normals_tiles_dense",
-                   "normals_single", "normals_huge", "fpfh_spfh_points", "narf_candidates", "narf_keypoints",
-                   "narf_interest_fullimage"]:
+        for nm in VERBOSE_STATS:
             try:
                 stats[nm] = ctx.stat(nm)
             except Exception:
@@ -138,8 +165,10 @@ def main():
         # covariance chains.  Algorithmic bytes per launch = sum_q |N_0.05(q)| * 12 B (xyz) +
         # N * 16 B (normal + curvature out); time = its HIP-event duration on the ctx stream.
         algo_bytes = neighbors * 12 + N_POINTS * 16
-        chain_s = (chain_ms / max(chain_launches, 1)) / 1e3
-        stage_s = (stage_ms / max(stage_launches, 1)) / 1e3
+        chain_ms, chain_n = timers["normals_chain"]
+        stage_ms, stage_n = timers["normals"]
+        chain_s = (chain_ms / max(chain_n, 1)) / 1e3
+        stage_s = (stage_ms / max(stage_n, 1)) / 1e3
         achieved = algo_bytes / chain_s / 1e9 if chain_s > 0 else 0.0
         stage_gbs = algo_bytes / stage_s / 1e9 if stage_s > 0 else 0.0
         traffic = None
@@ -147,17 +176,38 @@ def main():
         if os.path.exists(pmc):  # FETCH_SIZE x2 + WRITE_SIZE of k_normals_chain (scripts/gpu_pmc.sh)
             with open(pmc) as f:
                 traffic = json.load(f).get("hbm_bytes_per_launch")
+        roofline = {"bound": "hbm", "kernel": "k_normals_chain", "achieved": round(achieved, 2),
+                    "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
+                    "traffic": traffic, "algorithmic_bytes_per_launch": int(algo_bytes),
+                    "avg_launch_ms": round(chain_s * 1e3, 4), "neighbors_per_launch": int(neighbors),
+                    "stage": {"name": "normals: grid + FLANN-ordered lists + chains",
+                              "avg_ms": round(stage_s * 1e3, 4), "achieved": round(stage_gbs, 2),
+                              "frac": round(stage_gbs / HBM_PEAK_GBS, 5)}}
+        if shot:  # SHOT kernel: sum_q |N(q)| x 24 B (xyz + normal) per launch
+            shot_ms, shot_n = timers["shot"]
+            shot_s = (shot_ms / max(shot_n, 1)) / 1e3
+            sb = ctx.stat("shot_neighbors") * 24
+            roofline["shot"] = {"kernel": "k_shot", "avg_ms": round(shot_s * 1e3, 4),
+                                "algorithmic_bytes_per_launch": int(sb),
+                                "achieved": round(sb / shot_s / 1e9, 2) if shot_s > 0 else 0.0}
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
-            cb = cpu_baseline(x, y, z)
+            cb = cpu_baseline(x, y, z, args.workload, sample_np)
             cpu = {"value": round(N_POINTS / cb["seconds"] / 1e6, 6), "unit": "Mpoints/s",
-                   "cores": cb["threads"], "kind": "port",
-                   "sample": (f"the same 1M-point scan through the CPU restatement (oracle/): NARF 1 thread "
-                              f"{cb['narf_s']:.1f}s, normals {cb['threads']} threads {cb['normals_s']:.1f}s, "
-                              f"FPFH 1 thread {cb['fpfh_s']:.1f}s at {cb['keypoints']} keypoints; real PCL "
-                              f"is not available anywhere in this pipeline")}
+                   "cores": cb["threads"], "kind": "port", "sample": cb["sample"]}
+        if shot:
+            metric = "Mpoints/s through NARF keypoint + normals + SHOT-352 descriptor on 1M-pt underwater-style cloud"
+            workload = (f"configs[3] 1M-pt synthetic seabed, NARF(support 0.2) + normals(r 0.05) + SHOT-352(r 0.08) "
+                        f"at the keypoints + a fixed {SHOT_SAMPLE}-point sample")
+            data = "synthetic (synth_seabed: seeded fBm height field under a pinhole camera, k(0.08)~1000)"
+        else:
+            metric = "Mpoints/s through NARF keypoint + FPFH descriptor on 1M-pt cloud"
+            workload = ("configs[2] 1M-pt synthetic room, NARF(support 0.2) + normals(r 0.05) + FPFH(r 0.08) at "
+                        "the keypoints" if world == 1 else
+                        "configs[4] one 1M-pt room scan per GPU + RCCL all_gather of K x 33 descriptors")
+            data = "synthetic (synth_room: seeded pinhole room scan, k(0.05)~230; see synth.py)"
         line = {
-            "metric": "Mpoints/s through NARF keypoint + FPFH descriptor on 1M-pt cloud",
+            "metric": metric,
             "value": round(value, 4),
             "unit": "Mpoints/s",
             "n_gpus": world,
@@ -168,19 +218,10 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic (synth_room: seeded pinhole room scan, k(0.05)~230; see synth.py)",
-            "config": {"workload": "configs[2] 1M-pt synthetic room, NARF(support 0.2) + normals(r 0.05) + "
-                                   "FPFH(r 0.08) at the keypoints" if world == 1 else
-                                   "configs[4] one 1M-pt room scan per GPU + RCCL all_gather of K x 33 descriptors",
-                       "points_per_scan": N_POINTS, "keypoints": int(k), "image": "640x480",
-                       "parallelism": f"scan-per-gpu x{world}"},
-            "roofline": {"bound": "hbm", "kernel": "k_normals_chain", "achieved": round(achieved, 2),
-                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
-                         "traffic": traffic, "algorithmic_bytes_per_launch": int(algo_bytes),
-                         "avg_launch_ms": round(chain_s * 1e3, 4), "neighbors_per_launch": int(neighbors),
-                         "stage": {"name": "normals: grid + FLANN-ordered lists + chains", "avg_ms":
-                                   round(stage_s * 1e3, 4), "achieved": round(stage_gbs, 2),
-                                   "frac": round(stage_gbs / HBM_PEAK_GBS, 5)}},
+            "data": data,
+            "config": {"workload": workload, "points_per_scan": N_POINTS, "descriptor_rows": int(rows),
+                       "image": "640x480", "parallelism": f"scan-per-gpu x{world}"},
+            "roofline": roofline,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

@@ -18,7 +18,8 @@
 namespace pfx {
 namespace {
 
-constexpr int kCap = 16384;   // sorted-neighbour capacity (LDS keys)
+constexpr int kCapSmall = 2048;  // sorted-neighbour capacity of the first pass (LDS keys, 5 WG/CU)
+constexpr int kCap = 16384;      // second pass for the longer lists (1 WG/CU)
 constexpr int kChunk = 256;   // neighbours staged per chunk
 constexpr int kLen = 352, kBins = 10;
 constexpr double kRad45 = 0.78539816339744830961566084581988;
@@ -27,7 +28,7 @@ constexpr double kRad135 = 2.3561944901923449288469825374596;
 constexpr double kRadPi78 = 2.7488935718910690836548129603691;
 
 // oracle jacobi3 (or_shot.cpp): same operation sequence
-__device__ void jacobi3(double a[3][3], double evals[3], double V[3][3]) {
+__device__ __attribute__((noinline)) void jacobi3(double a[3][3], double evals[3], double V[3][3]) {
   for (int i = 0; i < 3; ++i)
     for (int j = 0; j < 3; ++j) V[i][j] = (i == j) ? 1.0 : 0.0;
   for (int sweep = 0; sweep < 50; ++sweep) {
@@ -178,18 +179,25 @@ struct ShotLds {
   int n_invalid, zero_prefix, plusT, plusN, ok;
 };
 
+// CAP: LDS key capacity.  `list` (nullable): query subset with its device-side count; queries
+// with more than CAP neighbours go to `over` (or raise err when over == nullptr).
+template <int CAP>
 __global__ void __launch_bounds__(256) k_shot(GridView g, const float* __restrict__ nx,
                                               const float* __restrict__ ny, const float* __restrict__ nz,
                                               const float* __restrict__ qx, const float* __restrict__ qy,
-                                              const float* __restrict__ qz, int64_t nq, double radius,
-                                              float* __restrict__ desc, float* __restrict__ rf_out,
-                                              int* __restrict__ err) {
-  extern __shared__ __attribute__((aligned(16))) uint64_t keys[];  // kCap
+                                              const float* __restrict__ qz, int64_t nq,
+                                              const int32_t* __restrict__ list, const int* __restrict__ n_list,
+                                              int32_t* __restrict__ over, int* __restrict__ n_over,
+                                              double radius, float* __restrict__ desc, float* __restrict__ rf_out,
+                                              int* __restrict__ err, unsigned long long* __restrict__ nbr) {
+  extern __shared__ __attribute__((aligned(16))) uint64_t keys[];  // CAP
   __shared__ ShotLds S;
   __shared__ int s_count;
   const int tid = threadIdx.x, lane = tid & 63;
   const float rr = (float)(radius * radius);
-  for (int64_t q = blockIdx.x; q < nq; q += gridDim.x) {
+  const int64_t count = list ? (int64_t)*n_list : nq;
+  for (int64_t w = blockIdx.x; w < count; w += gridDim.x) {
+    const int64_t q = list ? (int64_t)list[w] : w;
     float* d = desc + q * kLen;
     float* rfo = rf_out + q * 9;
     const float cx = qx[q], cy = qy[q], cz = qz[q];
@@ -198,12 +206,18 @@ __global__ void __launch_bounds__(256) k_shot(GridView g, const float* __restric
       if (tid < 9) rfo[tid] = __builtin_nanf("");
       continue;
     }
-    const int k = sorted_neighbors(g, cx, cy, cz, rr, keys, kCap, &s_count);
-    if (k > kCap) {
-      if (tid == 0) atomicMax(err, k);
+    const int k = sorted_neighbors(g, cx, cy, cz, rr, keys, CAP, &s_count);
+    if (k > CAP) {
+      if (tid == 0) {
+        if (over) over[atomicAdd(n_over, 1)] = (int32_t)q;
+        else atomicMax(err, k);
+      }
       continue;
     }
-    if (tid == 0) { S.n_invalid = 0; S.zero_prefix = 0; S.plusT = 0; S.plusN = 0; }
+    if (tid == 0) {
+      S.n_invalid = 0; S.zero_prefix = 0; S.plusT = 0; S.plusN = 0;
+      atomicAdd(nbr, (unsigned long long)k);
+    }
     // ---- local reference frame: ordered double covariance ----
     double acc = 0.0;  // lanes 0..8: cov[a][b], lane 9: weight sum
     for (int c0 = 0; c0 < k; c0 += kChunk) {
@@ -386,19 +400,29 @@ void shot_dev(pfx_ctx* ctx, const float* sx, const float* sy, const float* sz, c
   }
   build_grid(ctx, ctx->grid_b, sx, sy, sz, ns, r);
   GridView g = view(ctx->grid_b);
-  int* err = ctx->buf("shot_err").as<int>(1);
-  PFX_HIP(hipMemsetAsync(err, 0, sizeof(int), st));
+  int* err = ctx->buf("shot_err").as<int>(4);
+  unsigned long long* nbr = reinterpret_cast<unsigned long long*>(err + 2);
+  PFX_HIP(hipMemsetAsync(err, 0, 4 * sizeof(int), st));
   {
     TimeScope ts(ctx, "shot");
-    const size_t lds = sizeof(uint64_t) * kCap;
-    PFX_HIP(hipFuncSetAttribute((const void*)k_shot, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    const unsigned blocks = (unsigned)std::min<int64_t>(nq, 256 * 8);
-    k_shot<<<blocks, 256, lds, st>>>(g, snx, sny, snz, qx, qy, qz, nq, r, desc, rf, err);
+    int32_t* over = ctx->buf("shot_over").as<int32_t>(nq);
+    int* n_over = err + 1;
+    const size_t lds_s = sizeof(uint64_t) * kCapSmall, lds = sizeof(uint64_t) * kCap;
+    PFX_HIP(hipFuncSetAttribute((const void*)k_shot<kCap>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    const unsigned blocks = (unsigned)std::min<int64_t>(nq, 256 * 10);
+    k_shot<kCapSmall><<<blocks, 256, lds_s, st>>>(g, snx, sny, snz, qx, qy, qz, nq, nullptr, nullptr, over, n_over,
+                                                   r, desc, rf, err, nbr);
+    // longer lists: grid sized for the worst case, the count stays on the device
+    k_shot<kCap><<<(unsigned)std::min<int64_t>(nq, 256 * 2), 256, lds, st>>>(
+        g, snx, sny, snz, qx, qy, qz, nq, over, n_over, nullptr, nullptr, r, desc, rf, err, nbr);
     check_launch("k_shot");
   }
   int h = 0;
+  unsigned long long h_nbr = 0;
   PFX_HIP(hipMemcpyAsync(&h, err, sizeof(int), hipMemcpyDeviceToHost, st));
+  PFX_HIP(hipMemcpyAsync(&h_nbr, nbr, sizeof(h_nbr), hipMemcpyDeviceToHost, st));
   PFX_HIP(hipStreamSynchronize(st));
+  ctx->stats["shot_neighbors"] = (int64_t)h_nbr;
   if (h > 0)
     throw Error(PFX_ERR_CAPACITY, "shot: a query has " + std::to_string(h) + " neighbours (> " +
                                       std::to_string(kCap) + " supported)");

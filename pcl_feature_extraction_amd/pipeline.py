@@ -56,3 +56,36 @@ def keypoint_rows(kp: np.ndarray, n: int) -> np.ndarray:
     """Cloud indices the descriptors belong to (keypoints.h:229 uses pixel index as cloud index)."""
     kp = np.asarray(kp)
     return kp[(kp >= 0) & (kp < n)]
+
+
+@dataclasses.dataclass
+class ShotBuffers:
+    qx: object
+    qy: object
+    qz: object
+    desc: object
+    rf: object
+
+
+def alloc_shot(torch, nq: int, device) -> ShotBuffers:
+    f = dict(dtype=torch.float32, device=device)
+    return ShotBuffers(torch.empty(nq, **f), torch.empty(nq, **f), torch.empty(nq, **f),
+                       torch.empty((nq, 352), **f), torch.empty((nq, 9), **f))
+
+
+def narf_shot(ctx: Context, b: ScanBuffers, s: ShotBuffers, sample, normal_radius: float = 0.05,
+              feat_radius: float = 0.08, params=None, cam=None):
+    """configs[3]: normals, then SHOT-352 at the NARF keypoints followed by a
+    fixed sample of cloud indices (`sample`: int64 CUDA tensor).  Returns the number of rows."""
+    import torch
+    kp = ctx.narf_keypoints_dev(b.x, b.y, b.z, params or narf_params(support_size=0.2), cam or camera())
+    k = ctx.gather_points_dev(b.x, b.y, b.z, kp, s.qx, s.qy, s.qz)
+    m = sample.numel()
+    torch.index_select(b.x, 0, sample, out=s.qx[k:k + m])
+    torch.index_select(b.y, 0, sample, out=s.qy[k:k + m])
+    torch.index_select(b.z, 0, sample, out=s.qz[k:k + m])
+    ctx.normals_dev(b.x, b.y, b.z, normal_radius, b.nx, b.ny, b.nz, b.curv)
+    rows = k + m
+    ctx.shot_dev(b.x, b.y, b.z, b.nx, b.ny, b.nz, s.qx[:rows], s.qy[:rows], s.qz[:rows], feat_radius,
+                 s.desc[:rows], s.rf[:rows])
+    return rows
