@@ -1,0 +1,513 @@
+// pfx_pcl.hpp -- PCL 1.7-compatible C++ facade over the libpfx C-ABI (include/pfx.h).
+//
+// The reference's wrapper headers call PCL's class API on the hot path and nothing else:
+//   include/pcl_feature_extraction/keypoints.h:199-231  RangeImagePlanar, RangeImageBorderExtractor,
+//                                                       NarfKeypoint, PointCloud<int>
+//   include/pcl_feature_extraction/features.h:175-196   Feature / FeatureFromNormals (polymorphic,
+//                                                       probed with dynamic_pointer_cast),
+//                                                       search::KdTree, setRadiusSearch, compute
+//   include/pcl_feature_extraction/tools.h:22-32        NormalEstimationOMP
+//   src/evaluation.cpp:593-612, :766-785                FPFHEstimation, SHOTEstimationOMP
+// This header provides those names in namespace pcl (plus the minimal Eigen subset the calls
+// touch), implemented on the GPU through libpfx, so the wrapper headers compile unchanged when
+// this header stands in for the PCL includes.  Point types keep PCL's 16-byte-aligned layouts.
+//
+// Behaviour mirrors PCL 1.7: compute() never throws on algorithmic failure -- a failed
+// initCompute / device error prints PCL_ERROR and leaves an empty output cloud; per-point failure
+// is NaN in the row, is_dense = false.  Objects are not re-entrant; one libpfx context per
+// process (device from $PFX_DEVICE, default 0), calls are synchronous on the caller's thread.
+//
+// Define PFX_PCL_BOOST_SHIM before including to get boost::shared_ptr / dynamic_pointer_cast
+// aliases for code written against PCL 1.7's boost pointers (features.h:181-182).
+#ifndef PFX_PCL_HPP_
+#define PFX_PCL_HPP_
+
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <limits>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "pfx.h"
+
+#ifndef PCL_ERROR
+#define PCL_ERROR(...) std::fprintf(stderr, __VA_ARGS__)
+#endif
+
+#ifdef PFX_PCL_BOOST_SHIM
+namespace boost {
+using std::dynamic_pointer_cast;
+using std::shared_ptr;
+}  // namespace boost
+#endif
+
+// ---- the Eigen subset used by keypoints.h:207-210 ------------------------------------------
+namespace Eigen {
+
+struct Vector3f {
+  float v[3] = {0, 0, 0};
+  Vector3f() = default;
+  Vector3f(float x, float y, float z) : v{x, y, z} {}
+  float& operator[](int i) { return v[i]; }
+  float operator[](int i) const { return v[i]; }
+};
+
+struct Vector4f {
+  float v[4] = {0, 0, 0, 0};
+  Vector4f() = default;
+  Vector4f(float x, float y, float z, float w) : v{x, y, z, w} {}
+  float& operator[](int i) { return v[i]; }
+  float operator[](int i) const { return v[i]; }
+  static Vector4f Zero() { return Vector4f(); }
+};
+
+struct Quaternionf {
+  float qw = 1, qx = 0, qy = 0, qz = 0;
+  Quaternionf() = default;
+  Quaternionf(float w, float x, float y, float z) : qw(w), qx(x), qy(y), qz(z) {}
+  static Quaternionf Identity() { return Quaternionf(); }
+  float w() const { return qw; }
+  float x() const { return qx; }
+  float y() const { return qy; }
+  float z() const { return qz; }
+};
+
+struct Translation3f {
+  float t[3];
+  Translation3f(float x, float y, float z) : t{x, y, z} {}
+};
+
+// 4x4 affine transform, row-major storage
+struct Affine3f {
+  float m[16];
+  Affine3f() { setIdentity(); }
+  explicit Affine3f(const Translation3f& tr) {
+    setIdentity();
+    m[3] = tr.t[0]; m[7] = tr.t[1]; m[11] = tr.t[2];
+  }
+  // Eigen's Quaternion::toRotationMatrix (unit quaternion)
+  explicit Affine3f(const Quaternionf& q) {
+    setIdentity();
+    const float tx = 2.f * q.qx, ty = 2.f * q.qy, tz = 2.f * q.qz;
+    const float twx = tx * q.qw, twy = ty * q.qw, twz = tz * q.qw;
+    const float txx = tx * q.qx, txy = ty * q.qx, txz = tz * q.qx;
+    const float tyy = ty * q.qy, tyz = tz * q.qy, tzz = tz * q.qz;
+    m[0] = 1.f - (tyy + tzz); m[1] = txy - twz;         m[2] = txz + twy;
+    m[4] = txy + twz;         m[5] = 1.f - (txx + tzz); m[6] = tyz - twx;
+    m[8] = txz - twy;         m[9] = tyz + twx;         m[10] = 1.f - (txx + tyy);
+  }
+  static Affine3f Identity() { return Affine3f(); }
+  void setIdentity() {
+    for (int i = 0; i < 16; ++i) m[i] = (i % 5 == 0) ? 1.f : 0.f;
+  }
+  float& operator()(int r, int c) { return m[4 * r + c]; }
+  float operator()(int r, int c) const { return m[4 * r + c]; }
+  Affine3f operator*(const Affine3f& o) const {
+    Affine3f r;
+    for (int i = 0; i < 4; ++i)
+      for (int j = 0; j < 4; ++j) {
+        float s = 0.f;
+        for (int k = 0; k < 4; ++k) s += m[4 * i + k] * o.m[4 * k + j];
+        r.m[4 * i + j] = s;
+      }
+    return r;
+  }
+};
+
+}  // namespace Eigen
+
+namespace pcl {
+
+namespace detail {
+// one libpfx context per process (thread-affine use, as PCL objects are not re-entrant)
+inline pfx_ctx* context() {
+  static pfx_ctx* ctx = [] {
+    pfx_ctx* c = nullptr;
+    const char* dev = std::getenv("PFX_DEVICE");
+    if (pfx_ctx_create(dev ? std::atoi(dev) : 0, &c) != PFX_OK) {
+      PCL_ERROR("[pfx_pcl] no HIP device: %s\n", c ? pfx_last_error(c) : "pfx_ctx_create failed");
+      return static_cast<pfx_ctx*>(nullptr);
+    }
+    return c;
+  }();
+  return ctx;
+}
+inline float nanf() { return std::numeric_limits<float>::quiet_NaN(); }
+}  // namespace detail
+
+// ---- point types (PCL 1.7 layouts, 16-byte aligned) ----------------------------------------
+struct alignas(16) PointXYZRGB {
+  float x = 0, y = 0, z = 0, data_pad = 1.f;
+  union { float rgb; uint32_t rgba = 0; };
+  float pad_[3] = {0, 0, 0};
+};
+struct alignas(16) Normal {
+  float normal_x = 0, normal_y = 0, normal_z = 0, data_pad = 0.f;
+  float curvature = 0;
+  float pad_[3] = {0, 0, 0};
+};
+struct alignas(16) PointWithRange {
+  float x = 0, y = 0, z = 0, data_pad = 1.f;
+  float range = 0;
+  float pad_[3] = {0, 0, 0};
+};
+struct FPFHSignature33 { float histogram[33]; };
+struct SHOT352 { float descriptor[352]; float rf[9]; };
+struct ReferenceFrame { float x_axis[3], y_axis[3], z_axis[3]; };
+
+template <typename T>
+class PointCloud {
+ public:
+  typedef std::shared_ptr<PointCloud<T> > Ptr;
+  typedef std::shared_ptr<const PointCloud<T> > ConstPtr;
+  std::vector<T> points;
+  uint32_t width = 0, height = 1;
+  bool is_dense = true;
+  Eigen::Vector4f sensor_origin_ = Eigen::Vector4f(0, 0, 0, 0);
+  Eigen::Quaternionf sensor_orientation_ = Eigen::Quaternionf::Identity();
+  size_t size() const { return points.size(); }
+  bool empty() const { return points.empty(); }
+  void push_back(const T& p) { points.push_back(p); width = (uint32_t)points.size(); height = 1; }
+  void resize(size_t n) { points.resize(n); width = (uint32_t)n; height = 1; }
+  void clear() { points.clear(); width = 0; height = 1; }
+  T& operator[](size_t i) { return points[i]; }
+  const T& operator[](size_t i) const { return points[i]; }
+};
+
+namespace detail {
+struct SoA {
+  std::vector<float> x, y, z;
+};
+template <typename P>
+inline SoA soa_xyz(const PointCloud<P>& c) {
+  SoA s;
+  const size_t n = c.size();
+  s.x.resize(n); s.y.resize(n); s.z.resize(n);
+  for (size_t i = 0; i < n; ++i) { s.x[i] = c.points[i].x; s.y[i] = c.points[i].y; s.z[i] = c.points[i].z; }
+  return s;
+}
+inline SoA soa_normals(const PointCloud<Normal>& c) {
+  SoA s;
+  const size_t n = c.size();
+  s.x.resize(n); s.y.resize(n); s.z.resize(n);
+  for (size_t i = 0; i < n; ++i) {
+    s.x[i] = c.points[i].normal_x; s.y[i] = c.points[i].normal_y; s.z[i] = c.points[i].normal_z;
+  }
+  return s;
+}
+inline bool ok(pfx_status st, const char* who) {
+  if (st == PFX_OK) return true;
+  PCL_ERROR("[pcl::%s::compute] %s\n", who, context() ? pfx_last_error(context()) : "no device");
+  return false;
+}
+}  // namespace detail
+
+namespace search {
+// The GPU path builds its own uniform-grid index; the tree object only carries the type.
+template <typename PointT>
+class KdTree {
+ public:
+  typedef std::shared_ptr<KdTree<PointT> > Ptr;
+  explicit KdTree(bool sorted = true) : sorted_(sorted) {}
+  virtual ~KdTree() = default;
+ private:
+  bool sorted_;
+};
+}  // namespace search
+
+// ---- Feature hierarchy (features.h:175-196 probes FeatureFromNormals by dynamic cast) -------
+template <typename PointInT, typename PointOutT>
+class Feature {
+ public:
+  typedef PointCloud<PointInT> PointCloudIn;
+  typedef typename PointCloudIn::ConstPtr PointCloudInConstPtr;
+  typedef PointCloud<PointOutT> PointCloudOut;
+  typedef std::shared_ptr<Feature<PointInT, PointOutT> > Ptr;
+  typedef typename search::KdTree<PointInT>::Ptr KdTreePtr;
+  virtual ~Feature() = default;
+  void setInputCloud(const PointCloudInConstPtr& cloud) { input_ = cloud; }
+  void setSearchSurface(const PointCloudInConstPtr& cloud) { surface_ = cloud; }
+  void setSearchMethod(const KdTreePtr& tree) { tree_ = tree; }
+  void setRadiusSearch(double r) { search_radius_ = r; }
+  void setKSearch(int k) { k_ = k; }
+  double getRadiusSearch() const { return search_radius_; }
+  // Feature::compute: initCompute -> computeFeature -> deinitCompute
+  void compute(PointCloudOut& output) {
+    output.clear();
+    if (!input_ || input_->empty() || k_ != 0 || !(search_radius_ > 0.0)) {
+      PCL_ERROR("[pcl::%s::compute] initCompute failed (needs an input cloud and a radius; "
+                "k-NN search is not on the accelerated path)\n", name_.c_str());
+      return;
+    }
+    if (!detail::context()) return;
+    computeFeature(output);
+  }
+
+ protected:
+  virtual void computeFeature(PointCloudOut& output) = 0;
+  const PointCloudIn& surface() const { return surface_ ? *surface_ : *input_; }
+  bool input_is_surface() const { return !surface_ || surface_.get() == input_.get(); }
+  std::string name_ = "Feature";
+  PointCloudInConstPtr input_, surface_;
+  KdTreePtr tree_;
+  double search_radius_ = 0.0;
+  int k_ = 0;
+};
+
+template <typename PointInT, typename PointNT, typename PointOutT>
+class FeatureFromNormals : public Feature<PointInT, PointOutT> {
+ public:
+  typedef typename PointCloud<PointNT>::ConstPtr PointCloudNConstPtr;
+  typedef std::shared_ptr<FeatureFromNormals<PointInT, PointNT, PointOutT> > Ptr;
+  void setInputNormals(const PointCloudNConstPtr& normals) { normals_ = normals; }
+
+ protected:
+  PointCloudNConstPtr normals_;
+};
+
+// NormalEstimationOMP<In, Normal> (tools.h:22-32): viewpoint (0,0,0) unless set
+template <typename PointInT, typename PointOutT>
+class NormalEstimationOMP : public Feature<PointInT, PointOutT> {
+ public:
+  explicit NormalEstimationOMP(unsigned int /*nr_threads*/ = 0) { this->name_ = "NormalEstimationOMP"; }
+  void setViewPoint(float vx, float vy, float vz) { vp_[0] = vx; vp_[1] = vy; vp_[2] = vz; }
+  void setNumberOfThreads(unsigned int) {}
+
+ protected:
+  void computeFeature(PointCloud<PointOutT>& out) override {
+    const PointCloud<PointInT>& in = *this->input_;
+    if (!this->input_is_surface()) {
+      PCL_ERROR("[pcl::NormalEstimationOMP::compute] a search surface other than the input is not on "
+                "the accelerated path\n");
+      return;
+    }
+    const detail::SoA s = detail::soa_xyz(in);
+    const size_t n = in.size();
+    std::vector<float> nx(n), ny(n), nz(n), cv(n);
+    if (!detail::ok(pfx_normals(detail::context(), s.x.data(), s.y.data(), s.z.data(), (int64_t)n,
+                                this->search_radius_, vp_, nx.data(), ny.data(), nz.data(), cv.data()),
+                    "NormalEstimationOMP"))
+      return;
+    out.resize(n);
+    out.is_dense = true;
+    for (size_t i = 0; i < n; ++i) {
+      out.points[i].normal_x = nx[i]; out.points[i].normal_y = ny[i];
+      out.points[i].normal_z = nz[i]; out.points[i].curvature = cv[i];
+      if (std::isnan(nx[i])) out.is_dense = false;
+    }
+  }
+  float vp_[3] = {0.f, 0.f, 0.f};
+};
+
+// FPFHEstimation<In, Normal, FPFHSignature33> (evaluation.cpp:597)
+template <typename PointInT, typename PointNT, typename PointOutT = FPFHSignature33>
+class FPFHEstimation : public FeatureFromNormals<PointInT, PointNT, PointOutT> {
+ public:
+  typedef std::shared_ptr<FPFHEstimation<PointInT, PointNT, PointOutT> > Ptr;
+  FPFHEstimation() { this->name_ = "FPFHEstimation"; }
+
+ protected:
+  void computeFeature(PointCloud<PointOutT>& out) override {
+    const PointCloud<PointInT>& surf = this->surface();
+    if (!this->normals_ || this->normals_->size() != surf.size()) {
+      PCL_ERROR("[pcl::FPFHEstimation::compute] normals missing or not matching the surface\n");
+      return;
+    }
+    const detail::SoA s = detail::soa_xyz(surf), nrm = detail::soa_normals(*this->normals_);
+    const detail::SoA q = detail::soa_xyz(*this->input_);
+    const size_t nq = this->input_->size();
+    std::vector<float> h(nq * 33);
+    if (!detail::ok(pfx_fpfh(detail::context(), s.x.data(), s.y.data(), s.z.data(), nrm.x.data(), nrm.y.data(),
+                             nrm.z.data(), (int64_t)surf.size(), q.x.data(), q.y.data(), q.z.data(), (int64_t)nq,
+                             this->input_is_surface() ? 1 : 0, this->search_radius_, h.data()),
+                    "FPFHEstimation"))
+      return;
+    out.resize(nq);
+    out.is_dense = true;
+    for (size_t i = 0; i < nq; ++i) {
+      for (int b = 0; b < 33; ++b) out.points[i].histogram[b] = h[i * 33 + b];
+      if (std::isnan(h[i * 33])) out.is_dense = false;
+    }
+  }
+};
+
+// SHOTEstimationOMP<In, Normal, SHOT352> + SHOTLocalReferenceFrameEstimation (evaluation.cpp:770)
+template <typename PointInT, typename PointNT, typename PointOutT = SHOT352,
+          typename PointRFT = ReferenceFrame>
+class SHOTEstimationOMP : public FeatureFromNormals<PointInT, PointNT, PointOutT> {
+ public:
+  typedef std::shared_ptr<SHOTEstimationOMP<PointInT, PointNT, PointOutT, PointRFT> > Ptr;
+  explicit SHOTEstimationOMP(unsigned int /*nr_threads*/ = 0) { this->name_ = "SHOTEstimationOMP"; }
+  void setNumberOfThreads(unsigned int) {}
+
+ protected:
+  void computeFeature(PointCloud<PointOutT>& out) override {
+    const PointCloud<PointInT>& surf = this->surface();
+    if (!this->normals_ || this->normals_->size() != surf.size()) {
+      PCL_ERROR("[pcl::SHOTEstimationOMP::compute] normals missing or not matching the surface\n");
+      return;
+    }
+    const detail::SoA s = detail::soa_xyz(surf), nrm = detail::soa_normals(*this->normals_);
+    const detail::SoA q = detail::soa_xyz(*this->input_);
+    const size_t nq = this->input_->size();
+    std::vector<float> d(nq * 352), rf(nq * 9);
+    if (!detail::ok(pfx_shot(detail::context(), s.x.data(), s.y.data(), s.z.data(), nrm.x.data(), nrm.y.data(),
+                             nrm.z.data(), (int64_t)surf.size(), q.x.data(), q.y.data(), q.z.data(), (int64_t)nq,
+                             this->search_radius_, d.data(), rf.data()),
+                    "SHOTEstimationOMP"))
+      return;
+    out.resize(nq);
+    out.is_dense = true;
+    for (size_t i = 0; i < nq; ++i) {
+      for (int b = 0; b < 352; ++b) out.points[i].descriptor[b] = d[i * 352 + b];
+      for (int b = 0; b < 9; ++b) out.points[i].rf[b] = rf[i * 9 + b];
+      if (std::isnan(d[i * 352])) out.is_dense = false;
+    }
+  }
+};
+
+// ---- range image + NARF (keypoints.h:203-224) ---------------------------------------------
+class RangeImage : public PointCloud<PointWithRange> {
+ public:
+  enum CoordinateFrame { CAMERA_FRAME = 0, LASER_FRAME = 1 };
+  virtual ~RangeImage() = default;
+};
+
+class RangeImagePlanar : public RangeImage {
+ public:
+  // Keeps the SoA cloud and the camera for the accelerated NARF pass and materialises the
+  // range image itself (PointWithRange per pixel, like PCL) through pfx_range_image_planar.
+  template <typename PointCloudType>
+  void createFromPointCloudWithFixedSize(const PointCloudType& cloud, int di_width, int di_height,
+                                         float di_center_x, float di_center_y, float di_focal_length_x,
+                                         float di_focal_length_y, const Eigen::Affine3f& sensor_pose,
+                                         CoordinateFrame coordinate_frame = CAMERA_FRAME,
+                                         float noise_level = 0.0f, float min_range = 0.0f) {
+    cloud_ = detail::soa_xyz(cloud);
+    pfx_camera_default(&cam_);
+    cam_.width = di_width; cam_.height = di_height;
+    cam_.center_x = di_center_x; cam_.center_y = di_center_y;
+    cam_.focal_length_x = di_focal_length_x; cam_.focal_length_y = di_focal_length_y;
+    for (int i = 0; i < 16; ++i) cam_.sensor_pose[i] = sensor_pose.m[i];
+    cam_.coordinate_frame = (int32_t)coordinate_frame;
+    cam_.noise_level = noise_level;
+    cam_.min_range = min_range;
+    width = (uint32_t)di_width;
+    height = (uint32_t)di_height;
+    points.clear();
+    if (!detail::context()) return;
+    std::vector<float> pr((size_t)di_width * di_height * 4);
+    if (!detail::ok(pfx_range_image_planar(detail::context(), cloud_.x.data(), cloud_.y.data(), cloud_.z.data(),
+                                           (int64_t)cloud_.x.size(), &cam_, pr.data()),
+                    "RangeImagePlanar"))
+      return;
+    points.resize((size_t)di_width * di_height);
+    for (size_t i = 0; i < points.size(); ++i) {
+      points[i].x = pr[4 * i]; points[i].y = pr[4 * i + 1]; points[i].z = pr[4 * i + 2];
+      points[i].range = pr[4 * i + 3];
+    }
+    is_dense = false;
+  }
+  const detail::SoA& source_cloud() const { return cloud_; }
+  const pfx_camera& camera() const { return cam_; }
+
+ private:
+  detail::SoA cloud_;
+  pfx_camera cam_;
+};
+
+class RangeImageBorderExtractor {
+ public:
+  struct Parameters {
+    int pixel_radius_borders = 3;
+    int pixel_radius_plane_extraction = 2;
+    int pixel_radius_border_direction = 2;
+    float minimum_border_probability = 0.8f;
+    int pixel_radius_principal_curvature = 2;
+  };
+  explicit RangeImageBorderExtractor(const RangeImage* = nullptr) {}
+  Parameters& getParameters() { return parameters_; }
+
+ private:
+  Parameters parameters_;
+};
+
+class NarfKeypoint {
+ public:
+  struct Parameters {
+    float support_size = -1.0f;
+    int max_no_of_interest_points = -1;
+    float min_distance_between_interest_points = 0.25f;
+    float optimal_distance_to_high_surface_change = 0.25f;
+    float min_interest_value = 0.45f;
+    float min_surface_change_score = 0.2f;
+    int optimal_range_image_patch_size = 10;
+    float distance_for_additional_points = 0.0f;
+    bool add_points_on_straight_edges = false;
+    bool do_non_maximum_suppression = true;
+    int no_of_polynomial_approximations_per_point = 0;
+    int max_no_of_threads = 1;
+    bool use_recursive_scale_reduction = false;
+    bool calculate_sparse_interest_image = true;
+  };
+  explicit NarfKeypoint(RangeImageBorderExtractor* border_extractor = nullptr, float support_size = -1.0f)
+      : border_extractor_(border_extractor) {
+    parameters_.support_size = support_size;
+  }
+  void setRangeImage(const RangeImage* range_image) {
+    range_image_ = dynamic_cast<const RangeImagePlanar*>(range_image);
+  }
+  Parameters& getParameters() { return parameters_; }
+  // NarfKeypoint::compute: ascending pixel indices of the keypoints
+  void compute(PointCloud<int>& out) {
+    out.clear();
+    if (!range_image_ || !(parameters_.support_size > 0.0f)) {
+      PCL_ERROR("[pcl::NarfKeypoint::compute] needs a RangeImagePlanar and support_size > 0\n");
+      return;
+    }
+    if (!detail::context()) return;
+    pfx_narf_params p;
+    pfx_narf_params_default(&p);
+    p.support_size = parameters_.support_size;
+    p.max_no_of_interest_points = parameters_.max_no_of_interest_points;
+    p.min_distance_between_interest_points = parameters_.min_distance_between_interest_points;
+    p.optimal_distance_to_high_surface_change = parameters_.optimal_distance_to_high_surface_change;
+    p.min_interest_value = parameters_.min_interest_value;
+    p.min_surface_change_score = parameters_.min_surface_change_score;
+    p.do_non_maximum_suppression = parameters_.do_non_maximum_suppression ? 1 : 0;
+    p.calculate_sparse_interest_image = parameters_.calculate_sparse_interest_image ? 1 : 0;
+    p.no_of_polynomial_approximations_per_point = parameters_.no_of_polynomial_approximations_per_point ? 1 : 0;
+    p.add_points_on_straight_edges = parameters_.add_points_on_straight_edges ? 1 : 0;
+    if (border_extractor_) {
+      const RangeImageBorderExtractor::Parameters& b = border_extractor_->getParameters();
+      p.pixel_radius_borders = b.pixel_radius_borders;
+      p.pixel_radius_plane_extraction = b.pixel_radius_plane_extraction;
+      p.pixel_radius_border_direction = b.pixel_radius_border_direction;
+      p.minimum_border_probability = b.minimum_border_probability;
+      p.pixel_radius_principal_curvature = b.pixel_radius_principal_curvature;
+    }
+    const detail::SoA& c = range_image_->source_cloud();
+    const pfx_camera cam = range_image_->camera();
+    std::vector<int32_t> idx((size_t)cam.width * cam.height);
+    int64_t k = 0;
+    if (!detail::ok(pfx_narf_keypoints(detail::context(), c.x.data(), c.y.data(), c.z.data(), (int64_t)c.x.size(),
+                                       &cam, &p, idx.data(), (int64_t)idx.size(), &k),
+                    "NarfKeypoint"))
+      return;
+    out.points.assign(idx.begin(), idx.begin() + k);
+    out.width = (uint32_t)k;
+    out.height = 1;
+  }
+
+ private:
+  RangeImageBorderExtractor* border_extractor_;
+  const RangeImagePlanar* range_image_ = nullptr;
+  Parameters parameters_;
+};
+
+}  // namespace pcl
+
+#endif  // PFX_PCL_HPP_

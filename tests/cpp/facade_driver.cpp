@@ -1,0 +1,149 @@
+// facade_driver.cpp -- the reference's NARF + Features flow written against include/pfx_pcl.hpp.
+//
+// Mirrors, call for call, include/pcl_feature_extraction/keypoints.h:199-231 (NARF branch),
+// features.h:175-196 (Features<T>::compute with the FeatureFromNormals probe) and tools.h:22-32
+// (estimateNormals), as src/evaluation.cpp:593-612 / :766-785 drive them.  Reads a PCL 1.7 binary
+// PCD (x y z rgb, 16 B per point), writes raw float/int arrays for tests/test_facade.py:
+//   facade_driver <cloud.pcd> <out_dir>
+//   -> keypoints.i32, normals.f32 (n x 4), fpfh.f32 (K x 33), shot.f32 (K x 352), shot_rf.f32 (K x 9)
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+#include <sstream>
+#include <string>
+
+#define PFX_PCL_BOOST_SHIM
+#include "pfx_pcl.hpp"
+
+using namespace pcl;
+typedef PointXYZRGB PointRGB;
+typedef PointCloud<PointRGB> PointCloudRGB;
+
+static bool read_pcd(const char* path, PointCloudRGB& c) {
+  std::ifstream f(path, std::ios::binary);
+  if (!f) return false;
+  std::string line;
+  size_t n = 0;
+  while (std::getline(f, line)) {
+    std::istringstream ss(line);
+    std::string key;
+    ss >> key;
+    if (key == "POINTS") ss >> n;
+    if (key == "DATA") {
+      std::string kind;
+      ss >> kind;
+      if (kind != "binary") return false;
+      break;
+    }
+  }
+  std::vector<float> raw(n * 4);
+  f.read(reinterpret_cast<char*>(raw.data()), (std::streamsize)(raw.size() * sizeof(float)));
+  if (!f) return false;
+  c.points.resize(n);
+  for (size_t i = 0; i < n; ++i) {
+    c.points[i].x = raw[4 * i]; c.points[i].y = raw[4 * i + 1]; c.points[i].z = raw[4 * i + 2];
+    c.points[i].rgb = raw[4 * i + 3];
+  }
+  c.width = (uint32_t)n;
+  c.height = 1;
+  return true;
+}
+
+template <typename T>
+static void dump(const std::string& path, const T* p, size_t count) {
+  FILE* f = std::fopen(path.c_str(), "wb");
+  if (f) { std::fwrite(p, sizeof(T), count, f); std::fclose(f); }
+}
+
+// tools.h:22-32
+static void estimateNormals(const PointCloudRGB::Ptr& cloud, PointCloud<Normal>::Ptr& normals, double radius) {
+  NormalEstimationOMP<PointRGB, Normal> normal_estimation_omp;
+  normal_estimation_omp.setInputCloud(cloud);
+  normal_estimation_omp.setRadiusSearch(radius);
+  search::KdTree<PointRGB>::Ptr kdtree_omp(new search::KdTree<PointRGB>);
+  normal_estimation_omp.setSearchMethod(kdtree_omp);
+  normal_estimation_omp.compute(*normals);
+}
+
+// features.h:175-196
+template <typename FeatureType>
+static void features_compute(typename Feature<PointRGB, FeatureType>::Ptr feature_extractor, double feat_radius,
+                             double normal_radius, const PointCloudRGB::Ptr cloud,
+                             const PointCloudRGB::Ptr keypoints, typename PointCloud<FeatureType>::Ptr& descriptors,
+                             PointCloud<Normal>::Ptr* normals_out = nullptr) {
+  typename FeatureFromNormals<PointRGB, Normal, FeatureType>::Ptr feature_from_normals =
+      boost::dynamic_pointer_cast<FeatureFromNormals<PointRGB, Normal, FeatureType> >(feature_extractor);
+  if (feature_from_normals) {
+    PointCloud<Normal>::Ptr normals(new PointCloud<Normal>);
+    estimateNormals(cloud, normals, normal_radius);
+    feature_from_normals->setInputNormals(normals);
+    if (normals_out) *normals_out = normals;
+  }
+  feature_extractor->setSearchSurface(cloud);
+  feature_extractor->setInputCloud(keypoints);
+  search::KdTree<PointRGB>::Ptr kdtree(new search::KdTree<PointRGB>);
+  feature_extractor->setSearchMethod(kdtree);
+  feature_extractor->setRadiusSearch(feat_radius);
+  feature_extractor->compute(*descriptors);
+}
+
+int main(int argc, char** argv) {
+  if (argc < 3) {
+    std::fprintf(stderr, "usage: %s cloud.pcd out_dir\n", argv[0]);
+    return 2;
+  }
+  PointCloudRGB::Ptr cloud(new PointCloudRGB);
+  if (!read_pcd(argv[1], *cloud)) {
+    std::fprintf(stderr, "cannot read %s\n", argv[1]);
+    return 2;
+  }
+  const std::string out = argv[2];
+
+  // ---- keypoints.h:199-231 (NARF) ----
+  int image_size_x = 640, image_size_y = 480;
+  float center_x = (640.0f / 2.0f), center_y = (480.0f / 2.0f);
+  float focal_length_x = 525.0f;
+  Eigen::Affine3f sensor_pose = Eigen::Affine3f(Eigen::Translation3f(cloud->sensor_origin_[0],
+                                                                     cloud->sensor_origin_[1],
+                                                                     cloud->sensor_origin_[2])) *
+                                Eigen::Affine3f(cloud->sensor_orientation_);
+  float noise_level = 0.0f, minimum_range = 0.0f;
+  RangeImagePlanar range_image;
+  range_image.createFromPointCloudWithFixedSize(*cloud, image_size_x, image_size_y, center_x, center_y,
+                                                focal_length_x, focal_length_x, sensor_pose,
+                                                RangeImage::CAMERA_FRAME, noise_level, minimum_range);
+  PointCloud<int>::Ptr keypoints(new PointCloud<int>);
+  RangeImageBorderExtractor border_extractor;
+  NarfKeypoint detector(&border_extractor);
+  detector.setRangeImage(&range_image);
+  detector.getParameters().support_size = 0.2f;
+  detector.compute(*keypoints);
+  PointCloudRGB::Ptr cloud_keypoints(new PointCloudRGB);
+  for (size_t i = 0; i < keypoints->points.size(); ++i)
+    if ((size_t)keypoints->points[i] < cloud->size())  // keypoints.h:229 indexes the cloud by pixel index
+      cloud_keypoints->points.push_back(cloud->points[keypoints->points[i]]);
+  dump(out + "/keypoints.i32", keypoints->points.data(), keypoints->points.size());
+
+  // ---- evaluation.cpp:593-612 (FPFH, r 0.08, normals r 0.05) ----
+  Feature<PointRGB, FPFHSignature33>::Ptr fpfh(new FPFHEstimation<PointRGB, Normal, FPFHSignature33>);
+  PointCloud<FPFHSignature33>::Ptr fdesc(new PointCloud<FPFHSignature33>);
+  PointCloud<Normal>::Ptr normals;
+  features_compute<FPFHSignature33>(fpfh, 0.08, 0.05, cloud, cloud_keypoints, fdesc, &normals);
+  dump(out + "/normals.f32", reinterpret_cast<const float*>(normals->points.data()), normals->size() * 8);
+  dump(out + "/fpfh.f32", reinterpret_cast<const float*>(fdesc->points.data()), fdesc->size() * 33);
+
+  // ---- evaluation.cpp:766-785 (SHOT, r 0.08) ----
+  Feature<PointRGB, SHOT352>::Ptr shot(new SHOTEstimationOMP<PointRGB, Normal, SHOT352>);
+  PointCloud<SHOT352>::Ptr sdesc(new PointCloud<SHOT352>);
+  features_compute<SHOT352>(shot, 0.08, 0.05, cloud, cloud_keypoints, sdesc);
+  std::vector<float> d, rf;
+  for (const SHOT352& s : sdesc->points) {
+    d.insert(d.end(), s.descriptor, s.descriptor + 352);
+    rf.insert(rf.end(), s.rf, s.rf + 9);
+  }
+  dump(out + "/shot.f32", d.data(), d.size());
+  dump(out + "/shot_rf.f32", rf.data(), rf.size());
+  std::printf("points %zu keypoints %zu fpfh %zu shot %zu\n", cloud->size(), keypoints->size(), fdesc->size(),
+              sdesc->size());
+  return 0;
+}

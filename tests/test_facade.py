@@ -1,0 +1,56 @@
+"""The C++ PCL-compatible facade (include/pfx_pcl.hpp): tests/cpp/facade_driver.cpp writes the
+reference's NARF + Features<T> flow (keypoints.h:199-231, features.h:175-196, tools.h:22-32) against
+it.  CPU: the driver compiles and links against libpfx.so.  GPU: its outputs equal the Python
+C-ABI path (itself bit-exact against the oracle) on a reference cloud."""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SRC = os.path.join(ROOT, "tests", "cpp", "facade_driver.cpp")
+EXE = os.path.join(ROOT, "tests", "cpp", "build", "facade_driver")
+PCD = os.path.join(ROOT, "tests", "golden", "clouds", "indoor_source.pcd")
+
+
+def build_driver():
+    os.makedirs(os.path.dirname(EXE), exist_ok=True)
+    lib = os.path.join(ROOT, "pcl_feature_extraction_amd")
+    cmd = ["g++", "-std=c++14", "-O2", "-Wall", "-Wextra", "-Werror", "-I", os.path.join(ROOT, "include"), SRC,
+           "-L", lib, "-lpfx", f"-Wl,-rpath,{lib}", "-o", EXE]
+    subprocess.run(cmd, check=True, capture_output=True, text=True)
+    return EXE
+
+
+def test_facade_compiles_and_links():
+    exe = build_driver()
+    assert os.access(exe, os.X_OK)
+
+
+@pytest.mark.gpu
+def test_facade_matches_c_abi(ctx, tmp_path):
+    from pcl_feature_extraction_amd.pcd import read_pcd
+    exe = build_driver()
+    r = subprocess.run([exe, PCD, str(tmp_path)], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    c = read_pcd(PCD)
+    x, y, z = c.x, c.y, c.z
+    kp = np.fromfile(tmp_path / "keypoints.i32", np.int32)
+    assert np.array_equal(kp, np.asarray(ctx.narf_keypoints(x, y, z), np.int32))
+    nrm = np.fromfile(tmp_path / "normals.f32", np.float32).reshape(-1, 8)
+    want = np.stack(ctx.normals(x, y, z, 0.05))
+    got = nrm[:, [0, 1, 2, 4]].T
+    assert np.array_equal(np.isnan(got), np.isnan(want))
+    ok = ~np.isnan(want)
+    assert np.array_equal(got[ok].view(np.uint32), want[ok].view(np.uint32))
+    rows = kp[kp < len(x)]
+    fp = np.fromfile(tmp_path / "fpfh.f32", np.float32).reshape(-1, 33)
+    wf = ctx.fpfh(x, y, z, want[0], want[1], want[2], x[rows], y[rows], z[rows], 0.08)
+    assert fp.shape == wf.shape
+    assert np.array_equal(np.nan_to_num(fp, nan=-1.0).view(np.uint32), np.nan_to_num(wf, nan=-1.0).view(np.uint32))
+    sd = np.fromfile(tmp_path / "shot.f32", np.float32).reshape(-1, 352)
+    wd, _ = ctx.shot(x, y, z, want[0], want[1], want[2], x[rows], y[rows], z[rows], 0.08)
+    assert sd.shape == wd.shape
+    ok = ~np.isnan(wd).any(1)
+    assert np.linalg.norm(sd[ok].astype(np.float64) - wd[ok], axis=1).max() <= 1e-4
