@@ -34,13 +34,13 @@ enum {
 struct NarfState {
   int w = 0, h = 0;
   DevBuf direct, fill, pts, surf, svalid, sL, sR, sT, sB, uL, uR, uT, uB, shadow, traits, rawdir, dir, scs, scd,
-      interest, cand, counters, sat;
+      interest, cand, counters, sat, work, fb1;
   std::vector<float> h_interest, h_scs, h_range;
   std::vector<uint32_t> h_traits;
   bool have_debug = false;
   void release() {
     DevBuf* all[] = {&direct, &fill, &pts, &surf, &svalid, &sL, &sR, &sT, &sB, &uL, &uR, &uT, &uB, &shadow,
-                     &traits, &rawdir, &dir, &scs, &scd, &interest, &cand, &counters, &sat};
+                     &traits, &rawdir, &dir, &scs, &scd, &interest, &cand, &counters, &sat, &work, &fb1};
     for (auto* b : all) b->release();
   }
 };
@@ -540,9 +540,10 @@ __device__ __forceinline__ float norm_angle(float a) {
   return a >= 0 ? fmodf(a + pi, 2.0f * pi) - pi : -(fmodf(pi - a, 2.0f * pi) - pi);
 }
 
-// Row prefix counts of "contributing" pixels (valid, not shadow/veil, scs >= min_scs): a pixel
-// whose region-grow window holds none of them has interest exactly 0 (no histogram entry, no
-// negative score: 1 * sqrt(0)), so it skips the region grow.  rowp is h x (w+1).
+// Row prefix counts of "contributing" pixels (valid, not shadow/veil, scs >= thr): with
+// thr = min_scs a pixel whose region-grow window holds none of them has interest exactly 0 (no
+// histogram entry, no negative score: 1 * sqrt(0)), so it skips the region grow; the sparse mode
+// raises thr (see narf_dev).  rowp is h x (w+1).
 __global__ void k_contrib_rows(Img I, const float4* __restrict__ P, const uint32_t* __restrict__ traits,
                                const float* __restrict__ scs, float min_scs, int* __restrict__ rowp) {
   __shared__ int part[1024];
@@ -609,22 +610,88 @@ struct InterestParams {
   double R;  // search radius for the window bound
 };
 
+// region-grow window of pixel (x, y): |du| <= fx R (tz + |tx|) / ((tz - R) tz) (+3 px margin
+// for touched neighbours), the whole image when the point is within ~R of the sensor plane
+__device__ __forceinline__ void interest_window(const Img& I, float4 point, int x, int y, double R, int& x0,
+                                                int& y0, int& ww, int& wh) {
+  x0 = 0; y0 = 0; ww = I.w; wh = I.h;
+  const f3 t = aff_apply(I.to_ri, mk3(point.x, point.y, point.z));
+  const double tz = t.z;
+  if (!(tz > 1.02 * R)) return;
+  const double den = (tz - R) * tz;
+  const double wx = (double)I.fx * R * (tz + fabs((double)t.x)) / den * 1.01 + 3.0;
+  const double wy = (double)I.fy * R * (tz + fabs((double)t.y)) / den * 1.01 + 3.0;
+  const int hx = wx > 1e6 ? 1000000 : (int)ceil(wx), hy = wy > 1e6 ? 1000000 : (int)ceil(wy);
+  x0 = max(0, x - hx); y0 = max(0, y - hy);
+  ww = min(I.w - 1, x + hx) - x0 + 1;
+  wh = min(I.h - 1, y + hy) - y0 + 1;
+}
+
+// NarfKeypoint's per-pixel contribution of an accepted pixel with scs >= min_scs: histogram
+// maximum of the positive score per direction cell, minimum of the negative score (both
+// order-free, LDS atomics on float bit patterns of non-negative values)
+__device__ __forceinline__ void contribute(const InterestParams& ip, float sc, float4 dv, float d2, float pd, f3 tmp0,
+                                           f3 tmp1, f3 tmp2, unsigned* hist, unsigned* neg_bits) {
+  const f3 dir = mk3(dv.x, dv.y, dv.z);
+  const float distance = sqrtf(d2);
+  const float df = ip.radius_reciprocal * distance;
+  float neg = 1.0f - 0.5f * sc * fmaxf(1.0f - df / ip.opt_dist, 0.0f);
+  neg = neg * neg;
+  const float pos = (pd < 2.0f) ? sc : sc * (1.0f - df);
+  const f3 rot = mk3(0.0f + dot3(tmp0, dir), 0.0f + dot3(tmp1, dir), 0.0f + dot3(tmp2, dir));
+  const float nrm = sqrtf(rot.x * rot.x + rot.y * rot.y);
+  const float dvx = rot.x / nrm;
+  const int cell = angle_cell(dvx, ip.d90, ip.d180);
+  if (pos > 0.0f) atomicMax(&hist[cell], __float_as_uint(pos));
+  if (neg < 1.0f) atomicMin(neg_bits, __float_as_uint(neg));
+}
+
+// interest = negative score * sqrt(max over cell pairs of h1 h2 normalised angle distance)
+__device__ __forceinline__ float interest_value(const unsigned* hist, unsigned neg_bits) {
+  float h[18];
+  for (int c = 0; c < 18; ++c) h[c] = __uint_as_float(hist[c]);
+  float acv = 0.0f;
+  for (int c1 = 0; c1 < 17; ++c1) {
+    if (h[c1] == 0.0f) continue;
+    for (int c2 = c1 + 1; c2 < 18; ++c2) {
+      if (h[c2] == 0.0f) continue;
+      float nd = 2.0f * (float)(c2 - c1) / (float)18;
+      nd = (nd <= 1.0f ? nd : 2.0f - nd);
+      float v = h[c1] * h[c2] * nd;
+      acv = (v < acv) ? acv : v;
+    }
+  }
+  acv = sqrtf(acv);
+  return __uint_as_float(neg_bits) * acv;
+}
+
+// rotation to the viewer frame: getTransFromUnitVectorsZY(view, (0,-1,0))
+__device__ __forceinline__ void viewer_frame(const Img& I, float4 point, f3& tmp0, f3& tmp1, f3& tmp2) {
+  const f3 sensor = mk3(I.to_world.m[3], I.to_world.m[7], I.to_world.m[11]);
+  const f3 view = normalized3(sub3(mk3(point.x, point.y, point.z), sensor));
+  tmp0 = normalized3(cross3(mk3(0.0f, -1.0f, 0.0f), view));
+  tmp1 = normalized3(cross3(view, tmp0));
+  tmp2 = normalized3(view);
+}
+
 template <int WORDS, bool FULL>
 __global__ void __launch_bounds__(64) k_interest(Img I, const float4* __restrict__ P, const uint32_t* __restrict__ traits,
                                                  const float* __restrict__ scs, const float4* __restrict__ scd,
                                                  const int* __restrict__ sat, InterestParams ip,
-                                                 const int* __restrict__ list, int nlist,
+                                                 const int* __restrict__ list, const int* __restrict__ n_list,
                                                  float* __restrict__ interest, int* __restrict__ fallback,
-                                                 int* __restrict__ n_fallback, int* __restrict__ err) {
+                                                 int* __restrict__ n_fallback, int* __restrict__ err,
+                                                 unsigned long long* __restrict__ work) {
   __shared__ uint32_t bitmap[WORDS];
   __shared__ int queue[kQueue];
   __shared__ unsigned hist[18];
   __shared__ unsigned neg_bits;
   const int lane = threadIdx.x;
-  const int npx = FULL ? nlist : I.w * I.h;
+  const int npx = list ? *n_list : I.w * I.h;
   const uint32_t skip = TB(T_SHADOW_BORDER) | TB(T_VEIL_POINT);
+  unsigned long long n_grown = 0, n_window = 0, n_visits = 0;  // lane 0: region-grow statistics
   for (int it = blockIdx.x; it < npx; it += gridDim.x) {
-    const int index = FULL ? list[it] : it;
+    const int index = list ? list[it] : it;
     const float4 point = P[index];
     if (!isfinite(point.w) || (traits[index] & skip)) {
       if (lane == 0) interest[index] = 0.0f;
@@ -632,20 +699,7 @@ __global__ void __launch_bounds__(64) k_interest(Img I, const float4* __restrict
     }
     const int y = index / I.w, x = index - y * I.w;
     int x0 = 0, y0 = 0, ww = I.w, wh = I.h;
-    if (!FULL) {
-      const f3 t = aff_apply(I.to_ri, mk3(point.x, point.y, point.z));
-      const double tz = t.z, R = ip.R;
-      bool whole = !(tz > 1.02 * R);
-      if (!whole) {
-        const double den = (tz - R) * tz;
-        const double wx = (double)I.fx * R * (tz + fabs((double)t.x)) / den * 1.01 + 3.0;
-        const double wy = (double)I.fy * R * (tz + fabs((double)t.y)) / den * 1.01 + 3.0;
-        const int hx = wx > 1e6 ? 1000000 : (int)ceil(wx), hy = wy > 1e6 ? 1000000 : (int)ceil(wy);
-        x0 = max(0, x - hx); y0 = max(0, y - hy);
-        ww = min(I.w - 1, x + hx) - x0 + 1;
-        wh = min(I.h - 1, y + hy) - y0 + 1;
-      }
-    }
+    if (!FULL) interest_window(I, point, x, y, ip.R, x0, y0, ww, wh);
     if (!window_contributes(I, sat, x0, y0, ww, wh, lane)) {  // nothing can contribute: interest 0
       if (lane == 0) interest[index] = 0.0f;
       continue;
@@ -654,14 +708,11 @@ __global__ void __launch_bounds__(64) k_interest(Img I, const float4* __restrict
       if (lane == 0) fallback[atomicAdd(n_fallback, 1)] = index;
       continue;
     }
+    if (lane == 0) { n_grown += 1; n_window += (unsigned long long)ww * wh; }
     const int nwords = (ww * wh + 31) >> 5;
     for (int k = lane; k < nwords; k += 64) bitmap[k] = 0u;
-    // rotation to the viewer frame: getTransFromUnitVectorsZY(view, (0,-1,0))
-    const f3 sensor = mk3(I.to_world.m[3], I.to_world.m[7], I.to_world.m[11]);
-    const f3 view = normalized3(sub3(mk3(point.x, point.y, point.z), sensor));
-    const f3 tmp0 = normalized3(cross3(mk3(0.0f, -1.0f, 0.0f), view));
-    const f3 tmp1 = normalized3(cross3(view, tmp0));
-    const f3 tmp2 = normalized3(view);
+    f3 tmp0, tmp1, tmp2;
+    viewer_frame(I, point, tmp0, tmp1, tmp2);
     if (lane < 18) hist[lane] = 0u;
     __syncthreads();
     if (lane == 0) {
@@ -711,21 +762,7 @@ __global__ void __launch_bounds__(64) k_interest(Img I, const float4* __restrict
       }
       if (ok) {
         const float sc = scs[index2];
-        if (sc >= ip.min_scs) {  // contributions are max / min: order-free
-          const float4 dv = scd[index2];
-          const f3 dir = mk3(dv.x, dv.y, dv.z);
-          const float distance = sqrtf(d2);
-          const float df = ip.radius_reciprocal * distance;
-          float neg = 1.0f - 0.5f * sc * fmaxf(1.0f - df / ip.opt_dist, 0.0f);
-          neg = neg * neg;
-          const float pos = (pd < 2.0f) ? sc : sc * (1.0f - df);
-          const f3 rot = mk3(0.0f + dot3(tmp0, dir), 0.0f + dot3(tmp1, dir), 0.0f + dot3(tmp2, dir));
-          const float nrm = sqrtf(rot.x * rot.x + rot.y * rot.y);
-          const float dvx = rot.x / nrm;
-          const int cell = angle_cell(dvx, ip.d90, ip.d180);
-          if (pos > 0.0f) atomicMax(&hist[cell], __float_as_uint(pos));
-          if (neg < 1.0f) atomicMin(&neg_bits, __float_as_uint(neg));
-        }
+        if (sc >= ip.min_scs) contribute(ip, sc, scd[index2], d2, pd, tmp0, tmp1, tmp2, hist, &neg_bits);
       }
       head += take;
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -737,23 +774,178 @@ __global__ void __launch_bounds__(64) k_interest(Img I, const float4* __restrict
     }
     __syncthreads();
     if (lane == 0) {
-      float h[18];
-      for (int c = 0; c < 18; ++c) h[c] = __uint_as_float(hist[c]);
-      float acv = 0.0f;
-      for (int c1 = 0; c1 < 17; ++c1) {
-        if (h[c1] == 0.0f) continue;
-        for (int c2 = c1 + 1; c2 < 18; ++c2) {
-          if (h[c2] == 0.0f) continue;
-          float nd = 2.0f * (float)(c2 - c1) / (float)18;
-          nd = (nd <= 1.0f ? nd : 2.0f - nd);
-          float v = h[c1] * h[c2] * nd;
-          acv = (v < acv) ? acv : v;
-        }
-      }
-      acv = sqrtf(acv);
-      interest[index] = __uint_as_float(neg_bits) * acv;
+      interest[index] = interest_value(hist, neg_bits);
+      n_visits += (unsigned long long)tail;
     }
     __syncthreads();
+  }
+  if (lane == 0 && work && n_grown) {
+    atomicAdd(&work[0], n_grown);
+    atomicAdd(&work[1], n_window);
+    atomicAdd(&work[2], n_visits);
+  }
+}
+
+// ---- flood-fill region grow (windows of <= 128 rows x <= 128 columns) ---------------------
+// Lane l holds rows l and l + 64 of the window, each as two 64-bit masks: A = pixels the region
+// grow accepts (valid, not shadow/veil, within 2 px or R of p) and C = accepted pixels that
+// contribute (scs >= min_scs).  PCL's breadth-first grow accepts exactly the 8-connected
+// component of p in A, obtained here by R <- dilate3x3(R) & A until stable (bit shifts within a
+// row, lane shuffles across rows).  Larger windows go to the queue-based k_interest.
+struct Rows2 {  // [half h: rows l + 64 h][word w: columns 64 w .. 64 w + 63]
+  uint64_t m00 = 0, m01 = 0, m10 = 0, m11 = 0;
+};
+
+// horizontal 3-dilation of one row held as (lo, hi) words
+__device__ __forceinline__ void hdil(uint64_t lo, uint64_t hi, uint64_t& dlo, uint64_t& dhi) {
+  dlo = lo | (lo << 1) | (lo >> 1) | (hi << 63);
+  dhi = hi | (hi << 1) | (hi >> 1) | (lo >> 63);
+}
+
+__global__ void __launch_bounds__(64) k_interest_ff(Img I, const float4* __restrict__ P,
+                                                    const uint32_t* __restrict__ traits,
+                                                    const float* __restrict__ scs, const float4* __restrict__ scd,
+                                                    const int* __restrict__ rowp, InterestParams ip,
+                                                    float* __restrict__ interest, int* __restrict__ fallback,
+                                                    int* __restrict__ n_fallback, int* __restrict__ err,
+                                                    unsigned long long* __restrict__ work) {
+  __shared__ unsigned hist[18];
+  __shared__ unsigned neg_bits;
+  const int lane = threadIdx.x;
+  const int npx = I.w * I.h;
+  const uint32_t skip = TB(T_SHADOW_BORDER) | TB(T_VEIL_POINT);
+  unsigned long long n_grown = 0, n_window = 0, n_visits = 0;
+  for (int index = blockIdx.x; index < npx; index += gridDim.x) {
+    const float4 point = P[index];
+    if (!isfinite(point.w) || (traits[index] & skip)) {
+      if (lane == 0) interest[index] = 0.0f;
+      continue;
+    }
+    const int y = index / I.w, x = index - y * I.w;
+    int x0, y0, ww, wh;
+    interest_window(I, point, x, y, ip.R, x0, y0, ww, wh);
+    if (!window_contributes(I, rowp, x0, y0, ww, wh, lane)) {  // nothing can contribute: interest 0
+      if (lane == 0) interest[index] = 0.0f;
+      continue;
+    }
+    if (wh > 128 || ww > 128) {
+      if (lane == 0) fallback[atomicAdd(n_fallback, 1)] = index;
+      continue;
+    }
+    // acceptance / contribution masks, one row per iteration (lanes = columns)
+    Rows2 A, C;
+    for (int r = 0; r < wh; ++r) {
+      const int yy = y0 + r;
+      const bool mine = lane == (r & 63), hi = r >= 64;
+      for (int wd = 0; wd * 64 < ww; ++wd) {
+        const int c = wd * 64 + lane;
+        bool acc = false, con = false;
+        if (c < ww) {
+          const int idx2 = yy * I.w + x0 + c;
+          const float4 p2 = P[idx2];
+          acc = isfinite(p2.w) && !(traits[idx2] & skip);
+          const float pd = (float)max(abs(x0 + c - x), abs(yy - y));
+          const float d2 = sq_dist(point, p2);
+          if (acc && pd > 2.0f && d2 > ip.radius_squared) acc = false;
+          con = acc && scs[idx2] >= ip.min_scs;
+        }
+        const uint64_t ma = __ballot(acc), mc = __ballot(con);
+        if (mine) {
+          if (!hi && wd == 0) { A.m00 = ma; C.m00 = mc; }
+          if (!hi && wd == 1) { A.m01 = ma; C.m01 = mc; }
+          if (hi && wd == 0) { A.m10 = ma; C.m10 = mc; }
+          if (hi && wd == 1) { A.m11 = ma; C.m11 = mc; }
+        }
+      }
+    }
+    // 8-connected component of p in A
+    Rows2 R;
+    {
+      const int ry = y - y0, rx = x - x0;
+      if (lane == (ry & 63)) {
+        const uint64_t bit = 1ull << (rx & 63);
+        if (ry < 64) { if (rx < 64) R.m00 = bit; else R.m01 = bit; }
+        else { if (rx < 64) R.m10 = bit; else R.m11 = bit; }
+      }
+    }
+    while (true) {
+      uint64_t h00, h01, h10, h11;
+      hdil(R.m00, R.m01, h00, h01);
+      hdil(R.m10, R.m11, h10, h11);
+      // row above: lane-1 of the same half; lane 0 of the upper half takes lane 63 of the lower
+      uint64_t u00 = __shfl_up(h00, 1), u01 = __shfl_up(h01, 1), u10 = __shfl_up(h10, 1), u11 = __shfl_up(h11, 1);
+      const uint64_t l63_0 = __shfl(h00, 63), l63_1 = __shfl(h01, 63);
+      const uint64_t f0_0 = __shfl(h10, 0), f0_1 = __shfl(h11, 0);
+      uint64_t d00 = __shfl_down(h00, 1), d01 = __shfl_down(h01, 1), d10 = __shfl_down(h10, 1), d11 = __shfl_down(h11, 1);
+      if (lane == 0) { u00 = 0; u01 = 0; u10 = l63_0; u11 = l63_1; }
+      if (lane == 63) { d00 = f0_0; d01 = f0_1; d10 = 0; d11 = 0; }
+      Rows2 N;
+      N.m00 = (h00 | u00 | d00) & A.m00;
+      N.m01 = (h01 | u01 | d01) & A.m01;
+      N.m10 = (h10 | u10 | d10) & A.m10;
+      N.m11 = (h11 | u11 | d11) & A.m11;
+      const bool changed = N.m00 != R.m00 || N.m01 != R.m01 || N.m10 != R.m10 || N.m11 != R.m11;
+      R = N;
+      if (!__ballot(changed)) break;
+    }
+    // checked invariant: the component stays strictly inside the window (unless at the image edge)
+    {
+      const uint64_t last0 = (ww <= 64) ? (1ull << (ww - 1)) : 0ull;
+      const uint64_t last1 = (ww > 64) ? (1ull << (ww - 65)) : 0ull;
+      const uint64_t row_lo = R.m00 | R.m01, row_hi = R.m10 | R.m11;
+      bool edge = false;
+      if (y0 > 0 && lane == 0) edge |= row_lo != 0;
+      if (y0 + wh < I.h && lane == ((wh - 1) & 63)) edge |= (wh - 1 < 64 ? row_lo : row_hi) != 0;
+      if (x0 > 0) edge |= ((R.m00 | R.m10) & 1ull) != 0;
+      if (x0 + ww < I.w) edge |= (((R.m00 | R.m10) & last0) | ((R.m01 | R.m11) & last1)) != 0;
+      if (__ballot(edge) && lane == 0) atomicOr(err, 2);
+    }
+    // contributions of the accepted contributing pixels
+    f3 tmp0, tmp1, tmp2;
+    viewer_frame(I, point, tmp0, tmp1, tmp2);
+    if (lane < 18) hist[lane] = 0u;
+    if (lane == 0) neg_bits = __float_as_uint(1.0f);
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+      const uint64_t M0 = half ? (R.m10 & C.m10) : (R.m00 & C.m00);
+      const uint64_t M1 = half ? (R.m11 & C.m11) : (R.m01 & C.m01);
+      uint64_t rows = __ballot((M0 | M1) != 0);
+      while (rows) {
+        const int r = __builtin_ctzll(rows);
+        rows &= rows - 1;
+        const uint64_t m0 = __shfl(M0, r), m1 = __shfl(M1, r);
+        for (int wd = 0; wd < 2; ++wd) {
+          const uint64_t m = wd ? m1 : m0;
+          if (!((m >> lane) & 1ull)) continue;
+          const int xx = x0 + wd * 64 + lane, yy = y0 + 64 * half + r;
+          const int idx2 = yy * I.w + xx;
+          const float4 p2 = P[idx2];
+          const float pd = (float)max(abs(xx - x), abs(yy - y));
+          contribute(ip, scs[idx2], scd[idx2], sq_dist(point, p2), pd, tmp0, tmp1, tmp2, hist, &neg_bits);
+        }
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    const int accepted = __popcll(R.m00) + __popcll(R.m01) + __popcll(R.m10) + __popcll(R.m11);
+    int tot = accepted;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o);
+    if (lane == 0) {
+      interest[index] = interest_value(hist, neg_bits);
+      n_grown += 1;
+      n_window += (unsigned long long)ww * wh;
+      n_visits += (unsigned long long)tot;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+  }
+  if (lane == 0 && work && n_grown) {
+    atomicAdd(&work[0], n_grown);
+    atomicAdd(&work[1], n_window);
+    atomicAdd(&work[2], n_visits);
   }
 }
 
@@ -928,11 +1120,24 @@ int64_t narf_dev(pfx_ctx* ctx, const float* x, const float* y, const float* z, i
   ip.R = search_radius;
   PFX_HIP(hipMemsetAsync(counters, 0, 4 * sizeof(int), st));
   int* sat = S.sat.as<int>((I.w + 1) * I.h);
+  unsigned long long* work = S.work.as<unsigned long long>(4);
+  PFX_HIP(hipMemsetAsync(work, 0, 4 * sizeof(unsigned long long), st));
   {
     TimeScope ts(ctx, "narf_interest");
-    k_contrib_rows<<<I.h, 1024, 0, st>>>(I, P, traits, scs, ip.min_scs, sat);
-    k_interest<kWinWords, false><<<256 * 10, 64, 0, st>>>(I, P, traits, scs, scd, sat, ip, nullptr, 0, interest,
-                                                           cand, counters + 2, counters + 1);
+    // calculate_sparse_interest_image (PCL default): a pixel can only reach min_interest_value
+    // if a contributing pixel with scs >= min_interest_value lies in its region (interest =
+    // neg * sqrt(max h1 h2 nd) <= max scs, neg <= 1); pixels without one keep interest 0, which
+    // changes no keypoint (NMS and selection only look at pixels >= min_interest_value).
+    const float thr = p.calculate_sparse_interest_image
+                          ? std::max(ip.min_scs, p.min_interest_value * 0.9999f) : ip.min_scs;
+    k_contrib_rows<<<I.h, 1024, 0, st>>>(I, P, traits, scs, thr, sat);
+    int* fb1 = S.fb1.as<int>(npx);
+    k_interest_ff<<<256 * 16, 64, 0, st>>>(I, P, traits, scs, scd, sat, ip, interest, fb1, counters + 3,
+                                            counters + 1, work);
+    check_launch("k_interest_ff");
+    // windows beyond the flood-fill masks: queue-based grow in a windowed LDS bitmap
+    k_interest<kWinWords, false><<<256 * 4, 64, 0, st>>>(I, P, traits, scs, scd, sat, ip, fb1, counters + 3,
+                                                          interest, cand, counters + 2, counters + 1, work);
     check_launch("k_interest");
     int nfb = 0;
     PFX_HIP(hipMemcpyAsync(&nfb, counters + 2, sizeof(int), hipMemcpyDeviceToHost, st));
@@ -940,8 +1145,8 @@ int64_t narf_dev(pfx_ctx* ctx, const float* x, const float* y, const float* z, i
     ctx->stats["narf_interest_fullimage"] = nfb;
     if (nfb > 0) {
       k_interest<kFullWords, true><<<std::min(nfb, 256 * 3), 64, 0, st>>>(I, P, traits, scs, scd, sat, ip, cand,
-                                                                          nfb, interest, nullptr, nullptr,
-                                                                          counters + 1);
+                                                                          counters + 2, interest, nullptr, nullptr,
+                                                                          counters + 1, work);
       check_launch("k_interest_full");
     }
   }
@@ -951,8 +1156,14 @@ int64_t narf_dev(pfx_ctx* ctx, const float* x, const float* y, const float* z, i
     check_launch("k_nms");
   }
   int h_cnt[4];
+  unsigned long long h_work[4];
   PFX_HIP(hipMemcpyAsync(h_cnt, counters, sizeof(h_cnt), hipMemcpyDeviceToHost, st));
+  PFX_HIP(hipMemcpyAsync(h_work, work, sizeof(h_work), hipMemcpyDeviceToHost, st));
   PFX_HIP(hipStreamSynchronize(st));
+  ctx->stats["narf_interest_grown"] = (int64_t)h_work[0];
+  ctx->stats["narf_interest_queue_grown"] = h_cnt[3];
+  ctx->stats["narf_interest_window_px"] = (int64_t)h_work[1];
+  ctx->stats["narf_interest_visits"] = (int64_t)h_work[2];
   if (h_cnt[1] & 1) throw Error(PFX_ERR_CAPACITY, "narf: interest region-grow queue overflow");
   if (h_cnt[1] & 2) throw Error(PFX_ERR_DEVICE, "narf: interest region left its window bound (internal error)");
   const int nc = h_cnt[0];

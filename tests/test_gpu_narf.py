@@ -41,15 +41,26 @@ def test_range_image_bit_exact(ctx, name):
 
 @pytest.mark.parametrize("name", CLOUDS)
 def test_narf_keypoints_bit_exact(ctx, name):
+    from pcl_feature_extraction_amd import narf_params
     x, y, z = _cloud(name)
-    kp = ctx.narf_keypoints(x, y, z)
     okp, dbg = O.narf_keypoints(x, y, z, debug=True)
+    # dense interest image (calculate_sparse_interest_image = false): every pixel bit-exact
+    kp_dense = ctx.narf_keypoints(x, y, z, params=narf_params(calculate_sparse_interest_image=0))
     traits = ctx.narf_debug_image("border_traits")
     scs = ctx.narf_debug_image("surface_change")
     interest = ctx.narf_debug_image("interest")
     assert np.array_equal(traits, dbg["border_traits"]), "border traits differ"
     assert _same(scs, dbg["surface_change"]), "surface change scores differ"
     assert _same(interest, dbg["interest"]), "interest image differs"
+    assert np.array_equal(kp_dense, okp)
+    # PCL's default sparse mode: same keypoints; the interest image is exact wherever it can
+    # reach min_interest_value and 0 (skipped) or exact elsewhere
+    kp = ctx.narf_keypoints(x, y, z)
+    sparse = np.asarray(ctx.narf_debug_image("interest"), np.float32).ravel()
+    dense = np.asarray(dbg["interest"], np.float32).ravel()
+    hi = dense >= 0.45
+    assert np.array_equal(sparse[hi].view(np.uint32), dense[hi].view(np.uint32))
+    assert np.all((sparse[~hi] == 0) | (sparse[~hi] == dense[~hi]) | (np.isnan(sparse[~hi]) & np.isnan(dense[~hi])))
     assert np.array_equal(kp, okp)
     assert len(kp) > 0
     assert np.all(np.diff(kp) > 0)  # ascending pixel indices
