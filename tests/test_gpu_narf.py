@@ -79,3 +79,26 @@ def test_narf_points_behind_camera_ignored(ctx):
     zb = np.concatenate([z, -z[:5000]])
     assert _same(ctx.range_image_planar(xb, yb, zb), O.range_image_planar(x, y, z))
     assert np.array_equal(ctx.narf_keypoints(xb, yb, zb), O.narf_keypoints(x, y, z))
+
+
+def test_narf_every_region_grow_path(ctx):
+    """Near-sensor points give region-grow windows beyond the flood-fill masks (> 128 px: queue
+    grow in a windowed LDS bitmap) and beyond that bitmap (whole-image grow); the dense interest
+    image must stay bit-exact on all three paths."""
+    from pcl_feature_extraction_amd import narf_params
+    from pcl_feature_extraction_amd.synth import synth_room
+    x, y, z, _ = synth_room(40_000, 11)
+    rng = np.random.default_rng(12)
+    # a small box 0.16-0.5 m in front of the sensor: corners and edges (high surface change)
+    u = rng.uniform(-0.03, 0.03, (3000, 2))
+    near = np.c_[u, rng.choice([0.16, 0.5], 3000)].astype(np.float32)
+    side = np.c_[np.full(1500, 0.03), rng.uniform(-0.03, 0.03, 1500), rng.uniform(0.16, 0.5, 1500)]
+    pts = np.concatenate([np.c_[x, y, z], near, side.astype(np.float32)]).astype(np.float32)
+    x, y, z = pts[:, 0].copy(), pts[:, 1].copy(), pts[:, 2].copy()
+    dense = narf_params(calculate_sparse_interest_image=0)
+    kp = ctx.narf_keypoints(x, y, z, params=dense)
+    assert ctx.stat("narf_interest_queue_grown") > 0
+    assert ctx.stat("narf_interest_fullimage") > 0
+    okp, dbg = O.narf_keypoints(x, y, z, debug=True)
+    assert _same(ctx.narf_debug_image("interest"), dbg["interest"])
+    assert np.array_equal(kp, okp)
