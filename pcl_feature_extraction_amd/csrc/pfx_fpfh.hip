@@ -277,23 +277,49 @@ __global__ void __launch_bounds__(256) k_fpfh_weight(GridView g, const float* __
       }
       __syncthreads();
     }
+    __shared__ int s_inexact;
+    if (tid == 0) s_inexact = 0;
+    __syncthreads();
     if (tid < 3) {
       const int blk = tid;
-      double sum = red_s[blk][0];
+      const double sum = red_s[blk][0];
       const int L = red_l[blk][0];
       const bool exact = sum == 0.0 || (L < 1000 && sum < ldexp(1.0, L + 52));
-      if (!exact) {  // PCL's sequential double loop
-        sum = 0.0;
-        for (int j = 0; j < k; ++j) {
-          const float d2 = key_d2(keys[j]);
-          if (d2 == 0.0f) continue;
-          const float w = 1.0f / d2;
-          const float* row = spfh + (int64_t)key_idx(keys[j]) * kDesc + blk * kBins;
-          for (int b = 0; b < kBins; ++b) sum = sum + (double)(row[b] * w);
-        }
-      }
-      if (sum != 0.0) sum = 100.0 / sum;
       s_sum[blk] = sum;
+      if (!exact) atomicOr(&s_inexact, 1 << blk);
+    }
+    __syncthreads();
+    const int inexact = s_inexact;
+    if (inexact) {  // PCL's sequential double loop for the blocks that need it, rows staged in LDS
+      double seq = 0.0;
+      for (int c0 = 0; c0 < k; c0 += kChunkW) {
+        const int m = min(kChunkW, k - c0);
+        for (int e = tid; e < m * kDesc; e += 256) {
+          const int j = e / kDesc, b = e - j * kDesc;
+          rows[j][b] = spfh[(int64_t)key_idx(keys[c0 + j]) * kDesc + b];
+        }
+        if (tid < m) {
+          const float d2 = key_d2(keys[c0 + tid]);
+          wts[tid] = d2 == 0.0f ? 0.0f : 1.0f / d2;
+        }
+        __syncthreads();
+        if (tid < 3 && ((inexact >> tid) & 1)) {
+          for (int j = 0; j < m; ++j) {
+            const float w = wts[j];
+            if (w == 0.0f) continue;
+#pragma unroll
+            for (int b = 0; b < kBins; ++b) seq = seq + (double)(rows[j][tid * kBins + b] * w);
+          }
+        }
+        __syncthreads();
+      }
+      if (tid < 3 && ((inexact >> tid) & 1)) s_sum[tid] = seq;
+      __syncthreads();
+    }
+    if (tid < 3) {
+      double sum = s_sum[tid];
+      if (sum != 0.0) sum = 100.0 / sum;
+      s_sum[tid] = sum;
     }
     __syncthreads();
     if (tid < kDesc) out[q * kDesc + tid] = fh * (float)s_sum[tid / kBins];

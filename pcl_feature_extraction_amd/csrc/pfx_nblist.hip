@@ -7,7 +7,7 @@
 // d2 (exact (d2, caller index) rank inside a bucket).  The tile's lists are written to HBM
 // interleaved (stride 2^lg >= tile size) with one global atomic per tile.
 //   sparse tiles: <= 1280 candidates, <= 512 neighbours per query in LDS  (3 workgroups / CU)
-//   dense tiles:  <= 8000 candidates, <= 1024 neighbours per query in LDS (1 workgroup / CU)
+//   dense tiles:  <= 8000 candidates read from L2, <= 1024 neighbours per query (2 WG / CU)
 // Queries of larger blocks and overflowing lists go to k_nb_query (one 256-thread workgroup per
 // query, candidates streamed from L2/HBM, <= 4096 neighbours sorted in LDS); beyond that the
 // same kernel runs with its sort arrays in global scratch (<= 262144 neighbours).
@@ -145,18 +145,33 @@ struct ListOut {
   unsigned long long cap;
 };
 
+// Candidate coordinates of a tile: staged in LDS, or read from the packed grid copy (L2).
+struct CandLds {
+  const float *cx, *cy, *cz;
+  __device__ __forceinline__ void get(int t, float& x, float& y, float& z) const { x = cx[t]; y = cy[t]; z = cz[t]; }
+};
+struct CandGlobal {
+  const float4* sp;
+  const Runs* R;
+  __device__ __forceinline__ void get(int t, float& x, float& y, float& z) const {
+    const float4 c = sp[run_pos(*R, t)];
+    x = c.x; y = c.y; z = c.z;
+  }
+};
+
 // Wave-local bucket sort of one query's list L[0..k) (u16 candidate indices) into FLANN order.
 // Sd/St: wave-private scratch (k entries), bcount/bpos: wave-private NB buckets.
-template <int NB>
-__device__ __forceinline__ void wave_sort(uint16_t* L, int k, float qx, float qy, float qz, const float* cx,
-                                          const float* cy, const float* cz, float bscale, uint32_t* Sd,
-                                          uint16_t* St, int* bcount, int* bpos, const GridView& g, const Runs& R,
-                                          int lane) {
+template <int NB, class Cand>
+__device__ __forceinline__ void wave_sort(uint16_t* L, int k, float qx, float qy, float qz, const Cand& cand,
+                                          float bscale, uint32_t* Sd, uint16_t* St, int* bcount, int* bpos,
+                                          const GridView& g, const Runs& R, int lane) {
   for (int b = lane; b < NB; b += 64) bcount[b] = 0;
   wave_sync();
   for (int e = lane; e < k; e += 64) {
     const int t = L[e];
-    const int b = (int)(flann_d2(qx, qy, qz, cx[t], cy[t], cz[t]) * bscale);
+    float px, py, pz;
+    cand.get(t, px, py, pz);
+    const int b = (int)(flann_d2(qx, qy, qz, px, py, pz) * bscale);
     atomicAdd(&bcount[b < NB ? b : NB - 1], 1);
   }
   wave_sync();
@@ -178,7 +193,9 @@ __device__ __forceinline__ void wave_sort(uint16_t* L, int k, float qx, float qy
   wave_sync();
   for (int e = lane; e < k; e += 64) {
     const int t = L[e];
-    const float d2 = flann_d2(qx, qy, qz, cx[t], cy[t], cz[t]);
+    float px, py, pz;
+    cand.get(t, px, py, pz);
+    const float d2 = flann_d2(qx, qy, qz, px, py, pz);
     int b = (int)(d2 * bscale);
     b = b < NB ? b : NB - 1;
     const int slot = atomicAdd(&bpos[b], 1);
@@ -203,14 +220,16 @@ __device__ __forceinline__ void wave_sort(uint16_t* L, int k, float qx, float qy
   wave_sync();
 }
 
-template <int LCAP, int NB, int TCAP>
+// STAGE: candidates staged in LDS (sparse tiles); otherwise read from L2 (dense tiles, where
+// staging 8000 candidates would cap the kernel at one workgroup per CU)
+template <int LCAP, int NB, int TCAP, bool STAGE>
 __global__ void __launch_bounds__(256) k_nb_tile(GridView g, const int32_t* __restrict__ qpos,
                                                  const uint32_t* __restrict__ skeys,
                                                  const uint32_t* __restrict__ tiles, const int* __restrict__ ntiles_ptr,
                                                  float rr, float bscale, int sorted, ListOut out,
                                                  int32_t* __restrict__ single, int* __restrict__ n_single) {
   constexpr int Q = kQ, QW = Q / 4;  // queries per tile / per wave
-  __shared__ float cx[TCAP], cy[TCAP], cz[TCAP];
+  __shared__ float cx[STAGE ? TCAP : 1], cy[STAGE ? TCAP : 1], cz[STAGE ? TCAP : 1];
   __shared__ uint16_t lists[Q][LCAP + 2];  // +2: odd dword row stride (no bank conflicts)
   __shared__ uint32_t sd[4][LCAP];
   __shared__ uint16_t stt[4][LCAP];
@@ -230,11 +249,13 @@ __global__ void __launch_bounds__(256) k_nb_tile(GridView g, const int32_t* __re
       if (tid < qn) single[atomicAdd(n_single, 1)] = start + tid;
       continue;
     }
-    for (int t = tid; t < T; t += 256) {
-      const int32_t pos = run_pos(R, t);
-      cx[t] = g.sx[pos];
-      cy[t] = g.sy[pos];
-      cz[t] = g.sz[pos];
+    if (STAGE) {
+      for (int t = tid; t < T; t += 256) {
+        const int32_t pos = run_pos(R, t);
+        cx[t] = g.sx[pos];
+        cy[t] = g.sy[pos];
+        cz[t] = g.sz[pos];
+      }
     }
     __syncthreads();
     float qx[QW], qy[QW], qz[QW];
@@ -252,7 +273,15 @@ __global__ void __launch_bounds__(256) k_nb_tile(GridView g, const int32_t* __re
     for (int t0 = 0; t0 < T; t0 += 64) {
       const int t = t0 + lane;
       const bool in = t < T;
-      const float px = in ? cx[t] : 0.f, py = in ? cy[t] : 0.f, pz = in ? cz[t] : 0.f;
+      float px = 0.f, py = 0.f, pz = 0.f;
+      if (in) {
+        if (STAGE) {
+          px = cx[t]; py = cy[t]; pz = cz[t];
+        } else {
+          const float4 c = g.sp[run_pos(R, t)];
+          px = c.x; py = c.y; pz = c.z;
+        }
+      }
 #pragma unroll
       for (int u = 0; u < QW; ++u) {
         const int j = wv + 4 * u;
@@ -300,9 +329,17 @@ __global__ void __launch_bounds__(256) k_nb_tile(GridView g, const int32_t* __re
       for (int u = 0; u < QW; ++u) {
         const int j = wv + 4 * u;
         const int k = cursor[u];
-        if (j < qn && k <= LCAP && k > 1)  // wave-uniform
-          wave_sort<NB>(lists[j], k, qx[u], qy[u], qz[u], cx, cy, cz, bscale, sd[wv], stt[wv], bcount[wv],
-                        bpos[wv], g, R, lane);
+        if (j < qn && k <= LCAP && k > 1) {  // wave-uniform
+          if (STAGE) {
+            const CandLds cand{cx, cy, cz};
+            wave_sort<NB>(lists[j], k, qx[u], qy[u], qz[u], cand, bscale, sd[wv], stt[wv], bcount[wv], bpos[wv],
+                          g, R, lane);
+          } else {
+            const CandGlobal cand{g.sp, &R};
+            wave_sort<NB>(lists[j], k, qx[u], qy[u], qz[u], cand, bscale, sd[wv], stt[wv], bcount[wv], bpos[wv],
+                          g, R, lane);
+          }
+        }
       }
     }
     __syncthreads();
@@ -521,12 +558,12 @@ void build_lists(pfx_ctx* ctx, const Grid& G, const uint8_t* mask, double radius
       TimeScope ts(ctx, std::string(tag) + "_lists");
       {
         TimeScope t1(ctx, std::string(tag) + "_lists_sparse");
-        k_nb_tile<512, 256, kTcapSparse><<<256 * 3 * 4, 256, 0, st>>>(
+        k_nb_tile<512, 256, kTcapSparse, true><<<256 * 3 * 4, 256, 0, st>>>(
             g, qpos, G.skeys, sparse, counters + 0, rr, 256.0f / rr, isort, lo, single, counters + 2);
       }
       {
         TimeScope t2(ctx, std::string(tag) + "_lists_dense");
-        k_nb_tile<1024, 256, kTcapDense><<<256 * 2, 256, 0, st>>>(
+        k_nb_tile<1024, 256, kTcapDense, false><<<256 * 2 * 4, 256, 0, st>>>(
             g, qpos, G.skeys, dense, counters + 1, rr, 256.0f / rr, isort, lo, single, counters + 2);
       }
       {
