@@ -37,7 +37,8 @@ VERBOSE_TIMERS = ["grid_bbox", "grid_build", "normals", "normals_tiles", "normal
 VERBOSE_STATS = ["normals_neighbors", "normals_queries", "normals_tiles_sparse", "normals_tiles_dense",
                  "normals_single", "normals_huge", "fpfh_spfh_points", "narf_candidates", "narf_keypoints",
                  "narf_interest_fullimage", "narf_interest_grown", "narf_interest_window_px",
-                 "narf_interest_visits", "narf_interest_queue_grown", "shot_neighbors"]
+                 "narf_interest_visits", "narf_interest_queue_grown", "fpfh_weight_kmax", "fpfh_weight_sequential",
+                 "shot_neighbors"]
 
 
 def cpu_baseline(x, y, z, workload, sample=None):

@@ -24,6 +24,7 @@ constexpr int kBins = 11;
 constexpr int kDesc = 33;
 constexpr int kCapW = 16384;  // sorted-neighbour capacity of the weighting kernel (LDS)
 constexpr int kChunkW = 128;  // SPFH rows staged per chunk in the weighting kernel
+constexpr int kWT = 1024;     // weighting workgroup: few queries, each as wide as possible
 
 // PCL 1.7 `acos (fabs (a1)) > acos (fabs (a2))` (double acos, correctly rounded by glibc):
 // acos is strictly decreasing and distinct floats >= 2^-26 map to distinct rounded values, so
@@ -201,21 +202,21 @@ __device__ __forceinline__ int lsb_exp(float v) {
   return (e ? e : 1) - 150 + __builtin_ctz(m);
 }
 
-// Weighting: one 256-thread workgroup per query.  The 33 float chains (strict FLANN order)
+// Weighting: one 1024-thread workgroup per query.  The 33 float chains (strict FLANN order)
 // run one per lane over SPFH rows staged in LDS.  The three double block sums are formed in
 // parallel: every value is a non-negative float, so when all of them are multiples of 2^L and
 // the total is below 2^(L+52) every partial sum -- of the sequential loop or of any other order
 // -- is exact and the parallel sum is bit-identical to PCL's loop; otherwise the block sum is
 // recomputed sequentially.
-__global__ void __launch_bounds__(256) k_fpfh_weight(GridView g, const float* __restrict__ qx,
+__global__ void __launch_bounds__(kWT) k_fpfh_weight(GridView g, const float* __restrict__ qx,
                                                      const float* __restrict__ qy, const float* __restrict__ qz,
                                                      int64_t nq, float rr, const float* __restrict__ spfh,
                                                      float* __restrict__ out, int* __restrict__ err) {
   extern __shared__ __attribute__((aligned(16))) uint64_t keys[];  // kCapW
   __shared__ float rows[kChunkW][kDesc + 1];
   __shared__ float wts[kChunkW];
-  __shared__ double red_s[3][256];
-  __shared__ int red_l[3][256];
+  __shared__ double red_s[3][kWT / 64];
+  __shared__ int red_l[3][kWT / 64];
   __shared__ int s_count;
   __shared__ double s_sum[3];
   const int tid = threadIdx.x;
@@ -235,7 +236,7 @@ __global__ void __launch_bounds__(256) k_fpfh_weight(GridView g, const float* __
     int pl0 = 1 << 20, pl1 = 1 << 20, pl2 = 1 << 20;
     for (int c0 = 0; c0 < k; c0 += kChunkW) {
       const int m = min(kChunkW, k - c0);
-      for (int e = tid; e < m * kDesc; e += 256) {
+      for (int e = tid; e < m * kDesc; e += kWT) {
         const int j = e / kDesc, b = e - j * kDesc;
         rows[j][b] = spfh[(int64_t)key_idx(keys[c0 + j]) * kDesc + b];
       }
@@ -245,12 +246,12 @@ __global__ void __launch_bounds__(256) k_fpfh_weight(GridView g, const float* __
       }
       __syncthreads();
       if (tid < kDesc) {
-        for (int j = 0; j < m; ++j) {
-          const float w = wts[j];
-          if (w != 0.0f) fh = fh + rows[j][tid] * w;
-        }
+        // skipped neighbours have w = 0: SPFH rows are finite and fh >= +0, so adding the +0
+        // product leaves fh unchanged bit for bit (== PCL's `continue`)
+#pragma unroll 8
+        for (int j = 0; j < m; ++j) fh = fh + rows[j][tid] * wts[j];
       }
-      for (int e = tid; e < m * kDesc; e += 256) {
+      for (int e = tid; e < m * kDesc; e += kWT) {
         const int j = e / kDesc, b = e - j * kDesc;
         const float w = wts[j];
         if (w == 0.0f) continue;
@@ -264,21 +265,30 @@ __global__ void __launch_bounds__(256) k_fpfh_weight(GridView g, const float* __
       }
       __syncthreads();
     }
-    red_s[0][tid] = ps0; red_s[1][tid] = ps1; red_s[2][tid] = ps2;
-    red_l[0][tid] = pl0; red_l[1][tid] = pl1; red_l[2][tid] = pl2;
-    __syncthreads();
-    for (int o = 128; o > 0; o >>= 1) {
-      if (tid < o) {
+    // block reduction (any order: only used when every partial sum is exact)
 #pragma unroll
-        for (int blk = 0; blk < 3; ++blk) {
-          red_s[blk][tid] += red_s[blk][tid + o];
-          red_l[blk][tid] = min(red_l[blk][tid], red_l[blk][tid + o]);
-        }
-      }
-      __syncthreads();
+    for (int o = 32; o > 0; o >>= 1) {
+      ps0 += __shfl_xor(ps0, o); ps1 += __shfl_xor(ps1, o); ps2 += __shfl_xor(ps2, o);
+      pl0 = min(pl0, __shfl_xor(pl0, o)); pl1 = min(pl1, __shfl_xor(pl1, o)); pl2 = min(pl2, __shfl_xor(pl2, o));
+    }
+    if ((tid & 63) == 0) {
+      const int wv = tid >> 6;
+      red_s[0][wv] = ps0; red_s[1][wv] = ps1; red_s[2][wv] = ps2;
+      red_l[0][wv] = pl0; red_l[1][wv] = pl1; red_l[2][wv] = pl2;
+    }
+    __syncthreads();
+    if (tid < 3) {
+      double t = 0.0;
+      int l = 1 << 20;
+      for (int wv = 0; wv < kWT / 64; ++wv) { t += red_s[tid][wv]; l = min(l, red_l[tid][wv]); }
+      red_s[tid][0] = t;
+      red_l[tid][0] = l;
     }
     __shared__ int s_inexact;
-    if (tid == 0) s_inexact = 0;
+    if (tid == 0) {
+      s_inexact = 0;
+      atomicMax(err + 1, k);
+    }
     __syncthreads();
     if (tid < 3) {
       const int blk = tid;
@@ -290,11 +300,12 @@ __global__ void __launch_bounds__(256) k_fpfh_weight(GridView g, const float* __
     }
     __syncthreads();
     const int inexact = s_inexact;
+    if (tid == 0 && inexact) atomicAdd(err + 2, 1);
     if (inexact) {  // PCL's sequential double loop for the blocks that need it, rows staged in LDS
       double seq = 0.0;
       for (int c0 = 0; c0 < k; c0 += kChunkW) {
         const int m = min(kChunkW, k - c0);
-        for (int e = tid; e < m * kDesc; e += 256) {
+        for (int e = tid; e < m * kDesc; e += kWT) {
           const int j = e / kDesc, b = e - j * kDesc;
           rows[j][b] = spfh[(int64_t)key_idx(keys[c0 + j]) * kDesc + b];
         }
@@ -377,22 +388,24 @@ void fpfh_dev(pfx_ctx* ctx, const float* sx, const float* sy, const float* sz, c
                                                                                           spfh);
     check_launch("k_fpfh_spfh");
   }
-  int* err = ctx->buf("fpfh_err").as<int>(1);
-  PFX_HIP(hipMemsetAsync(err, 0, sizeof(int), st));
+  int* err = ctx->buf("fpfh_err").as<int>(4);  // [0] k over capacity, [1] max k, [2] inexact sums
+  PFX_HIP(hipMemsetAsync(err, 0, 4 * sizeof(int), st));
   {
     TimeScope ts(ctx, "fpfh_weight");
     const size_t lds = sizeof(uint64_t) * kCapW;
     PFX_HIP(hipFuncSetAttribute((const void*)k_fpfh_weight, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    const unsigned blocks = (unsigned)std::min<int64_t>(nq, 256 * 8);
-    k_fpfh_weight<<<blocks, 256, lds, st>>>(g, qx, qy, qz, nq, rr, spfh, out, err);
+    const unsigned blocks = (unsigned)std::min<int64_t>(nq, 256 * 2);
+    k_fpfh_weight<<<blocks, kWT, lds, st>>>(g, qx, qy, qz, nq, rr, spfh, out, err);
     check_launch("k_fpfh_weight");
   }
-  int h[2] = {0, 0};
+  int h[4] = {0, 0, 0, 0};
   int64_t count = 0;
-  PFX_HIP(hipMemcpyAsync(h, err, sizeof(int), hipMemcpyDeviceToHost, st));
+  PFX_HIP(hipMemcpyAsync(h, err, sizeof(h), hipMemcpyDeviceToHost, st));
   PFX_HIP(hipMemcpyAsync(&count, d_sel, sizeof(int64_t), hipMemcpyDeviceToHost, st));
   PFX_HIP(hipStreamSynchronize(st));
   ctx->stats["fpfh_spfh_points"] = count;
+  ctx->stats["fpfh_weight_kmax"] = h[1];
+  ctx->stats["fpfh_weight_sequential"] = h[2];
   if (h[0] > 0)
     throw Error(PFX_ERR_CAPACITY, "fpfh: a query has " + std::to_string(h[0]) + " neighbours (> " +
                                       std::to_string(kCapW) + " supported)");

@@ -83,7 +83,8 @@ __device__ __forceinline__ int gather_keys(const GridView& g, float qx, float qy
     uint64_t key = 0;
     if (t < T) {
       int32_t p = run_pos(R, t);
-      float d2 = flann_d2(qx, qy, qz, g.sx[p], g.sy[p], g.sz[p]);
+      const float4 c = g.sp[p];
+      float d2 = flann_d2(qx, qy, qz, c.x, c.y, c.z);
       hit = d2 < rr;
       if (hit) key = nb_key(d2, g.perm[p]);
     }
