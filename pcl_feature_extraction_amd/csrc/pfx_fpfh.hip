@@ -383,7 +383,7 @@ void fpfh_dev(pfx_ctx* ctx, const float* sx, const float* sy, const float* sz, c
   {
     // the S count stays on the device: a grid-stride launch sized for the worst case
     TimeScope ts(ctx, "fpfh_spfh");
-    const int64_t waves = std::min<int64_t>(ns, 256 * 4 * 8);
+    const int64_t waves = std::min<int64_t>(ns, 256 * 4 * 20);  // up to 20 waves per CU in flight
     k_fpfh_spfh<<<(unsigned)std::max<int64_t>(8, ceil_div(waves, 4) & ~7), 256, 0, st>>>(g, snp, slist, d_sel, rr,
                                                                                           spfh);
     check_launch("k_fpfh_spfh");
