@@ -389,26 +389,29 @@ __global__ void __launch_bounds__(256) k_nb_query(GridView g, const int32_t* __r
     if (tid == 0) s_count = 0;
     for (int b = tid; b < NB; b += 256) bcount[b] = 0;
     __syncthreads();
-    for (int t0 = 0; t0 < R.pref[9]; t0 += 256) {
-      const int t = t0 + tid;
-      bool hit = false;
-      int32_t pos = 0;
-      float d2 = 0.f;
-      if (t < R.pref[9]) {
-        pos = run_pos(R, t);
-        const float4 c = g.sp[pos];
-        d2 = flann_d2(q.x, q.y, q.z, c.x, c.y, c.z);
-        hit = d2 < rr;
+    for (int t0 = 0; t0 < R.pref[9]; t0 += 4 * 256) {  // 4 candidates per thread in flight
+      float4 c[4];
+      int32_t pos[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int t = t0 + u * 256 + tid;
+        pos[u] = t < R.pref[9] ? run_pos(R, t) : -1;
+        c[u] = g.sp[pos[u] < 0 ? 0 : pos[u]];
       }
-      const uint64_t m = __ballot(hit);
-      int base = 0;
-      if ((tid & 63) == 0 && m) base = atomicAdd(&s_count, __popcll(m));
-      base = __shfl(base, 0);
-      if (hit) {
-        const int slot = base + __popcll(m & lanemask_lt());
-        if (slot < CAP) {
-          hits[slot] = (uint32_t)pos;
-          hd[slot] = __float_as_uint(d2);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const float d2 = flann_d2(q.x, q.y, q.z, c[u].x, c[u].y, c[u].z);
+        const bool hit = pos[u] >= 0 && d2 < rr;
+        const uint64_t m = __ballot(hit);
+        int base = 0;
+        if ((tid & 63) == 0 && m) base = atomicAdd(&s_count, __popcll(m));
+        base = __shfl(base, 0);
+        if (hit) {
+          const int slot = base + __popcll(m & lanemask_lt());
+          if (slot < CAP) {
+            hits[slot] = (uint32_t)pos[u];
+            hd[slot] = __float_as_uint(d2);
+          }
         }
       }
     }
