@@ -14,7 +14,8 @@
 //      the caller's order; lists longer than kLaneMax go to k_normals_long (nine lanes per
 //      query, one per chain).
 #include "pfx_nblist.h"
-#include "pfx_normals_tile.h"
+#include "pfx_neighbors.h"
+#include "pfx_normal_math.h"
 
 namespace pfx {
 namespace {
