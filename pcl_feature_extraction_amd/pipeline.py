@@ -52,6 +52,43 @@ def narf_fpfh(ctx: Context, b: ScanBuffers, normal_radius: float = 0.05, feat_ra
     return kp, k
 
 
+class OverlappedNarfFpfh:
+    """narf_fpfh with the two independent halves of the pass overlapped on the device: NARF (+ the
+    keypoint gather) on the main context/stream, normal estimation -- which needs only the cloud --
+    on a second context/stream driven from a worker thread (the C-ABI calls release the GIL), then
+    FPFH on the main stream after an event wait for the normals.  Same results as narf_fpfh."""
+
+    def __init__(self, torch, ctx_main: Context, ctx_side: Context, device):
+        from concurrent.futures import ThreadPoolExecutor
+        self.torch = torch
+        self.ctx, self.ctx_side = ctx_main, ctx_side
+        self.s_main = torch.cuda.current_stream(device)
+        self.s_side = torch.cuda.Stream(device)
+        ctx_main.set_stream(self.s_main.cuda_stream)
+        ctx_side.set_stream(self.s_side.cuda_stream)
+        self.pool = ThreadPoolExecutor(max_workers=1)
+
+    def __call__(self, b: ScanBuffers, normal_radius: float = 0.05, feat_radius: float = 0.08, params=None,
+                 cam=None):
+        fut = self.pool.submit(self.ctx_side.normals_dev, b.x, b.y, b.z, normal_radius, b.nx, b.ny, b.nz, b.curv)
+        try:
+            kp = self.ctx.narf_keypoints_dev(b.x, b.y, b.z, params or narf_params(support_size=0.2),
+                                             cam or camera())
+            k = self.ctx.gather_points_dev(b.x, b.y, b.z, kp, b.kx, b.ky, b.kz)
+        finally:
+            fut.result()
+        ev = self.torch.cuda.Event()
+        ev.record(self.s_side)
+        self.s_main.wait_event(ev)
+        if k > 0:
+            self.ctx.fpfh_dev(b.x, b.y, b.z, b.nx, b.ny, b.nz, b.kx[:k], b.ky[:k], b.kz[:k], feat_radius,
+                              b.desc[:k])
+        return kp, k
+
+    def close(self):
+        self.pool.shutdown()
+
+
 def keypoint_rows(kp: np.ndarray, n: int) -> np.ndarray:
     """Cloud indices the descriptors belong to (keypoints.h:229 uses pixel index as cloud index)."""
     kp = np.asarray(kp)
