@@ -132,6 +132,13 @@ pfx_status pfx_fpfh_dev(pfx_ctx* ctx, const float* d_sx, const float* d_sy, cons
                         const float* d_qz, int64_t nq, int same_as_surface, double radius,
                         float* d_out);
 
+/* Builds the search-surface index of the next pfx_fpfh_dev call on this ctx ahead of time (the
+ * surface grid needs only the coordinates, so it can overlap normal estimation -- PCL builds the
+ * same tree inside FPFHEstimation::compute, features.h:192-195).  The next pfx_fpfh_dev with the
+ * same (d_sx, n_surface, radius) consumes it; the surface must not change in between. */
+pfx_status pfx_fpfh_prepare_dev(pfx_ctx* ctx, const float* d_sx, const float* d_sy, const float* d_sz,
+                                int64_t n_surface, double radius);
+
 /* ---- SHOT-352: SHOTEstimationOMP + SHOTLocalReferenceFrameEstimation ---------------- */
 /* desc: nq x 352, rf: nq x 9 (x_axis, y_axis, z_axis) -- SHOT352::{descriptor, rf}. */
 pfx_status pfx_shot(pfx_ctx* ctx, const float* sx, const float* sy, const float* sz,

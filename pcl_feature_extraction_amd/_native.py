@@ -79,6 +79,7 @@ _SIGS = {
                          c_int, c_dbl, c_vp]),
     "pfx_fpfh_dev": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp,
                              c_i64, c_int, c_dbl, c_vp]),
+    "pfx_fpfh_prepare_dev": (c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_dbl]),
     "pfx_shot": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_i64,
                          c_dbl, c_vp, c_vp]),
     "pfx_shot_dev": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp,

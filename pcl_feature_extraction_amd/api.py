@@ -179,6 +179,10 @@ class Context:
                                            sx.numel(), _ptr(qx), _ptr(qy), _ptr(qz), qx.numel(),
                                            1 if same_as_surface else 0, float(r), _ptr(out)))
 
+    def fpfh_prepare_dev(self, sx, sy, sz, r):
+        """Build the FPFH search-surface index ahead of fpfh_dev (see pfx_fpfh_prepare_dev)."""
+        self._check(self._lib.pfx_fpfh_prepare_dev(self.h, _ptr(sx), _ptr(sy), _ptr(sz), sx.numel(), float(r)))
+
     def shot_dev(self, sx, sy, sz, nx, ny, nz, qx, qy, qz, r, desc, rf):
         self._check(self._lib.pfx_shot_dev(self.h, _ptr(sx), _ptr(sy), _ptr(sz), _ptr(nx), _ptr(ny), _ptr(nz),
                                            sx.numel(), _ptr(qx), _ptr(qy), _ptr(qz), qx.numel(), float(r),

@@ -340,6 +340,16 @@ __global__ void __launch_bounds__(kWT) k_fpfh_weight(GridView g, const float* __
 
 }  // namespace
 
+void fpfh_prepare_dev(pfx_ctx* ctx, const float* sx, const float* sy, const float* sz, int64_t ns, double r) {
+  ctx->prep_x = nullptr;
+  ctx->prep_n = -1;
+  if (ns == 0) return;
+  build_grid(ctx, ctx->grid_b, sx, sy, sz, ns, r);
+  ctx->prep_x = sx;
+  ctx->prep_n = ns;
+  ctx->prep_r = r;
+}
+
 void fpfh_dev(pfx_ctx* ctx, const float* sx, const float* sy, const float* sz, const float* snx,
               const float* sny, const float* snz, int64_t ns, const float* qx, const float* qy, const float* qz,
               int64_t nq, int same, double r, float* out) {
@@ -353,7 +363,10 @@ void fpfh_dev(pfx_ctx* ctx, const float* sx, const float* sy, const float* sz, c
     PFX_HIP(hipStreamSynchronize(st));
     return;
   }
-  build_grid(ctx, ctx->grid_b, sx, sy, sz, ns, r);
+  if (!(ctx->prep_x == sx && ctx->prep_n == ns && ctx->prep_r == r))
+    build_grid(ctx, ctx->grid_b, sx, sy, sz, ns, r);
+  ctx->prep_x = nullptr;  // one-shot
+  ctx->prep_n = -1;
   const Grid& G = ctx->grid_b;
   GridView g = view(G);
   const float rr = (float)(r * r);

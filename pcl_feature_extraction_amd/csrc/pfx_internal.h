@@ -105,6 +105,10 @@ struct pfx_ctx {
   pfx::KernelTimer timer;
   std::map<std::string, int64_t> stats;
   pfx::Grid grid_a, grid_b;          // normal-radius grid, feature-radius grid
+  // grid_b built ahead by pfx_fpfh_prepare_dev for (surface x pointer, n, radius)
+  const float* prep_x = nullptr;
+  int64_t prep_n = -1;
+  double prep_r = 0.0;
   std::map<std::string, pfx::DevBuf> bufs;  // named scratch
   pfx::NarfState* narf = nullptr;
   pfx::DevBuf& buf(const char* name) { return bufs[name]; }
@@ -160,6 +164,7 @@ void radius_search_dev(pfx_ctx* ctx, const float* x, const float* y, const float
 void fpfh_dev(pfx_ctx* ctx, const float* sx, const float* sy, const float* sz, const float* snx,
               const float* sny, const float* snz, int64_t ns, const float* qx, const float* qy,
               const float* qz, int64_t nq, int same, double r, float* out);
+void fpfh_prepare_dev(pfx_ctx* ctx, const float* sx, const float* sy, const float* sz, int64_t ns, double r);
 void shot_dev(pfx_ctx* ctx, const float* sx, const float* sy, const float* sz, const float* snx,
               const float* sny, const float* snz, int64_t ns, const float* qx, const float* qy,
               const float* qz, int64_t nq, double r, float* desc, float* rf);

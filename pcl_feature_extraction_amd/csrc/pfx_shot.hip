@@ -398,6 +398,8 @@ void shot_dev(pfx_ctx* ctx, const float* sx, const float* sy, const float* sz, c
     PFX_HIP(hipStreamSynchronize(st));
     return;
   }
+  ctx->prep_x = nullptr;  // grid_b is rebuilt: a pending pfx_fpfh_prepare_dev no longer holds
+  ctx->prep_n = -1;
   build_grid(ctx, ctx->grid_b, sx, sy, sz, ns, r);
   GridView g = view(ctx->grid_b);
   int* err = ctx->buf("shot_err").as<int>(4);

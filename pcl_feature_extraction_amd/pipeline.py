@@ -72,6 +72,7 @@ class OverlappedNarfFpfh:
                  cam=None):
         fut = self.pool.submit(self.ctx_side.normals_dev, b.x, b.y, b.z, normal_radius, b.nx, b.ny, b.nz, b.curv)
         try:
+            self.ctx.fpfh_prepare_dev(b.x, b.y, b.z, feat_radius)  # the FPFH surface grid, also normals-free
             kp = self.ctx.narf_keypoints_dev(b.x, b.y, b.z, params or narf_params(support_size=0.2),
                                              cam or camera())
             k = self.ctx.gather_points_dev(b.x, b.y, b.z, kp, b.kx, b.ky, b.kz)
