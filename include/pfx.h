@@ -88,9 +88,11 @@ void pfx_camera_default(pfx_camera* c);
 pfx_status pfx_ctx_create(int device, pfx_ctx** out);
 void pfx_ctx_destroy(pfx_ctx* ctx);
 const char* pfx_last_error(const pfx_ctx* ctx);
-/* Use an external hipStream_t (e.g. torch.cuda.current_stream().cuda_stream); NULL restores
- * the ctx-owned stream. */
+/* Use an external hipStream_t (e.g. torch.cuda.current_stream().cuda_stream); NULL is HIP's
+ * null stream (torch's default stream).  A new ctx runs on its own non-blocking stream. */
 pfx_status pfx_ctx_set_stream(pfx_ctx* ctx, void* hip_stream);
+/* Back to the ctx-owned non-blocking stream. */
+pfx_status pfx_ctx_use_own_stream(pfx_ctx* ctx);
 void* pfx_ctx_get_stream(pfx_ctx* ctx);
 pfx_status pfx_ctx_synchronize(pfx_ctx* ctx);
 /* Per-kernel HIP-event timing on the ctx stream (for bench.py's live roofline). */

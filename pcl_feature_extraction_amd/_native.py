@@ -65,6 +65,7 @@ _SIGS = {
     "pfx_ctx_destroy": (None, [c_vp]),
     "pfx_last_error": (ctypes.c_char_p, [c_vp]),
     "pfx_ctx_set_stream": (c_int, [c_vp, c_vp]),
+    "pfx_ctx_use_own_stream": (c_int, [c_vp]),
     "pfx_ctx_get_stream": (c_vp, [c_vp]),
     "pfx_ctx_synchronize": (c_int, [c_vp]),
     "pfx_ctx_set_timing": (c_int, [c_vp, c_int]),

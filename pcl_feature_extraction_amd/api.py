@@ -78,7 +78,11 @@ class Context:
 
     # ---- plumbing ------------------------------------------------------------------
     def set_stream(self, stream_handle):
+        """Run on an external HIP stream (torch's `stream.cuda_stream`; 0 = the null stream)."""
         self._check(self._lib.pfx_ctx_set_stream(self.h, ctypes.c_void_p(stream_handle)))
+
+    def use_own_stream(self):
+        self._check(self._lib.pfx_ctx_use_own_stream(self.h))
 
     def synchronize(self):
         self._check(self._lib.pfx_ctx_synchronize(self.h))

@@ -127,7 +127,15 @@ pfx_status pfx_ctx_set_stream(pfx_ctx* ctx, void* hip_stream) {
   PFX_API_BEGIN
   check_ctx(ctx);
   harvest_timing(ctx);
-  ctx->stream = hip_stream ? static_cast<hipStream_t>(hip_stream) : ctx->own_stream;
+  ctx->stream = static_cast<hipStream_t>(hip_stream);  // NULL = HIP's null (legacy default) stream
+  PFX_API_END(ctx)
+}
+
+pfx_status pfx_ctx_use_own_stream(pfx_ctx* ctx) {
+  PFX_API_BEGIN
+  check_ctx(ctx);
+  harvest_timing(ctx);
+  ctx->stream = ctx->own_stream;
   PFX_API_END(ctx)
 }
 

@@ -70,6 +70,7 @@ class OverlappedNarfFpfh:
 
     def __call__(self, b: ScanBuffers, normal_radius: float = 0.05, feat_radius: float = 0.08, params=None,
                  cam=None):
+        self.s_side.wait_stream(self.s_main)  # the scan was written on the main stream
         fut = self.pool.submit(self.ctx_side.normals_dev, b.x, b.y, b.z, normal_radius, b.nx, b.ny, b.nz, b.curv)
         try:
             self.ctx.fpfh_prepare_dev(b.x, b.y, b.z, feat_radius)  # the FPFH surface grid, also normals-free
