@@ -56,17 +56,36 @@ def cpu_baseline(x, y, z, workload, sample=None):
     t2 = time.perf_counter()
     rows = kp[kp < len(x)]
     if workload == "fpfh":
-        O.fpfh(x, y, z, nx, ny, nz, x[rows], y[rows], z[rows], 0.08, threads=1)
+        desc = O.fpfh(x, y, z, nx, ny, nz, x[rows], y[rows], z[rows], 0.08, threads=1)
         feat = "FPFH 1 thread"
     else:
         rows = np.r_[rows, sample]
-        O.shot(x, y, z, nx, ny, nz, x[rows], y[rows], z[rows], 0.08, threads=threads)
+        desc = O.shot(x, y, z, nx, ny, nz, x[rows], y[rows], z[rows], 0.08, threads=threads)
         feat = f"SHOT {threads} threads"
     t3 = time.perf_counter()
-    return dict(seconds=t3 - t0, threads=threads,
+    return dict(seconds=t3 - t0, threads=threads, outputs=(kp, (nx, ny, nz), desc),
                 sample=(f"the same 1M-point scan through the CPU restatement (oracle/): NARF 1 thread "
                         f"{t1 - t0:.1f}s, normals {threads} threads {t2 - t1:.1f}s, {feat} {t3 - t2:.1f}s at "
                         f"{len(rows)} rows; real PCL is not available anywhere in this pipeline"))
+
+
+def full_size_parity(outputs, kp, b, desc, rows, shot):
+    """The last timed step's outputs against the CPU restatement's on the whole scan: bit-exact
+    (NaN positions equal) for keypoints, normals and descriptor rows."""
+    import numpy as np
+    okp, onorm, odesc = outputs
+    if shot:
+        odesc = odesc[0]
+
+    def same(a, c):
+        a, c = np.asarray(a, np.float32), np.asarray(c, np.float32)
+        return bool(a.shape == c.shape and np.array_equal(np.nan_to_num(a, nan=7).view(np.uint32),
+                                                          np.nan_to_num(c, nan=7).view(np.uint32)))
+    res = {"normals": all(same(t.cpu().numpy(), o) for t, o in zip((b.nx, b.ny, b.nz), onorm)),
+           "descriptors": same(desc[:rows].cpu().numpy(), odesc)}
+    if kp is not None:
+        res["keypoints"] = bool(np.array_equal(np.asarray(kp), okp))
+    return res
 
 
 def main():
@@ -115,14 +134,15 @@ def main():
         s = alloc_shot(torch, 1 << 16, dev)
         sample = torch.from_numpy(sample_np.astype(np.int64)).to(dev)
     gathered = None
+    last_kp = None
 
     def step():
-        nonlocal gathered
+        nonlocal gathered, last_kp
         if shot:
             rows = narf_shot(ctx, b, s, sample)
             desc = s.desc
         else:
-            _, rows = run_fpfh(b)
+            last_kp, rows = run_fpfh(b)
             desc = b.desc
         if world > 1:
             gathered = gather_descriptors(torch, dist, desc, rows)
@@ -212,7 +232,8 @@ def main():
         if world == 1 and not args.no_cpu_baseline:
             cb = cpu_baseline(x, y, z, args.workload, sample_np)
             cpu = {"value": round(N_POINTS / cb["seconds"] / 1e6, 6), "unit": "Mpoints/s",
-                   "cores": cb["threads"], "kind": "port", "sample": cb["sample"]}
+                   "cores": cb["threads"], "kind": "port", "sample": cb["sample"],
+                   "parity": full_size_parity(cb["outputs"], last_kp, b, s.desc if shot else b.desc, rows, shot)}
         if shot:
             metric = "Mpoints/s through NARF keypoint + normals + SHOT-352 descriptor on 1M-pt underwater-style cloud"
             workload = (f"configs[3] 1M-pt synthetic seabed, NARF(support 0.2) + normals(r 0.05) + SHOT-352(r 0.08) "

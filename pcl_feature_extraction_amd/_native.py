@@ -10,7 +10,7 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libpfx.so")
+LIB_PATH = os.environ.get("PFX_LIB") or os.path.join(_HERE, "libpfx.so")
 
 PFX_OK, PFX_ERR_INVALID, PFX_ERR_DEVICE, PFX_ERR_CAPACITY, PFX_ERR_UNSUPPORTED = 0, 1, 2, 3, 4
 _ERRNAMES = {1: "PFX_ERR_INVALID", 2: "PFX_ERR_DEVICE", 3: "PFX_ERR_CAPACITY", 4: "PFX_ERR_UNSUPPORTED"}
@@ -110,6 +110,14 @@ def lib():
     if _lib is None:
         if not os.path.exists(LIB_PATH):
             raise OSError(f"{LIB_PATH} not built: run `make -C {os.path.join(_HERE, 'csrc')}`")
+        # One HIP runtime per process: torch wheels ship their own libamdhip64 (SONAME
+        # libamdhip64.so.7, but torch's NEEDED entry is the unversioned name).  Loading torch first
+        # makes libpfx's NEEDED libamdhip64.so.7 bind to that copy; the other order would load two
+        # runtimes and torch would find no GPU (and stream handles could not be shared).
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         lb = ctypes.CDLL(LIB_PATH)
         for name, (res, args) in _SIGS.items():
             fn = getattr(lb, name)

@@ -8,11 +8,9 @@
 //      LDS-staged neighbour chunks; cyclic Jacobi eigen solver (the oracle's operation
 //      sequence, double); sign disambiguation counts reduced over the block;
 //   3. SHOT: every neighbour's (up to) five interpolated bin updates are computed in parallel and
-//      applied by one wave with LDS float atomics in neighbour order; normalizeHistogram by one
-//      lane (double accumulation, as PCL).
-// The histogram adds are float additions whose order differs from PCL's loop only inside a
-// wave instruction, so descriptors agree with the restatement to float rounding (the
-// north_star bar is 1e-4 L2); the reference frame is bit-exact.
+//      applied per bin in PCL's sequential order (each wave owns a quarter of the bins; lanes
+//      that collide on a bin are serialised lowest-first); normalizeHistogram by one lane (double accumulation, as PCL).
+// Descriptors and reference frames are bit-exact against the restatement.
 #include "pfx_neighbors.h"
 
 namespace pfx {
@@ -167,10 +165,27 @@ __device__ __forceinline__ void shot_updates(f3 delta, double distance, double b
   vals[4] = (float)intWeight;
 }
 
+#ifdef PFX_SHOT_PROFILE
+__device__ unsigned long long g_shot_prof[8];
+#define PROF_T(v) long long v = (tid == 0) ? clock64() : 0
+#define PROF_ADD(i, a, b) if (tid == 0) atomicAdd(&g_shot_prof[i], (unsigned long long)((b) - (a)))
+#else
+#define PROF_T(v)
+#define PROF_ADD(i, a, b)
+#endif
+
+// the seven distinct LRF chains: cov (0,0) (0,1) (0,2) (1,1) (1,2) (2,2) and the weight sum
+constexpr int kChains = 7;
+constexpr int kMaskWords = kChunk / 64;
+
 struct ShotLds {
   union {
-    struct { double v[kChunk][4]; int valid[kChunk]; } lrf;   // (vx, vy, vz, radius - dist)
-    struct { int bin[kChunk][5]; float val[kChunk][5]; } upd;
+    double lrf[kChains][kChunk];  // per-neighbour chain terms of one chunk (0 for invalid ones)
+    struct {
+      uint64_t mask[kLen][kMaskWords];  // which neighbours of the chunk hit each bin
+      int off[kLen + 1];                // bucket offsets (exclusive scan of the hit counts)
+      float val[5 * kChunk];            // the chunk's update values bucketed by bin, neighbour order
+    } upd;
   };
   float hist[kLen];
   double cov[10];
@@ -206,7 +221,10 @@ __global__ void __launch_bounds__(256) k_shot(GridView g, const float* __restric
       if (tid < 9) rfo[tid] = __builtin_nanf("");
       continue;
     }
+    PROF_T(t0);
     const int k = sorted_neighbors(g, cx, cy, cz, rr, keys, CAP, &s_count);
+    PROF_T(t1);
+    PROF_ADD(0, t0, t1);
     if (k > CAP) {
       if (tid == 0) {
         if (over) over[atomicAdd(n_over, 1)] = (int32_t)q;
@@ -219,7 +237,10 @@ __global__ void __launch_bounds__(256) k_shot(GridView g, const float* __restric
       atomicAdd(nbr, (unsigned long long)k);
     }
     // ---- local reference frame: ordered double covariance ----
-    double acc = 0.0;  // lanes 0..8: cov[a][b], lane 9: weight sum
+    // Every thread forms its neighbour's chain terms dist * (v_a * v_b) and dist exactly as the
+    // reference loop does; lanes 0..6 then add them in neighbour order (the only sequential part).
+    // An invalid neighbour (a copy of the query) contributes +0.0, which leaves a chain unchanged.
+    double acc = 0.0;
     for (int c0 = 0; c0 < k; c0 += kChunk) {
       const int m = min(kChunk, k - c0);
       __syncthreads();
@@ -227,27 +248,43 @@ __global__ void __launch_bounds__(256) k_shot(GridView g, const float* __restric
         const uint64_t key = keys[c0 + tid];
         const int32_t p = key_idx(key);
         const float px = g.ux[p], py = g.uy[p], pz = g.uz[p];
-        const int valid = !(px == cx && py == cy && pz == cz);
-        S.lrf.valid[tid] = valid;
-        S.lrf.v[tid][0] = (double)(px - cx);
-        S.lrf.v[tid][1] = (double)(py - cy);
-        S.lrf.v[tid][2] = (double)(pz - cz);
-        S.lrf.v[tid][3] = radius - sqrt((double)key_d2(key));
+        const bool valid = !(px == cx && py == cy && pz == cz);
+        const double vx = (double)(px - cx), vy = (double)(py - cy), vz = (double)(pz - cz);
+        const double dist = radius - sqrt((double)key_d2(key));
+        S.lrf[0][tid] = valid ? dist * (vx * vx) : 0.0;
+        S.lrf[1][tid] = valid ? dist * (vx * vy) : 0.0;
+        S.lrf[2][tid] = valid ? dist * (vx * vz) : 0.0;
+        S.lrf[3][tid] = valid ? dist * (vy * vy) : 0.0;
+        S.lrf[4][tid] = valid ? dist * (vy * vz) : 0.0;
+        S.lrf[5][tid] = valid ? dist * (vz * vz) : 0.0;
+        S.lrf[6][tid] = valid ? dist : 0.0;
         if (!valid) atomicAdd(&S.n_invalid, 1);
         if (key_d2(key) == 0.0f) atomicAdd(&S.zero_prefix, 1);
       }
       __syncthreads();
-      if (tid < 10) {
-        const int a = tid / 3, b = tid - 3 * (tid / 3);
-        for (int t = 0; t < m; ++t) {
-          if (!S.lrf.valid[t]) continue;
-          const double dist = S.lrf.v[t][3];
-          acc = (tid < 9) ? acc + dist * (S.lrf.v[t][a] * S.lrf.v[t][b]) : acc + dist;
+      if (tid < kChains) {
+        const double* row = S.lrf[tid];
+        int t = 0;
+        for (; t + 8 <= m; t += 8) {
+          const double2 a = *reinterpret_cast<const double2*>(row + t);
+          const double2 b = *reinterpret_cast<const double2*>(row + t + 2);
+          const double2 c = *reinterpret_cast<const double2*>(row + t + 4);
+          const double2 e = *reinterpret_cast<const double2*>(row + t + 6);
+          acc = acc + a.x; acc = acc + a.y; acc = acc + b.x; acc = acc + b.y;
+          acc = acc + c.x; acc = acc + c.y; acc = acc + e.x; acc = acc + e.y;
         }
+        for (; t < m; ++t) acc = acc + row[t];
       }
     }
-    if (tid < 10) S.cov[tid] = acc;
     __syncthreads();
+    if (tid < kChains) {  // chain -> cov[3a + b] (v_a v_b == v_b v_a exactly), cov[9] = weight sum
+      constexpr int kSlot[kChains][2] = {{0, 0}, {1, 3}, {2, 6}, {4, 4}, {5, 7}, {8, 8}, {9, 9}};
+      S.cov[kSlot[tid][0]] = acc;
+      S.cov[kSlot[tid][1]] = acc;
+    }
+    __syncthreads();
+    PROF_T(t2);
+    PROF_ADD(1, t1, t2);
     const int valid = k - S.n_invalid;
     if (tid == 0) {
       S.ok = 0;
@@ -330,20 +367,31 @@ __global__ void __launch_bounds__(256) k_shot(GridView g, const float* __restric
       S.rf[3] = y.x; S.rf[4] = y.y; S.rf[5] = y.z;
       S.rf[6] = z.x; S.rf[7] = z.y; S.rf[8] = z.z;
     }
-    for (int i = tid; i < kLen; i += 256) S.hist[i] = 0.0f;
+    // Bin ownership for the histogram: thread j accumulates bins j and j + 256 in registers.
+    const int b0 = tid, b1 = tid + 256;
+    float h0 = 0.0f, h1 = 0.0f;
+    for (int i = tid; i < kLen; i += 256)
+      for (int w = 0; w < kMaskWords; ++w) S.upd.mask[i][w] = 0;
     __syncthreads();
+    PROF_T(t3);
+    PROF_ADD(2, t2, t3);
     const f3 fx = mk3(S.rf[0], S.rf[1], S.rf[2]), fy = mk3(S.rf[3], S.rf[4], S.rf[5]),
              fz = mk3(S.rf[6], S.rf[7], S.rf[8]);
     // ---- SHOT histogram ----
+    // Each neighbour adds to at most one bin per update statement (its <= 5 bins are distinct),
+    // so PCL's sequential order restricted to one bin is neighbour order.  Per chunk: hit masks
+    // per bin -> counts -> offsets -> every update written to its bin's bucket at its rank among
+    // the bin's hits (a stable counting sort) -> each bin's owner adds its bucket in order.
     for (int c0 = 0; c0 < k; c0 += kChunk) {
       const int m = min(kChunk, k - c0);
+      PROF_T(t4);
+      int bins[5];
+      float vals[5];
+#pragma unroll
+      for (int s = 0; s < 5; ++s) bins[s] = -1;
       if (tid < m) {
         const uint64_t key = keys[c0 + tid];
         const int32_t p = key_idx(key);
-        int bins[5];
-        float vals[5];
-#pragma unroll
-        for (int s = 0; s < 5; ++s) bins[s] = -1;
         const float pnx = nx[p], pny = ny[p], pnz = nz[p];
         const double distance = sqrt((double)key_d2(key));
         if (isfinite(pnx) && isfinite(pny) && isfinite(pnz) && !(fabs(distance - 0.0) < 1E-15)) {
@@ -354,22 +402,81 @@ __global__ void __launch_bounds__(256) k_shot(GridView g, const float* __restric
           const f3 delta = mk3(g.ux[p] - cx, g.uy[p] - cy, g.uz[p] - cz);
           shot_updates(delta, distance, binDist, fx, fy, fz, radius, bins, vals);
         }
+        const uint64_t bit = 1ull << (tid & 63);
 #pragma unroll
-        for (int s = 0; s < 5; ++s) { S.upd.bin[tid][s] = bins[s]; S.upd.val[tid][s] = vals[s]; }
+        for (int s = 0; s < 5; ++s)
+          if (bins[s] >= 0) atomicOr(reinterpret_cast<unsigned long long*>(&S.upd.mask[bins[s]][tid >> 6]), bit);
       }
       __syncthreads();
-      if (tid < 64) {  // one wave applies the updates in neighbour order
-        for (int t0 = 0; t0 < m; t0 += 64) {
-          const int t = t0 + lane;
+      PROF_T(t5);
+      PROF_ADD(3, t4, t5);
+      // hit counts -> exclusive offsets (wave 0: 6 bins per lane, then a wave scan)
+      if (tid < 64) {
+        int c[6], tot = 0;
 #pragma unroll
-          for (int s = 0; s < 5; ++s) {
-            const int b = t < m ? S.upd.bin[t][s] : -1;
-            if (b >= 0) atomicAdd(&S.hist[b], S.upd.val[t][s]);
-          }
+        for (int i = 0; i < 6; ++i) {
+          const int bb = tid * 6 + i;
+          c[i] = 0;
+          if (bb < kLen)
+            for (int w = 0; w < kMaskWords; ++w) c[i] += __popcll(S.upd.mask[bb][w]);
+          tot += c[i];
+        }
+        int incl = tot;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+          const int y = __shfl_up(incl, o);
+          if (lane >= o) incl += y;
+        }
+        int run = incl - tot;
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+          const int bb = tid * 6 + i;
+          if (bb < kLen) S.upd.off[bb] = run;
+          run += c[i];
         }
       }
       __syncthreads();
+      if (tid < m) {  // scatter: rank = hits of the bin from lower neighbours of the chunk
+        const int wq = tid >> 6;
+        const uint64_t below = lanemask_lt();
+#pragma unroll
+        for (int s = 0; s < 5; ++s) {
+          const int bb = bins[s];
+          if (bb < 0) continue;
+          int r = __popcll(S.upd.mask[bb][wq] & below);
+          for (int w = 0; w < wq; ++w) r += __popcll(S.upd.mask[bb][w]);
+          S.upd.val[S.upd.off[bb] + r] = vals[s];
+        }
+      }
+      __syncthreads();
+#pragma unroll
+      for (int o = 0; o < 2; ++o) {
+        const int b = o ? b1 : b0;
+        if (b < kLen) {
+          int cnt = 0;
+          for (int w = 0; w < kMaskWords; ++w) {
+            cnt += __popcll(S.upd.mask[b][w]);
+            S.upd.mask[b][w] = 0;  // ready for the next chunk
+          }
+          const float* v = S.upd.val + S.upd.off[b];
+          float h = o ? h1 : h0;
+          int i = 0;
+          for (; i + 4 <= cnt; i += 4) {
+            const float a0 = v[i], a1 = v[i + 1], a2 = v[i + 2], a3 = v[i + 3];
+            h = h + a0; h = h + a1; h = h + a2; h = h + a3;
+          }
+          for (; i < cnt; ++i) h = h + v[i];
+          if (o) h1 = h; else h0 = h;
+        }
+      }
+      __syncthreads();
+      PROF_T(t6);
+      PROF_ADD(4, t5, t6);
     }
+    S.hist[b0] = h0;
+    if (b1 < kLen) S.hist[b1] = h1;
+    __syncthreads();
+    PROF_T(t7);
     if (tid == 0) {  // normalizeHistogram
       double acc_norm = 0;
       for (int j = 0; j < kLen; ++j) acc_norm += S.hist[j] * S.hist[j];
@@ -380,6 +487,8 @@ __global__ void __launch_bounds__(256) k_shot(GridView g, const float* __restric
     for (int i = tid; i < kLen; i += 256) d[i] = S.hist[i] / nrm;
     if (tid < 9) rfo[tid] = S.rf[tid];
     __syncthreads();
+    PROF_T(t8);
+    PROF_ADD(5, t7, t8);
   }
 }
 
@@ -425,6 +534,14 @@ void shot_dev(pfx_ctx* ctx, const float* sx, const float* sy, const float* sz, c
   PFX_HIP(hipMemcpyAsync(&h_nbr, nbr, sizeof(h_nbr), hipMemcpyDeviceToHost, st));
   PFX_HIP(hipStreamSynchronize(st));
   ctx->stats["shot_neighbors"] = (int64_t)h_nbr;
+#ifdef PFX_SHOT_PROFILE
+  {
+    unsigned long long pr[8];
+    PFX_HIP(hipMemcpyFromSymbol(pr, HIP_SYMBOL(g_shot_prof), sizeof(pr)));
+    fprintf(stderr, "shot phase cycles (summed over queries): sort %llu lrf %llu frame %llu hist %llu apply %llu out %llu\n",
+            pr[0], pr[1], pr[2], pr[3], pr[4], pr[5]);
+  }
+#endif
   if (h > 0)
     throw Error(PFX_ERR_CAPACITY, "shot: a query has " + std::to_string(h) + " neighbours (> " +
                                       std::to_string(kCap) + " supported)");

@@ -154,3 +154,19 @@ def test_fpfh_isolated_query_is_nan(ctx):
     o = O.fpfh(x, y, z, nx, ny, nz, qx, qy, qz, 0.08)
     assert np.isnan(g[1]).all() and np.isnan(o[1]).all()
     assert _nan_aware_equal(g, o)
+
+
+def test_config1_normals_fpfh_all_points():
+    """BASELINE configs[1]: 100k-point synthetic room (seed 1), NormalEstimation + FPFH (r 0.05)
+    at every point (input == surface: PCL's all-points SPFH branch)."""
+    from pcl_feature_extraction_amd import Context
+    from pcl_feature_extraction_amd.synth import synth_room
+    x, y, z, _ = synth_room(100_000, 1)
+    with Context(0) as c:
+        g = c.normals(x, y, z, 0.05)
+        o = O.normals(x, y, z, 0.05, threads=8)
+        for a, b in zip(g, o):
+            assert _nan_aware_equal(a, b)
+        d = c.fpfh(x, y, z, g[0], g[1], g[2], None, None, None, 0.05, same_as_surface=True)
+    od = O.fpfh(x, y, z, o[0], o[1], o[2], x, y, z, 0.05, same_as_surface=True, threads=8)
+    assert _nan_aware_equal(d, od)

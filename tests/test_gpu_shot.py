@@ -1,10 +1,9 @@
 """GPU parity: SHOTEstimationOMP<PointXYZRGB,Normal,SHOT352> + SHOTLocalReferenceFrameEstimation
 (evaluation.cpp:766-785) through the C-ABI, against the CPU restatement (oracle/or_shot.cpp).
 
-Bar: the local reference frame is bit-exact (same double operation sequence, no
-transcendentals); the descriptor is within 1e-4 L2 per row (north_star tolerance) -- its float
-histogram adds are applied with LDS atomics, so their order differs from PCL's loop only inside
-a wave instruction; NaN rows exactly where the restatement has them."""
+Bar: the local reference frame and the descriptor are bit-exact (same double operation sequence
+for the frame; the float histogram adds are applied in PCL's sequential order); the north_star
+tolerance, 1e-4 L2 per row, is asserted as well; NaN rows exactly where the restatement has them."""
 import os
 
 import numpy as np
@@ -29,6 +28,7 @@ def _check(g, o):
     assert np.array_equal(np.isnan(grf), np.isnan(orf))
     ok = ~gn
     assert np.array_equal(grf[ok].view(np.uint32), orf[ok].view(np.uint32))
+    assert np.array_equal(gd[ok].view(np.uint32), od[ok].view(np.uint32))
     l2 = np.linalg.norm(gd[ok].astype(np.float64) - od[ok], axis=1)
     assert l2.max() <= TOL, l2.max()
     return ok.sum()
