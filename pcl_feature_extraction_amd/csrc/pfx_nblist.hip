@@ -159,6 +159,15 @@ struct CandGlobal {
   }
 };
 
+#ifdef PFX_SHOT_PROFILE
+__device__ unsigned long long g_tile_prof[8];
+#define TPROF_T(v) long long v = (threadIdx.x == 0) ? clock64() : 0
+#define TPROF_ADD(i, a, b) if (threadIdx.x == 0) atomicAdd(&g_tile_prof[i], (unsigned long long)((b) - (a)))
+#else
+#define TPROF_T(v)
+#define TPROF_ADD(i, a, b)
+#endif
+
 // Wave-local bucket sort of one query's list L[0..k) (u16 candidate indices) into FLANN order.
 // Sd/St: wave-private scratch (k entries), bcount/bpos: wave-private NB buckets.
 template <int NB, class Cand>
@@ -240,6 +249,7 @@ __global__ void __launch_bounds__(256) k_nb_tile(GridView g, const int32_t* __re
   const int ntiles = *ntiles_ptr;
   const int64_t vb = xcd_block(blockIdx.x, gridDim.x);
   for (int64_t tile = vb; tile < ntiles; tile += gridDim.x) {
+    TPROF_T(p0);
     const uint32_t te = tiles[tile];
     const int32_t start = tile_start(te);
     const int qn = tile_qn(te);
@@ -258,6 +268,8 @@ __global__ void __launch_bounds__(256) k_nb_tile(GridView g, const int32_t* __re
       }
     }
     __syncthreads();
+    TPROF_T(p1);
+    TPROF_ADD(STAGE ? 0 : 4, p0, p1);
     float qx[QW], qy[QW], qz[QW];
     int cursor[QW];
 #pragma unroll
@@ -302,6 +314,8 @@ __global__ void __launch_bounds__(256) k_nb_tile(GridView g, const int32_t* __re
         if (wv + 4 * u < qn) s_k[wv + 4 * u] = cursor[u];
     }
     __syncthreads();
+    TPROF_T(p2);
+    TPROF_ADD(STAGE ? 1 : 5, p1, p2);
     int lg = 0;
     while ((1 << lg) < qn) ++lg;
     int maxk = 0;
@@ -343,6 +357,8 @@ __global__ void __launch_bounds__(256) k_nb_tile(GridView g, const int32_t* __re
       }
     }
     __syncthreads();
+    TPROF_T(p3);
+    TPROF_ADD(STAGE ? 2 : 6, p2, p3);
     const int64_t base = (int64_t)s_base;
     if (tid < qn && s_k[tid] <= LCAP) out.off[start + tid] = base + tid;
     // coalesced write of the interleaved block (padding slots are left unwritten)
@@ -357,6 +373,8 @@ __global__ void __launch_bounds__(256) k_nb_tile(GridView g, const int32_t* __re
       }
     }
     __syncthreads();  // LDS is reused by the next tile
+    TPROF_T(p4);
+    TPROF_ADD(STAGE ? 3 : 7, p3, p4);
   }
 }
 
@@ -612,6 +630,14 @@ void build_lists(pfx_ctx* ctx, const Grid& G, const uint8_t* mask, double radius
     ctx->stats[std::string(tag) + "_tiles_dense"] = h_cnt[1];
     ctx->stats[std::string(tag) + "_single"] = h_cnt[2];
     ctx->stats[std::string(tag) + "_huge"] = h_cnt[3];
+#ifdef PFX_SHOT_PROFILE
+    {
+      unsigned long long pr[8];
+      PFX_HIP(hipMemcpyFromSymbol(pr, HIP_SYMBOL(g_tile_prof), sizeof(pr)));
+      fprintf(stderr, "%s tile cycles: sparse stage %llu test %llu sort %llu write %llu | dense - %llu test %llu "
+              "sort %llu write %llu (cumulative)\n", tag, pr[0], pr[1], pr[2], pr[3], pr[4], pr[5], pr[6], pr[7]);
+    }
+#endif
     return;
   }
   throw Error(PFX_ERR_DEVICE, std::string(tag) + ": neighbour-list buffer growth failed");

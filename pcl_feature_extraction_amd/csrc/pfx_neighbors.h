@@ -138,4 +138,81 @@ __device__ __forceinline__ int sorted_neighbors(const GridView& g, float qx, flo
   return k;
 }
 
+// ---- bucketed sort (256-thread blocks): FLANN order without a bitonic network ----
+// d2 -> bucket is monotone (one multiplication by a positive constant, then floor), so bucket
+// order is d2 order; inside a bucket every key's final slot is its exact rank among the bucket's
+// keys (keys are unique: the index breaks ties).  Neighbours of a surface point spread evenly
+// over d2 (area grows with d2), so buckets hold a handful of keys; a bucket above kMaxBucket
+// makes the caller fall back to the bitonic sort.
+constexpr int kSortBuckets = 256;
+constexpr int kMaxBucket = 96;
+
+struct BucketLds {
+  int off[kSortBuckets + 1];
+  int cur[kSortBuckets];
+  int wsum[4];
+  int maxn;
+};
+
+__device__ __forceinline__ int d2_bucket(float d2, float inv) {
+  const int b = (int)(d2 * inv);
+  return b < kSortBuckets - 1 ? b : kSortBuckets - 1;
+}
+
+// gather (as gather_keys) + sort into keys[0..k); tmp: cap more keys.  Requires blockDim.x == 256.
+// Returns k (> cap: nothing sorted, as sorted_neighbors).
+__device__ __forceinline__ int sorted_neighbors_bucketed(const GridView& g, float qx, float qy, float qz,
+                                                         float rr, uint64_t* keys, uint64_t* tmp, int cap,
+                                                         int* s_count, BucketLds& B) {
+  const int tid = threadIdx.x, lane = tid & 63;
+  const float inv = (float)kSortBuckets / rr;
+  B.off[tid] = 0;  // counts first
+  if (tid == 0) B.maxn = 0;
+  const int k = gather_keys(g, qx, qy, qz, rr, keys, cap, s_count);  // (its barriers order the zeroing)
+  if (k > cap) return k;
+  for (int i = tid; i < k; i += 256) atomicAdd(&B.off[d2_bucket(key_d2(keys[i]), inv)], 1);
+  __syncthreads();
+  const int c = B.off[tid];
+  int incl = c;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(incl, o);
+    if (lane >= o) incl += y;
+  }
+  if (lane == 63) B.wsum[tid >> 6] = incl;
+  atomicMax(&B.maxn, c);
+  __syncthreads();
+  int base = 0;
+  for (int w = 0; w < (tid >> 6); ++w) base += B.wsum[w];
+  const int ex = base + incl - c;
+  __syncthreads();  // every count read before the offsets overwrite them
+  B.off[tid] = ex;
+  B.cur[tid] = ex;
+  if (tid == 0) B.off[kSortBuckets] = k;
+  const bool fallback = B.maxn > kMaxBucket;
+  __syncthreads();
+  if (fallback) {
+    const int P = next_pow2(k);
+    for (int i = k + tid; i < P; i += 256) keys[i] = ~0ull;
+    __syncthreads();
+    bitonic_sort(keys, P);
+    return k;
+  }
+  for (int i = tid; i < k; i += 256) {
+    const uint64_t key = keys[i];
+    tmp[atomicAdd(&B.cur[d2_bucket(key_d2(key), inv)], 1)] = key;
+  }
+  __syncthreads();
+  for (int i = tid; i < k; i += 256) {
+    const uint64_t key = tmp[i];
+    const int b = d2_bucket(key_d2(key), inv);
+    const int o = B.off[b], e = B.off[b + 1];
+    int r = 0;
+    for (int j = o; j < e; ++j) r += tmp[j] < key;
+    keys[o + r] = key;
+  }
+  __syncthreads();
+  return k;
+}
+
 }  // namespace pfx

@@ -205,8 +205,9 @@ __global__ void __launch_bounds__(256) k_shot(GridView g, const float* __restric
                                               int32_t* __restrict__ over, int* __restrict__ n_over,
                                               double radius, float* __restrict__ desc, float* __restrict__ rf_out,
                                               int* __restrict__ err, unsigned long long* __restrict__ nbr) {
-  extern __shared__ __attribute__((aligned(16))) uint64_t keys[];  // CAP
+  extern __shared__ __attribute__((aligned(16))) uint64_t keys[];  // CAP (+ CAP sort scratch, first pass)
   __shared__ ShotLds S;
+  __shared__ BucketLds SB;
   __shared__ int s_count;
   const int tid = threadIdx.x, lane = tid & 63;
   const float rr = (float)(radius * radius);
@@ -222,7 +223,9 @@ __global__ void __launch_bounds__(256) k_shot(GridView g, const float* __restric
       continue;
     }
     PROF_T(t0);
-    const int k = sorted_neighbors(g, cx, cy, cz, rr, keys, CAP, &s_count);
+    const int k = CAP == kCapSmall
+                      ? sorted_neighbors_bucketed(g, cx, cy, cz, rr, keys, keys + CAP, CAP, &s_count, SB)
+                      : sorted_neighbors(g, cx, cy, cz, rr, keys, CAP, &s_count);
     PROF_T(t1);
     PROF_ADD(0, t0, t1);
     if (k > CAP) {
@@ -518,7 +521,7 @@ void shot_dev(pfx_ctx* ctx, const float* sx, const float* sy, const float* sz, c
     TimeScope ts(ctx, "shot");
     int32_t* over = ctx->buf("shot_over").as<int32_t>(nq);
     int* n_over = err + 1;
-    const size_t lds_s = sizeof(uint64_t) * kCapSmall, lds = sizeof(uint64_t) * kCap;
+    const size_t lds_s = 2 * sizeof(uint64_t) * kCapSmall, lds = sizeof(uint64_t) * kCap;
     PFX_HIP(hipFuncSetAttribute((const void*)k_shot<kCap>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     const unsigned blocks = (unsigned)std::min<int64_t>(nq, 256 * 10);
     k_shot<kCapSmall><<<blocks, 256, lds_s, st>>>(g, snx, sny, snz, qx, qy, qz, nq, nullptr, nullptr, over, n_over,
