@@ -160,7 +160,7 @@ struct CandGlobal {
 };
 
 #ifdef PFX_SHOT_PROFILE
-__device__ unsigned long long g_tile_prof[8];
+__device__ unsigned long long g_tile_prof[16];
 #define TPROF_T(v) long long v = (threadIdx.x == 0) ? clock64() : 0
 #define TPROF_ADD(i, a, b) if (threadIdx.x == 0) atomicAdd(&g_tile_prof[i], (unsigned long long)((b) - (a)))
 #else
@@ -168,12 +168,107 @@ __device__ unsigned long long g_tile_prof[8];
 #define TPROF_ADD(i, a, b)
 #endif
 
+// wave_sort for k <= 64 * E with every element's (t, d2, bucket, slot) kept in registers
+// (element i of a lane is e = lane + 64 i): one LDS round trip per phase instead of one per
+// 64 elements, and the candidate coordinates are read once.
+template <int NB, int E, class Cand>
+__device__ __forceinline__ void wave_sort_regs(uint16_t* L, int k, float qx, float qy, float qz, const Cand& cand,
+                                               float bscale, uint32_t* Sd, uint16_t* St, int* bcount, int* bpos,
+                                               const GridView& g, const Runs& R, int lane) {
+  for (int b = lane; b < NB; b += 64) bcount[b] = 0;
+  int t[E], b[E];
+  uint32_t d[E];
+#pragma unroll
+  for (int i = 0; i < E; ++i) t[i] = lane + 64 * i < k ? L[lane + 64 * i] : 0;
+  wave_sync();
+#pragma unroll
+  for (int i = 0; i < E; ++i) {
+    float px, py, pz;
+    cand.get(t[i], px, py, pz);
+    const float d2 = flann_d2(qx, qy, qz, px, py, pz);
+    d[i] = __float_as_uint(d2);  // d2 >= +0: bit order == value order
+    const int bb = (int)(d2 * bscale);
+    b[i] = bb < NB ? bb : NB - 1;
+    if (lane + 64 * i < k) atomicAdd(&bcount[b[i]], 1);
+  }
+  wave_sync();
+  {
+    constexpr int PER = NB / 64;
+    int c[PER], sum = 0;
+#pragma unroll
+    for (int v = 0; v < PER; ++v) { c[v] = bcount[lane * PER + v]; sum += c[v]; }
+    int inc = sum;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int x = __shfl_up(inc, o);
+      if (lane >= o) inc += x;
+    }
+    int ex = inc - sum;
+#pragma unroll
+    for (int v = 0; v < PER; ++v) { bpos[lane * PER + v] = ex; ex += c[v]; }
+  }
+  wave_sync();
+  int slot[E];
+#pragma unroll
+  for (int i = 0; i < E; ++i) slot[i] = lane + 64 * i < k ? atomicAdd(&bpos[b[i]], 1) : 0;
+#pragma unroll
+  for (int i = 0; i < E; ++i)
+    if (lane + 64 * i < k) {
+      Sd[slot[i]] = d[i];
+      St[slot[i]] = (uint16_t)t[i];
+    }
+  wave_sync();
+  // bucket [st, en): en = bpos after the scatter; rank = keys of the bucket below mine
+  int st[E], en[E];
+#pragma unroll
+  for (int i = 0; i < E; ++i) {
+    en[i] = bpos[b[i]];
+    st[i] = en[i] - bcount[b[i]];
+  }
+  int rank[E];
+  bool tie = false;
+#pragma unroll
+  for (int i = 0; i < E; ++i) {
+    uint32_t dv[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) dv[j] = st[i] + j < en[i] ? Sd[st[i] + j] : 0xffffffffu;
+    int r = 0, eq = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      r += dv[j] < d[i];
+      eq += dv[j] == d[i];
+    }
+    for (int v = st[i] + 4; v < en[i]; ++v) {
+      const uint32_t x = Sd[v];
+      r += x < d[i];
+      eq += x == d[i];
+    }
+    rank[i] = r;
+    tie |= lane + 64 * i < k && eq > 1;
+  }
+  if (__builtin_amdgcn_ballot_w64(tie)) {  // equal d2: the caller index decides (FLANN); rare
+#pragma unroll
+    for (int i = 0; i < E; ++i) {
+      if (lane + 64 * i >= k) continue;
+      const int32_t mine = g.perm[run_pos(R, t[i])];
+      for (int v = st[i]; v < en[i]; ++v)
+        if (v != slot[i] && Sd[v] == d[i] && g.perm[run_pos(R, St[v])] < mine) ++rank[i];
+    }
+  }
+  wave_sync();
+#pragma unroll
+  for (int i = 0; i < E; ++i)
+    if (lane + 64 * i < k) L[st[i] + rank[i]] = (uint16_t)t[i];
+  wave_sync();
+}
+
 // Wave-local bucket sort of one query's list L[0..k) (u16 candidate indices) into FLANN order.
 // Sd/St: wave-private scratch (k entries), bcount/bpos: wave-private NB buckets.
 template <int NB, class Cand>
 __device__ __forceinline__ void wave_sort(uint16_t* L, int k, float qx, float qy, float qz, const Cand& cand,
                                           float bscale, uint32_t* Sd, uint16_t* St, int* bcount, int* bpos,
                                           const GridView& g, const Runs& R, int lane) {
+  TPROF_T(w0);
   for (int b = lane; b < NB; b += 64) bcount[b] = 0;
   wave_sync();
   for (int e = lane; e < k; e += 64) {
@@ -184,6 +279,8 @@ __device__ __forceinline__ void wave_sort(uint16_t* L, int k, float qx, float qy
     atomicAdd(&bcount[b < NB ? b : NB - 1], 1);
   }
   wave_sync();
+  TPROF_T(w1);
+  TPROF_ADD(8, w0, w1);
   {
     constexpr int PER = NB / 64;
     int c[PER], s = 0;
@@ -200,6 +297,8 @@ __device__ __forceinline__ void wave_sort(uint16_t* L, int k, float qx, float qy
     for (int v = 0; v < PER; ++v) { bpos[lane * PER + v] = ex; ex += c[v]; }
   }
   wave_sync();
+  TPROF_T(w2);
+  TPROF_ADD(9, w1, w2);
   for (int e = lane; e < k; e += 64) {
     const int t = L[e];
     float px, py, pz;
@@ -212,27 +311,64 @@ __device__ __forceinline__ void wave_sort(uint16_t* L, int k, float qx, float qy
     St[slot] = (uint16_t)t;
   }
   wave_sync();
-  for (int s = lane; s < k; s += 64) {
-    const uint32_t d = Sd[s];
-    int b = (int)(__uint_as_float(d) * bscale);
-    b = b < NB ? b : NB - 1;
-    const int en = bpos[b], st = en - bcount[b];
-    const int t = St[s];
+  TPROF_T(w3);
+  TPROF_ADD(10, w2, w3);
+  // rank inside the bucket; two elements per lane per round and the first four bucket entries
+  // read at once, so the LDS round trips of a round overlap
+  auto bucket_rank = [&](int s, uint32_t d, int t, int st, int en) {
+    uint32_t dv[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) dv[i] = st + i < en ? Sd[st + i] : 0xffffffffu;
     int rank = 0;
-    for (int v = st; v < en; ++v) {
-      const uint32_t dv = Sd[v];
-      if (dv < d) ++rank;
-      else if (dv == d && v != s && g.perm[run_pos(R, St[v])] < g.perm[run_pos(R, t)]) ++rank;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int v = st + i;
+      if (v < en) {
+        if (dv[i] < d) ++rank;
+        else if (dv[i] == d && v != s && g.perm[run_pos(R, St[v])] < g.perm[run_pos(R, t)]) ++rank;
+      }
     }
-    L[st + rank] = (uint16_t)t;
+    for (int v = st + 4; v < en; ++v) {
+      const uint32_t x = Sd[v];
+      if (x < d) ++rank;
+      else if (x == d && v != s && g.perm[run_pos(R, St[v])] < g.perm[run_pos(R, t)]) ++rank;
+    }
+    return rank;
+  };
+  for (int s0 = lane; s0 < k; s0 += 128) {
+    const int s1 = s0 + 64;
+    const bool h1 = s1 < k;
+    const uint32_t d0 = Sd[s0], d1 = h1 ? Sd[s1] : 0u;
+    const int t0 = St[s0], t1 = h1 ? St[s1] : 0;
+    int b0 = (int)(__uint_as_float(d0) * bscale), b1 = (int)(__uint_as_float(d1) * bscale);
+    b0 = b0 < NB ? b0 : NB - 1;
+    b1 = b1 < NB ? b1 : NB - 1;
+    const int en0 = bpos[b0], c0 = bcount[b0], en1 = bpos[b1], c1 = bcount[b1];
+    const int st0 = en0 - c0, st1 = en1 - c1;
+    const int r0 = bucket_rank(s0, d0, t0, st0, en0);
+    const int r1 = h1 ? bucket_rank(s1, d1, t1, st1, en1) : 0;
+    L[st0 + r0] = (uint16_t)t0;
+    if (h1) L[st1 + r1] = (uint16_t)t1;
   }
   wave_sync();
+  TPROF_T(w4);
+  TPROF_ADD(11, w3, w4);
+}
+
+template <int NB, class Cand>
+__device__ __forceinline__ void sort_list(uint16_t* L, int k, float qx, float qy, float qz, const Cand& cand,
+                                          float bscale, uint32_t* Sd, uint16_t* St, int* bcount, int* bpos,
+                                          const GridView& g, const Runs& R, int lane) {
+  if (k <= 128) wave_sort_regs<NB, 2>(L, k, qx, qy, qz, cand, bscale, Sd, St, bcount, bpos, g, R, lane);
+  else if (k <= 256) wave_sort_regs<NB, 4>(L, k, qx, qy, qz, cand, bscale, Sd, St, bcount, bpos, g, R, lane);
+  else if (k <= 512) wave_sort_regs<NB, 8>(L, k, qx, qy, qz, cand, bscale, Sd, St, bcount, bpos, g, R, lane);
+  else wave_sort<NB>(L, k, qx, qy, qz, cand, bscale, Sd, St, bcount, bpos, g, R, lane);
 }
 
 // STAGE: candidates staged in LDS (sparse tiles); otherwise read from L2 (dense tiles, where
 // staging 8000 candidates would cap the kernel at one workgroup per CU)
 template <int LCAP, int NB, int TCAP, bool STAGE>
-__global__ void __launch_bounds__(256) k_nb_tile(GridView g, const int32_t* __restrict__ qpos,
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) k_nb_tile(GridView g, const int32_t* __restrict__ qpos,
                                                  const uint32_t* __restrict__ skeys,
                                                  const uint32_t* __restrict__ tiles, const int* __restrict__ ntiles_ptr,
                                                  float rr, float bscale, int sorted, ListOut out,
@@ -346,11 +482,11 @@ __global__ void __launch_bounds__(256) k_nb_tile(GridView g, const int32_t* __re
         if (j < qn && k <= LCAP && k > 1) {  // wave-uniform
           if (STAGE) {
             const CandLds cand{cx, cy, cz};
-            wave_sort<NB>(lists[j], k, qx[u], qy[u], qz[u], cand, bscale, sd[wv], stt[wv], bcount[wv], bpos[wv],
+            sort_list<NB>(lists[j], k, qx[u], qy[u], qz[u], cand, bscale, sd[wv], stt[wv], bcount[wv], bpos[wv],
                           g, R, lane);
           } else {
             const CandGlobal cand{g.sp, &R};
-            wave_sort<NB>(lists[j], k, qx[u], qy[u], qz[u], cand, bscale, sd[wv], stt[wv], bcount[wv], bpos[wv],
+            sort_list<NB>(lists[j], k, qx[u], qy[u], qz[u], cand, bscale, sd[wv], stt[wv], bcount[wv], bpos[wv],
                           g, R, lane);
           }
         }
@@ -632,8 +768,10 @@ void build_lists(pfx_ctx* ctx, const Grid& G, const uint8_t* mask, double radius
     ctx->stats[std::string(tag) + "_huge"] = h_cnt[3];
 #ifdef PFX_SHOT_PROFILE
     {
-      unsigned long long pr[8];
+      unsigned long long pr[16];
       PFX_HIP(hipMemcpyFromSymbol(pr, HIP_SYMBOL(g_tile_prof), sizeof(pr)));
+      fprintf(stderr, "%s wave_sort cycles (wave 0): count %llu scan %llu scatter %llu rank %llu\n", tag, pr[8],
+              pr[9], pr[10], pr[11]);
       fprintf(stderr, "%s tile cycles: sparse stage %llu test %llu sort %llu write %llu | dense - %llu test %llu "
               "sort %llu write %llu (cumulative)\n", tag, pr[0], pr[1], pr[2], pr[3], pr[4], pr[5], pr[6], pr[7]);
     }
