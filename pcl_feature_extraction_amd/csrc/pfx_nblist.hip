@@ -362,13 +362,14 @@ __device__ __forceinline__ void sort_list(uint16_t* L, int k, float qx, float qy
   if (k <= 128) wave_sort_regs<NB, 2>(L, k, qx, qy, qz, cand, bscale, Sd, St, bcount, bpos, g, R, lane);
   else if (k <= 256) wave_sort_regs<NB, 4>(L, k, qx, qy, qz, cand, bscale, Sd, St, bcount, bpos, g, R, lane);
   else if (k <= 512) wave_sort_regs<NB, 8>(L, k, qx, qy, qz, cand, bscale, Sd, St, bcount, bpos, g, R, lane);
+  else if (k <= 1024) wave_sort_regs<NB, 16>(L, k, qx, qy, qz, cand, bscale, Sd, St, bcount, bpos, g, R, lane);
   else wave_sort<NB>(L, k, qx, qy, qz, cand, bscale, Sd, St, bcount, bpos, g, R, lane);
 }
 
 // STAGE: candidates staged in LDS (sparse tiles); otherwise read from L2 (dense tiles, where
 // staging 8000 candidates would cap the kernel at one workgroup per CU)
 template <int LCAP, int NB, int TCAP, bool STAGE>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) k_nb_tile(GridView g, const int32_t* __restrict__ qpos,
+__global__ void __launch_bounds__(256, STAGE ? 3 : 2) k_nb_tile(GridView g, const int32_t* __restrict__ qpos,
                                                  const uint32_t* __restrict__ skeys,
                                                  const uint32_t* __restrict__ tiles, const int* __restrict__ ntiles_ptr,
                                                  float rr, float bscale, int sorted, ListOut out,
