@@ -35,7 +35,7 @@ VERBOSE_TIMERS = ["grid_bbox", "grid_build", "normals", "normals_tiles", "normal
                   "narf_border", "narf_interest", "narf_nms", "narf_gather", "fpfh_mark", "fpfh_spfh",
                   "fpfh_weight", "shot"]
 VERBOSE_STATS = ["normals_neighbors", "normals_queries", "normals_tiles_sparse", "normals_tiles_dense",
-                 "normals_single", "normals_huge", "fpfh_spfh_points", "narf_candidates", "narf_keypoints",
+                 "normals_single", "normals_huge", "fpfh_spfh_points", "fpfh_spfh_pairs", "fpfh_spfh_exact_pairs", "narf_candidates", "narf_keypoints",
                  "narf_interest_fullimage", "narf_interest_grown", "narf_interest_window_px",
                  "narf_interest_visits", "narf_interest_queue_grown", "fpfh_weight_kmax", "fpfh_weight_sequential",
                  "shot_neighbors"]

@@ -25,6 +25,7 @@ constexpr int kDesc = 33;
 constexpr int kCapW = 16384;  // sorted-neighbour capacity of the weighting kernel (LDS)
 constexpr int kChunkW = 128;  // SPFH rows staged per chunk in the weighting kernel
 constexpr int kWT = 1024;     // weighting workgroup: few queries, each as wide as possible
+constexpr int kHistCopies = 16;  // SPFH per-wave counter copies
 
 // PCL 1.7 `acos (fabs (a1)) > acos (fabs (a2))` (double acos, correctly rounded by glibc):
 // acos is strictly decreasing and distinct floats >= 2^-26 map to distinct rounded values, so
@@ -92,6 +93,134 @@ __device__ __forceinline__ void pair_bins(f3 p1, f3 n1, f3 p2, f3 n2, int& h1, i
   h3 = bin_of((double)kBins * (((double)f3o + 1.0) * 0.5));
 }
 
+// c sequential float additions of incr starting from 0 (PCL's hist_incr loop), in O(binades):
+// inside a binade of s every step adds the same multiple of ulp(s) (incr's position between two
+// grid points does not depend on s) unless incr is an exact half-way case, which falls back to
+// the loop; steps that would reach the next binade are taken one by one.
+__device__ __forceinline__ float repeated_add(float incr, int c) {
+  float s = 0.0f;
+  int rem = c;
+  while (rem > 0) {
+    s = s + incr;
+    --rem;
+    if (rem == 0 || !(s > 0.0f) || !isfinite(s)) break;
+    const int e = ilogbf(s);
+    const double ulp = ldexp(1.0, e - 23), top = ldexp(1.0, e + 1);
+    const double t = (double)incr / ulp;
+    if (t - floor(t) == 0.5) {  // tie: the step depends on the parity of s
+      for (; rem > 0; --rem) s = s + incr;
+      break;
+    }
+    const double delta = (double)(s + incr) - (double)s;
+    if (delta <= 0.0) {  // s no longer changes
+      rem = 0;
+      break;
+    }
+    int64_t n = (int64_t)ceil((top - (double)s) / delta) - 1;  // s + n delta < top
+    if (n > rem) n = rem;
+    if (n > 0) {
+      s = (float)((double)s + (double)n * delta);
+      rem -= (int)n;
+    }
+  }
+  for (; rem > 0; --rem) s = s + incr;  // (after a break on a non-finite or zero sum)
+  return s;
+}
+
+// ---- fast path of pair_bins ----
+// The same float operations as pair_bins up to the first division; then approximate quotients
+// (v_rcp / v_rsq), a polynomial atan2 and the bin maps, each feature checked against its bin
+// edges with a bound on |approximate - exact-path value| (fractions of a bin: tol).  Any check
+// too close to call (an edge within the bound, |angle1| ~ |angle2|, non-finite normals, tiny
+// angles) returns false and the caller runs the exact pair_bins.  Bounds (normals |n| <= 1.01):
+//   f3 = dot/f4:            |approx - exact| <= 4e-7         used 1e-6
+//   f2 = v . n2:            v components within 4e-7, dot    used 4e-6
+//   f1 = atan2(w . n2, x):  y within 8e-6 -> 8e-6 / r, atan poly + ops 6e-7, CR rounding 1.2e-7
+//                                                            used 1e-6 + 8e-6 / r
+// (polynomial: max |atan_poly(a) - atan(a)| = 1.5e-7 on [0, 1] in float Horner, measured).
+__device__ __forceinline__ float atan_poly(float a) {
+  const float z = a * a;
+  float p = -0.00405456405133009f;
+  p = p * z + 0.021862948313355446f;
+  p = p * z + -0.0559123195707798f;
+  p = p * z + 0.0964219719171524f;
+  p = p * z + -0.1390862911939621f;
+  p = p * z + 0.19946566224098206f;
+  p = p * z + -0.33329859375953674f;
+  p = p * z + 0.9999993443489075f;
+  return p * a;
+}
+
+__device__ __forceinline__ bool bin_fast(double vd, double tol, int& h) {
+  const double m = floor(vd);
+  const double fr = vd - m;
+  if (!(fr > tol && fr < 1.0 - tol)) return false;  // also rejects NaN
+  const int b = (int)m;
+  h = b < 0 ? 0 : (b >= kBins ? kBins - 1 : b);
+  return true;
+}
+
+__device__ __forceinline__ bool pair_bins_fast(f3 p1, f3 n1, f3 p2, f3 n2, int& h1, int& h2, int& h3) {
+  f3 dp = sub3(p2, p1);
+  const float s4 = sqn4(dp);
+  if (s4 == 0.0f) {  // f4 == 0 in pair_bins
+    h1 = bin_of(f1_scaled(0.0));
+    h2 = h3 = bin_of((double)kBins * ((0.0 + 1.0) * 0.5));
+    return true;
+  }
+  if (!(isfinite(n1.x) && isfinite(n1.y) && isfinite(n1.z) && isfinite(n2.x) && isfinite(n2.y) && isfinite(n2.z)))
+    return false;
+  const float d1 = dot4(n1, dp), d2 = dot4(n2, dp);
+  const float ad1 = fabsf(d1), ad2 = fabsf(d2);
+  const float rf4 = __builtin_amdgcn_rsqf(s4);  // ~ 1 / f4
+  if (fmaxf(ad1, ad2) * rf4 < 2e-8f) return false;  // acos_greater's tiny-angle branch
+  bool swap;
+  if (ad1 < ad2 * (1.0f - 4e-7f)) swap = true;        // |angle1| < |angle2|
+  else if (ad1 > ad2 * (1.0f + 4e-7f)) swap = false;
+  else return false;
+  f3 n1c = n1, n2c = n2;
+  float f3a;
+  if (swap) {
+    n1c = n2; n2c = n1;
+    dp = scale3(dp, -1.0f);
+    f3a = -d2 * rf4;
+  } else {
+    f3a = d1 * rf4;
+  }
+  const f3 v = cross3(dp, n1c);
+  const float sv = sqn4(v);
+  if (sv == 0.0f) {  // v_norm == 0 in pair_bins
+    h1 = bin_of(f1_scaled(0.0));
+    h2 = h3 = bin_of((double)kBins * ((0.0 + 1.0) * 0.5));
+    return true;
+  }
+  const f3 vh = scale3(v, __builtin_amdgcn_rsqf(sv));
+  const f3 w = cross3(n1c, vh);
+  const float f2a = dot4(vh, n2c);
+  const float y = dot4(w, n2c), x = dot4(n1c, n2c);
+  const float ax = fabsf(x), ay = fabsf(y);
+  const float mx = fmaxf(ax, ay), mn = fminf(ax, ay);
+  if (!(mx > 1e-20f)) return false;
+  float t = atan_poly(mn * __builtin_amdgcn_rcpf(mx));
+  if (ay > ax) t = 1.57079637f - t;
+  if (x < 0.0f) t = 3.14159274f - t;
+  const float f1a = y < 0.0f ? -t : t;
+  const double d_pi = (double)(1.0f / (2.0f * 3.14159265358979323846f));
+  const double tol1 = (1e-6 + 8e-6 / (double)mx) * (double)kBins * d_pi;
+  return bin_fast(f1_scaled((double)f1a), tol1, h1) &&
+         bin_fast((double)kBins * (((double)f2a + 1.0) * 0.5), 4e-6 * 0.5 * kBins, h2) &&
+         bin_fast((double)kBins * (((double)f3a + 1.0) * 0.5), 1e-6 * 0.5 * kBins, h3);
+}
+
+// the exact path out of line (rare), bins packed h1 | h2 << 8 | h3 << 16
+__device__ __attribute__((noinline)) int pair_bins_exact(float p1x, float p1y, float p1z, float n1x, float n1y,
+                                                         float n1z, float p2x, float p2y, float p2z, float n2x,
+                                                         float n2y, float n2z) {
+  int h1, h2, h3;
+  pair_bins(mk3(p1x, p1y, p1z), mk3(n1x, n1y, n1z), mk3(p2x, p2y, p2z), mk3(n2x, n2y, n2z), h1, h2, h3);
+  return h1 | (h2 << 8) | (h3 << 16);
+}
+
 __global__ void k_sorted_normals(const int32_t* __restrict__ perm, int64_t n, const float* __restrict__ nx,
                                  const float* __restrict__ ny, const float* __restrict__ nz,
                                  float4* __restrict__ out) {
@@ -128,9 +257,11 @@ __global__ void k_all_finite(const uint32_t* __restrict__ skeys, int64_t n, uint
 __global__ void __launch_bounds__(256) k_fpfh_spfh(GridView g, const float4* __restrict__ snp,
                                                    const int32_t* __restrict__ slist,
                                                    const int64_t* __restrict__ count_ptr, float rr,
-                                                   float* __restrict__ spfh) {
+                                                   float* __restrict__ spfh, unsigned long long* __restrict__ pairs) {
   __shared__ uint32_t queue[4][128];
-  __shared__ int hist[4][kDesc];
+  // 16 copies of each wave's counters (lane & 15): pairs of a planar patch pile into a few bins,
+  // and same-address LDS atomics serialise
+  __shared__ int hist[4][kHistCopies][kDesc];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int64_t count = *count_ptr;
   const int64_t stride = (int64_t)gridDim.x * 4;
@@ -138,7 +269,7 @@ __global__ void __launch_bounds__(256) k_fpfh_spfh(GridView g, const float4* __r
     const int32_t s = slist[w];
     const float4 pc = g.sp[s], pnc = snp[s];
     const f3 pp = mk3(pc.x, pc.y, pc.z), pn = mk3(pnc.x, pnc.y, pnc.z);
-    if (lane < kDesc) hist[wv][lane] = 0;
+    for (int i = lane; i < kHistCopies * kDesc; i += 64) (&hist[wv][0][0])[i] = 0;
     Runs R;
     query_runs(g, pc.x, pc.y, pc.z, R);
     int k = 0, qn = 0;
@@ -149,10 +280,20 @@ __global__ void __launch_bounds__(256) k_fpfh_spfh(GridView g, const float4* __r
         const uint32_t q = queue[wv][lane];
         const float4 qc = g.sp[q], qnv = snp[q];
         int h1, h2, h3;
-        pair_bins(pp, pn, mk3(qc.x, qc.y, qc.z), mk3(qnv.x, qnv.y, qnv.z), h1, h2, h3);
-        atomicAdd(&hist[wv][h1], 1);
-        atomicAdd(&hist[wv][kBins + h2], 1);
-        atomicAdd(&hist[wv][2 * kBins + h3], 1);
+        const f3 qp = mk3(qc.x, qc.y, qc.z), qn3 = mk3(qnv.x, qnv.y, qnv.z);
+        const bool fast = pair_bins_fast(pp, pn, qp, qn3, h1, h2, h3);
+        const uint64_t slow = __ballot(!fast);
+        if (lane == 0 && slow) atomicAdd(pairs + 1, (unsigned long long)__popcll(slow));
+        if (!fast) {
+          const int hb = pair_bins_exact(pp.x, pp.y, pp.z, pn.x, pn.y, pn.z, qp.x, qp.y, qp.z, qn3.x, qn3.y, qn3.z);
+          h1 = hb & 0xff;
+          h2 = (hb >> 8) & 0xff;
+          h3 = hb >> 16;
+        }
+        int* hc = hist[wv][lane & (kHistCopies - 1)];
+        atomicAdd(&hc[h1], 1);
+        atomicAdd(&hc[kBins + h2], 1);
+        atomicAdd(&hc[2 * kBins + h3], 1);
       }
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
       __builtin_amdgcn_wave_barrier();
@@ -182,12 +323,12 @@ __global__ void __launch_bounds__(256) k_fpfh_spfh(GridView g, const float4* __r
     }
     process(qn);
     if (lane < kDesc) {
-      const int c = hist[wv][lane];
+      int c = 0;
+      for (int j = 0; j < kHistCopies; ++j) c += hist[wv][j][lane];
       const float incr = 100.0f / (float)(k - 1);
-      float v = 0.0f;
-      for (int j = 0; j < c; ++j) v = v + incr;
-      spfh[(int64_t)g.perm[s] * kDesc + lane] = v;
+      spfh[(int64_t)g.perm[s] * kDesc + lane] = repeated_add(incr, c);
     }
+    if (lane == 0) atomicAdd(pairs, (unsigned long long)(k - 1));
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
   }
@@ -393,16 +534,17 @@ void fpfh_dev(pfx_ctx* ctx, const float* sx, const float* sy, const float* sz, c
     PFX_HIP(rocprim::select(tmp, tmp_bytes, rocprim::counting_iterator<int32_t>(0), flags, slist, d_sel,
                             (size_t)ns, st));
   }
+  int* err = ctx->buf("fpfh_err").as<int>(8);  // [0] k over capacity, [1] max k, [2] inexact sums, [4..5] pairs
+  PFX_HIP(hipMemsetAsync(err, 0, 8 * sizeof(int), st));
+  unsigned long long* d_pairs = reinterpret_cast<unsigned long long*>(err + 4);
   {
     // the S count stays on the device: a grid-stride launch sized for the worst case
     TimeScope ts(ctx, "fpfh_spfh");
     const int64_t waves = std::min<int64_t>(ns, 256 * 4 * 20);  // up to 20 waves per CU in flight
     k_fpfh_spfh<<<(unsigned)std::max<int64_t>(8, ceil_div(waves, 4) & ~7), 256, 0, st>>>(g, snp, slist, d_sel, rr,
-                                                                                          spfh);
+                                                                                          spfh, d_pairs);
     check_launch("k_fpfh_spfh");
   }
-  int* err = ctx->buf("fpfh_err").as<int>(4);  // [0] k over capacity, [1] max k, [2] inexact sums
-  PFX_HIP(hipMemsetAsync(err, 0, 4 * sizeof(int), st));
   {
     TimeScope ts(ctx, "fpfh_weight");
     const size_t lds = sizeof(uint64_t) * kCapW;
@@ -411,12 +553,19 @@ void fpfh_dev(pfx_ctx* ctx, const float* sx, const float* sy, const float* sz, c
     k_fpfh_weight<<<blocks, kWT, lds, st>>>(g, qx, qy, qz, nq, rr, spfh, out, err);
     check_launch("k_fpfh_weight");
   }
-  int h[4] = {0, 0, 0, 0};
+  int h[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   int64_t count = 0;
   PFX_HIP(hipMemcpyAsync(h, err, sizeof(h), hipMemcpyDeviceToHost, st));
   PFX_HIP(hipMemcpyAsync(&count, d_sel, sizeof(int64_t), hipMemcpyDeviceToHost, st));
   PFX_HIP(hipStreamSynchronize(st));
   ctx->stats["fpfh_spfh_points"] = count;
+  {
+    unsigned long long pr;
+    std::memcpy(&pr, h + 4, sizeof(pr));
+    ctx->stats["fpfh_spfh_pairs"] = (int64_t)pr;
+    std::memcpy(&pr, h + 6, sizeof(pr));
+    ctx->stats["fpfh_spfh_exact_pairs"] = (int64_t)pr;
+  }
   ctx->stats["fpfh_weight_kmax"] = h[1];
   ctx->stats["fpfh_weight_sequential"] = h[2];
   if (h[0] > 0)
