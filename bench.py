@@ -11,6 +11,9 @@ inside the step.
 
 `--workload shot` measures configs[3] instead (secondary line): a 1M-point underwater-style
 seabed, normals + SHOT-352 (r = 0.08) at the NARF keypoints and a fixed 10,000-point sample.
+`--workload match` measures the next row of SURVEY 8(f) (F1, Features<T>::findCorrespondences,
+features.h:224-253): mutual 1-NN between the SHOT-352 descriptor sets of two such scans
+(descriptors computed before the timed region; one step = one correspondence search).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--workload fpfh|shot] [--no-cpu-baseline]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
@@ -27,15 +30,17 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+BF16_PEAK_TFLOPS = 2500.0  # dense bf16 MFMA (MI355X_MICROARCH.md: ~2.5 PF dense)
 N_POINTS = 1_000_000
 SHOT_SAMPLE = 10_000
 
 VERBOSE_TIMERS = ["grid_bbox", "grid_build", "normals", "normals_tiles", "normals_lists", "normals_lists_sparse",
-                  "normals_lists_dense", "normals_lists_query", "normals_chain", "normals_long", "range_image",
+                  "normals_lists_dense", "normals_lists_query", "normals_chain", "normals_chain_big", "normals_long", "range_image",
                   "narf_border", "narf_interest", "narf_nms", "narf_gather", "fpfh_mark", "fpfh_spfh",
                   "fpfh_weight", "shot"]
 VERBOSE_STATS = ["normals_neighbors", "normals_queries", "normals_tiles_sparse", "normals_tiles_dense",
-                 "normals_single", "normals_huge", "fpfh_spfh_points", "fpfh_spfh_pairs", "fpfh_spfh_exact_pairs", "narf_candidates", "narf_keypoints",
+                 "normals_single", "normals_huge", "normals_long_lists", "normals_chain_wg_staged",
+                 "normals_chain_wg_table", "normals_chain_wg_lane", "normals_chain_wg_deferred", "fpfh_spfh_points", "fpfh_spfh_pairs", "fpfh_spfh_exact_pairs", "narf_candidates", "narf_keypoints",
                  "narf_interest_fullimage", "narf_interest_grown", "narf_interest_window_px",
                  "narf_interest_visits", "narf_interest_queue_grown", "fpfh_weight_kmax", "fpfh_weight_sequential",
                  "shot_neighbors"]
@@ -93,9 +98,11 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--workload", choices=["fpfh", "shot"], default="fpfh")
+    ap.add_argument("--workload", choices=["fpfh", "shot", "match"], default="fpfh")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
+    if os.environ.get("PFX_BENCH_VERBOSE"):
+        os.environ["PFX_VERBOSE_STATS"] = "1"  # libpfx diagnostics (extra host syncs): verbose runs only
 
     import numpy as np
     import torch
@@ -115,6 +122,9 @@ def main():
     dev = torch.device("cuda", local)
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
+
+    if args.workload == "match":
+        return bench_match(args, torch, dev, world, rank, local)
 
     shot = args.workload == "shot"
     if shot:  # configs[3]: seabed seed 3 (per-rank seeds 300 + rank at N > 1)
@@ -203,7 +213,11 @@ def main():
         # covariance chains.  Algorithmic bytes per launch = sum_q |N_0.05(q)| * 12 B (xyz) +
         # N * 16 B (normal + curvature out); time = its HIP-event duration on the ctx stream.
         algo_bytes = neighbors * 12 + N_POINTS * 16
+        # the chain stage is two launches: k_normals_chain (LDS-staged workgroups) and
+        # k_normals_chain_big (the dense workgroups it defers to a 144 KB-LDS pass)
         chain_ms, chain_n = timers["normals_chain"]
+        big_ms, _ = timers["normals_chain_big"]
+        chain_ms += big_ms
         stage_ms, stage_n = timers["normals"]
         chain_s = (chain_ms / max(chain_n, 1)) / 1e3
         stage_s = (stage_ms / max(stage_n, 1)) / 1e3
@@ -214,7 +228,7 @@ def main():
         if os.path.exists(pmc):  # FETCH_SIZE x2 + WRITE_SIZE of k_normals_chain (scripts/gpu_pmc.sh)
             with open(pmc) as f:
                 traffic = json.load(f).get("hbm_bytes_per_launch")
-        roofline = {"bound": "hbm", "kernel": "k_normals_chain", "achieved": round(achieved, 2),
+        roofline = {"bound": "hbm", "kernel": "k_normals_chain + k_normals_chain_big", "achieved": round(achieved, 2),
                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
                     "traffic": traffic, "algorithmic_bytes_per_launch": int(algo_bytes),
                     "avg_launch_ms": round(chain_s * 1e3, 4), "neighbors_per_launch": int(neighbors),
@@ -269,6 +283,101 @@ def main():
     ctx_n.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def bench_match(args, torch, dev, world, rank, local):
+    """F1: Features<SHOT352>::findCorrespondences between two 1M-point seabed scans (the second
+    is the first turned by 3 degrees about the optical axis, re-noised), SHOT-352 at the NARF
+    keypoints + the fixed 10,000-point sample of each.  Scans are independent per rank
+    (replicas, no collective)."""
+    import numpy as np
+    from pcl_feature_extraction_amd import Context
+    from pcl_feature_extraction_amd.pipeline import alloc, alloc_shot, narf_shot
+    from pcl_feature_extraction_amd.synth import synth_seabed
+
+    x, y, z, _ = synth_seabed(N_POINTS, 3 + 100 * rank)
+    th = np.deg2rad(3.0)
+    rng = np.random.default_rng(77 + rank)
+    x2 = (np.cos(th) * x - np.sin(th) * y + rng.normal(0, 1e-3, N_POINTS)).astype(np.float32)
+    y2 = (np.sin(th) * x + np.cos(th) * y + rng.normal(0, 1e-3, N_POINTS)).astype(np.float32)
+    z2 = (z + rng.normal(0, 1e-3, N_POINTS)).astype(np.float32)
+    ctx = Context(local)
+    ctx.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+    sample = torch.from_numpy(np.sort(np.random.default_rng(10).choice(N_POINTS, SHOT_SAMPLE, replace=False))
+                              .astype(np.int64)).to(dev)
+    descs = []
+    for cx, cy, cz in ((x, y, z), (x2, y2, z2)):
+        b = alloc(torch, N_POINTS, dev)
+        b.x.copy_(torch.from_numpy(cx))
+        b.y.copy_(torch.from_numpy(cy))
+        b.z.copy_(torch.from_numpy(cz))
+        sb = alloc_shot(torch, 1 << 16, dev)
+        rows = narf_shot(ctx, b, sb, sample)
+        descs.append(sb.desc[:rows].clone())
+    src, tgt = descs
+    q = torch.empty(len(src), dtype=torch.int32, device=dev)
+    m = torch.empty(len(src), dtype=torch.int32, device=dev)
+    npairs = 0
+    for _ in range(args.warmup):
+        npairs = ctx.correspondences_dev(src, tgt, q, m)
+    torch.cuda.synchronize(dev)
+    ctx.set_timing(True)
+    ctx.reset_timing()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        npairs = ctx.correspondences_dev(src, tgt, q, m)
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        elapsed = float(t.item())
+    ns, nt = len(src), len(tgt)
+    if rank == 0:
+        # MFMA work per step: two tile passes over the padded (ns x nt) grid, K = 3 x 352 (bf16 split)
+        pad = lambda v: (v + 127) // 128 * 128  # noqa: E731
+        flops = 2 * 2.0 * pad(ns) * pad(nt) * 3 * 352
+        tb, nb = ctx.kernel_time("match_bound")
+        tf, _ = ctx.kernel_time("match_filter")
+        tiles_s = (tb + tf) / max(nb, 1) / 1e3
+        achieved = flops / tiles_s / 1e12 if tiles_s > 0 else 0.0
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline:
+            sys.path.insert(0, os.path.join(ROOT, "tests"))
+            import oracle_lib as O
+            threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
+            s_np, t_np = src.cpu().numpy(), tgt.cpu().numpy()
+            c0 = time.perf_counter()
+            oq, om = O.correspondences(s_np, t_np, threads=threads)
+            csec = time.perf_counter() - c0
+            same = bool(np.array_equal(oq, q[:npairs].cpu().numpy()) and np.array_equal(om, m[:npairs].cpu().numpy()))
+            cpu = {"value": round(ns * nt / csec / 1e6, 3), "unit": "Mpairs/s", "cores": threads, "kind": "port",
+                   "sample": (f"the same {ns} x {nt} SHOT-352 sets through the CPU restatement (oracle/or_match.cpp: "
+                              f"exhaustive L2_Simple 1-NN both directions, OpenMP), {csec:.1f}s"),
+                   "parity": {"correspondences": same}}
+        line = {
+            "metric": "Mpairs/s descriptor matching (Features::findCorrespondences, SHOT-352 mutual 1-NN)",
+            "value": round(world * ns * nt * args.steps / elapsed / 1e6, 3),
+            "unit": "Mpairs/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "f32 (bf16-split MFMA bound + exact f32 L2_Simple)",
+            "data": "synthetic (two synth_seabed scans, the second rotated 3 deg and re-noised)",
+            "config": {"workload": "SURVEY 8(f) F1: mutual nearest SHOT-352 descriptors of two 1M-pt scans",
+                       "source_rows": ns, "target_rows": nt, "correspondences": int(npairs),
+                       "parallelism": f"replica x{world}"},
+            "roofline": {"bound": "mfma", "kernel": "k_match_tiles<0> + k_match_tiles<1>", "achieved": round(achieved, 2),
+                         "peak": BF16_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": round(achieved / BF16_PEAK_TFLOPS, 5),
+                         "traffic": None, "flops_per_step": flops, "avg_tiles_ms": round(tiles_s * 1e3, 4),
+                         "candidates": {"rows": ctx.stat("match_candidates_rows"),
+                                        "cols": ctx.stat("match_candidates_cols")}},
+            "cpu_baseline": cpu,
+        }
+        if os.environ.get("PFX_BENCH_VERBOSE"):
+            rep = {nm: round(ctx.kernel_time(nm)[0] / args.steps, 4)
+                   for nm in ("match", "match_bound", "match_filter", "match_exact")}
+            print("per-step kernel ms:", json.dumps(rep), file=sys.stderr, flush=True)
+        print(json.dumps(line), flush=True)
+    ctx.close()
 
 
 if __name__ == "__main__":

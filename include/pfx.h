@@ -27,6 +27,9 @@
  *                          (keypoints.h:219-224)
  *   pfx_radius_search*  <- search::KdTree<PointXYZRGB>::radiusSearch (features.h:192,
  *                          tools.h:29; FLANN order: (d^2, index) ascending, strict d^2 < r^2)
+ *   pfx_nearest_descriptors_dev <- Features<T>::getCorrespondences (features.h:255-273):
+ *                          KdTreeFLANN<FeatureT>::nearestKSearch(k = 1) per descriptor
+ *   pfx_correspondences* <- Features<T>::findCorrespondences (features.h:224-253)
  * ===================================================================================== */
 #ifndef PFX_H_
 #define PFX_H_
@@ -179,6 +182,26 @@ pfx_status pfx_narf_debug_image(pfx_ctx* ctx, const char* which, void* out, int6
 pfx_status pfx_gather_points_dev(pfx_ctx* ctx, const float* d_x, const float* d_y,
                                  const float* d_z, int64_t n, const int32_t* idx, int64_t k,
                                  float* d_kx, float* d_ky, float* d_kz, int64_t* n_out);
+
+/* Descriptor matching.  Rows are `dim` floats, `*_stride` floats apart
+ * (FPFHSignature33: dim 33, stride 33; PointCloud<SHOT352> read in place: dim 352, stride 361).
+ * Distance = FLANN L2_Simple<float> (sequential float sum of squared differences), exact 1-NN;
+ * equal distances -> the lowest row (FLANN: first visited, unpinned); a source row with a
+ * non-finite value, or no finite target row -> -1 and NaN distance.
+ * Both directions in one pass: d_s2t[i] = nearest target row of source row i (+ its squared
+ * distance), d_t2s[j] = nearest source row of target row j.  Distance and t2s outputs are
+ * nullable.  Stream-ordered except for one host read of the candidate count. */
+pfx_status pfx_nearest_descriptors_dev(pfx_ctx* ctx, const float* d_src, int64_t n_src, int64_t src_stride,
+                                       const float* d_tgt, int64_t n_tgt, int64_t tgt_stride, int32_t dim,
+                                       int32_t* d_s2t, float* d_s2t_dist, int32_t* d_t2s, float* d_t2s_dist);
+/* Mutual nearest neighbours (index_query, index_match) in source order.  *n_out = the number
+ * of correspondences (host); PFX_ERR_CAPACITY (nothing written) when it exceeds cap. */
+pfx_status pfx_correspondences_dev(pfx_ctx* ctx, const float* d_src, int64_t n_src, int64_t src_stride,
+                                   const float* d_tgt, int64_t n_tgt, int64_t tgt_stride, int32_t dim,
+                                   int32_t* d_query, int32_t* d_match, int64_t cap, int64_t* n_out);
+pfx_status pfx_correspondences(pfx_ctx* ctx, const float* src, int64_t n_src, int64_t src_stride,
+                               const float* tgt, int64_t n_tgt, int64_t tgt_stride, int32_t dim,
+                               int32_t* query, int32_t* match, int64_t cap, int64_t* n_out);
 
 #ifdef __cplusplus
 } /* extern "C" */

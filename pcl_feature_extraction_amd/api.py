@@ -208,3 +208,35 @@ class Context:
         self._check(self._lib.pfx_gather_points_dev(self.h, _ptr(x), _ptr(y), _ptr(z), x.numel(), _ptr(idx),
                                                     len(idx), _ptr(kx), _ptr(ky), _ptr(kz), ctypes.byref(nout)))
         return nout.value
+
+    # ---- descriptor matching: Features<T>::findCorrespondences / getCorrespondences ----------
+    def correspondences(self, src, tgt):
+        """features.h:224-253: mutual nearest neighbours (index_query, index_match) in source
+        order; src / tgt are (n, D) float32 descriptor matrices (host)."""
+        src = np.ascontiguousarray(src, dtype=np.float32)
+        tgt = np.ascontiguousarray(tgt, dtype=np.float32)
+        ns, d = src.shape
+        q = np.empty(max(ns, 1), np.int32)
+        m = np.empty(max(ns, 1), np.int32)
+        n = ctypes.c_int64()
+        self._check(self._lib.pfx_correspondences(self.h, _ptr(src), ns, d, _ptr(tgt), tgt.shape[0], tgt.shape[1], d,
+                                                  _ptr(q), _ptr(m), ns, ctypes.byref(n)))
+        return q[: n.value].copy(), m[: n.value].copy()
+
+    def nearest_descriptors_dev(self, src, tgt, s2t, s2t_dist=None, t2s=None, t2s_dist=None, dim=None):
+        """features.h:255-273 in both directions: (n, stride) device tensors, `dim` leading floats
+        of each row compared (default: the whole row)."""
+        dim = dim or src.shape[1]
+        self._check(self._lib.pfx_nearest_descriptors_dev(self.h, _ptr(src), src.shape[0], src.stride(0),
+                                                          _ptr(tgt), tgt.shape[0], tgt.stride(0), dim, _ptr(s2t),
+                                                          _ptr(s2t_dist), _ptr(t2s), _ptr(t2s_dist)))
+
+    def correspondences_dev(self, src, tgt, query, match, dim=None):
+        """Device version of correspondences(); returns the number of pairs written."""
+        dim = dim or src.shape[1]
+        n = ctypes.c_int64()
+        self._check(self._lib.pfx_correspondences_dev(self.h, _ptr(src), src.shape[0], src.stride(0), _ptr(tgt),
+                                                      tgt.shape[0], tgt.stride(0), dim, _ptr(query), _ptr(match),
+                                                      query.numel(), ctypes.byref(n)))
+        return n.value
+

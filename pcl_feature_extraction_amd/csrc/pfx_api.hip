@@ -429,3 +429,64 @@ extern "C" pfx_status pfx_gather_points_dev(pfx_ctx* ctx, const float* d_x, cons
   PFX_HIP(hipStreamSynchronize(ctx->stream));  // `keep` is pageable host memory
   PFX_API_END(ctx)
 }
+
+namespace {
+void check_match_args(const float* src, int64_t ns, int64_t ss, const float* tgt, int64_t nt, int64_t ts,
+                      int32_t dim) {
+  if (dim <= 0 || ns < 0 || nt < 0 || ss < dim || ts < dim || (ns && !src) || (nt && !tgt))
+    throw Error(PFX_ERR_INVALID, "correspondences: invalid arguments");
+}
+}  // namespace
+
+extern "C" pfx_status pfx_nearest_descriptors_dev(pfx_ctx* ctx, const float* d_src, int64_t n_src,
+                                                  int64_t src_stride, const float* d_tgt, int64_t n_tgt,
+                                                  int64_t tgt_stride, int32_t dim, int32_t* d_s2t,
+                                                  float* d_s2t_dist, int32_t* d_t2s, float* d_t2s_dist) {
+  PFX_API_BEGIN
+  check_ctx(ctx);
+  check_match_args(d_src, n_src, src_stride, d_tgt, n_tgt, tgt_stride, dim);
+  if (n_src && !d_s2t) throw Error(PFX_ERR_INVALID, "nearest_descriptors: null output");
+  pfx::match_nearest_dev(ctx, d_src, n_src, src_stride, d_tgt, n_tgt, tgt_stride, dim, d_s2t, d_s2t_dist, d_t2s,
+                         d_t2s_dist);
+  PFX_API_END(ctx)
+}
+
+extern "C" pfx_status pfx_correspondences_dev(pfx_ctx* ctx, const float* d_src, int64_t n_src, int64_t src_stride,
+                                              const float* d_tgt, int64_t n_tgt, int64_t tgt_stride, int32_t dim,
+                                              int32_t* d_query, int32_t* d_match, int64_t cap, int64_t* n_out) {
+  PFX_API_BEGIN
+  check_ctx(ctx);
+  check_match_args(d_src, n_src, src_stride, d_tgt, n_tgt, tgt_stride, dim);
+  if (!n_out || cap < 0 || (cap && (!d_query || !d_match)))
+    throw Error(PFX_ERR_INVALID, "correspondences: invalid output arguments");
+  const int64_t n = pfx::correspondences_dev(ctx, d_src, n_src, src_stride, d_tgt, n_tgt, tgt_stride, dim, d_query,
+                                             d_match, cap);
+  *n_out = n;
+  if (n > cap) throw Error(PFX_ERR_CAPACITY, "correspondences: " + std::to_string(n) + " pairs > cap");
+  PFX_API_END(ctx)
+}
+
+extern "C" pfx_status pfx_correspondences(pfx_ctx* ctx, const float* src, int64_t n_src, int64_t src_stride,
+                                          const float* tgt, int64_t n_tgt, int64_t tgt_stride, int32_t dim,
+                                          int32_t* query, int32_t* match, int64_t cap, int64_t* n_out) {
+  PFX_API_BEGIN
+  check_ctx(ctx);
+  check_match_args(src, n_src, src_stride, tgt, n_tgt, tgt_stride, dim);
+  if (!n_out || cap < 0 || (cap && (!query || !match)))
+    throw Error(PFX_ERR_INVALID, "correspondences: invalid output arguments");
+  // the last row needs only `dim` floats of its stride
+  const int64_t cs = n_src ? (n_src - 1) * src_stride + dim : 0, ct = n_tgt ? (n_tgt - 1) * tgt_stride + dim : 0;
+  float* ds = stage_in(ctx, "in_match_src", src, cs);
+  float* dt = stage_in(ctx, "in_match_tgt", tgt, ct);
+  int32_t* dq = ctx->buf("out_match_q").as<int32_t>(n_src + 1);
+  int32_t* dm = ctx->buf("out_match_m").as<int32_t>(n_src + 1);
+  const int64_t n = pfx::correspondences_dev(ctx, ds, n_src, src_stride, dt, n_tgt, tgt_stride, dim, dq, dm, n_src);
+  *n_out = n;
+  if (n > cap) throw Error(PFX_ERR_CAPACITY, "correspondences: " + std::to_string(n) + " pairs > cap");
+  if (n) {
+    PFX_HIP(hipMemcpyAsync(query, dq, sizeof(int32_t) * n, hipMemcpyDeviceToHost, ctx->stream));
+    PFX_HIP(hipMemcpyAsync(match, dm, sizeof(int32_t) * n, hipMemcpyDeviceToHost, ctx->stream));
+  }
+  PFX_HIP(hipStreamSynchronize(ctx->stream));
+  PFX_API_END(ctx)
+}

@@ -1,0 +1,361 @@
+// pfx_match.hip -- descriptor matching of the reference's evaluation loop:
+//   Features<T>::getCorrespondences  features.h:255-273  (1-NN through KdTreeFLANN<FeatureT>)
+//   Features<T>::findCorrespondences features.h:224-253  (both directions + mutual check)
+//
+// The reference distance is FLANN's L2_Simple<float>: a sequential float sum of (a_k - b_k)^2
+// over the D dimensions (oracle/or_match.cpp).  The 1-NN over all pairs is a dense contraction,
+// so it runs on the matrix cores, and exactness is restored afterwards:
+//
+//   1. prep:   every row -> validity (all finite), fp32 squared norm, and a bf16 split
+//              a = a_hi + a_lo + O(2^-16 |a|), packed as [a_hi | a_hi | a_lo] (source) and
+//              [b_hi | b_lo | b_hi] (target), so ONE bf16 MFMA product over K = 3 Dp gives
+//              a_hi.b_hi + a_hi.b_lo + a_lo.b_hi (error <= 3.1 2^-16 |a||b|).
+//   2. bound:  128x128 workgroup tiles of d^ = |a|^2 + |b|^2 - 2 a.b on v_mfma_f32_32x32x16_bf16;
+//              with the rigorous error bound e(a, b) (below) |d^ - L2_Simple(a, b)| <= e, every
+//              row keeps U_i = min_j (d^_ij + e_ij) and every column U_j likewise.
+//   3. filter: the tiles again; (i, j) is a candidate of row i iff d^_ij - e_ij <= U_i (the true
+//              minimiser always is), of column j iff d^_ij - e_ij <= U_j.
+//   4. exact:  one lane per candidate evaluates L2_Simple in the reference's order and keeps the
+//              minimum of the 64-bit key (float bits << 32 | row) -- ties go to the lowest row.
+//   5. mutual: target2source[source2target[c]] == c, compacted in source order.
+//
+// Error bound (u = 2^-24, P = (|a| + |b|)^2 >= |a|^2 + |b|^2, Q = |a||b|, S = the real sum of
+// squares |a|^2 + |b|^2 - 2 a.b):
+//   |L2_Simple - S|         <= (D + 3) u P             (sequential fp32, no FMA)
+//   |n2_a - |a|^2| + |n2_b - |b|^2| <= (D + 1) u P     (fp32 sums, any order)
+//   2 |MFMA - split dot|    <= 2 * 2 * 3D u 1.016 Q    (exact bf16 products, fp32 accumulation;
+//                                                       x2 if the accumulation truncates)
+//   2 |split dot - a.b|     <= 2 * 3.1 2^-16 Q
+//   the two final roundings <= 2.02 u P
+//   => e = 1.5 [(2D + 6.1) u P + (12.2 D u + 6.2 2^-16) Q] + 1e-30 (flushed denormals);
+//      x1.5: margin for evaluating e itself in fp32.
+#include <algorithm>
+#include <cstring>
+#include <rocprim/rocprim.hpp>
+
+#include "pfx_internal.h"
+
+namespace pfx {
+namespace {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(16))) float f32x16;
+
+constexpr int kTile = 128;  // workgroup tile (rows x cols); 4 waves of 64 x 64
+constexpr uint32_t kInfBits = 0x7f800000u;
+
+__device__ __forceinline__ uint16_t bf16_rne(float f) {
+  const uint32_t u = __float_as_uint(f);
+  return (uint16_t)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
+}
+__device__ __forceinline__ float bf16_val(uint16_t h) { return __uint_as_float((uint32_t)h << 16); }
+
+// one wave per row: validity, fp32 squared norm, packed bf16 split (pad rows/dims are zero)
+__global__ void __launch_bounds__(256) k_match_prep(const float* __restrict__ X, int64_t n, int64_t stride, int D,
+                                                    int Dp, int64_t n_pad, int is_target,
+                                                    uint16_t* __restrict__ P, float* __restrict__ n2,
+                                                    float* __restrict__ nrm, uint8_t* __restrict__ valid) {
+  const int lane = threadIdx.x & 63;
+  const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (i >= n_pad) return;
+  const int KP = 3 * Dp;
+  uint16_t* row = P + i * KP;
+  bool ok = i < n;
+  float s = 0.f;
+  if (ok) {
+    const float* x = X + i * stride;
+    bool fin = true;
+    for (int k = lane; k < D; k += 64) {
+      const float v = x[k];
+      fin = fin && isfinite(v);
+      s += v * v;
+    }
+    ok = !__any(!fin);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+  for (int k = lane; k < Dp; k += 64) {
+    uint16_t hi = 0, lo = 0;
+    if (ok && k < D) {
+      const float v = X[i * stride + k];
+      hi = bf16_rne(v);
+      lo = bf16_rne(v - bf16_val(hi));  // exact difference
+    }
+    row[k] = hi;
+    row[Dp + k] = is_target ? lo : hi;
+    row[2 * Dp + k] = is_target ? hi : lo;
+  }
+  if (lane == 0) {
+    n2[i] = ok ? s : 0.f;
+    nrm[i] = ok ? sqrtf(s) : 0.f;
+    valid[i] = ok ? 1 : 0;
+  }
+}
+
+struct Side {
+  const uint16_t* P;
+  const float* n2;
+  const float* nrm;
+  const uint8_t* valid;
+  int64_t n;
+};
+
+// PASS 0: row / column upper bounds.  PASS 1: candidates.
+template <int PASS>
+__global__ void __launch_bounds__(256) k_match_tiles(Side A, Side B, int D, int Dp, float c1, float c2,
+                                                     uint32_t* __restrict__ Urow, uint32_t* __restrict__ Ucol,
+                                                     int2* __restrict__ crow, int2* __restrict__ ccol,
+                                                     unsigned* __restrict__ ncand, unsigned cap) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t r0 = (int64_t)blockIdx.y * kTile + (wv >> 1) * 64;
+  const int64_t q0 = (int64_t)blockIdx.x * kTile + (wv & 1) * 64;
+  const int KP = 3 * Dp;
+  const int h = lane >> 5, l32 = lane & 31;
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+  const uint16_t* pa0 = A.P + (r0 + l32) * KP + 8 * h;
+  const uint16_t* pa1 = pa0 + (int64_t)32 * KP;
+  const uint16_t* pb0 = B.P + (q0 + l32) * KP + 8 * h;
+  const uint16_t* pb1 = pb0 + (int64_t)32 * KP;
+  for (int k0 = 0; k0 < KP; k0 += 16) {
+    const bf16x8 fa0 = *reinterpret_cast<const bf16x8*>(pa0 + k0);
+    const bf16x8 fa1 = *reinterpret_cast<const bf16x8*>(pa1 + k0);
+    const bf16x8 fb0 = *reinterpret_cast<const bf16x8*>(pb0 + k0);
+    const bf16x8 fb1 = *reinterpret_cast<const bf16x8*>(pb1 + k0);
+    acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa0, fb0, acc[0][0], 0, 0, 0);
+    acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa0, fb1, acc[0][1], 0, 0, 0);
+    acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa1, fb0, acc[1][0], 0, 0, 0);
+    acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa1, fb1, acc[1][1], 0, 0, 0);
+  }
+  // epilogue: C/D map of 32x32 tiles: col = lane & 31, row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5)
+  float cn2[2], cnr[2];
+  bool cval[2];
+  uint32_t ucol[2];
+#pragma unroll
+  for (int b = 0; b < 2; ++b) {
+    const int64_t q = q0 + 32 * b + l32;
+    cn2[b] = B.n2[q];
+    cnr[b] = B.nrm[q];
+    cval[b] = B.valid[q] != 0;
+    ucol[b] = PASS ? Ucol[q] : kInfBits;
+  }
+  float cmin[2] = {__uint_as_float(kInfBits), __uint_as_float(kInfBits)};
+#pragma unroll
+  for (int a = 0; a < 2; ++a) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int64_t row = r0 + 32 * a + (r & 3) + 8 * (r >> 2) + 4 * h;
+      const float rn2 = A.n2[row], rnr = A.nrm[row];
+      const bool rval = A.valid[row] != 0;
+      const uint32_t urow = PASS ? Urow[row] : kInfBits;
+      float rmin = __uint_as_float(kInfBits);
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        const float dh = (rn2 + cn2[b]) - 2.0f * acc[a][b][r];
+        const float s = rnr + cnr[b];
+        const float e = 1.5f * (c1 * (s * s) + c2 * (rnr * cnr[b])) + 1e-30f;
+        const bool ok = rval && cval[b];
+        if (PASS == 0) {
+          const float ub = ok ? fmaxf(dh + e, 0.f) : __uint_as_float(kInfBits);
+          rmin = fminf(rmin, ub);
+          cmin[b] = fminf(cmin[b], ub);
+        } else if (ok) {
+          const float lb = dh - e;
+          const int64_t col = q0 + 32 * b + l32;
+          if (lb <= __uint_as_float(urow)) {
+            const unsigned slot = atomicAdd(&ncand[0], 1u);
+            if (slot < cap) crow[slot] = make_int2((int)row, (int)col);
+          }
+          if (lb <= __uint_as_float(ucol[b])) {
+            const unsigned slot = atomicAdd(&ncand[1], 1u);
+            if (slot < cap) ccol[slot] = make_int2((int)col, (int)row);
+          }
+        }
+      }
+      if (PASS == 0) {
+#pragma unroll
+        for (int o = 16; o > 0; o >>= 1) rmin = fminf(rmin, __shfl_xor(rmin, o));
+        if (l32 == 0 && rmin < __uint_as_float(kInfBits) && row < A.n) atomicMin(&Urow[row], __float_as_uint(rmin));
+      }
+    }
+  }
+  if (PASS == 0) {
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      float v = fminf(cmin[b], __shfl_xor(cmin[b], 32));
+      const int64_t q = q0 + 32 * b + l32;
+      if (h == 0 && v < __uint_as_float(kInfBits) && q < B.n) atomicMin(&Ucol[q], __float_as_uint(v));
+    }
+  }
+}
+
+// one lane per candidate (i, j): FLANN L2_Simple in the reference order, 64-bit min key
+__global__ void __launch_bounds__(256) k_match_exact(const float* __restrict__ A, int64_t sa,
+                                                     const float* __restrict__ B, int64_t sb, int D,
+                                                     const int2* __restrict__ cand, const unsigned* __restrict__ ncand,
+                                                     unsigned long long* __restrict__ best) {
+  const unsigned n = *ncand;
+  for (unsigned t = blockIdx.x * 256 + threadIdx.x; t < n; t += gridDim.x * 256) {
+    const int2 c = cand[t];
+    const float* a = A + (int64_t)c.x * sa;
+    const float* b = B + (int64_t)c.y * sb;
+    float result = 0.0f;
+    for (int k = 0; k < D; ++k) {
+      const float diff = a[k] - b[k];
+      result = result + diff * diff;
+    }
+    atomicMin(&best[c.x], ((unsigned long long)__float_as_uint(result) << 32) | (uint32_t)c.y);
+  }
+}
+
+__global__ void k_match_finish(const unsigned long long* __restrict__ best, int64_t n, int32_t* __restrict__ idx,
+                               float* __restrict__ dist) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const unsigned long long k = best[i];
+  const bool found = k != ~0ull;
+  idx[i] = found ? (int32_t)(uint32_t)(k & 0xffffffffu) : -1;
+  if (dist) dist[i] = found ? __uint_as_float((uint32_t)(k >> 32)) : __builtin_nanf("");
+}
+
+__global__ void k_match_mutual(const int32_t* __restrict__ s2t, int64_t ns, const int32_t* __restrict__ t2s,
+                               uint8_t* __restrict__ flags) {
+  const int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (c >= ns) return;
+  const int32_t m = s2t[c];
+  flags[c] = (m >= 0 && t2s[m] == (int32_t)c) ? 1 : 0;
+}
+
+__global__ void k_match_gather(const int32_t* __restrict__ q, const int64_t* __restrict__ nsel,
+                               const int32_t* __restrict__ s2t, int32_t* __restrict__ m) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t < *nsel) m[t] = s2t[q[t]];
+}
+
+struct Prepared {
+  Side side;
+  int64_t n_pad;
+};
+
+Prepared prep(pfx_ctx* ctx, const char* tag, const float* X, int64_t n, int64_t stride, int D, int Dp,
+              bool target) {
+  const int64_t n_pad = std::max<int64_t>(ceil_div(n, kTile), 1) * kTile;
+  const std::string t(tag);
+  uint16_t* P = ctx->buf((t + "_pk").c_str()).as<uint16_t>((size_t)n_pad * 3 * Dp);
+  float* n2 = ctx->buf((t + "_n2").c_str()).as<float>(n_pad);
+  float* nr = ctx->buf((t + "_nr").c_str()).as<float>(n_pad);
+  uint8_t* v = ctx->buf((t + "_v").c_str()).as<uint8_t>(n_pad);
+  k_match_prep<<<(unsigned)ceil_div(n_pad, 4), 256, 0, ctx->stream>>>(X, n, stride, D, Dp, n_pad, target ? 1 : 0, P,
+                                                                       n2, nr, v);
+  check_launch("k_match_prep");
+  return Prepared{Side{P, n2, nr, v, n}, n_pad};
+}
+
+}  // namespace
+
+// Both directions at once (the tiles serve rows and columns): s2t[i] = nearest target row of
+// source row i, t2s[j] = nearest source row of target row j (-1: no finite row / no target).
+void match_nearest_dev(pfx_ctx* ctx, const float* src, int64_t ns, int64_t ss, const float* tgt, int64_t nt,
+                       int64_t ts, int D, int32_t* s2t, float* ds2t, int32_t* t2s, float* dt2s) {
+  PFX_CHECK(D > 0 && ns >= 0 && nt >= 0 && ss >= D && ts >= D, "match: invalid dimensions");
+  PFX_CHECK(ns < (int64_t(1) << 31) && nt < (int64_t(1) << 31), "match: too many rows");
+  hipStream_t st = ctx->stream;
+  if (ns == 0 && nt == 0) return;
+  if (ns == 0 || nt == 0) {  // nothing to match against
+    if (ns) PFX_HIP(hipMemsetAsync(s2t, 0xff, sizeof(int32_t) * ns, st));
+    if (nt && t2s) PFX_HIP(hipMemsetAsync(t2s, 0xff, sizeof(int32_t) * nt, st));
+    if (ns && ds2t) PFX_HIP(hipMemsetAsync(ds2t, 0xff, sizeof(float) * ns, st));
+    if (nt && dt2s) PFX_HIP(hipMemsetAsync(dt2s, 0xff, sizeof(float) * nt, st));
+    return;
+  }
+  TimeScope total(ctx, "match");
+  const int Dp = (D + 15) / 16 * 16;
+  const Prepared a = prep(ctx, "match_a", src, ns, ss, D, Dp, false);
+  const Prepared b = prep(ctx, "match_b", tgt, nt, ts, D, Dp, true);
+  uint32_t* Urow = ctx->buf("match_urow").as<uint32_t>(a.n_pad);
+  uint32_t* Ucol = ctx->buf("match_ucol").as<uint32_t>(b.n_pad);
+  unsigned long long* bs = ctx->buf("match_bs").as<unsigned long long>(ns);
+  unsigned long long* bt = ctx->buf("match_bt").as<unsigned long long>(nt);
+  unsigned* ncand = ctx->buf("match_ncand").as<unsigned>(2);
+  PFX_HIP(hipMemsetAsync(Urow, 0x7f, sizeof(uint32_t) * a.n_pad, st));  // 0x7f7f7f7f: above any bound
+  PFX_HIP(hipMemsetAsync(Ucol, 0x7f, sizeof(uint32_t) * b.n_pad, st));
+  PFX_HIP(hipMemsetAsync(bs, 0xff, sizeof(unsigned long long) * ns, st));
+  PFX_HIP(hipMemsetAsync(bt, 0xff, sizeof(unsigned long long) * nt, st));
+  const float u = 5.9604645e-8f;  // 2^-24
+  const float c1 = (2.0f * (float)D + 6.1f) * u, c2 = 12.2f * (float)D * u + 6.2f / 65536.0f;
+  const dim3 grid((unsigned)(b.n_pad / kTile), (unsigned)(a.n_pad / kTile));
+  {
+    TimeScope ts1(ctx, "match_bound");
+    k_match_tiles<0><<<grid, 256, 0, st>>>(a.side, b.side, D, Dp, c1, c2, Urow, Ucol, nullptr, nullptr, nullptr, 0);
+    check_launch("k_match_tiles<0>");
+  }
+  DevBuf& cb = ctx->buf("match_cand");
+  unsigned cap = (unsigned)std::min<int64_t>(std::max<int64_t>(8 * (ns + nt), 1 << 20), int64_t(1) << 30);
+  for (int attempt = 0; attempt < 2; ++attempt) {
+    int2* crow = static_cast<int2*>(cb.get(sizeof(int2) * 2 * (size_t)cap));
+    int2* ccol = crow + cap;
+    PFX_HIP(hipMemsetAsync(ncand, 0, 2 * sizeof(unsigned), st));
+    {
+      TimeScope ts2(ctx, "match_filter");
+      k_match_tiles<1><<<grid, 256, 0, st>>>(a.side, b.side, D, Dp, c1, c2, Urow, Ucol, crow, ccol, ncand, cap);
+      check_launch("k_match_tiles<1>");
+    }
+    unsigned h[2];
+    PFX_HIP(hipMemcpyAsync(h, ncand, sizeof(h), hipMemcpyDeviceToHost, st));
+    PFX_HIP(hipStreamSynchronize(st));
+    ctx->stats["match_candidates_rows"] = h[0];
+    ctx->stats["match_candidates_cols"] = h[1];
+    if (std::max(h[0], h[1]) > cap) {
+      PFX_CHECK(attempt == 0, "match: candidate buffer growth failed");
+      cap = std::max(h[0], h[1]);
+      continue;
+    }
+    TimeScope ts3(ctx, "match_exact");
+    const unsigned g0 = (unsigned)std::max<int64_t>(1, std::min<int64_t>(ceil_div(h[0], 256), 8192));
+    const unsigned g1 = (unsigned)std::max<int64_t>(1, std::min<int64_t>(ceil_div(h[1], 256), 8192));
+    k_match_exact<<<g0, 256, 0, st>>>(src, ss, tgt, ts, D, crow, ncand, bs);
+    k_match_exact<<<g1, 256, 0, st>>>(tgt, ts, src, ss, D, ccol, ncand + 1, bt);
+    check_launch("k_match_exact");
+    break;
+  }
+  k_match_finish<<<(unsigned)ceil_div(ns, 256), 256, 0, st>>>(bs, ns, s2t, ds2t);
+  if (t2s) k_match_finish<<<(unsigned)ceil_div(nt, 256), 256, 0, st>>>(bt, nt, t2s, dt2s);
+  check_launch("k_match_finish");
+}
+
+int64_t correspondences_dev(pfx_ctx* ctx, const float* src, int64_t ns, int64_t ss, const float* tgt, int64_t nt,
+                            int64_t ts, int D, int32_t* query, int32_t* match, int64_t cap) {
+  hipStream_t st = ctx->stream;
+  int32_t* s2t = ctx->buf("match_s2t").as<int32_t>(ns + 1);
+  int32_t* t2s = ctx->buf("match_t2s").as<int32_t>(nt + 1);
+  match_nearest_dev(ctx, src, ns, ss, tgt, nt, ts, D, s2t, nullptr, t2s, nullptr);
+  if (ns == 0 || nt == 0) return 0;
+  uint8_t* flags = ctx->buf("match_flags").as<uint8_t>(ns);
+  int32_t* qsel = ctx->buf("match_qsel").as<int32_t>(ns);
+  int64_t* nsel = ctx->buf("match_nsel").as<int64_t>(1);
+  k_match_mutual<<<(unsigned)ceil_div(ns, 256), 256, 0, st>>>(s2t, ns, t2s, flags);
+  check_launch("k_match_mutual");
+  size_t tb = 0;
+  PFX_HIP(rocprim::select(nullptr, tb, rocprim::counting_iterator<int32_t>(0), flags, qsel, nsel, (size_t)ns, st));
+  void* tmp = ctx->buf("match_tmp").get(tb + 16);
+  PFX_HIP(rocprim::select(tmp, tb, rocprim::counting_iterator<int32_t>(0), flags, qsel, nsel, (size_t)ns, st));
+  int32_t* msel = ctx->buf("match_msel").as<int32_t>(ns);
+  k_match_gather<<<(unsigned)ceil_div(ns, 256), 256, 0, st>>>(qsel, nsel, s2t, msel);
+  check_launch("k_match_gather");
+  int64_t n = 0;
+  PFX_HIP(hipMemcpyAsync(&n, nsel, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+  PFX_HIP(hipStreamSynchronize(st));
+  if (n > 0 && n <= cap) {
+    PFX_HIP(hipMemcpyAsync(query, qsel, sizeof(int32_t) * n, hipMemcpyDeviceToDevice, st));
+    PFX_HIP(hipMemcpyAsync(match, msel, sizeof(int32_t) * n, hipMemcpyDeviceToDevice, st));
+  }
+  ctx->stats["match_correspondences"] = n;
+  return n;
+}
+
+}  // namespace pfx

@@ -3,8 +3,13 @@
 // For a set of query points that are points of the grid (all of them, or a masked subset),
 // build_lists() produces, per query j:
 //   cnt[j]  = |N_r(q_j)| (FLANN semantics: d2 < (float)(r*r), self and duplicates included)
-//   list[off[j] + (m << lg[j])], m < cnt[j]  = neighbours as cell-sorted positions, in FLANN
-//                                order (d2, caller index) ascending when `sorted`
+//   list[off[j] + (m << lg[j])], m < cnt[j]  = neighbours in FLANN order (d2, caller index)
+//                                ascending when `sorted`, as run entries (below)
+// Run entry: (r << 28) | off -- the neighbour is the off-th point of run r (0..8) of the query
+// cell's 3x3x3 block (run r = cells (ix + r/3 - 1, iy + r%3 - 1, iz-1..iz+1), clipped to the
+// grid), i.e. cell-sorted position cell_start[first cell of run r] + off.  Consumers resolve r
+// through a per-cell table, so a workgroup can stage its candidate runs in LDS and index them
+// directly (k_normals_chain).
 // Layout: queries are ordered by cell (qpos[j] = sorted position of query j).  The lists of one
 // tile (<= 16 consecutive queries of one cell) are interleaved (stride 2^lg >= tile size), so a
 // consumer that gives consecutive queries to consecutive lanes reads whole cache lines per load.
@@ -12,6 +17,10 @@
 #include "pfx_internal.h"
 
 namespace pfx {
+
+constexpr uint32_t kEntryOffMask = 0x0fffffffu;
+__host__ __device__ __forceinline__ int entry_run(uint32_t e) { return (int)(e >> 28); }
+__host__ __device__ __forceinline__ uint32_t entry_off(uint32_t e) { return e & kEntryOffMask; }
 
 struct NbLists {
   int64_t nq = 0;            // number of queries
@@ -21,7 +30,8 @@ struct NbLists {
   const int64_t* off = nullptr;    // [nq]
   const int32_t* cnt = nullptr;    // [nq]
   const uint8_t* lg = nullptr;     // [nq] log2 of the entry stride
-  const uint32_t* list = nullptr;  // [total]
+  const uint32_t* list = nullptr;  // [slots] run entries
+  const uint32_t* skeys = nullptr; // cell key of each sorted position (the grid's)
 };
 
 // mask (nullable): per *caller* index, queries are the masked points (in cell order).

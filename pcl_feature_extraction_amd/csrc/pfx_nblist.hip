@@ -37,33 +37,6 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_wave_barrier();
 }
 
-__device__ __forceinline__ void cell_runs(const GridView& g, uint32_t key, int r, int32_t& s, int32_t& len) {
-  const int64_t iz = key % g.nz, iy = (key / g.nz) % g.ny, ix = key / ((uint64_t)g.nz * g.ny);
-  const int64_t bx = ix + (r / 3) - 1, by = iy + (r % 3) - 1;
-  const int64_t z0 = iz - 1 < 0 ? 0 : iz - 1, z1 = iz + 1 >= g.nz ? g.nz - 1 : iz + 1;
-  s = 0;
-  len = 0;
-  if (bx >= 0 && bx < g.nx && by >= 0 && by < g.ny) {
-    const int64_t base = (bx * g.ny + by) * g.nz;
-    s = g.cell_start[base + z0];
-    len = g.cell_start[base + z1 + 1] - s;
-  }
-}
-
-__device__ __forceinline__ int block_runs(const GridView& g, uint32_t key, Runs& R) {
-  int acc = 0;
-#pragma unroll
-  for (int r = 0; r < 9; ++r) {
-    int32_t s, len;
-    cell_runs(g, key, r, s, len);
-    R.start[r] = s;
-    R.pref[r] = acc;
-    acc += len;
-  }
-  R.pref[9] = acc;
-  return acc;
-}
-
 __global__ void k_iota(int32_t* __restrict__ out, int64_t n) {
   int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   if (i < n) out[i] = (int32_t)i;
@@ -373,7 +346,8 @@ __global__ void __launch_bounds__(256, STAGE ? 3 : 2) k_nb_tile(GridView g, cons
                                                  const uint32_t* __restrict__ skeys,
                                                  const uint32_t* __restrict__ tiles, const int* __restrict__ ntiles_ptr,
                                                  float rr, float bscale, int sorted, ListOut out,
-                                                 int32_t* __restrict__ single, int* __restrict__ n_single) {
+                                                 int32_t* __restrict__ single, int* __restrict__ n_single,
+                                                 int* __restrict__ next_tile) {
   constexpr int Q = kQ, QW = Q / 4;  // queries per tile / per wave
   __shared__ float cx[STAGE ? TCAP : 1], cy[STAGE ? TCAP : 1], cz[STAGE ? TCAP : 1];
   __shared__ uint16_t lists[Q][LCAP + 2];  // +2: odd dword row stride (no bank conflicts)
@@ -383,9 +357,15 @@ __global__ void __launch_bounds__(256, STAGE ? 3 : 2) k_nb_tile(GridView g, cons
   __shared__ int s_k[Q];
   __shared__ unsigned long long s_base;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  __shared__ int s_tile;
   const int ntiles = *ntiles_ptr;
-  const int64_t vb = xcd_block(blockIdx.x, gridDim.x);
-  for (int64_t tile = vb; tile < ntiles; tile += gridDim.x) {
+  // dynamic tile queue: tile costs vary by orders of magnitude with the local density
+  for (;;) {
+    if (tid == 0) s_tile = atomicAdd(next_tile, 1);
+    __syncthreads();
+    const int64_t tile = s_tile;
+    __syncthreads();  // every thread holds `tile` before thread 0 may fetch the next one
+    if (tile >= ntiles) break;
     TPROF_T(p0);
     const uint32_t te = tiles[tile];
     const int32_t start = tile_start(te);
@@ -505,7 +485,7 @@ __global__ void __launch_bounds__(256, STAGE ? 3 : 2) k_nb_tile(GridView g, cons
         const int m = e >> lg, j = e & ((1 << lg) - 1);
         if (j < qn) {
           const int k = s_k[j];
-          if (m < k && k <= LCAP) out.list[base + e] = (uint32_t)run_pos(R, lists[j][m]);
+          if (m < k && k <= LCAP) out.list[base + e] = run_entry(R, lists[j][m]);
         }
       }
     }
@@ -520,10 +500,12 @@ __global__ void __launch_bounds__(256, STAGE ? 3 : 2) k_nb_tile(GridView g, cons
 // Lists longer than CAP go to `over` (or raise err when over == nullptr).
 template <int CAP, int NB, bool GLOBAL>
 __global__ void __launch_bounds__(256) k_nb_query(GridView g, const int32_t* __restrict__ qpos,
+                                                  const uint32_t* __restrict__ skeys,
                                                   const int32_t* __restrict__ work, const int* __restrict__ n_ptr,
                                                   float rr, float bscale, int sorted, ListOut out,
                                                   int32_t* __restrict__ over, int* __restrict__ n_over,
-                                                  int* __restrict__ err, uint32_t* __restrict__ scratch) {
+                                                  int* __restrict__ err, uint32_t* __restrict__ scratch,
+                                                  int* __restrict__ next_work) {
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   __shared__ int bcount[NB], bpos[NB];
   __shared__ int s_count;
@@ -535,12 +517,18 @@ __global__ void __launch_bounds__(256) k_nb_query(GridView g, const int32_t* __r
   uint32_t* spv = base_arr + 3 * CAP;
   const int tid = threadIdx.x;
   const int count = *n_ptr;
-  for (int w = blockIdx.x; w < count; w += gridDim.x) {
+  __shared__ int s_w;
+  for (;;) {  // dynamic queue: list lengths (and costs) differ by orders of magnitude
+    if (tid == 0) s_w = atomicAdd(next_work, 1);
+    __syncthreads();
+    const int w = s_w;
+    __syncthreads();
+    if (w >= count) break;
     const int32_t j = work[w];
     const int32_t qp = qpos[j];
     const float4 q = g.sp[qp];
     Runs R;
-    query_runs(g, q.x, q.y, q.z, R);
+    block_runs(g, skeys[qp], R);  // the query's own cell: the runs its list entries refer to
     if (tid == 0) s_count = 0;
     for (int b = tid; b < NB; b += 256) bcount[b] = 0;
     __syncthreads();
@@ -634,7 +622,15 @@ __global__ void __launch_bounds__(256) k_nb_query(GridView g, const int32_t* __r
     __syncthreads();
     const int64_t off = (int64_t)s_base;
     if ((unsigned long long)(off + k) <= out.cap)
-      for (int m = tid; m < k; m += 256) out.list[off + m] = hits[m];
+      for (int m = tid; m < k; m += 256) {
+        const int32_t p = (int32_t)hits[m];
+        uint32_t e = 0;
+#pragma unroll
+        for (int r = 0; r < 9; ++r)
+          if (p >= R.start[r] && p < R.start[r] + (R.pref[r + 1] - R.pref[r]))
+            e = ((uint32_t)r << 28) | (uint32_t)(p - R.start[r]);
+        out.list[off + m] = e;
+      }
     __syncthreads();
   }
 }
@@ -668,8 +664,9 @@ void build_lists(pfx_ctx* ctx, const Grid& G, const uint8_t* mask, double radius
   int32_t* cnt = B("cnt").as<int32_t>(n);
   uint8_t* lgs = B("lg").as<uint8_t>(n);
   // counters: 0 sparse tiles, 1 dense tiles, 2 per-query work, 3 huge work, 4 max k over cap,
-  // 6 per-query work queued by the classifier (restored for a rerun)
-  int* counters = B("counters").as<int>(8);
+  // 5 / 7 sparse / dense tile queue heads, 6 per-query work queued by the classifier (restored
+  // for a rerun), 8 / 9 per-query / huge work queue heads
+  int* counters = B("counters").as<int>(10);
   unsigned long long* cursor = B("cursor").as<unsigned long long>(2);
   size_t t1 = 0, t2 = 0, t3 = 0;
   PFX_HIP(rocprim::select(nullptr, t1, rocprim::counting_iterator<int32_t>(0), flags, qpos, d_nq, (size_t)n, st));
@@ -677,7 +674,7 @@ void build_lists(pfx_ctx* ctx, const Grid& G, const uint8_t* mask, double radius
   PFX_HIP(rocprim::select(nullptr, t3, rocprim::counting_iterator<int32_t>(0), flags, tiles, d_ntiles, (size_t)n,
                           st));
   void* tmp = B("tmp").get(std::max(t1, std::max(t2, t3)) + 16);
-  PFX_HIP(hipMemsetAsync(counters, 0, 8 * sizeof(int), st));
+  PFX_HIP(hipMemsetAsync(counters, 0, 10 * sizeof(int), st));
   const unsigned nb = (unsigned)ceil_div(n, 256);
   {
     TimeScope ts(ctx, std::string(tag) + "_tiles");
@@ -709,7 +706,8 @@ void build_lists(pfx_ctx* ctx, const Grid& G, const uint8_t* mask, double radius
     PFX_HIP(hipMemsetAsync(cursor, 0, 2 * sizeof(unsigned long long), st));
     if (attempt) {
       PFX_HIP(hipMemcpyAsync(counters + 2, counters + 6, sizeof(int), hipMemcpyDeviceToDevice, st));
-      PFX_HIP(hipMemsetAsync(counters + 3, 0, 2 * sizeof(int), st));
+      PFX_HIP(hipMemsetAsync(counters + 3, 0, 3 * sizeof(int), st));  // huge, max k, sparse queue
+      PFX_HIP(hipMemsetAsync(counters + 7, 0, 3 * sizeof(int), st));  // dense, query, huge queues
     }
     int h_cnt[8];
     {
@@ -717,18 +715,18 @@ void build_lists(pfx_ctx* ctx, const Grid& G, const uint8_t* mask, double radius
       {
         TimeScope t1(ctx, std::string(tag) + "_lists_sparse");
         k_nb_tile<512, 256, kTcapSparse, true><<<256 * 3 * 4, 256, 0, st>>>(
-            g, qpos, G.skeys, sparse, counters + 0, rr, 256.0f / rr, isort, lo, single, counters + 2);
+            g, qpos, G.skeys, sparse, counters + 0, rr, 256.0f / rr, isort, lo, single, counters + 2, counters + 5);
       }
       {
         TimeScope t2(ctx, std::string(tag) + "_lists_dense");
         k_nb_tile<1024, 256, kTcapDense, false><<<256 * 2 * 4, 256, 0, st>>>(
-            g, qpos, G.skeys, dense, counters + 1, rr, 256.0f / rr, isort, lo, single, counters + 2);
+            g, qpos, G.skeys, dense, counters + 1, rr, 256.0f / rr, isort, lo, single, counters + 2, counters + 7);
       }
       {
         TimeScope t3(ctx, std::string(tag) + "_lists_query");
         k_nb_query<kCapQuery, kBucketsQuery, false><<<256 * 4, 256, lds_q, st>>>(
-            g, qpos, single, counters + 2, rr, (float)kBucketsQuery / rr, isort, lo, huge, counters + 3,
-            counters + 4, nullptr);
+            g, qpos, G.skeys, single, counters + 2, rr, (float)kBucketsQuery / rr, isort, lo, huge, counters + 3,
+            counters + 4, nullptr, counters + 8);
       }
       check_launch("nblist lists");
       PFX_HIP(hipMemcpyAsync(h_cnt, counters, sizeof(h_cnt), hipMemcpyDeviceToHost, st));
@@ -736,8 +734,8 @@ void build_lists(pfx_ctx* ctx, const Grid& G, const uint8_t* mask, double radius
       if (h_cnt[3] > 0) {  // very long lists: sort arrays in global scratch
         uint32_t* scratch = B("scratch").as<uint32_t>((size_t)kHugeBlocks * 4 * kCapHuge);
         k_nb_query<kCapHuge, kBucketsHuge, true><<<kHugeBlocks, 256, 0, st>>>(
-            g, qpos, huge, counters + 3, rr, (float)kBucketsHuge / rr, isort, lo, nullptr, nullptr, counters + 4,
-            scratch);
+            g, qpos, G.skeys, huge, counters + 3, rr, (float)kBucketsHuge / rr, isort, lo, nullptr, nullptr, counters + 4,
+            scratch, counters + 9);
         check_launch("nblist huge lists");
       }
     }
@@ -763,6 +761,7 @@ void build_lists(pfx_ctx* ctx, const Grid& G, const uint8_t* mask, double radius
     out.cnt = cnt;
     out.lg = lgs;
     out.list = lo.list;
+    out.skeys = G.skeys;
     ctx->stats[std::string(tag) + "_tiles_sparse"] = h_cnt[0];
     ctx->stats[std::string(tag) + "_tiles_dense"] = h_cnt[1];
     ctx->stats[std::string(tag) + "_single"] = h_cnt[2];

@@ -58,12 +58,49 @@ __device__ __forceinline__ void query_runs(const GridView& g, float qx, float qy
   R.pref[9] = acc;
 }
 
+// Run r of the block of grid cell `key` (the cell a grid point lies in): start position and length.
+__device__ __forceinline__ void block_run(const GridView& g, uint32_t key, int r, int32_t& s, int32_t& len) {
+  const int64_t iz = key % g.nz, iy = (key / g.nz) % g.ny, ix = key / ((uint64_t)g.nz * g.ny);
+  const int64_t bx = ix + (r / 3) - 1, by = iy + (r % 3) - 1;
+  const int64_t z0 = iz - 1 < 0 ? 0 : iz - 1, z1 = iz + 1 >= g.nz ? g.nz - 1 : iz + 1;
+  s = 0;
+  len = 0;
+  if (bx >= 0 && bx < g.nx && by >= 0 && by < g.ny) {
+    const int64_t base = (bx * g.ny + by) * g.nz;
+    s = g.cell_start[base + z0];
+    len = g.cell_start[base + z1 + 1] - s;
+  }
+}
+
+__device__ __forceinline__ int block_runs(const GridView& g, uint32_t key, Runs& R) {
+  int acc = 0;
+#pragma unroll
+  for (int r = 0; r < 9; ++r) {
+    int32_t s, len;
+    block_run(g, key, r, s, len);
+    R.start[r] = s;
+    R.pref[r] = acc;
+    acc += len;
+  }
+  R.pref[9] = acc;
+  return acc;
+}
+
 __device__ __forceinline__ int32_t run_pos(const Runs& R, int32_t t) {
   int32_t p = R.start[0] + t;
 #pragma unroll
   for (int r = 1; r < 9; ++r)
     if (t >= R.pref[r]) p = R.start[r] + (t - R.pref[r]);
   return p;
+}
+
+// run entry (pfx_nblist.h) of candidate t of the block: (run << 28) | offset within the run
+__device__ __forceinline__ uint32_t run_entry(const Runs& R, int32_t t) {
+  uint32_t e = (uint32_t)(t - R.pref[0]);
+#pragma unroll
+  for (int r = 1; r < 9; ++r)
+    if (t >= R.pref[r]) e = ((uint32_t)r << 28) | (uint32_t)(t - R.pref[r]);
+  return e;
 }
 
 // Gather the neighbours of q into keys[0..min(k,cap)) (unsorted); returns k (may exceed cap).

@@ -13,6 +13,10 @@
 //      strictly ordered float chains in registers, eigen33 + viewpoint flip, output scattered to
 //      the caller's order; lists longer than kLaneMax go to k_normals_long (nine lanes per
 //      query, one per chain).
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+
 #include "pfx_nblist.h"
 #include "pfx_neighbors.h"
 #include "pfx_normal_math.h"
@@ -47,88 +51,411 @@ __device__ __forceinline__ void store_normal(const GridView& g, int32_t p, const
   curv[orig] = o[3];
 }
 
-// one lane per query: the nine ordered chains in registers; list positions are fetched one
-// batch ahead of the coordinate gathers
-__global__ void __launch_bounds__(256) k_normals_chain(GridView g, NbLists L, float vpx, float vpy, float vpz,
-                                                       float* __restrict__ nx, float* __restrict__ ny,
-                                                       float* __restrict__ nz, float* __restrict__ curv,
-                                                       int32_t* __restrict__ longq, int* __restrict__ n_long) {
-  const int64_t j = xcd_block(blockIdx.x, gridDim.x) * 256 + threadIdx.x;
-  if (j >= L.nq) return;
-  const int k = L.cnt[j];
+// ---- k_normals_chain: one lane per query, candidate coordinates staged in LDS ----------------
+//
+// A workgroup takes 256 consecutive queries (cell order: a few z-consecutive cells of one or a
+// few grid columns).  Their lists only reference the 3x3x3 blocks of their cells, i.e. runs of
+// the grid columns around the query columns.  The workgroup collects those columns (LDS hash),
+// takes per column the z range its queries need, and stages the union (contiguous position
+// ranges of the cell-sorted packed copy) in LDS once; a per-cell table maps a list entry's run
+// to its LDS base.  The nine chains then read neighbour coordinates with ds_read_b128 instead
+// of 64-address global gathers (the TA/L2 latency that bounded the previous version).
+// Fallbacks keep every list exact: union > kStageCap -> the same table with global bases;
+// > kMaxCells distinct cells -> per-lane run starts.
+constexpr int kMaxCells = 64;
+constexpr int kHash = 1024;
+constexpr int kStageSmall = 3584;  // SoA floats: 42 KB, three workgroups per CU
+constexpr int kStageBig = 12288;   // 144 KB, one workgroup per CU: the dense regions
+constexpr int kMaxCols = kMaxCells * 9;
+constexpr uint32_t kEmpty = 0xffffffffu;
+
+template <int CAP>
+struct ChainLds {
+  static_assert(CAP * 3 >= 256 * 9, "lane-mode run tables live in the staging LDS");
+  union {
+    struct {
+      float x[CAP], y[CAP], z[CAP];
+    } c;
+    struct {
+      uint32_t key[kHash];
+      int32_t a[kHash];  // z low, then the run start
+      int32_t b[kHash];  // z high, then the LDS base
+    } h;
+  } u;
+  int32_t tbl[kMaxCells * 9];
+  int32_t ostart[kMaxCols], olen[kMaxCols], obase[kMaxCols];
+  uint32_t ckey[kMaxCells];
+  int32_t wsum[4], wocc[4];
+};
+__device__ __forceinline__ uint32_t col_hash(uint32_t c) { return (c * 2654435761u) >> 22; }  // 10 bits
+
+struct CellXYZ { int32_t x, y, z; };
+__device__ __forceinline__ CellXYZ cell_of(const GridView& g, uint32_t key) {
+  CellXYZ c;
+  c.z = (int32_t)(key % (uint32_t)g.nz);
+  const uint32_t xy = key / (uint32_t)g.nz;
+  c.y = (int32_t)(xy % (uint32_t)g.ny);
+  c.x = (int32_t)(xy / (uint32_t)g.ny);
+  return c;
+}
+
+// block-wide exclusive scan of v (256 threads); returns the prefix, *total = sum
+__device__ __forceinline__ int block_scan(int v, int* wsum, int* total) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  int inc = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int x = __shfl_up(inc, o);
+    if (lane >= o) inc += x;
+  }
+  if (lane == 63) wsum[wv] = inc;
+  __syncthreads();
+  int off = 0, tot = 0;
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    const int x = wsum[w];
+    off += w < wv ? x : 0;
+    tot += x;
+  }
+  __syncthreads();  // wsum may be reused by the next scan
+  *total = tot;
+  return off + inc - v;
+}
+
+template <int KB, class Fetch>
+__device__ __forceinline__ void run_chain(const uint32_t* lst, int lg, int k, Fetch fetch, float a[9]) {
+  // list entries stream from HBM: two batches in flight ahead of the coordinate fetches
+  uint32_t e0[KB], e1[KB];
+#pragma unroll
+  for (int b = 0; b < KB; ++b) {
+    e0[b] = (b < k) ? lst[(int64_t)b << lg] : 0u;
+    e1[b] = (KB + b < k) ? lst[(int64_t)(KB + b) << lg] : 0u;
+  }
+  for (int m0 = 0; m0 < k; m0 += KB) {
+    float4 c[KB];
+#pragma unroll
+    for (int b = 0; b < KB; ++b) c[b] = fetch(e0[b]);
+#pragma unroll
+    for (int b = 0; b < KB; ++b) {
+      const int m = m0 + 2 * KB + b;
+      e0[b] = e1[b];
+      e1[b] = (m < k) ? lst[(int64_t)m << lg] : 0u;
+    }
+#pragma unroll
+    for (int b = 0; b < KB; ++b)
+      if (m0 + b < k) chain_add(a, c[b].x, c[b].y, c[b].z);
+  }
+}
+
+// One workgroup of 256 consecutive queries [j0, j0 + 256).  DEFER: a workgroup whose union
+// does not fit CAP is queued for the big-LDS pass instead of gathering from L2 (returns false).
+#ifdef PFX_SHOT_PROFILE
+__device__ unsigned long long g_chain_prof[16];  // [0|8] prologue cycles, [1|9] wave chain cycles,
+                                                 // [2|10] sum of wave max k, [3|11] waves, [4|12] WGs
+#endif
+
+template <int CAP, bool DEFER>
+__device__ __forceinline__ void chain_wg(ChainLds<CAP>& S, const GridView& g, const NbLists& L, int64_t j0,
+                                         float vpx, float vpy, float vpz, float* __restrict__ nx,
+                                         float* __restrict__ ny, float* __restrict__ nz, float* __restrict__ curv,
+                                         int32_t* __restrict__ longq, int* __restrict__ n_long,
+                                         int* __restrict__ modes, int64_t* __restrict__ deferq) {
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int64_t j = j0 + tid;
+#ifdef PFX_SHOT_PROFILE
+  constexpr int PO = CAP == kStageSmall ? 0 : 8;
+  const long long pt0 = clock64();
+#endif
+  const bool valid = j < L.nq;
+  int32_t p = 0;
+  uint32_t key = 0, prev = kEmpty;
+  int k = 0;
+  if (valid) {
+    p = L.qpos[j];
+    key = L.skeys[p];
+    k = L.cnt[j];
+    if (tid > 0) prev = L.skeys[L.qpos[j - 1]];
+  }
+  // cell slots: first query of each distinct cell in the workgroup
+  const bool first = valid && key != prev;
+  const uint64_t fm = __ballot(first);
+  if (lane == 0) S.wsum[wv] = __popcll(fm);
+  __syncthreads();
+  int cbase = 0, ncell = 0;
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    cbase += w < wv ? S.wsum[w] : 0;
+    ncell += S.wsum[w];
+  }
+  const int cs = cbase + __popcll(fm & (lanemask_lt() | (1ull << lane))) - 1;
+  __syncthreads();
+  const bool indexed = ncell <= kMaxCells;
+  bool staged = false;
+  if (indexed) {
+    if (first) S.ckey[cs] = key;
+    for (int s = tid; s < kHash; s += 256) {
+      S.u.h.key[s] = kEmpty;
+      S.u.h.a[s] = 0x7fffffff;
+      S.u.h.b[s] = -1;
+    }
+    __syncthreads();
+    // touched columns and the z range each needs
+    for (int i = tid; i < ncell * 9; i += 256) {
+      const CellXYZ c = cell_of(g, S.ckey[i / 9]);
+      const int r = i % 9, X = c.x + r / 3 - 1, Y = c.y + r % 3 - 1;
+      if (X < 0 || X >= g.nx || Y < 0 || Y >= g.ny) continue;
+      const uint32_t col = (uint32_t)X * (uint32_t)g.ny + (uint32_t)Y;
+      uint32_t h = col_hash(col);
+      for (;;) {
+        const uint32_t old = atomicCAS(&S.u.h.key[h], kEmpty, col);
+        if (old == kEmpty || old == col) break;
+        h = (h + 1) & (kHash - 1);
+      }
+      atomicMin(&S.u.h.a[h], c.z > 0 ? c.z - 1 : 0);
+      atomicMax(&S.u.h.b[h], c.z + 1 < g.nz ? c.z + 1 : g.nz - 1);
+    }
+    __syncthreads();
+    // position range of every touched column, LDS bases by a block scan
+    int st4[4], len4[4], lsum = 0, osum = 0;
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const int s = tid * 4 + v;
+      const uint32_t col = S.u.h.key[s];
+      st4[v] = len4[v] = 0;
+      if (col != kEmpty) {
+        const int64_t c0 = (int64_t)col * g.nz;
+        st4[v] = g.cell_start[c0 + S.u.h.a[s]];
+        len4[v] = g.cell_start[c0 + S.u.h.b[s] + 1] - st4[v];
+      }
+      lsum += len4[v];
+      osum += len4[v] > 0;
+    }
+    int total = 0, nocc = 0;
+    int lb = block_scan(lsum, S.wsum, &total);
+    int ob = block_scan(osum, S.wocc, &nocc);
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const int s = tid * 4 + v;
+      S.u.h.a[s] = st4[v];
+      S.u.h.b[s] = lb;
+      if (len4[v] > 0) {
+        S.ostart[ob] = st4[v];
+        S.olen[ob] = len4[v];
+        S.obase[ob] = lb;
+        ++ob;
+      }
+      lb += len4[v];
+    }
+    staged = total <= CAP;
+    if (DEFER && !staged) {  // the big-LDS pass takes this workgroup (every thread agrees)
+      if (tid == 0) deferq[atomicAdd(&modes[3], 1)] = j0;
+      __syncthreads();
+      return;
+    }
+    __syncthreads();
+    // run table: list entry (r, off) of a query of cell cs -> tbl[cs * 9 + r] + off
+    for (int i = tid; i < ncell * 9; i += 256) {
+      const CellXYZ c = cell_of(g, S.ckey[i / 9]);
+      const int r = i % 9, X = c.x + r / 3 - 1, Y = c.y + r % 3 - 1;
+      int32_t t = 0;
+      if (X >= 0 && X < g.nx && Y >= 0 && Y < g.ny) {
+        const uint32_t col = (uint32_t)X * (uint32_t)g.ny + (uint32_t)Y;
+        const int32_t s_r = g.cell_start[(int64_t)col * g.nz + (c.z > 0 ? c.z - 1 : 0)];
+        t = s_r;
+        if (staged) {
+          uint32_t h = col_hash(col);
+          while (S.u.h.key[h] != col) h = (h + 1) & (kHash - 1);
+          t = S.u.h.b[h] + (s_r - S.u.h.a[h]);
+        }
+      }
+      S.tbl[i] = t;
+    }
+    __syncthreads();  // the hash is dead from here on: its LDS holds the staged candidates
+    if (staged) {
+      // flattened over the whole union (runs are short in sparse regions: a loop per run would
+      // serialise one global latency per run): element i -> run by binary search over the LDS
+      // bases, four elements per thread in flight
+      for (int i0 = 0; i0 < total; i0 += 4 * 256) {
+        int32_t src[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int i = i0 + u * 256 + tid;
+          int lo = 0, hi = nocc - 1;
+          while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (S.obase[mid] <= i) lo = mid;
+            else hi = mid - 1;
+          }
+          src[u] = i < total ? S.ostart[lo] + (i - S.obase[lo]) : -1;
+        }
+        float vx[4], vy[4], vz[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int32_t q = src[u] < 0 ? 0 : src[u];
+          vx[u] = g.sx[q];
+          vy[u] = g.sy[q];
+          vz[u] = g.sz[q];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int i = i0 + u * 256 + tid;
+          if (src[u] >= 0) {
+            S.u.c.x[i] = vx[u];
+            S.u.c.y[i] = vy[u];
+            S.u.c.z[i] = vz[u];
+          }
+        }
+      }
+    }
+    __syncthreads();
+    if (tid == 0) atomicAdd(&modes[staged ? 0 : 1], 1);
+  } else if (tid == 0) {
+    atomicAdd(&modes[2], 1);
+  }
+  __syncthreads();  // LDS reuse: every thread has passed the shared phases
+#ifdef PFX_SHOT_PROFILE
+  const long long pt1 = clock64();
+  if (tid == 0) {
+    atomicAdd(&g_chain_prof[PO + 0], (unsigned long long)(pt1 - pt0));
+    atomicAdd(&g_chain_prof[PO + 4], 1ull);
+  }
+  int wk = (valid && k <= kLaneMax) ? k : 0;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) wk = max(wk, __shfl_xor(wk, o));
+  const uint64_t wm = __ballot(valid && k == wk);
+  const bool rec = wm && lane == __builtin_ctzll(wm);
+#endif
+  if (!valid) return;
   if (k > kLaneMax) {
     longq[atomicAdd(n_long, 1)] = (int32_t)j;
     return;
   }
-  const int32_t p = L.qpos[j];
   const uint32_t* lst = L.list + L.off[j];
   const int lg = L.lg[j];
   float a[9];
 #pragma unroll
   for (int i = 0; i < 9; ++i) a[i] = 0.0f;
-  uint32_t pos[kBatch];
+  if (staged) {
+    const int32_t* tb = S.tbl + cs * 9;
+    const float *cxs = S.u.c.x, *cys = S.u.c.y, *czs = S.u.c.z;
+    run_chain<kBatch>(lst, lg, k, [&](uint32_t e) {
+      const int32_t i = tb[entry_run(e)] + (int32_t)entry_off(e);
+      return make_float4(cxs[i], cys[i], czs[i], 0.f);
+    }, a);
+  } else if (indexed) {
+    const int32_t* tb = S.tbl + cs * 9;
+    const float4* sp = g.sp;
+    run_chain<kBatch>(lst, lg, k, [&](uint32_t e) { return sp[tb[entry_run(e)] + (int32_t)entry_off(e)]; }, a);
+  } else {
+    // too many cells for the shared table: each lane keeps its own nine run starts in the
+    // (unused) staging LDS
+    int32_t* tb = reinterpret_cast<int32_t*>(S.u.c.x) + tid * 9;
 #pragma unroll
-  for (int b = 0; b < kBatch; ++b) pos[b] = (b < k) ? lst[(int64_t)b << lg] : (uint32_t)p;
-  for (int m0 = 0; m0 < k; m0 += kBatch) {
-    float4 c[kBatch];
-#pragma unroll
-    for (int b = 0; b < kBatch; ++b) c[b] = g.sp[pos[b]];
-#pragma unroll
-    for (int b = 0; b < kBatch; ++b) {
-      const int m = m0 + kBatch + b;
-      pos[b] = (m < k) ? lst[(int64_t)m << lg] : (uint32_t)p;
+    for (int r = 0; r < 9; ++r) {
+      int32_t st, len;
+      block_run(g, key, r, st, len);
+      tb[r] = st;
     }
-#pragma unroll
-    for (int b = 0; b < kBatch; ++b)
-      if (m0 + b < k) chain_add(a, c[b].x, c[b].y, c[b].z);
+    const float4* sp = g.sp;
+    run_chain<kBatch>(lst, lg, k, [&](uint32_t e) { return sp[tb[entry_run(e)] + (int32_t)entry_off(e)]; }, a);
   }
   store_normal(g, p, a, k, vpx, vpy, vpz, nx, ny, nz, curv);
+#ifdef PFX_SHOT_PROFILE
+  if (rec) {
+    atomicAdd(&g_chain_prof[PO + 1], (unsigned long long)(clock64() - pt1));
+    atomicAdd(&g_chain_prof[PO + 2], (unsigned long long)wk);
+    atomicAdd(&g_chain_prof[PO + 3], 1ull);
+  }
+#endif
+}
+
+__global__ void __launch_bounds__(256, 3) k_normals_chain(GridView g, NbLists L, float vpx, float vpy, float vpz,
+                                                          float* __restrict__ nx, float* __restrict__ ny,
+                                                          float* __restrict__ nz, float* __restrict__ curv,
+                                                          int32_t* __restrict__ longq, int* __restrict__ n_long,
+                                                          int* __restrict__ modes, int64_t* __restrict__ deferq) {
+  __shared__ ChainLds<kStageSmall> S;
+  chain_wg<kStageSmall, true>(S, g, L, (int64_t)blockIdx.x * 256, vpx, vpy, vpz, nx, ny, nz, curv,
+                              longq, n_long, modes, deferq);
+}
+
+// the deferred (dense) workgroups: one 144 KB workgroup per CU, persistent over the queue
+__global__ void __launch_bounds__(256, 1) k_normals_chain_big(GridView g, NbLists L, float vpx, float vpy,
+                                                              float vpz, float* __restrict__ nx,
+                                                              float* __restrict__ ny, float* __restrict__ nz,
+                                                              float* __restrict__ curv, int32_t* __restrict__ longq,
+                                                              int* __restrict__ n_long, int* __restrict__ modes,
+                                                              const int64_t* __restrict__ deferq) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char dyn[];
+  ChainLds<kStageBig>& S = *reinterpret_cast<ChainLds<kStageBig>*>(dyn);
+  const int count = modes[3];
+  for (int w = blockIdx.x; w < count; w += gridDim.x) {
+    __syncthreads();  // the previous workgroup's chains have finished reading the LDS
+    chain_wg<kStageBig, false>(S, g, L, deferq[w], vpx, vpy, vpz, nx, ny, nz, curv, longq, n_long, modes, nullptr);
+  }
 }
 
 // long lists: nine lanes per query (one chain each), seven queries per wave; every lane of a
-// query loads the same entries (one cache line per query per load), positions one batch ahead
+// query loads the same entries (one cache line per query per load), entries two batches ahead.
+// Persistent waves (grid-stride over groups of seven queries): the queue length is only known
+// on the device, and a grid sized for the worst case spends its time dispatching empty waves.
 __global__ void __launch_bounds__(256) k_normals_long(GridView g, NbLists L, const int32_t* __restrict__ longq,
                                                       const int* __restrict__ n_long, float vpx, float vpy,
                                                       float vpz, float* __restrict__ nx, float* __restrict__ ny,
                                                       float* __restrict__ nz, float* __restrict__ curv) {
   constexpr int kPerWave = 7, kB = 16;
-  const int lane = threadIdx.x & 63;
+  __shared__ int32_t rtab[4][kPerWave * 9];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int qi = lane / 9, a = lane - 9 * qi;
-  const int64_t w = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  const int64_t slot = w * kPerWave + qi;
   const int count = *n_long;
-  const bool active = qi < kPerWave && slot < count;
-  int k = 0, lg = 0;
-  int32_t j = 0;
-  const uint32_t* lst = L.list;
-  if (active) {
-    j = longq[slot];
-    k = L.cnt[j];
-    lg = L.lg[j];
-    lst = L.list + L.off[j];
-  }
-  float acc = 0.0f;
-  uint32_t pos[kB];
-#pragma unroll
-  for (int b = 0; b < kB; ++b) pos[b] = (b < k) ? lst[(int64_t)b << lg] : 0u;
-  for (int m0 = 0; m0 < k; m0 += kB) {
-    float4 c[kB];
-#pragma unroll
-    for (int b = 0; b < kB; ++b) c[b] = g.sp[pos[b]];
+  const int64_t nwaves = (int64_t)gridDim.x * 4;
+  for (int64_t w = (int64_t)blockIdx.x * 4 + wv; w * kPerWave < count; w += nwaves) {
+    const int64_t slot = w * kPerWave + qi;
+    const bool active = qi < kPerWave && slot < count;
+    int k = 0, lg = 0;
+    int32_t j = 0;
+    const uint32_t* lst = L.list;
+    if (active) {
+      j = longq[slot];
+      k = L.cnt[j];
+      lg = L.lg[j];
+      lst = L.list + L.off[j];
+      int32_t s, len;
+      block_run(g, L.skeys[L.qpos[j]], a, s, len);
+      rtab[wv][9 * qi + a] = s;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    const int32_t* tb = rtab[wv] + 9 * (qi < kPerWave ? qi : 0);
+    float acc = 0.0f;
+    uint32_t e[kB], e1[kB];
 #pragma unroll
     for (int b = 0; b < kB; ++b) {
-      const int m = m0 + kB + b;
-      pos[b] = (m < k) ? lst[(int64_t)m << lg] : 0u;
+      e[b] = (b < k) ? lst[(int64_t)b << lg] : 0u;
+      e1[b] = (kB + b < k) ? lst[(int64_t)(kB + b) << lg] : 0u;
     }
+    for (int m0 = 0; m0 < k; m0 += kB) {
+      float4 c[kB];
 #pragma unroll
-    for (int b = 0; b < kB; ++b)
-      if (m0 + b < k) acc = acc + chain_term(a, c[b].x, c[b].y, c[b].z);
+      for (int b = 0; b < kB; ++b) c[b] = g.sp[tb[entry_run(e[b])] + (int32_t)entry_off(e[b])];
+#pragma unroll
+      for (int b = 0; b < kB; ++b) {
+        const int m = m0 + 2 * kB + b;
+        e[b] = e1[b];
+        e1[b] = (m < k) ? lst[(int64_t)m << lg] : 0u;
+      }
+#pragma unroll
+      for (int b = 0; b < kB; ++b)
+        if (m0 + b < k) acc = acc + chain_term(a, c[b].x, c[b].y, c[b].z);
+    }
+    float accu[9];
+    const int base = 9 * (lane < 63 ? qi : 0);
+#pragma unroll
+    for (int i = 0; i < 9; ++i) accu[i] = __shfl(acc, base + i);
+    if (active && a == 0) store_normal(g, L.qpos[j], accu, k, vpx, vpy, vpz, nx, ny, nz, curv);
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();  // rtab is rewritten by the next group
   }
-  float accu[9];
-  const int base = 9 * (lane < 63 ? qi : 0);
-#pragma unroll
-  for (int i = 0; i < 9; ++i) accu[i] = __shfl(acc, base + i);
-  if (active && a == 0) store_normal(g, L.qpos[j], accu, k, vpx, vpy, vpz, nx, ny, nz, curv);
 }
 
 }  // namespace
@@ -151,23 +478,63 @@ void normals_dev(pfx_ctx* ctx, const float* x, const float* y, const float* z, i
   build_lists(ctx, G, nullptr, r, true, L, "normals");
   if (L.nq > 0) {
     int32_t* longq = ctx->buf("normals_longq").as<int32_t>(L.nq);
-    int* n_long = ctx->buf("normals_nlong").as<int>(1);
-    PFX_HIP(hipMemsetAsync(n_long, 0, sizeof(int), st));
+    // [0] long lists, [1..3] chain modes (staged, table, lane), [4] deferred workgroups
+    int* n_long = ctx->buf("normals_nlong").as<int>(5);
+    PFX_HIP(hipMemsetAsync(n_long, 0, 5 * sizeof(int), st));
     const int64_t nb = ceil_div(L.nq, 256);
-    const int64_t grid = (nb + 7) / 8 * 8;  // multiple of 8 for the XCD remap
+    // natural block order = round-robin over the 8 XCDs: the dense (heavy) workgroups cluster in
+    // space, so contiguous per-XCD slices would leave one XCD with ~1.4x the mean work
+    const int64_t grid = nb;
     {
       TimeScope ts(ctx, "normals_chain");  // exactly one kernel: the roofline figure of bench.py
+      int64_t* deferq = ctx->buf("normals_deferq").as<int64_t>(nb);
       k_normals_chain<<<(unsigned)grid, 256, 0, st>>>(view(G), L, vp[0], vp[1], vp[2], nx, ny, nz, curv, longq,
-                                                      n_long);
+                                                      n_long, n_long + 1, deferq);
       check_launch("k_normals_chain");
+      static bool attr = false;
+      if (!attr) {
+        PFX_HIP(hipFuncSetAttribute((const void*)k_normals_chain_big, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)sizeof(ChainLds<kStageBig>)));
+        attr = true;
+      }
+      TimeScope tb(ctx, "normals_chain_big");
+      k_normals_chain_big<<<256, 256, sizeof(ChainLds<kStageBig>), st>>>(view(G), L, vp[0], vp[1], vp[2], nx, ny,
+                                                                           nz, curv, longq, n_long, n_long + 1,
+                                                                           deferq);
+      check_launch("k_normals_chain_big");
     }
     TimeScope ts(ctx, "normals_long");
-    // upper bound on the long lists without a host round trip: every query (7 per wave)
-    const int64_t lb = ceil_div(L.nq, 7 * 4);
+    // persistent: the queue length stays on the device (no host round trip)
+    const int64_t lb = std::min<int64_t>(ceil_div(L.nq, 7 * 4), 2048);
     k_normals_long<<<(unsigned)lb, 256, 0, st>>>(view(G), L, longq, n_long, vp[0], vp[1], vp[2], nx, ny, nz,
                                                  curv);
     check_launch("k_normals_long");
   }
+  static const bool verbose = getenv("PFX_VERBOSE_STATS") != nullptr;
+  if (verbose && L.nq > 0) {  // diagnostics only (host sync): how the chain workgroups fetched
+    int h[5];
+    PFX_HIP(hipMemcpyAsync(h, ctx->buf("normals_nlong").ptr, sizeof(h), hipMemcpyDeviceToHost, st));
+    PFX_HIP(hipStreamSynchronize(st));
+    ctx->stats["normals_long_lists"] = h[0];
+    ctx->stats["normals_chain_wg_staged"] = h[1];
+    ctx->stats["normals_chain_wg_table"] = h[2];
+    ctx->stats["normals_chain_wg_lane"] = h[3];
+    ctx->stats["normals_chain_wg_deferred"] = h[4];
+  }
+#ifdef PFX_SHOT_PROFILE
+  {
+    unsigned long long pr[16];
+    PFX_HIP(hipStreamSynchronize(st));
+    PFX_HIP(hipMemcpyFromSymbol(pr, HIP_SYMBOL(g_chain_prof), sizeof(pr)));
+    for (int b = 0; b < 16; b += 8)
+      fprintf(stderr, "chain%s: WGs %llu prologue %.0f cyc/WG | waves %llu chain %.0f cyc/wave, max k %.1f/wave, "
+              "%.1f cyc/step\n", b ? "_big" : "", pr[b + 4], pr[b + 0] / (double)(pr[b + 4] + !pr[b + 4]), pr[b + 3],
+              pr[b + 1] / (double)(pr[b + 3] + !pr[b + 3]), pr[b + 2] / (double)(pr[b + 3] + !pr[b + 3]),
+              pr[b + 1] / (double)(pr[b + 2] + !pr[b + 2]));
+    const unsigned long long z[16] = {};
+    PFX_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_chain_prof), z, sizeof(z)));
+  }
+#endif
   ctx->stats["normals_neighbors"] = L.total;
   ctx->stats["normals_queries"] = L.nq;
 }

@@ -1,0 +1,39 @@
+"""Profiling aid: normal estimation alone (no concurrent NARF stream) on the bench scans, with
+the per-kernel HIP-event times -- the chain-stage roofline without cross-stream interference."""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+os.environ.setdefault("PFX_VERBOSE_STATS", "1")
+
+import torch  # noqa: E402
+
+from pcl_feature_extraction_amd import Context  # noqa: E402
+from pcl_feature_extraction_amd.pipeline import alloc  # noqa: E402
+from pcl_feature_extraction_amd.synth import synth_room, synth_seabed  # noqa: E402
+
+for name, gen, seed in (("room", synth_room, 2), ("seabed", synth_seabed, 3)):
+    x, y, z, _ = gen(1_000_000, seed)
+    dev = torch.device("cuda", 0)
+    b = alloc(torch, len(x), dev)
+    b.x.copy_(torch.from_numpy(x)); b.y.copy_(torch.from_numpy(y)); b.z.copy_(torch.from_numpy(z))
+    with Context(0) as ctx:
+        ctx.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+        for _ in range(2):
+            ctx.normals_dev(b.x, b.y, b.z, 0.05, b.nx, b.ny, b.nz, b.curv)
+        torch.cuda.synchronize()
+        ctx.set_timing(True)
+        ctx.reset_timing()
+        steps = 5
+        for _ in range(steps):
+            ctx.normals_dev(b.x, b.y, b.z, 0.05, b.nx, b.ny, b.nz, b.curv)
+        torch.cuda.synchronize()
+        names = ["grid_build", "normals", "normals_lists_sparse", "normals_lists_dense", "normals_lists_query",
+                 "normals_chain", "normals_chain_big", "normals_long"]
+        t = {n: round(ctx.kernel_time(n)[0] / steps, 4) for n in names}
+        nb = ctx.stat("normals_neighbors")
+        chain = t["normals_chain"] + t["normals_chain_big"]
+        gbs = (nb * 12 + len(x) * 16) / (chain / 1e3) / 1e9
+        print(name, json.dumps(t), "chain GB/s %.0f frac %.3f" % (gbs, gbs / 8000.0), flush=True)

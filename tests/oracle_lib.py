@@ -147,3 +147,33 @@ def shot(sx, sy, sz, nx, ny, nz, qx, qy, qz, r, threads=0):
     lib().orc_shot(_p(sx), _p(sy), _p(sz), _p(nx), _p(ny), _p(nz), _i64(len(sx)), _p(qx), _p(qy), _p(qz), _i64(nq),
                    ctypes.c_double(r), _p(desc), _p(rf), ctypes.c_int(threads))
     return desc, rf
+
+
+def nearest_descriptor(src, tgt, threads=0):
+    """Features::getCorrespondences (features.h:255-273): 1-NN target row of every source row
+    (-1 for a non-finite source row), and the L2_Simple squared distance."""
+    src = np.ascontiguousarray(src, np.float32)
+    tgt = np.ascontiguousarray(tgt, np.float32)
+    ns, dim = src.shape
+    idx = np.empty(ns, np.int32)
+    dist = np.empty(ns, np.float32)
+    rc = lib().orc_nearest_descriptor(_p(src), _i64(ns), _p(tgt), _i64(len(tgt)), ctypes.c_int(dim),
+                                      _p(idx, _i32p), _p(dist), ctypes.c_int(threads))
+    assert rc == 0
+    return idx, dist
+
+
+def correspondences(src, tgt, threads=0):
+    """Features::findCorrespondences (features.h:224-253): mutual nearest neighbours as
+    (index_query, index_match) arrays in source order."""
+    src = np.ascontiguousarray(src, np.float32)
+    tgt = np.ascontiguousarray(tgt, np.float32)
+    ns, dim = src.shape
+    cap = ns
+    q = np.empty(cap, np.int32)
+    m = np.empty(cap, np.int32)
+    n = ctypes.c_int64()
+    rc = lib().orc_correspondences(_p(src), _i64(ns), _p(tgt), _i64(len(tgt)), ctypes.c_int(dim), _p(q, _i32p),
+                                   _p(m, _i32p), _i64(cap), ctypes.byref(n), ctypes.c_int(threads))
+    assert rc == 0
+    return q[: n.value].copy(), m[: n.value].copy()
