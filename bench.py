@@ -34,10 +34,10 @@ BF16_PEAK_TFLOPS = 2500.0  # dense bf16 MFMA (MI355X_MICROARCH.md: ~2.5 PF dense
 N_POINTS = 1_000_000
 SHOT_SAMPLE = 10_000
 
-VERBOSE_TIMERS = ["grid_bbox", "grid_build", "normals", "normals_tiles", "normals_lists", "normals_lists_sparse",
+VERBOSE_TIMERS = ["grid_bbox", "grid_build", "normals", "normals_lists_phase", "normals_tiles", "normals_lists", "normals_lists_sparse",
                   "normals_lists_dense", "normals_lists_query", "normals_chain", "normals_chain_big", "normals_long", "range_image",
                   "narf_border", "narf_interest", "narf_nms", "narf_gather", "fpfh_mark", "fpfh_spfh",
-                  "fpfh_weight", "shot"]
+                  "fpfh_support", "fpfh_weight", "shot"]
 VERBOSE_STATS = ["normals_neighbors", "normals_queries", "normals_tiles_sparse", "normals_tiles_dense",
                  "normals_single", "normals_huge", "normals_long_lists", "normals_chain_wg_staged",
                  "normals_chain_wg_table", "normals_chain_wg_lane", "normals_chain_wg_deferred", "fpfh_spfh_points", "fpfh_spfh_pairs", "fpfh_spfh_exact_pairs", "narf_candidates", "narf_keypoints",
@@ -213,14 +213,15 @@ def main():
         # covariance chains.  Algorithmic bytes per launch = sum_q |N_0.05(q)| * 12 B (xyz) +
         # N * 16 B (normal + curvature out); time = its HIP-event duration on the ctx stream.
         algo_bytes = neighbors * 12 + N_POINTS * 16
-        # the chain stage is two launches: k_normals_chain (LDS-staged workgroups) and
-        # k_normals_chain_big (the dense workgroups it defers to a 144 KB-LDS pass)
-        chain_ms, chain_n = timers["normals_chain"]
-        big_ms, _ = timers["normals_chain_big"]
-        chain_ms += big_ms
-        stage_ms, stage_n = timers["normals"]
-        chain_s = (chain_ms / max(chain_n, 1)) / 1e3
-        stage_s = (stage_ms / max(stage_n, 1)) / 1e3
+        # the chain stage is k_normals_chain (LDS-staged workgroups) + k_normals_chain_big (the
+        # dense workgroups it defers to a 144 KB-LDS pass), run as two masked passes per step
+        # (FPFH support points on the main stream, the rest on the side stream): its time per
+        # step is the sum over both contexts' launches
+        chain_ms = timers["normals_chain"][0] + timers["normals_chain_big"][0]
+        stage_ms = timers["normals"][0] or sum(timers[nm][0] for nm in ("normals_lists_phase", "normals_chain",
+                                                                          "normals_chain_big", "normals_long"))
+        chain_s = chain_ms / args.steps / 1e3
+        stage_s = stage_ms / args.steps / 1e3
         achieved = algo_bytes / chain_s / 1e9 if chain_s > 0 else 0.0
         stage_gbs = algo_bytes / stage_s / 1e9 if stage_s > 0 else 0.0
         traffic = None
@@ -231,7 +232,7 @@ def main():
         roofline = {"bound": "hbm", "kernel": "k_normals_chain + k_normals_chain_big", "achieved": round(achieved, 2),
                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
                     "traffic": traffic, "algorithmic_bytes_per_launch": int(algo_bytes),
-                    "avg_launch_ms": round(chain_s * 1e3, 4), "neighbors_per_launch": int(neighbors),
+                    "chain_ms_per_step": round(chain_s * 1e3, 4), "neighbors_per_launch": int(neighbors),
                     "stage": {"name": "normals: grid + FLANN-ordered lists + chains",
                               "avg_ms": round(stage_s * 1e3, 4), "achieved": round(stage_gbs, 2),
                               "frac": round(stage_gbs / HBM_PEAK_GBS, 5)}}

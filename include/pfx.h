@@ -123,6 +123,19 @@ pfx_status pfx_normals(pfx_ctx* ctx, const float* x, const float* y, const float
 pfx_status pfx_normals_dev(pfx_ctx* ctx, const float* d_x, const float* d_y, const float* d_z,
                            int64_t n, double radius, const float viewpoint[3], float* d_nx,
                            float* d_ny, float* d_nz, float* d_curvature);
+/* The same computation in two phases, so that a caller can order the points it needs first
+ * (results identical to pfx_normals_dev):
+ *   lists  -- radius-neighbour lists of every finite point, kept in ctx; outputs NaN-filled;
+ *   chains -- the normals of the points with (d_mask[i] != 0) == want (all when d_mask is
+ *             null), on ctx's stream, from the lists held by `lists_ctx` (ctx itself or another
+ *             context on the same device whose lists phase is ordered before this call).  Two
+ *             chains calls with complementary masks may run concurrently on two contexts. */
+pfx_status pfx_normals_lists_dev(pfx_ctx* ctx, const float* d_x, const float* d_y, const float* d_z,
+                                 int64_t n, double radius, float* d_nx, float* d_ny, float* d_nz,
+                                 float* d_curvature);
+pfx_status pfx_normals_chains_dev(pfx_ctx* ctx, pfx_ctx* lists_ctx, const uint8_t* d_mask, int32_t want,
+                                  const float viewpoint[3], float* d_nx, float* d_ny, float* d_nz,
+                                  float* d_curvature);
 
 /* ---- FPFH-33: FPFHEstimation (surface + normals, queries = input cloud) ------------- */
 /* same_as_surface != 0 selects PCL's "input_ == surface_ && indices == all" branch (queries
@@ -143,6 +156,13 @@ pfx_status pfx_fpfh_dev(pfx_ctx* ctx, const float* d_sx, const float* d_sy, cons
  * same (d_sx, n_surface, radius) consumes it; the surface must not change in between. */
 pfx_status pfx_fpfh_prepare_dev(pfx_ctx* ctx, const float* d_sx, const float* d_sy, const float* d_sz,
                                 int64_t n_surface, double radius);
+/* d_mask[i] = 1 for every surface point whose normal FPFHEstimation reads for these queries
+ * (the r-neighbours of the SPFH set S = the r-neighbourhoods of the queries, fpfh.hpp), else 0.
+ * n_surface bytes.  The next pfx_fpfh_dev on ctx reads only these normals, so the others may
+ * still be computed concurrently (pfx_normals_chains_dev with want = 0 on another stream). */
+pfx_status pfx_fpfh_support_mask_dev(pfx_ctx* ctx, const float* d_sx, const float* d_sy, const float* d_sz,
+                                     int64_t n_surface, const float* d_qx, const float* d_qy,
+                                     const float* d_qz, int64_t nq, double radius, uint8_t* d_mask);
 
 /* ---- SHOT-352: SHOTEstimationOMP + SHOTLocalReferenceFrameEstimation ---------------- */
 /* desc: nq x 352, rf: nq x 9 (x_axis, y_axis, z_axis) -- SHOT352::{descriptor, rf}. */

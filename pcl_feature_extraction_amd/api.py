@@ -183,6 +183,23 @@ class Context:
                                            sx.numel(), _ptr(qx), _ptr(qy), _ptr(qz), qx.numel(),
                                            1 if same_as_surface else 0, float(r), _ptr(out)))
 
+    def normals_lists_dev(self, x, y, z, r, nx, ny, nz, curv):
+        """Phase 1 of normals_dev: neighbour lists of every point (kept in this context)."""
+        self._check(self._lib.pfx_normals_lists_dev(self.h, _ptr(x), _ptr(y), _ptr(z), x.numel(), float(r), _ptr(nx),
+                                                    _ptr(ny), _ptr(nz), _ptr(curv)))
+
+    def normals_chains_dev(self, lists_ctx, nx, ny, nz, curv, mask=None, want=1, viewpoint=(0.0, 0.0, 0.0)):
+        """Phase 2 on this context's stream for the points with (mask != 0) == want (all if mask
+        is None), from the lists held by `lists_ctx`."""
+        vp = (ctypes.c_float * 3)(*viewpoint)
+        self._check(self._lib.pfx_normals_chains_dev(self.h, lists_ctx.h, _ptr(mask), int(want), vp, _ptr(nx),
+                                                     _ptr(ny), _ptr(nz), _ptr(curv)))
+
+    def fpfh_support_mask_dev(self, sx, sy, sz, qx, qy, qz, r, mask):
+        """mask[i] = 1 for the surface points FPFH reads normals of (within r of a query)."""
+        self._check(self._lib.pfx_fpfh_support_mask_dev(self.h, _ptr(sx), _ptr(sy), _ptr(sz), sx.numel(), _ptr(qx),
+                                                         _ptr(qy), _ptr(qz), qx.numel(), float(r), _ptr(mask)))
+
     def fpfh_prepare_dev(self, sx, sy, sz, r):
         """Build the FPFH search-surface index ahead of fpfh_dev (see pfx_fpfh_prepare_dev)."""
         self._check(self._lib.pfx_fpfh_prepare_dev(self.h, _ptr(sx), _ptr(sy), _ptr(sz), sx.numel(), float(r)))

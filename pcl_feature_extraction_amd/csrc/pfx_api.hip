@@ -112,6 +112,7 @@ void pfx_ctx_destroy(pfx_ctx* ctx) {
   (void)hipSetDevice(ctx->device);
   (void)hipStreamSynchronize(ctx->stream);
   pfx::narf_release(ctx);
+  pfx::normals_release(ctx);
   ctx->grid_a.release();
   ctx->grid_b.release();
   for (auto& kv : ctx->bufs) kv.second.release();
@@ -223,6 +224,28 @@ pfx_status pfx_normals_dev(pfx_ctx* ctx, const float* d_x, const float* d_y, con
   PFX_API_END(ctx)
 }
 
+pfx_status pfx_normals_lists_dev(pfx_ctx* ctx, const float* d_x, const float* d_y, const float* d_z, int64_t n,
+                                 double radius, float* d_nx, float* d_ny, float* d_nz, float* d_curvature) {
+  PFX_API_BEGIN
+  check_ctx(ctx);
+  if (n < 0 || (n && (!d_x || !d_y || !d_z || !d_nx || !d_ny || !d_nz || !d_curvature)))
+    throw Error(PFX_ERR_INVALID, "normals lists: invalid arguments");
+  pfx::normals_lists_dev(ctx, d_x, d_y, d_z, n, radius, d_nx, d_ny, d_nz, d_curvature);
+  PFX_API_END(ctx)
+}
+
+pfx_status pfx_normals_chains_dev(pfx_ctx* ctx, pfx_ctx* lists_ctx, const uint8_t* d_mask, int32_t want,
+                                  const float viewpoint[3], float* d_nx, float* d_ny, float* d_nz,
+                                  float* d_curvature) {
+  PFX_API_BEGIN
+  check_ctx(ctx);
+  if (!lists_ctx || lists_ctx->device != ctx->device || !d_nx || !d_ny || !d_nz || !d_curvature)
+    throw Error(PFX_ERR_INVALID, "normals chains: invalid arguments");
+  const float vp0[3] = {0.f, 0.f, 0.f};
+  pfx::normals_chains_dev(ctx, lists_ctx, d_mask, want, viewpoint ? viewpoint : vp0, d_nx, d_ny, d_nz, d_curvature);
+  PFX_API_END(ctx)
+}
+
 pfx_status pfx_normals(pfx_ctx* ctx, const float* x, const float* y, const float* z, int64_t n, double radius,
                        const float viewpoint[3], float* nx, float* ny, float* nz, float* curvature) {
   PFX_API_BEGIN
@@ -296,6 +319,18 @@ pfx_status pfx_fpfh(pfx_ctx* ctx, const float* sx, const float* sy, const float*
   pfx::fpfh_dev(ctx, dsx, dsy, dsz, dnx, dny, dnz, n_surface, dqx, dqy, dqz, nq, same_as_surface, radius, dout);
   if (nq) PFX_HIP(hipMemcpyAsync(out, dout, sizeof(float) * nq * 33, hipMemcpyDeviceToHost, ctx->stream));
   PFX_HIP(hipStreamSynchronize(ctx->stream));
+  PFX_API_END(ctx)
+}
+
+pfx_status pfx_fpfh_support_mask_dev(pfx_ctx* ctx, const float* d_sx, const float* d_sy, const float* d_sz,
+                                     int64_t n_surface, const float* d_qx, const float* d_qy, const float* d_qz,
+                                     int64_t nq, double radius, uint8_t* d_mask) {
+  PFX_API_BEGIN
+  check_ctx(ctx);
+  if (n_surface < 0 || nq < 0 || (n_surface && (!d_sx || !d_sy || !d_sz || !d_mask)) ||
+      (nq && (!d_qx || !d_qy || !d_qz)))
+    throw Error(PFX_ERR_INVALID, "fpfh support mask: invalid arguments");
+  pfx::fpfh_support_mask_dev(ctx, d_sx, d_sy, d_sz, n_surface, d_qx, d_qy, d_qz, nq, radius, d_mask);
   PFX_API_END(ctx)
 }
 

@@ -221,12 +221,18 @@ __device__ __attribute__((noinline)) int pair_bins_exact(float p1x, float p1y, f
   return h1 | (h2 << 8) | (h3 << 16);
 }
 
+// support (nullable): only the points FPFH reads are copied -- the others may still be being
+// written by a concurrent normal-estimation pass (pfx_normals_chains_dev on another stream)
 __global__ void k_sorted_normals(const int32_t* __restrict__ perm, int64_t n, const float* __restrict__ nx,
                                  const float* __restrict__ ny, const float* __restrict__ nz,
-                                 float4* __restrict__ out) {
+                                 const uint8_t* __restrict__ support, float4* __restrict__ out) {
   const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   if (i >= n) return;
   const int32_t p = perm[i];
+  if (support && !support[p]) {
+    out[i] = make_float4(__builtin_nanf(""), __builtin_nanf(""), __builtin_nanf(""), 0.0f);
+    return;
+  }
   out[i] = make_float4(nx[p], ny[p], nz[p], 0.0f);
 }
 
@@ -242,6 +248,24 @@ __global__ void __launch_bounds__(256) k_fpfh_mark(GridView g, const float* __re
       const int32_t p = run_pos(R, t);
       const float4 c = g.sp[p];
       if (flann_d2(x, y, z, c.x, c.y, c.z) < rr) flags[p] = 1;
+    }
+  }
+}
+
+// Normals the SPFH stage reads: every r-neighbour of every S point (S = the r-neighbourhoods of
+// the queries), by caller index.  One workgroup per S point (sorted positions, device count).
+__global__ void __launch_bounds__(256) k_fpfh_mark_support(GridView g, const int32_t* __restrict__ plist,
+                                                           const int64_t* __restrict__ n_ptr, float rr,
+                                                           uint8_t* __restrict__ mask) {
+  const int64_t n = *n_ptr;
+  for (int64_t w = blockIdx.x; w < n; w += gridDim.x) {
+    Runs R;
+    const float4 q = g.sp[plist[w]];
+    query_runs(g, q.x, q.y, q.z, R);
+    for (int32_t t = threadIdx.x; t < R.pref[9]; t += blockDim.x) {
+      const int32_t p = run_pos(R, t);
+      const float4 c = g.sp[p];
+      if (flann_d2(q.x, q.y, q.z, c.x, c.y, c.z) < rr) mask[g.perm[p]] = 1;
     }
   }
 }
@@ -491,6 +515,35 @@ void fpfh_prepare_dev(pfx_ctx* ctx, const float* sx, const float* sy, const floa
   ctx->prep_r = r;
 }
 
+void fpfh_support_mask_dev(pfx_ctx* ctx, const float* sx, const float* sy, const float* sz, int64_t ns,
+                           const float* qx, const float* qy, const float* qz, int64_t nq, double r, uint8_t* mask) {
+  PFX_CHECK(r > 0.0, "fpfh support: radius must be > 0");
+  ctx->fpfh_support = nullptr;
+  if (ns == 0) return;
+  hipStream_t st = ctx->stream;
+  PFX_HIP(hipMemsetAsync(mask, 0, ns, st));
+  if (nq == 0) return;
+  if (!(ctx->prep_x == sx && ctx->prep_n == ns && ctx->prep_r == r)) fpfh_prepare_dev(ctx, sx, sy, sz, ns, r);
+  TimeScope ts(ctx, "fpfh_support");
+  const Grid& G = ctx->grid_b;
+  const GridView g = view(G);
+  const float rr = (float)(r * r);
+  uint8_t* flags = ctx->buf("fpfh_sflags").as<uint8_t>(ns);
+  int32_t* slist = ctx->buf("fpfh_slist").as<int32_t>(ns);
+  int64_t* d_sel = ctx->buf("fpfh_snsel").as<int64_t>(1);
+  size_t tmp_bytes = 0;
+  PFX_HIP(rocprim::select(nullptr, tmp_bytes, rocprim::counting_iterator<int32_t>(0), flags, slist, d_sel,
+                          (size_t)ns, st));
+  void* tmp = ctx->buf("fpfh_stmp").get(tmp_bytes + 16);
+  PFX_HIP(hipMemsetAsync(flags, 0, ns, st));
+  k_fpfh_mark<<<(unsigned)std::min<int64_t>(nq, 8192), 256, 0, st>>>(g, qx, qy, qz, nq, rr, flags);
+  PFX_HIP(rocprim::select(tmp, tmp_bytes, rocprim::counting_iterator<int32_t>(0), flags, slist, d_sel, (size_t)ns,
+                          st));
+  k_fpfh_mark_support<<<8192, 256, 0, st>>>(g, slist, d_sel, rr, mask);
+  check_launch("k_fpfh_mark_support");
+  ctx->fpfh_support = mask;  // consumed by the next fpfh_dev on this context
+}
+
 void fpfh_dev(pfx_ctx* ctx, const float* sx, const float* sy, const float* sz, const float* snx,
               const float* sny, const float* snz, int64_t ns, const float* qx, const float* qy, const float* qz,
               int64_t nq, int same, double r, float* out) {
@@ -523,7 +576,8 @@ void fpfh_dev(pfx_ctx* ctx, const float* sx, const float* sy, const float* sz, c
   const unsigned nb = (unsigned)ceil_div(ns, 256);
   {
     TimeScope ts(ctx, "fpfh_mark");
-    k_sorted_normals<<<nb, 256, 0, st>>>(G.perm, ns, snx, sny, snz, snp);
+    k_sorted_normals<<<nb, 256, 0, st>>>(G.perm, ns, snx, sny, snz, same ? nullptr : ctx->fpfh_support, snp);
+    ctx->fpfh_support = nullptr;  // one-shot
     if (same) {
       k_all_finite<<<nb, 256, 0, st>>>(G.skeys, ns, (uint64_t)G.ncells, flags);
     } else {

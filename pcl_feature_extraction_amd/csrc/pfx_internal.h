@@ -93,7 +93,8 @@ struct GridView {
   int32_t nx, ny, nz;
 };
 
-struct NarfState;  // pfx_narf.hip
+struct NarfState;     // pfx_narf.hip
+struct NormalsState;  // pfx_normals.hip
 
 }  // namespace pfx
 
@@ -109,8 +110,10 @@ struct pfx_ctx {
   const float* prep_x = nullptr;
   int64_t prep_n = -1;
   double prep_r = 0.0;
+  const uint8_t* fpfh_support = nullptr;  // pfx_fpfh_support_mask_dev -> next pfx_fpfh_dev
   std::map<std::string, pfx::DevBuf> bufs;  // named scratch
   pfx::NarfState* narf = nullptr;
+  pfx::NormalsState* normals = nullptr;  // neighbour lists between the two normal phases
   pfx::DevBuf& buf(const char* name) { return bufs[name]; }
 };
 
@@ -158,6 +161,13 @@ inline GridView view(const Grid& g) {
 // implemented in pfx_normals.hip / pfx_fpfh.hip / pfx_shot.hip / pfx_narf.hip
 void normals_dev(pfx_ctx* ctx, const float* x, const float* y, const float* z, int64_t n,
                  double r, const float vp[3], float* nx, float* ny, float* nz, float* curv);
+void normals_lists_dev(pfx_ctx* ctx, const float* x, const float* y, const float* z, int64_t n, double r,
+                       float* nx, float* ny, float* nz, float* curv);
+void normals_chains_dev(pfx_ctx* ctx, pfx_ctx* owner, const uint8_t* mask, int want, const float vp[3], float* nx,
+                        float* ny, float* nz, float* curv);
+void normals_release(pfx_ctx* ctx);
+void fpfh_support_mask_dev(pfx_ctx* ctx, const float* sx, const float* sy, const float* sz, int64_t ns,
+                           const float* qx, const float* qy, const float* qz, int64_t nq, double r, uint8_t* mask);
 void radius_search_dev(pfx_ctx* ctx, const float* x, const float* y, const float* z, int64_t n,
                        const float* qx, const float* qy, const float* qz, int64_t nq, double r,
                        int64_t* d_counts, int32_t* d_idx, float* d_d2, int64_t cap);

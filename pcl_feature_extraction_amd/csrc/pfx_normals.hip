@@ -24,7 +24,7 @@
 namespace pfx {
 namespace {
 
-constexpr int kBatch = 8;      // neighbour positions fetched ahead per lane
+constexpr int kBatch = 8;      // neighbour entries per half-batch (two in flight)
 constexpr int kLaneMax = 1024;  // longer lists go to k_normals_long
 
 __device__ __forceinline__ void chain_add(float a[9], float x, float y, float z) {
@@ -124,31 +124,36 @@ __device__ __forceinline__ int block_scan(int v, int* wsum, int* total) {
 
 template <int KB, class Fetch>
 __device__ __forceinline__ void run_chain(const uint32_t* lst, int lg, int k, Fetch fetch, float a[9]) {
-  // list entries stream from HBM: two batches in flight ahead of the coordinate fetches
-  uint32_t e0[KB], e1[KB];
+  // Branch-free batches: entry loads use a clamped index and padded terms are exact zeros
+  // (accumulators are never -0, so + 0.0f is the identity).  Two entry buffers alternate
+  // without register copies (a copy of a pending load forces a vmcnt wait), so one batch of
+  // entry loads is always in flight behind the batch being summed.
+  const int last = k - 1;
+  auto at = [&](int m) { return lst[(int64_t)(m < last ? m : last) << lg]; };
+  uint32_t eA[KB], eB[KB];
 #pragma unroll
   for (int b = 0; b < KB; ++b) {
-    e0[b] = (b < k) ? lst[(int64_t)b << lg] : 0u;
-    e1[b] = (KB + b < k) ? lst[(int64_t)(KB + b) << lg] : 0u;
+    eA[b] = at(b);
+    eB[b] = at(KB + b);
   }
-  for (int m0 = 0; m0 < k; m0 += KB) {
+  auto half = [&](uint32_t (&e)[KB], int m0) {
     float4 c[KB];
 #pragma unroll
-    for (int b = 0; b < KB; ++b) c[b] = fetch(e0[b]);
+    for (int b = 0; b < KB; ++b) c[b] = fetch(e[b]);
+#pragma unroll
+    for (int b = 0; b < KB; ++b) e[b] = at(m0 + 2 * KB + b);
 #pragma unroll
     for (int b = 0; b < KB; ++b) {
-      const int m = m0 + 2 * KB + b;
-      e0[b] = e1[b];
-      e1[b] = (m < k) ? lst[(int64_t)m << lg] : 0u;
+      const bool in = m0 + b < k;
+      chain_add(a, in ? c[b].x : 0.f, in ? c[b].y : 0.f, in ? c[b].z : 0.f);
     }
-#pragma unroll
-    for (int b = 0; b < KB; ++b)
-      if (m0 + b < k) chain_add(a, c[b].x, c[b].y, c[b].z);
+  };
+  for (int m0 = 0; m0 < k; m0 += 2 * KB) {
+    half(eA, m0);
+    half(eB, m0 + KB);  // unconditional (a branch here makes every wait conservative)
   }
 }
 
-// One workgroup of 256 consecutive queries [j0, j0 + 256).  DEFER: a workgroup whose union
-// does not fit CAP is queued for the big-LDS pass instead of gathering from L2 (returns false).
 #ifdef PFX_SHOT_PROFILE
 __device__ unsigned long long g_chain_prof[16];  // [0|8] prologue cycles, [1|9] wave chain cycles,
                                                  // [2|10] sum of wave max k, [3|11] waves, [4|12] WGs
@@ -159,7 +164,8 @@ __device__ __forceinline__ void chain_wg(ChainLds<CAP>& S, const GridView& g, co
                                          float vpx, float vpy, float vpz, float* __restrict__ nx,
                                          float* __restrict__ ny, float* __restrict__ nz, float* __restrict__ curv,
                                          int32_t* __restrict__ longq, int* __restrict__ n_long,
-                                         int* __restrict__ modes, int64_t* __restrict__ deferq) {
+                                         int* __restrict__ modes, int64_t* __restrict__ deferq,
+                                         const uint8_t* __restrict__ mask, int want) {
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int64_t j = j0 + tid;
 #ifdef PFX_SHOT_PROFILE
@@ -170,12 +176,15 @@ __device__ __forceinline__ void chain_wg(ChainLds<CAP>& S, const GridView& g, co
   int32_t p = 0;
   uint32_t key = 0, prev = kEmpty;
   int k = 0;
+  bool active = false;  // this pass computes the query (masked passes: mask[caller] == want)
   if (valid) {
     p = L.qpos[j];
     key = L.skeys[p];
     k = L.cnt[j];
     if (tid > 0) prev = L.skeys[L.qpos[j - 1]];
+    active = !mask || ((mask[g.perm[p]] != 0) == (want != 0));
   }
+  if (!__syncthreads_or(active)) return;  // nothing of this pass in the workgroup
   // cell slots: first query of each distinct cell in the workgroup
   const bool first = valid && key != prev;
   const uint64_t fm = __ballot(first);
@@ -319,13 +328,13 @@ __device__ __forceinline__ void chain_wg(ChainLds<CAP>& S, const GridView& g, co
     atomicAdd(&g_chain_prof[PO + 0], (unsigned long long)(pt1 - pt0));
     atomicAdd(&g_chain_prof[PO + 4], 1ull);
   }
-  int wk = (valid && k <= kLaneMax) ? k : 0;
+  int wk = (active && k <= kLaneMax) ? k : 0;
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) wk = max(wk, __shfl_xor(wk, o));
-  const uint64_t wm = __ballot(valid && k == wk);
+  const uint64_t wm = __ballot(active && k == wk);
   const bool rec = wm && lane == __builtin_ctzll(wm);
 #endif
-  if (!valid) return;
+  if (!active) return;
   if (k > kLaneMax) {
     longq[atomicAdd(n_long, 1)] = (int32_t)j;
     return;
@@ -373,10 +382,11 @@ __global__ void __launch_bounds__(256, 3) k_normals_chain(GridView g, NbLists L,
                                                           float* __restrict__ nx, float* __restrict__ ny,
                                                           float* __restrict__ nz, float* __restrict__ curv,
                                                           int32_t* __restrict__ longq, int* __restrict__ n_long,
-                                                          int* __restrict__ modes, int64_t* __restrict__ deferq) {
+                                                          int* __restrict__ modes, int64_t* __restrict__ deferq,
+                                                          const uint8_t* __restrict__ mask, int want) {
   __shared__ ChainLds<kStageSmall> S;
   chain_wg<kStageSmall, true>(S, g, L, (int64_t)blockIdx.x * 256, vpx, vpy, vpz, nx, ny, nz, curv,
-                              longq, n_long, modes, deferq);
+                              longq, n_long, modes, deferq, mask, want);
 }
 
 // the deferred (dense) workgroups: one 144 KB workgroup per CU, persistent over the queue
@@ -385,13 +395,15 @@ __global__ void __launch_bounds__(256, 1) k_normals_chain_big(GridView g, NbList
                                                               float* __restrict__ ny, float* __restrict__ nz,
                                                               float* __restrict__ curv, int32_t* __restrict__ longq,
                                                               int* __restrict__ n_long, int* __restrict__ modes,
-                                                              const int64_t* __restrict__ deferq) {
+                                                              const int64_t* __restrict__ deferq,
+                                                              const uint8_t* __restrict__ mask, int want) {
   extern __shared__ __attribute__((aligned(16))) unsigned char dyn[];
   ChainLds<kStageBig>& S = *reinterpret_cast<ChainLds<kStageBig>*>(dyn);
   const int count = modes[3];
   for (int w = blockIdx.x; w < count; w += gridDim.x) {
     __syncthreads();  // the previous workgroup's chains have finished reading the LDS
-    chain_wg<kStageBig, false>(S, g, L, deferq[w], vpx, vpy, vpz, nx, ny, nz, curv, longq, n_long, modes, nullptr);
+    chain_wg<kStageBig, false>(S, g, L, deferq[w], vpx, vpy, vpz, nx, ny, nz, curv, longq, n_long, modes, nullptr,
+                               mask, want);
   }
 }
 
@@ -429,10 +441,14 @@ __global__ void __launch_bounds__(256) k_normals_long(GridView g, NbLists L, con
     const int32_t* tb = rtab[wv] + 9 * (qi < kPerWave ? qi : 0);
     float acc = 0.0f;
     uint32_t e[kB], e1[kB];
+    const int last = k - 1;  // branch-free: clamped entry loads, exact-zero padded terms
+    auto at = [&](int m) { return lst[(int64_t)(m < last ? m : last) << lg]; };
+    if (k > 0) {
 #pragma unroll
-    for (int b = 0; b < kB; ++b) {
-      e[b] = (b < k) ? lst[(int64_t)b << lg] : 0u;
-      e1[b] = (kB + b < k) ? lst[(int64_t)(kB + b) << lg] : 0u;
+      for (int b = 0; b < kB; ++b) {
+        e[b] = at(b);
+        e1[b] = at(kB + b);
+      }
     }
     for (int m0 = 0; m0 < k; m0 += kB) {
       float4 c[kB];
@@ -440,13 +456,14 @@ __global__ void __launch_bounds__(256) k_normals_long(GridView g, NbLists L, con
       for (int b = 0; b < kB; ++b) c[b] = g.sp[tb[entry_run(e[b])] + (int32_t)entry_off(e[b])];
 #pragma unroll
       for (int b = 0; b < kB; ++b) {
-        const int m = m0 + 2 * kB + b;
         e[b] = e1[b];
-        e1[b] = (m < k) ? lst[(int64_t)m << lg] : 0u;
+        e1[b] = at(m0 + 2 * kB + b);
       }
 #pragma unroll
-      for (int b = 0; b < kB; ++b)
-        if (m0 + b < k) acc = acc + chain_term(a, c[b].x, c[b].y, c[b].z);
+      for (int b = 0; b < kB; ++b) {
+        const bool in = m0 + b < k;
+        acc = acc + chain_term(a, in ? c[b].x : 0.f, in ? c[b].y : 0.f, in ? c[b].z : 0.f);
+      }
     }
     float accu[9];
     const int base = 9 * (lane < 63 ? qi : 0);
@@ -460,60 +477,92 @@ __global__ void __launch_bounds__(256) k_normals_long(GridView g, NbLists L, con
 
 }  // namespace
 
-void normals_dev(pfx_ctx* ctx, const float* x, const float* y, const float* z, int64_t n, double r,
-                 const float vp[3], float* nx, float* ny, float* nz, float* curv) {
+struct NormalsState {
+  NbLists L;
+  int64_t n = 0;
+  bool ready = false;
+};
+
+void normals_release(pfx_ctx* ctx) {
+  delete ctx->normals;
+  ctx->normals = nullptr;
+}
+
+// Phase 1: grid + FLANN-ordered neighbour lists of every finite point (kept in ctx), outputs
+// NaN-filled (non-finite points are not queries: PCL writes NaN).
+void normals_lists_dev(pfx_ctx* ctx, const float* x, const float* y, const float* z, int64_t n, double r,
+                       float* nx, float* ny, float* nz, float* curv) {
   PFX_CHECK(r > 0.0, "normals: radius must be > 0");
   PFX_CHECK(n >= 0, "normals: negative point count");
-  if (n == 0) return;
+  if (!ctx->normals) ctx->normals = new NormalsState();
+  NormalsState& ns = *ctx->normals;
+  ns.ready = false;
+  ns.n = n;
+  ns.L = NbLists();
+  if (n == 0) {
+    ns.ready = true;
+    return;
+  }
   hipStream_t st = ctx->stream;
-  TimeScope total(ctx, "normals");
+  TimeScope total(ctx, "normals_lists_phase");
   build_grid(ctx, ctx->grid_a, x, y, z, n, r);
-  const Grid& G = ctx->grid_a;
-  // non-finite points are not queries: NaN outputs (PCL: NaN)
   PFX_HIP(hipMemsetAsync(nx, 0xff, sizeof(float) * n, st));
   PFX_HIP(hipMemsetAsync(ny, 0xff, sizeof(float) * n, st));
   PFX_HIP(hipMemsetAsync(nz, 0xff, sizeof(float) * n, st));
   PFX_HIP(hipMemsetAsync(curv, 0xff, sizeof(float) * n, st));
-  NbLists L;
-  build_lists(ctx, G, nullptr, r, true, L, "normals");
-  if (L.nq > 0) {
-    int32_t* longq = ctx->buf("normals_longq").as<int32_t>(L.nq);
-    // [0] long lists, [1..3] chain modes (staged, table, lane), [4] deferred workgroups
-    int* n_long = ctx->buf("normals_nlong").as<int>(5);
-    PFX_HIP(hipMemsetAsync(n_long, 0, 5 * sizeof(int), st));
-    const int64_t nb = ceil_div(L.nq, 256);
+  build_lists(ctx, ctx->grid_a, nullptr, r, true, ns.L, "normals");
+  ctx->stats["normals_neighbors"] = ns.L.total;
+  ctx->stats["normals_queries"] = ns.L.nq;
+  ns.ready = true;
+}
+
+// Phase 2 on ctx's stream: the ordered covariance chains of the queries whose caller index has
+// (mask[i] != 0) == want (every query when mask is null), from the lists held by `owner`
+// (which may be another context on the same device: the workspace used here is ctx's own, so
+// two passes with complementary masks can run concurrently on two streams).
+void normals_chains_dev(pfx_ctx* ctx, pfx_ctx* owner, const uint8_t* mask, int want, const float vp[3], float* nx,
+                        float* ny, float* nz, float* curv) {
+  PFX_CHECK(owner->normals && owner->normals->ready, "normals: lists not built (call the lists phase first)");
+  const NbLists& L = owner->normals->L;
+  if (L.nq == 0) return;
+  hipStream_t st = ctx->stream;
+  const Grid& G = owner->grid_a;
+  int32_t* longq = ctx->buf("normals_longq").as<int32_t>(L.nq);
+  // [0] long lists, [1..3] chain modes (staged, table, lane), [4] deferred workgroups
+  int* n_long = ctx->buf("normals_nlong").as<int>(5);
+  PFX_HIP(hipMemsetAsync(n_long, 0, 5 * sizeof(int), st));
+  const int64_t nb = ceil_div(L.nq, 256);
+  {
     // natural block order = round-robin over the 8 XCDs: the dense (heavy) workgroups cluster in
     // space, so contiguous per-XCD slices would leave one XCD with ~1.4x the mean work
-    const int64_t grid = nb;
-    {
-      TimeScope ts(ctx, "normals_chain");  // exactly one kernel: the roofline figure of bench.py
-      int64_t* deferq = ctx->buf("normals_deferq").as<int64_t>(nb);
-      k_normals_chain<<<(unsigned)grid, 256, 0, st>>>(view(G), L, vp[0], vp[1], vp[2], nx, ny, nz, curv, longq,
-                                                      n_long, n_long + 1, deferq);
-      check_launch("k_normals_chain");
-      static bool attr = false;
-      if (!attr) {
-        PFX_HIP(hipFuncSetAttribute((const void*)k_normals_chain_big, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    (int)sizeof(ChainLds<kStageBig>)));
-        attr = true;
-      }
-      TimeScope tb(ctx, "normals_chain_big");
-      k_normals_chain_big<<<256, 256, sizeof(ChainLds<kStageBig>), st>>>(view(G), L, vp[0], vp[1], vp[2], nx, ny,
-                                                                           nz, curv, longq, n_long, n_long + 1,
-                                                                           deferq);
-      check_launch("k_normals_chain_big");
+    TimeScope ts(ctx, "normals_chain");
+    int64_t* deferq = ctx->buf("normals_deferq").as<int64_t>(nb);
+    k_normals_chain<<<(unsigned)nb, 256, 0, st>>>(view(G), L, vp[0], vp[1], vp[2], nx, ny, nz, curv, longq, n_long,
+                                                  n_long + 1, deferq, mask, want);
+    check_launch("k_normals_chain");
+    static bool attr = false;
+    if (!attr) {
+      PFX_HIP(hipFuncSetAttribute((const void*)k_normals_chain_big, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)sizeof(ChainLds<kStageBig>)));
+      attr = true;
     }
+    TimeScope tb(ctx, "normals_chain_big");
+    k_normals_chain_big<<<256, 256, sizeof(ChainLds<kStageBig>), st>>>(view(G), L, vp[0], vp[1], vp[2], nx, ny, nz,
+                                                                         curv, longq, n_long, n_long + 1, deferq,
+                                                                         mask, want);
+    check_launch("k_normals_chain_big");
+  }
+  {
     TimeScope ts(ctx, "normals_long");
     // persistent: the queue length stays on the device (no host round trip)
     const int64_t lb = std::min<int64_t>(ceil_div(L.nq, 7 * 4), 2048);
-    k_normals_long<<<(unsigned)lb, 256, 0, st>>>(view(G), L, longq, n_long, vp[0], vp[1], vp[2], nx, ny, nz,
-                                                 curv);
+    k_normals_long<<<(unsigned)lb, 256, 0, st>>>(view(G), L, longq, n_long, vp[0], vp[1], vp[2], nx, ny, nz, curv);
     check_launch("k_normals_long");
   }
   static const bool verbose = getenv("PFX_VERBOSE_STATS") != nullptr;
-  if (verbose && L.nq > 0) {  // diagnostics only (host sync): how the chain workgroups fetched
+  if (verbose) {  // diagnostics only (host sync): how the chain workgroups fetched
     int h[5];
-    PFX_HIP(hipMemcpyAsync(h, ctx->buf("normals_nlong").ptr, sizeof(h), hipMemcpyDeviceToHost, st));
+    PFX_HIP(hipMemcpyAsync(h, n_long, sizeof(h), hipMemcpyDeviceToHost, st));
     PFX_HIP(hipStreamSynchronize(st));
     ctx->stats["normals_long_lists"] = h[0];
     ctx->stats["normals_chain_wg_staged"] = h[1];
@@ -535,8 +584,13 @@ void normals_dev(pfx_ctx* ctx, const float* x, const float* y, const float* z, i
     PFX_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_chain_prof), z, sizeof(z)));
   }
 #endif
-  ctx->stats["normals_neighbors"] = L.total;
-  ctx->stats["normals_queries"] = L.nq;
+}
+
+void normals_dev(pfx_ctx* ctx, const float* x, const float* y, const float* z, int64_t n, double r,
+                 const float vp[3], float* nx, float* ny, float* nz, float* curv) {
+  TimeScope total(ctx, "normals");
+  normals_lists_dev(ctx, x, y, z, n, r, nx, ny, nz, curv);
+  if (n > 0) normals_chains_dev(ctx, ctx, nullptr, 0, vp, nx, ny, nz, curv);
 }
 
 }  // namespace pfx

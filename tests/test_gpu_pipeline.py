@@ -29,7 +29,8 @@ def test_overlapped_pass_matches_sequential_and_oracle():
         else:
             kp, k = narf_fpfh(ctx, b)
         torch.cuda.synchronize(dev)
-        outs.append((np.asarray(kp), k, b.nx.cpu().numpy(), b.desc[:k].cpu().numpy()))
+        outs.append((np.asarray(kp), k, np.stack([t.cpu().numpy() for t in (b.nx, b.ny, b.nz, b.curv)]),
+                     b.desc[:k].cpu().numpy()))
         ctx.close(); ctx_n.close()
     (kp0, k0, n0, d0), (kp1, k1, n1, d1) = outs
     assert np.array_equal(kp0, kp1) and k0 == k1 and k0 > 0
@@ -38,8 +39,46 @@ def test_overlapped_pass_matches_sequential_and_oracle():
     # against the CPU restatement
     okp = O.narf_keypoints(x, y, z)
     assert np.array_equal(kp1, okp)
-    onx, ony, onz, _ = O.normals(x, y, z, 0.05)
-    assert np.array_equal(np.nan_to_num(n1, nan=7).view(np.uint32), np.nan_to_num(onx, nan=7).view(np.uint32))
+    onx, ony, onz, oc = O.normals(x, y, z, 0.05)
+    on = np.stack([onx, ony, onz, oc])
+    assert np.array_equal(np.nan_to_num(n1, nan=7).view(np.uint32), np.nan_to_num(on, nan=7).view(np.uint32))
     rows = okp[okp < n]
     od = O.fpfh(x, y, z, onx, ony, onz, x[rows], y[rows], z[rows], 0.08)
     assert np.array_equal(np.nan_to_num(d1, nan=7).view(np.uint32), np.nan_to_num(od, nan=7).view(np.uint32))
+
+
+def test_two_phase_normals_and_support_mask():
+    """pfx_normals_lists_dev + two complementary pfx_normals_chains_dev passes on two contexts
+    (two streams) == pfx_normals_dev; pfx_fpfh_support_mask_dev == the r-neighbours of the
+    r-neighbourhoods of the queries (oracle radius search)."""
+    import torch
+    from pcl_feature_extraction_amd import Context
+    from pcl_feature_extraction_amd.synth import synth_room
+    n = 120_000
+    x, y, z, _ = synth_room(n, 33)
+    dev = torch.device("cuda", 0)
+    X, Y, Z = (torch.from_numpy(a).to(dev) for a in (x, y, z))
+    ref = [torch.empty(n, device=dev) for _ in range(4)]
+    out = [torch.empty(n, device=dev) for _ in range(4)]
+    qi = np.arange(0, n, 997)
+    Q = [t[torch.from_numpy(qi).to(dev)].contiguous() for t in (X, Y, Z)]
+    mask = torch.empty(n, dtype=torch.uint8, device=dev)
+    with Context(0) as a, Context(0) as b:
+        a.normals_dev(X, Y, Z, 0.05, *ref)
+        a.fpfh_support_mask_dev(X, Y, Z, *Q, 0.08, mask)
+        b.normals_lists_dev(X, Y, Z, 0.05, *out)
+        b.synchronize()
+        a.normals_chains_dev(b, *out, mask=mask, want=1)
+        b.normals_chains_dev(b, *out, mask=mask, want=0)
+        a.synchronize(); b.synchronize()
+    for r, o in zip(ref, out):
+        r, o = r.cpu().numpy(), o.cpu().numpy()
+        assert np.array_equal(np.nan_to_num(r, nan=7).view(np.uint32), np.nan_to_num(o, nan=7).view(np.uint32))
+    cnt, idx, _ = O.radius_search(x, y, z, x[qi], y[qi], z[qi], 0.08, cap=4096)
+    assert cnt.max() <= 4096
+    S = np.unique(idx[idx >= 0])
+    cnt2, idx2, _ = O.radius_search(x, y, z, x[S], y[S], z[S], 0.08, cap=8192)
+    assert cnt2.max() <= 8192
+    expect = np.zeros(n, np.uint8)
+    expect[np.unique(idx2[idx2 >= 0])] = 1
+    assert np.array_equal(mask.cpu().numpy(), expect)
