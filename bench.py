@@ -200,6 +200,17 @@ def main():
     for c in (ctx, ctx_n):
         c.set_timing(False)
     neighbors = stat("normals_neighbors")
+    # the chain stage once more, alone on the GPU (after the timed region, not part of `value`):
+    # in the timed step it shares the device with NARF on the other stream
+    iso_ms = None
+    if rank == 0 and not shot:
+        ctx_n.set_timing(True)
+        ctx_n.reset_timing()
+        for _ in range(3):
+            ctx_n.normals_dev(b.x, b.y, b.z, 0.05, b.nx, b.ny, b.nz, b.curv)
+        torch.cuda.synchronize(dev)
+        iso_ms = (ctx_n.kernel_time("normals_chain")[0] + ctx_n.kernel_time("normals_chain_big")[0]) / 3
+        ctx_n.set_timing(False)
     if world > 1:
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -233,6 +244,10 @@ def main():
                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
                     "traffic": traffic, "algorithmic_bytes_per_launch": int(algo_bytes),
                     "chain_ms_per_step": round(chain_s * 1e3, 4), "neighbors_per_launch": int(neighbors),
+                    "isolated": None if iso_ms is None else {
+                        "chain_ms": round(iso_ms, 4), "achieved": round(algo_bytes / (iso_ms / 1e3) / 1e9, 2),
+                        "frac": round(algo_bytes / (iso_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 5),
+                        "note": "same kernels, normal estimation alone on the device after the timed region"},
                     "stage": {"name": "normals: grid + FLANN-ordered lists + chains",
                               "avg_ms": round(stage_s * 1e3, 4), "achieved": round(stage_gbs, 2),
                               "frac": round(stage_gbs / HBM_PEAK_GBS, 5)}}

@@ -14,5 +14,5 @@ for P in "$P1" "$P2" "$P3" "$P4"; do
   timeout -k 10 300 rocprofv3 --kernel-trace --pmc $P --output-format csv -d $R/gpurun_out/pmc_$TAG/p$i -o run -- \
     python3 $R/bench.py --steps 1 --warmup 1 --no-cpu-baseline > $R/gpurun_out/pmc_$TAG/p$i.log 2>&1 || exit 1
 done
-python3 $R/scripts/pmc_summary.py $R/gpurun_out/pmc_$TAG k_normals_chain $R/gpurun_out/pmc_$TAG/pmc_normals_chain.json > $R/gpurun_out/pmc_$TAG/summary.txt
+python3 $R/scripts/pmc_summary.py $R/gpurun_out/pmc_$TAG k_normals_chain,k_normals_chain_big $R/gpurun_out/pmc_$TAG/pmc_normals_chain.json > $R/gpurun_out/pmc_$TAG/summary.txt
 cat $R/gpurun_out/pmc_$TAG/summary.txt

@@ -42,17 +42,23 @@ for us, k, a in rows[:20]:
         extra["L2_hit"] = a["TCC_HIT_sum"] / (a["TCC_HIT_sum"] + a["TCC_MISS_sum"])
     print("   " + "  ".join(f"{c}={v:.4g}" for c, v in sorted({**a, **extra}.items())))
 
-# machine-readable per-launch HBM traffic of one kernel for bench.py's roofline.traffic
+# machine-readable HBM traffic of one stage for bench.py's roofline.traffic: the sum over the
+# named kernels (comma-separated prefixes) of their per-dispatch averages
 if len(sys.argv) > 3:
-    kernel, dest = sys.argv[2], sys.argv[3]
-    for us, k, a in rows:
-        if k.startswith(kernel):
-            fetch = a.get("FETCH_SIZE_x2_MB", 0.0) * 1024 * 1024
-            write = a.get("WRITE_SIZE_MB", 0.0) * 1024 * 1024
-            import json
-            with open(dest, "w") as f:
-                json.dump({"kernel": kernel, "hbm_bytes_per_launch": int(fetch + write),
-                           "fetch_bytes_x2": int(fetch), "write_bytes": int(write),
-                           "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes, FETCH x2 "
-                                     "(MI355X_MICROARCH.md gfx950 correction)"}, f, indent=1)
-            break
+    import json
+    kernels, dest = sys.argv[2].split(","), sys.argv[3]
+    fetch = write = 0.0
+    found = []
+    for kernel in kernels:
+        for us, k, a in rows:
+            if k == kernel or k.startswith(kernel + "<") or k.startswith(kernel + "("):
+                fetch += a.get("FETCH_SIZE_x2_MB", 0.0) * 1024 * 1024
+                write += a.get("WRITE_SIZE_MB", 0.0) * 1024 * 1024
+                found.append(k)
+                break
+    with open(dest, "w") as f:
+        json.dump({"kernel": " + ".join(found), "hbm_bytes_per_launch": int(fetch + write),
+                   "fetch_bytes_x2": int(fetch), "write_bytes": int(write),
+                   "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes, FETCH x2 "
+                             "(MI355X_MICROARCH.md gfx950 correction); sum of the kernels' per-dispatch "
+                             "averages over bench.py warmup + timed steps"}, f, indent=1)
