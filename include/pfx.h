@@ -214,6 +214,10 @@ pfx_status pfx_gather_points_dev(pfx_ctx* ctx, const float* d_x, const float* d_
 pfx_status pfx_nearest_descriptors_dev(pfx_ctx* ctx, const float* d_src, int64_t n_src, int64_t src_stride,
                                        const float* d_tgt, int64_t n_tgt, int64_t tgt_stride, int32_t dim,
                                        int32_t* d_s2t, float* d_s2t_dist, int32_t* d_t2s, float* d_t2s_dist);
+/* Host-pointer form of one direction (the facade's KdTreeFLANN<FeatureT>::nearestKSearch). */
+pfx_status pfx_nearest_descriptors(pfx_ctx* ctx, const float* src, int64_t n_src, int64_t src_stride,
+                                   const float* tgt, int64_t n_tgt, int64_t tgt_stride, int32_t dim,
+                                   int32_t* s2t, float* s2t_dist);
 /* Mutual nearest neighbours (index_query, index_match) in source order.  *n_out = the number
  * of correspondences (host); PFX_ERR_CAPACITY (nothing written) when it exceeds cap. */
 pfx_status pfx_correspondences_dev(pfx_ctx* ctx, const float* d_src, int64_t n_src, int64_t src_stride,

@@ -8,6 +8,8 @@
 //                                                       search::KdTree, setRadiusSearch, compute
 //   include/pcl_feature_extraction/tools.h:22-32        NormalEstimationOMP
 //   src/evaluation.cpp:593-612, :766-785                FPFHEstimation, SHOTEstimationOMP
+//   include/pcl_feature_extraction/features.h:224-273   KdTreeFLANN<FeatureT>::nearestKSearch,
+//                                                       Correspondence(s), boost::thread / ref
 // This header provides those names in namespace pcl (plus the minimal Eigen subset the calls
 // touch), implemented on the GPU through libpfx, so the wrapper headers compile unchanged when
 // this header stands in for the PCL includes.  Point types keep PCL's 16-byte-aligned layouts.
@@ -28,7 +30,9 @@
 #include <cstdlib>
 #include <limits>
 #include <memory>
+#include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "pfx.h"
@@ -40,7 +44,9 @@
 #ifdef PFX_PCL_BOOST_SHIM
 namespace boost {
 using std::dynamic_pointer_cast;
+using std::ref;
 using std::shared_ptr;
+using std::thread;  // features.h:234-239 runs the two getCorrespondences on boost::thread
 }  // namespace boost
 #endif
 
@@ -136,6 +142,12 @@ inline pfx_ctx* context() {
   return ctx;
 }
 inline float nanf() { return std::numeric_limits<float>::quiet_NaN(); }
+// serialises calls that may come from several threads at once (features.h:234-239 queries two
+// descriptor trees on two threads; a libpfx context is not re-entrant)
+inline std::mutex& context_mutex() {
+  static std::mutex m;
+  return m;
+}
 }  // namespace detail
 
 // ---- point types (PCL 1.7 layouts, 16-byte aligned) ----------------------------------------
@@ -506,6 +518,84 @@ class NarfKeypoint {
   RangeImageBorderExtractor* border_extractor_;
   const RangeImagePlanar* range_image_ = nullptr;
   Parameters parameters_;
+};
+
+// ---- descriptor matching (features.h:224-273) ------------------------------------------------
+struct Correspondence {
+  int index_query = 0;
+  int index_match = -1;
+  float distance = std::numeric_limits<float>::max();
+  Correspondence() = default;
+  Correspondence(int q, int m, float d) : index_query(q), index_match(m), distance(d) {}
+};
+typedef std::vector<Correspondence> Correspondences;
+typedef std::shared_ptr<Correspondences> CorrespondencesPtr;
+typedef std::shared_ptr<const Correspondences> CorrespondencesConstPtr;
+
+namespace detail {
+// DefaultFeatureRepresentation: the compared floats of a descriptor and the point stride
+template <typename T> struct DescriptorLayout;
+template <> struct DescriptorLayout<FPFHSignature33> { static constexpr int dim = 33, stride = 33; };
+template <> struct DescriptorLayout<SHOT352> { static constexpr int dim = 352, stride = 361; };
+}  // namespace detail
+
+// KdTreeFLANN<FeatureT> with nearestKSearch(k = 1), as the reference uses it (features.h:258-272):
+// exact 1-NN under FLANN's L2_Simple on the GPU (pfx_nearest_descriptors).  The reference asks
+// one source row at a time; the first query of a source cloud answers all its rows in one GPU
+// pass and the following calls read that batch (the cloud must not change in between, as with
+// the reference's loop).  A row without a match (non-finite values: undefined in FLANN) returns
+// 0 neighbours with k_indices = {0}, which the mutual check of findCorrespondences rejects
+// (target rows never match a non-finite source row).
+template <typename PointT>
+class KdTreeFLANN {
+ public:
+  typedef typename PointCloud<PointT>::ConstPtr PointCloudConstPtr;
+  typedef std::shared_ptr<KdTreeFLANN<PointT> > Ptr;
+  explicit KdTreeFLANN(bool sorted = true) : sorted_(sorted) {}
+  void setInputCloud(const PointCloudConstPtr& cloud) {
+    target_ = cloud;
+    batch_src_ = nullptr;
+  }
+  int nearestKSearch(const PointCloud<PointT>& cloud, int index, int k, std::vector<int>& k_indices,
+                     std::vector<float>& k_sqr_distances) const {
+    if (k != 1 || !target_ || index < 0 || (size_t)index >= cloud.size()) {
+      PCL_ERROR("[pcl::KdTreeFLANN::nearestKSearch] only k = 1 over a set input cloud is accelerated\n");
+      return 0;
+    }
+    if (batch_src_ != &cloud || batch_n_ != cloud.size()) {
+      idx_.assign(cloud.size(), -1);
+      dist_.assign(cloud.size(), detail::nanf());
+      std::lock_guard<std::mutex> lock(detail::context_mutex());
+      typedef detail::DescriptorLayout<PointT> L;
+      if (!detail::context() ||
+          !detail::ok(pfx_nearest_descriptors(detail::context(), reinterpret_cast<const float*>(cloud.points.data()),
+                                              (int64_t)cloud.size(), L::stride,
+                                              reinterpret_cast<const float*>(target_->points.data()),
+                                              (int64_t)target_->size(), L::stride, L::dim, idx_.data(), dist_.data()),
+                      "KdTreeFLANN"))
+        idx_.assign(cloud.size(), -1);
+      batch_src_ = &cloud;
+      batch_n_ = cloud.size();
+    }
+    k_indices.assign(1, idx_[index] < 0 ? 0 : idx_[index]);
+    k_sqr_distances.assign(1, dist_[index]);
+    return idx_[index] < 0 ? 0 : 1;
+  }
+  int nearestKSearch(const PointT& point, int k, std::vector<int>& k_indices, std::vector<float>& k_sqr_distances) const {
+    PointCloud<PointT> one;
+    one.push_back(point);
+    KdTreeFLANN<PointT> tmp;
+    tmp.setInputCloud(target_);
+    return tmp.nearestKSearch(one, 0, k, k_indices, k_sqr_distances);
+  }
+
+ private:
+  bool sorted_;
+  PointCloudConstPtr target_;
+  mutable const PointCloud<PointT>* batch_src_ = nullptr;
+  mutable size_t batch_n_ = 0;
+  mutable std::vector<int32_t> idx_;
+  mutable std::vector<float> dist_;
 };
 
 }  // namespace pcl

@@ -98,6 +98,7 @@ _SIGS = {
                                       c_i64p]),
     "pfx_nearest_descriptors_dev": (c_int, [c_vp, c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, ctypes.c_int32,
                                             c_vp, c_vp, c_vp, c_vp]),
+    "pfx_nearest_descriptors": (c_int, [c_vp, c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, ctypes.c_int32, c_vp, c_vp]),
     "pfx_correspondences_dev": (c_int, [c_vp, c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, ctypes.c_int32,
                                         c_vp, c_vp, c_i64, c_i64p]),
     "pfx_correspondences": (c_int, [c_vp, c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, ctypes.c_int32,

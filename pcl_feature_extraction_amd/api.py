@@ -240,6 +240,18 @@ class Context:
                                                   _ptr(q), _ptr(m), ns, ctypes.byref(n)))
         return q[: n.value].copy(), m[: n.value].copy()
 
+    def nearest_descriptors(self, src, tgt):
+        """features.h:255-273 (one direction, host arrays): nearest target row of every source row
+        (-1: non-finite row / empty target) and its L2_Simple squared distance."""
+        src = np.ascontiguousarray(src, dtype=np.float32)
+        tgt = np.ascontiguousarray(tgt, dtype=np.float32)
+        ns, d = src.shape
+        idx = np.empty(max(ns, 1), np.int32)
+        dist = np.empty(max(ns, 1), np.float32)
+        self._check(self._lib.pfx_nearest_descriptors(self.h, _ptr(src), ns, d, _ptr(tgt), tgt.shape[0], tgt.shape[1],
+                                                      d, _ptr(idx), _ptr(dist)))
+        return idx[:ns].copy(), dist[:ns].copy()
+
     def nearest_descriptors_dev(self, src, tgt, s2t, s2t_dist=None, t2s=None, t2s_dist=None, dim=None):
         """features.h:255-273 in both directions: (n, stride) device tensors, `dim` leading floats
         of each row compared (default: the whole row)."""

@@ -486,6 +486,27 @@ extern "C" pfx_status pfx_nearest_descriptors_dev(pfx_ctx* ctx, const float* d_s
   PFX_API_END(ctx)
 }
 
+extern "C" pfx_status pfx_nearest_descriptors(pfx_ctx* ctx, const float* src, int64_t n_src, int64_t src_stride,
+                                              const float* tgt, int64_t n_tgt, int64_t tgt_stride, int32_t dim,
+                                              int32_t* s2t, float* s2t_dist) {
+  PFX_API_BEGIN
+  check_ctx(ctx);
+  check_match_args(src, n_src, src_stride, tgt, n_tgt, tgt_stride, dim);
+  if (n_src && !s2t) throw Error(PFX_ERR_INVALID, "nearest_descriptors: null output");
+  const int64_t cs = n_src ? (n_src - 1) * src_stride + dim : 0, ct = n_tgt ? (n_tgt - 1) * tgt_stride + dim : 0;
+  float* ds = stage_in(ctx, "in_match_src", src, cs);
+  float* dt = stage_in(ctx, "in_match_tgt", tgt, ct);
+  int32_t* di = ctx->buf("out_match_i").as<int32_t>(n_src + 1);
+  float* dd = ctx->buf("out_match_d").as<float>(n_src + 1);
+  pfx::match_nearest_dev(ctx, ds, n_src, src_stride, dt, n_tgt, tgt_stride, dim, di, dd, nullptr, nullptr);
+  if (n_src) {
+    PFX_HIP(hipMemcpyAsync(s2t, di, sizeof(int32_t) * n_src, hipMemcpyDeviceToHost, ctx->stream));
+    if (s2t_dist) PFX_HIP(hipMemcpyAsync(s2t_dist, dd, sizeof(float) * n_src, hipMemcpyDeviceToHost, ctx->stream));
+  }
+  PFX_HIP(hipStreamSynchronize(ctx->stream));
+  PFX_API_END(ctx)
+}
+
 extern "C" pfx_status pfx_correspondences_dev(pfx_ctx* ctx, const float* d_src, int64_t n_src, int64_t src_stride,
                                               const float* d_tgt, int64_t n_tgt, int64_t tgt_stride, int32_t dim,
                                               int32_t* d_query, int32_t* d_match, int64_t cap, int64_t* n_out) {

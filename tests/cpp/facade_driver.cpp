@@ -4,8 +4,10 @@
 // features.h:175-196 (Features<T>::compute with the FeatureFromNormals probe) and tools.h:22-32
 // (estimateNormals), as src/evaluation.cpp:593-612 / :766-785 drive them.  Reads a PCL 1.7 binary
 // PCD (x y z rgb, 16 B per point), writes raw float/int arrays for tests/test_facade.py:
-//   facade_driver <cloud.pcd> <out_dir>
+//   facade_driver <cloud.pcd> <out_dir> [<target.pcd>]
 //   -> keypoints.i32, normals.f32 (n x 4), fpfh.f32 (K x 33), shot.f32 (K x 352), shot_rf.f32 (K x 9)
+//   with a target cloud also: fpfh_target.f32 and corr.i32 (index_query, index_match pairs) of
+//   features.h:224-273 (findCorrespondences / getCorrespondences, verbatim below).
 #include <cstdio>
 #include <cstring>
 #include <fstream>
@@ -55,6 +57,60 @@ static void dump(const std::string& path, const T* p, size_t count) {
   if (f) { std::fwrite(p, sizeof(T), count, f); std::fclose(f); }
 }
 
+// features.h:224-273, Features<FeatureType>::findCorrespondences / getCorrespondences, verbatim
+// apart from the class scaffolding (boost::thread / boost::ref through PFX_PCL_BOOST_SHIM)
+template <typename FeatureType>
+struct Features {
+  void findCorrespondences(typename PointCloud<FeatureType>::Ptr source,
+                           typename PointCloud<FeatureType>::Ptr target,
+                           CorrespondencesPtr& correspondences)
+  {
+    std::vector<int> source2target;
+    std::vector<int> target2source;
+
+    boost::thread thread1(&Features::getCorrespondences, this, boost::ref(source), boost::ref(target), boost::ref(source2target));
+    boost::thread thread2(&Features::getCorrespondences, this, boost::ref(target), boost::ref(source), boost::ref(target2source));
+
+    // Wait until both threads have finished
+    thread1.join();
+    thread2.join();
+
+    // now populate the correspondences vector
+    std::vector<std::pair<unsigned, unsigned> > c;
+    for (unsigned c_idx = 0; c_idx < source2target.size (); ++c_idx)
+      if (target2source[source2target[c_idx]] == (int)c_idx)
+        c.push_back(std::make_pair(c_idx, source2target[c_idx]));
+
+    correspondences->resize(c.size());
+    for (unsigned c_idx = 0; c_idx < c.size(); ++c_idx)
+    {
+      (*correspondences)[c_idx].index_query = c[c_idx].first;
+      (*correspondences)[c_idx].index_match = c[c_idx].second;
+    }
+  }
+
+  void getCorrespondences(typename PointCloud<FeatureType>::Ptr source,
+                          typename PointCloud<FeatureType>::Ptr target,
+                          std::vector<int>& source2target)
+  {
+    const int k = 1;
+    std::vector<int> k_indices(k);
+    std::vector<float> k_dist(k);
+    source2target.clear();
+    KdTreeFLANN<FeatureType> descriptor_kdtree;
+
+    // Find the index of the best match for each keypoint
+    // From source to target
+    descriptor_kdtree.setInputCloud(target);
+    source2target.resize(source->size());
+    for (size_t i = 0; i < source->size(); ++i)
+    {
+      descriptor_kdtree.nearestKSearch(*source, i, k, k_indices, k_dist);
+      source2target[i] = k_indices[0];
+    }
+  }
+};
+
 // tools.h:22-32
 static void estimateNormals(const PointCloudRGB::Ptr& cloud, PointCloud<Normal>::Ptr& normals, double radius) {
   NormalEstimationOMP<PointRGB, Normal> normal_estimation_omp;
@@ -87,6 +143,33 @@ static void features_compute(typename Feature<PointRGB, FeatureType>::Ptr featur
   feature_extractor->compute(*descriptors);
 }
 
+// keypoints.h:199-231 (NARF branch) -> the keypoint cloud (and the raw pixel indices)
+static PointCloudRGB::Ptr narf_keypoints(const PointCloudRGB::Ptr& cloud, PointCloud<int>::Ptr& keypoints) {
+  int image_size_x = 640, image_size_y = 480;
+  float center_x = (640.0f / 2.0f), center_y = (480.0f / 2.0f);
+  float focal_length_x = 525.0f;
+  Eigen::Affine3f sensor_pose = Eigen::Affine3f(Eigen::Translation3f(cloud->sensor_origin_[0],
+                                                                     cloud->sensor_origin_[1],
+                                                                     cloud->sensor_origin_[2])) *
+                                Eigen::Affine3f(cloud->sensor_orientation_);
+  float noise_level = 0.0f, minimum_range = 0.0f;
+  RangeImagePlanar range_image;
+  range_image.createFromPointCloudWithFixedSize(*cloud, image_size_x, image_size_y, center_x, center_y,
+                                                focal_length_x, focal_length_x, sensor_pose,
+                                                RangeImage::CAMERA_FRAME, noise_level, minimum_range);
+  keypoints.reset(new PointCloud<int>);
+  RangeImageBorderExtractor border_extractor;
+  NarfKeypoint detector(&border_extractor);
+  detector.setRangeImage(&range_image);
+  detector.getParameters().support_size = 0.2f;
+  detector.compute(*keypoints);
+  PointCloudRGB::Ptr cloud_keypoints(new PointCloudRGB);
+  for (size_t i = 0; i < keypoints->points.size(); ++i)
+    if ((size_t)keypoints->points[i] < cloud->size())  // keypoints.h:229 indexes the cloud by pixel index
+      cloud_keypoints->points.push_back(cloud->points[keypoints->points[i]]);
+  return cloud_keypoints;
+}
+
 int main(int argc, char** argv) {
   if (argc < 3) {
     std::fprintf(stderr, "usage: %s cloud.pcd out_dir\n", argv[0]);
@@ -100,28 +183,8 @@ int main(int argc, char** argv) {
   const std::string out = argv[2];
 
   // ---- keypoints.h:199-231 (NARF) ----
-  int image_size_x = 640, image_size_y = 480;
-  float center_x = (640.0f / 2.0f), center_y = (480.0f / 2.0f);
-  float focal_length_x = 525.0f;
-  Eigen::Affine3f sensor_pose = Eigen::Affine3f(Eigen::Translation3f(cloud->sensor_origin_[0],
-                                                                     cloud->sensor_origin_[1],
-                                                                     cloud->sensor_origin_[2])) *
-                                Eigen::Affine3f(cloud->sensor_orientation_);
-  float noise_level = 0.0f, minimum_range = 0.0f;
-  RangeImagePlanar range_image;
-  range_image.createFromPointCloudWithFixedSize(*cloud, image_size_x, image_size_y, center_x, center_y,
-                                                focal_length_x, focal_length_x, sensor_pose,
-                                                RangeImage::CAMERA_FRAME, noise_level, minimum_range);
-  PointCloud<int>::Ptr keypoints(new PointCloud<int>);
-  RangeImageBorderExtractor border_extractor;
-  NarfKeypoint detector(&border_extractor);
-  detector.setRangeImage(&range_image);
-  detector.getParameters().support_size = 0.2f;
-  detector.compute(*keypoints);
-  PointCloudRGB::Ptr cloud_keypoints(new PointCloudRGB);
-  for (size_t i = 0; i < keypoints->points.size(); ++i)
-    if ((size_t)keypoints->points[i] < cloud->size())  // keypoints.h:229 indexes the cloud by pixel index
-      cloud_keypoints->points.push_back(cloud->points[keypoints->points[i]]);
+  PointCloud<int>::Ptr keypoints;
+  PointCloudRGB::Ptr cloud_keypoints = narf_keypoints(cloud, keypoints);
   dump(out + "/keypoints.i32", keypoints->points.data(), keypoints->points.size());
 
   // ---- evaluation.cpp:593-612 (FPFH, r 0.08, normals r 0.05) ----
@@ -145,5 +208,30 @@ int main(int argc, char** argv) {
   dump(out + "/shot_rf.f32", rf.data(), rf.size());
   std::printf("points %zu keypoints %zu fpfh %zu shot %zu\n", cloud->size(), keypoints->size(), fdesc->size(),
               sdesc->size());
+
+  // ---- evaluation.cpp:342 (feat.findCorrespondences) between this cloud and a target ----
+  if (argc > 3) {
+    PointCloudRGB::Ptr target(new PointCloudRGB);
+    if (!read_pcd(argv[3], *target)) {
+      std::fprintf(stderr, "cannot read %s\n", argv[3]);
+      return 2;
+    }
+    PointCloud<int>::Ptr tkp;
+    PointCloudRGB::Ptr target_keypoints = narf_keypoints(target, tkp);
+    PointCloud<FPFHSignature33>::Ptr tdesc(new PointCloud<FPFHSignature33>);
+    Feature<PointRGB, FPFHSignature33>::Ptr tfpfh(new FPFHEstimation<PointRGB, Normal, FPFHSignature33>);
+    features_compute<FPFHSignature33>(tfpfh, 0.08, 0.05, target, target_keypoints, tdesc);
+    dump(out + "/fpfh_target.f32", reinterpret_cast<const float*>(tdesc->points.data()), tdesc->size() * 33);
+    CorrespondencesPtr corr(new Correspondences);
+    Features<FPFHSignature33> feat;
+    feat.findCorrespondences(fdesc, tdesc, corr);
+    std::vector<int32_t> pairs;
+    for (const Correspondence& c : *corr) {
+      pairs.push_back(c.index_query);
+      pairs.push_back(c.index_match);
+    }
+    dump(out + "/corr.i32", pairs.data(), pairs.size());
+    std::printf("target keypoints %zu correspondences %zu\n", tdesc->size(), corr->size());
+  }
   return 0;
 }

@@ -12,12 +12,13 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SRC = os.path.join(ROOT, "tests", "cpp", "facade_driver.cpp")
 EXE = os.path.join(ROOT, "tests", "cpp", "build", "facade_driver")
 PCD = os.path.join(ROOT, "tests", "golden", "clouds", "indoor_source.pcd")
+PCD_T = os.path.join(ROOT, "tests", "golden", "clouds", "indoor_target.pcd")
 
 
 def build_driver():
     os.makedirs(os.path.dirname(EXE), exist_ok=True)
     lib = os.path.join(ROOT, "pcl_feature_extraction_amd")
-    cmd = ["g++", "-std=c++14", "-O2", "-Wall", "-Wextra", "-Werror", "-I", os.path.join(ROOT, "include"), SRC,
+    cmd = ["g++", "-std=c++14", "-O2", "-Wall", "-Wextra", "-Werror", "-pthread", "-I", os.path.join(ROOT, "include"), SRC,
            "-L", lib, "-lpfx", f"-Wl,-rpath,{lib}", "-o", EXE]
     subprocess.run(cmd, check=True, capture_output=True, text=True)
     return EXE
@@ -32,7 +33,7 @@ def test_facade_compiles_and_links():
 def test_facade_matches_c_abi(ctx, tmp_path):
     from pcl_feature_extraction_amd.pcd import read_pcd
     exe = build_driver()
-    r = subprocess.run([exe, PCD, str(tmp_path)], capture_output=True, text=True, timeout=300)
+    r = subprocess.run([exe, PCD, str(tmp_path), PCD_T], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr
     c = read_pcd(PCD)
     x, y, z = c.x, c.y, c.z
@@ -53,3 +54,12 @@ def test_facade_matches_c_abi(ctx, tmp_path):
     wd, _ = ctx.shot(x, y, z, want[0], want[1], want[2], x[rows], y[rows], z[rows], 0.08)
     assert sd.shape == wd.shape
     assert np.array_equal(np.nan_to_num(sd, nan=-1.0).view(np.uint32), np.nan_to_num(wd, nan=-1.0).view(np.uint32))
+
+    # features.h:224-273 run verbatim against the facade (two threads, KdTreeFLANN<FPFHSignature33>)
+    tf = np.fromfile(tmp_path / "fpfh_target.f32", np.float32).reshape(-1, 33)
+    corr = np.fromfile(tmp_path / "corr.i32", np.int32).reshape(-1, 2)
+    q, m = ctx.correspondences(fp, tf)
+    assert np.array_equal(corr[:, 0], q) and np.array_equal(corr[:, 1], m)
+    import oracle_lib as O
+    oq, om = O.correspondences(fp, tf)
+    assert np.array_equal(q, oq) and np.array_equal(m, om) and len(q) > 0

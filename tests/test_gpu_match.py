@@ -93,3 +93,13 @@ def test_match_real_fpfh_descriptors(ctx):
         q = np.arange(0, len(x), 53)
         desc.append(O.fpfh(x, y, z, nx, ny, nz, x[q], y[q], z[q], 0.08))
     _check(ctx, desc[0], desc[1])
+
+
+def test_nearest_host_api(ctx):
+    """pfx_nearest_descriptors (host pointers, one direction: what the facade's
+    KdTreeFLANN<FeatureT>::nearestKSearch calls)."""
+    src, tgt = pair("fpfh", 700, 900, seed=5)
+    src[3, 4] = np.nan
+    idx, dist = ctx.nearest_descriptors(src, tgt)
+    oi, od = O.nearest_descriptor(src, tgt)
+    assert np.array_equal(idx, oi) and _same(dist, od)
