@@ -30,6 +30,7 @@
  *   pfx_nearest_descriptors_dev <- Features<T>::getCorrespondences (features.h:255-273):
  *                          KdTreeFLANN<FeatureT>::nearestKSearch(k = 1) per descriptor
  *   pfx_correspondences* <- Features<T>::findCorrespondences (features.h:224-253)
+ *   pfx_pcd_*           <- pcl::io::loadPCDFile<PointXYZRGB> (evaluation.cpp:226-235)
  * ===================================================================================== */
 #ifndef PFX_H_
 #define PFX_H_
@@ -226,6 +227,26 @@ pfx_status pfx_correspondences_dev(pfx_ctx* ctx, const float* d_src, int64_t n_s
 pfx_status pfx_correspondences(pfx_ctx* ctx, const float* src, int64_t n_src, int64_t src_stride,
                                const float* tgt, int64_t n_tgt, int64_t tgt_stride, int32_t dim,
                                int32_t* query, int32_t* match, int64_t cap, int64_t* n_out);
+
+/* ---- PCD v0.7 input ------------------------------------------------- */
+typedef struct pfx_pcd_header {
+  int64_t points;          /* POINTS (default WIDTH * HEIGHT)                                  */
+  int32_t width, height;
+  int32_t data;            /* 0 ascii, 1 binary, 2 binary_compressed                            */
+  int32_t point_size;      /* binary: bytes per point; ascii: columns per point                 */
+  int32_t x_offset, y_offset, z_offset; /* binary: byte offsets; ascii: column indices          */
+  int32_t nfields;
+  float viewpoint[7];      /* VIEWPOINT tx ty tz qw qx qy qz (sensor_origin_, sensor_orientation_) */
+  int64_t data_offset;     /* byte offset of the data block                                     */
+} pfx_pcd_header;
+/* Header only (host, no device, no context).  x, y, z must be single float32 fields. */
+pfx_status pfx_pcd_read_header(const char* path, pfx_pcd_header* out);
+/* loadPCDFile: x, y, z of every point into device SoA arrays (caller order = file order, NaN
+ * points kept as in PCL's non-dense clouds).  *n_out = POINTS; PFX_ERR_CAPACITY (nothing
+ * written) when it exceeds cap.  hdr (nullable) receives the header (viewpoint = the cloud's
+ * sensor pose, which NARF's range image uses: keypoints.h:207-210). */
+pfx_status pfx_pcd_load_xyz_dev(pfx_ctx* ctx, const char* path, float* d_x, float* d_y, float* d_z,
+                                int64_t cap, int64_t* n_out, pfx_pcd_header* hdr);
 
 #ifdef __cplusplus
 } /* extern "C" */

@@ -57,6 +57,15 @@ class Camera(ctypes.Structure):
     ]
 
 
+class PcdHeader(ctypes.Structure):
+    _fields_ = [
+        ("points", ctypes.c_int64), ("width", ctypes.c_int32), ("height", ctypes.c_int32),
+        ("data", ctypes.c_int32), ("point_size", ctypes.c_int32),
+        ("x_offset", ctypes.c_int32), ("y_offset", ctypes.c_int32), ("z_offset", ctypes.c_int32),
+        ("nfields", ctypes.c_int32), ("viewpoint", ctypes.c_float * 7), ("data_offset", ctypes.c_int64),
+    ]
+
+
 # name -> (restype, argtypes)
 _SIGS = {
     "pfx_narf_params_default": (None, [ctypes.POINTER(NarfParams)]),
@@ -98,6 +107,9 @@ _SIGS = {
                                       c_i64p]),
     "pfx_nearest_descriptors_dev": (c_int, [c_vp, c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, ctypes.c_int32,
                                             c_vp, c_vp, c_vp, c_vp]),
+    "pfx_pcd_read_header": (c_int, [ctypes.c_char_p, ctypes.POINTER(PcdHeader)]),
+    "pfx_pcd_load_xyz_dev": (c_int, [c_vp, ctypes.c_char_p, c_vp, c_vp, c_vp, c_i64, c_i64p,
+                                     ctypes.POINTER(PcdHeader)]),
     "pfx_nearest_descriptors": (c_int, [c_vp, c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, ctypes.c_int32, c_vp, c_vp]),
     "pfx_correspondences_dev": (c_int, [c_vp, c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, ctypes.c_int32,
                                         c_vp, c_vp, c_i64, c_i64p]),

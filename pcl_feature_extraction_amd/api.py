@@ -33,6 +33,15 @@ def narf_params(support_size=0.2, **kw) -> N.NarfParams:
     return p
 
 
+def pcd_header(path) -> N.PcdHeader:
+    """PCD header through the C-ABI (host only: no device needed)."""
+    h = N.PcdHeader()
+    st = N.lib().pfx_pcd_read_header(str(path).encode(), ctypes.byref(h))
+    if st != 0:
+        raise N.PfxError(st, f"pfx_pcd_read_header({path})")
+    return h
+
+
 def camera(**kw) -> N.Camera:
     c = N.Camera()
     N.lib().pfx_camera_default(ctypes.byref(c))
@@ -225,6 +234,16 @@ class Context:
         self._check(self._lib.pfx_gather_points_dev(self.h, _ptr(x), _ptr(y), _ptr(z), x.numel(), _ptr(idx),
                                                     len(idx), _ptr(kx), _ptr(ky), _ptr(kz), ctypes.byref(nout)))
         return nout.value
+
+    # ---- PCD input: pcl::io::loadPCDFile<PointXYZRGB> (evaluation.cpp:226-235) -------------
+    def pcd_load_xyz_dev(self, path, x, y, z):
+        """x, y, z (float32 device tensors of >= POINTS elements) <- the file's points; returns
+        (n, header)."""
+        n = ctypes.c_int64()
+        h = N.PcdHeader()
+        self._check(self._lib.pfx_pcd_load_xyz_dev(self.h, str(path).encode(), _ptr(x), _ptr(y), _ptr(z), x.numel(),
+                                                   ctypes.byref(n), ctypes.byref(h)))
+        return n.value, h
 
     # ---- descriptor matching: Features<T>::findCorrespondences / getCorrespondences ----------
     def correspondences(self, src, tgt):

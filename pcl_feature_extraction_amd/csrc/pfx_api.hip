@@ -546,3 +546,25 @@ extern "C" pfx_status pfx_correspondences(pfx_ctx* ctx, const float* src, int64_
   PFX_HIP(hipStreamSynchronize(ctx->stream));
   PFX_API_END(ctx)
 }
+
+extern "C" pfx_status pfx_pcd_read_header(const char* path, pfx_pcd_header* out) {
+  if (!path || !out) return PFX_ERR_INVALID;
+  std::string err;
+  try {
+    return pfx::pcd_read_header(path, out, err);
+  } catch (...) {
+    return PFX_ERR_INVALID;
+  }
+}
+
+extern "C" pfx_status pfx_pcd_load_xyz_dev(pfx_ctx* ctx, const char* path, float* d_x, float* d_y, float* d_z,
+                                           int64_t cap, int64_t* n_out, pfx_pcd_header* hdr) {
+  PFX_API_BEGIN
+  check_ctx(ctx);
+  if (!path || !n_out || cap < 0 || (cap && (!d_x || !d_y || !d_z)))
+    throw Error(PFX_ERR_INVALID, "pcd load: invalid arguments");
+  const int64_t n = pfx::pcd_load_xyz_dev(ctx, path, d_x, d_y, d_z, cap, hdr);
+  *n_out = n;
+  if (n > cap) throw Error(PFX_ERR_CAPACITY, "pcd load: " + std::to_string(n) + " points > cap");
+  PFX_API_END(ctx)
+}

@@ -151,10 +151,16 @@ __device__ __forceinline__ float atan_poly(float a) {
   return p * a;
 }
 
-__device__ __forceinline__ bool bin_fast(double vd, double tol, int& h) {
-  const double m = floor(vd);
-  const double fr = vd - m;
-  if (!(fr > tol && fr < 1.0 - tol)) return false;  // also rejects NaN
+// float evaluation of the bin maps for the fast path: the exact maps are evaluated in double;
+// the float forms below differ from them by at most 2.1e-6 bin units (f1: pi rounding + the sum
+// and product roundings, x 11/(2 pi); f2/f3: two roundings, x 5.5), so kBinMapSlack is added
+// to each feature's tolerance -- no double-precision work per pair.
+constexpr float kBinMapSlack = 3e-6f;
+
+__device__ __forceinline__ bool bin_fast_f(float v, float tol, int& h) {
+  const float m = floorf(v);
+  const float fr = v - m;  // exact (|v| < 2^23)
+  if (!(fr > tol && fr < 1.0f - tol)) return false;  // also rejects NaN
   const int b = (int)m;
   h = b < 0 ? 0 : (b >= kBins ? kBins - 1 : b);
   return true;
@@ -205,11 +211,11 @@ __device__ __forceinline__ bool pair_bins_fast(f3 p1, f3 n1, f3 p2, f3 n2, int& 
   if (ay > ax) t = 1.57079637f - t;
   if (x < 0.0f) t = 3.14159274f - t;
   const float f1a = y < 0.0f ? -t : t;
-  const double d_pi = (double)(1.0f / (2.0f * 3.14159265358979323846f));
-  const double tol1 = (1e-6 + 8e-6 / (double)mx) * (double)kBins * d_pi;
-  return bin_fast(f1_scaled((double)f1a), tol1, h1) &&
-         bin_fast((double)kBins * (((double)f2a + 1.0) * 0.5), 4e-6 * 0.5 * kBins, h2) &&
-         bin_fast((double)kBins * (((double)f3a + 1.0) * 0.5), 1e-6 * 0.5 * kBins, h3);
+  const float d_pi = 1.0f / (2.0f * 3.14159265358979323846f);
+  const float tol1 = (1e-6f + 8e-6f * __builtin_amdgcn_rcpf(mx)) * (1.01f * (float)kBins * d_pi) + kBinMapSlack;
+  return bin_fast_f((f1a + 3.14159265358979323846f) * ((float)kBins * d_pi), tol1, h1) &&
+         bin_fast_f((f2a + 1.0f) * (0.5f * kBins), 4e-6f * 0.5f * kBins + kBinMapSlack, h2) &&
+         bin_fast_f((f3a + 1.0f) * (0.5f * kBins), 1e-6f * 0.5f * kBins + kBinMapSlack, h3);
 }
 
 // the exact path out of line (rare), bins packed h1 | h2 << 8 | h3 << 16
@@ -322,12 +328,15 @@ __global__ void __launch_bounds__(256) k_fpfh_spfh(GridView g, const float4* __r
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
       __builtin_amdgcn_wave_barrier();
     };
-    for (int32_t t0 = 0; t0 < R.pref[9]; t0 += 64) {
+    // candidates run by run (contiguous positions: no per-candidate run lookup)
+#pragma unroll
+    for (int r = 0; r < 9; ++r) {
+      const int32_t rs = R.start[r], rn = R.pref[r + 1] - R.pref[r];
+    for (int32_t t0 = 0; t0 < rn; t0 += 64) {
       const int32_t t = t0 + lane;
       bool hit = false;
-      int32_t pos = 0;
-      if (t < R.pref[9]) {
-        pos = run_pos(R, t);
+      const int32_t pos = rs + t;
+      if (t < rn) {
         const float4 c = g.sp[pos];
         hit = flann_d2(pc.x, pc.y, pc.z, c.x, c.y, c.z) < rr;
       }
@@ -344,6 +353,7 @@ __global__ void __launch_bounds__(256) k_fpfh_spfh(GridView g, const float4* __r
         if (lane + 64 < qn) queue[wv][lane] = rest;
         qn -= 64;
       }
+    }
     }
     process(qn);
     if (lane < kDesc) {

@@ -184,6 +184,9 @@ int64_t narf_dev(pfx_ctx* ctx, const float* x, const float* y, const float* z, i
                  const pfx_camera& cam, const pfx_narf_params& p, std::vector<int32_t>& out);
 void narf_debug(pfx_ctx* ctx, const std::string& which, void* out, int64_t count);
 void narf_release(pfx_ctx* ctx);
+pfx_status pcd_read_header(const char* path, pfx_pcd_header* out, std::string& err);
+int64_t pcd_load_xyz_dev(pfx_ctx* ctx, const char* path, float* d_x, float* d_y, float* d_z, int64_t cap,
+                         pfx_pcd_header* hdr_out);
 void match_nearest_dev(pfx_ctx* ctx, const float* src, int64_t ns, int64_t ss, const float* tgt, int64_t nt,
                        int64_t ts, int D, int32_t* s2t, float* ds2t, int32_t* t2s, float* dt2s);
 int64_t correspondences_dev(pfx_ctx* ctx, const float* src, int64_t ns, int64_t ss, const float* tgt, int64_t nt,

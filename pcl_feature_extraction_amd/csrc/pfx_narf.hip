@@ -832,29 +832,44 @@ __global__ void __launch_bounds__(64) k_interest_ff(Img I, const float4* __restr
       if (lane == 0) fallback[atomicAdd(n_fallback, 1)] = index;
       continue;
     }
-    // acceptance / contribution masks, one row per iteration (lanes = columns)
+    // acceptance / contribution masks (lanes = columns); four rows per iteration so that their
+    // loads are in flight together (the window rows are independent)
     Rows2 A, C;
-    for (int r = 0; r < wh; ++r) {
-      const int yy = y0 + r;
-      const bool mine = lane == (r & 63), hi = r >= 64;
+    for (int r0 = 0; r0 < wh; r0 += 4) {
       for (int wd = 0; wd * 64 < ww; ++wd) {
         const int c = wd * 64 + lane;
-        bool acc = false, con = false;
-        if (c < ww) {
-          const int idx2 = yy * I.w + x0 + c;
-          const float4 p2 = P[idx2];
-          acc = isfinite(p2.w) && !(traits[idx2] & skip);
-          const float pd = (float)max(abs(x0 + c - x), abs(yy - y));
-          const float d2 = sq_dist(point, p2);
-          if (acc && pd > 2.0f && d2 > ip.radius_squared) acc = false;
-          con = acc && scs[idx2] >= ip.min_scs;
+        const bool col = c < ww;
+        float4 p2[4];
+        uint32_t tr[4];
+        float sv[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int rr = r0 + u < wh ? r0 + u : wh - 1;  // clamped: rows past the window are ignored
+          const int idx2 = (y0 + rr) * I.w + x0 + (col ? c : 0);
+          p2[u] = P[idx2];
+          tr[u] = traits[idx2];
+          sv[u] = scs[idx2];
         }
-        const uint64_t ma = __ballot(acc), mc = __ballot(con);
-        if (mine) {
-          if (!hi && wd == 0) { A.m00 = ma; C.m00 = mc; }
-          if (!hi && wd == 1) { A.m01 = ma; C.m01 = mc; }
-          if (hi && wd == 0) { A.m10 = ma; C.m10 = mc; }
-          if (hi && wd == 1) { A.m11 = ma; C.m11 = mc; }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int r = r0 + u;
+          if (r >= wh) break;  // wave-uniform
+          bool acc = false, con = false;
+          if (col) {
+            acc = isfinite(p2[u].w) && !(tr[u] & skip);
+            const float pd = (float)max(abs(x0 + c - x), abs(y0 + r - y));
+            const float d2 = sq_dist(point, p2[u]);
+            if (acc && pd > 2.0f && d2 > ip.radius_squared) acc = false;
+            con = acc && sv[u] >= ip.min_scs;
+          }
+          const uint64_t ma = __ballot(acc), mc = __ballot(con);
+          const bool mine = lane == (r & 63), hi = r >= 64;
+          if (mine) {
+            if (!hi && wd == 0) { A.m00 = ma; C.m00 = mc; }
+            if (!hi && wd == 1) { A.m01 = ma; C.m01 = mc; }
+            if (hi && wd == 0) { A.m10 = ma; C.m10 = mc; }
+            if (hi && wd == 1) { A.m11 = ma; C.m11 = mc; }
+          }
         }
       }
     }
@@ -912,19 +927,37 @@ __global__ void __launch_bounds__(64) k_interest_ff(Img I, const float4* __restr
       const uint64_t M0 = half ? (R.m10 & C.m10) : (R.m00 & C.m00);
       const uint64_t M1 = half ? (R.m11 & C.m11) : (R.m01 & C.m01);
       uint64_t rows = __ballot((M0 | M1) != 0);
-      while (rows) {
-        const int r = __builtin_ctzll(rows);
-        rows &= rows - 1;
-        const uint64_t m0 = __shfl(M0, r), m1 = __shfl(M1, r);
-        for (int wd = 0; wd < 2; ++wd) {
-          const uint64_t m = wd ? m1 : m0;
-          if (!((m >> lane) & 1ull)) continue;
-          const int xx = x0 + wd * 64 + lane, yy = y0 + 64 * half + r;
-          const int idx2 = yy * I.w + xx;
-          const float4 p2 = P[idx2];
-          const float pd = (float)max(abs(xx - x), abs(yy - y));
-          contribute(ip, scs[idx2], scd[idx2], sq_dist(point, p2), pd, tmp0, tmp1, tmp2, hist, &neg_bits);
+      while (rows) {  // up to four rows per iteration: their loads in flight together
+        int rr[4];
+        uint64_t mm[4][2];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          rr[u] = rows ? __builtin_ctzll(rows) : -1;
+          if (rows) rows &= rows - 1;
+          mm[u][0] = rr[u] >= 0 ? __shfl(M0, rr[u]) : 0ull;
+          mm[u][1] = rr[u] >= 0 ? __shfl(M1, rr[u]) : 0ull;
         }
+        float4 p2[4][2], dv[4][2];
+        float sv[4][2];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+          for (int wd = 0; wd < 2; ++wd) {
+            const bool on = (mm[u][wd] >> lane) & 1ull;
+            const int idx2 = on ? (y0 + 64 * half + rr[u]) * I.w + x0 + wd * 64 + lane : 0;
+            p2[u][wd] = on ? P[idx2] : make_float4(0.f, 0.f, 0.f, 0.f);
+            sv[u][wd] = on ? scs[idx2] : 0.f;
+            dv[u][wd] = on ? scd[idx2] : make_float4(0.f, 0.f, 0.f, 0.f);
+          }
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+          for (int wd = 0; wd < 2; ++wd) {
+            if (!((mm[u][wd] >> lane) & 1ull)) continue;
+            const int xx = x0 + wd * 64 + lane, yy = y0 + 64 * half + rr[u];
+            const float pd = (float)max(abs(xx - x), abs(yy - y));
+            contribute(ip, sv[u][wd], dv[u][wd], sq_dist(point, p2[u][wd]), pd, tmp0, tmp1, tmp2, hist, &neg_bits);
+          }
       }
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");

@@ -16,6 +16,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
+#include <mutex>
 
 #include "pfx_nblist.h"
 #include "pfx_neighbors.h"
@@ -540,12 +541,13 @@ void normals_chains_dev(pfx_ctx* ctx, pfx_ctx* owner, const uint8_t* mask, int w
     k_normals_chain<<<(unsigned)nb, 256, 0, st>>>(view(G), L, vp[0], vp[1], vp[2], nx, ny, nz, curv, longq, n_long,
                                                   n_long + 1, deferq, mask, want);
     check_launch("k_normals_chain");
-    static bool attr = false;
-    if (!attr) {
-      PFX_HIP(hipFuncSetAttribute((const void*)k_normals_chain_big, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)sizeof(ChainLds<kStageBig>)));
-      attr = true;
-    }
+    static std::once_flag attr;  // contexts may run on several host threads
+    hipError_t attr_err = hipSuccess;
+    std::call_once(attr, [&] {
+      attr_err = hipFuncSetAttribute((const void*)k_normals_chain_big, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     (int)sizeof(ChainLds<kStageBig>));
+    });
+    PFX_HIP(attr_err);
     TimeScope tb(ctx, "normals_chain_big");
     k_normals_chain_big<<<256, 256, sizeof(ChainLds<kStageBig>), st>>>(view(G), L, vp[0], vp[1], vp[2], nx, ny, nz,
                                                                          curv, longq, n_long, n_long + 1, deferq,

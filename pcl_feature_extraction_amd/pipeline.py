@@ -63,11 +63,11 @@ class OverlappedNarfFpfh:
     The exact support set (r-neighbours of the r-neighbourhoods of the keypoints) costs ~1 ms to
     mark and holds most of the long neighbour lists, so the step got slower: 11.0 vs 9.5 ms.)"""
 
-    def __init__(self, torch, ctx_main: Context, ctx_side: Context, device):
+    def __init__(self, torch, ctx_main: Context, ctx_side: Context, device, main_stream=None):
         from concurrent.futures import ThreadPoolExecutor
         self.torch = torch
         self.ctx, self.ctx_side = ctx_main, ctx_side
-        self.s_main = torch.cuda.current_stream(device)
+        self.s_main = main_stream if main_stream is not None else torch.cuda.current_stream(device)
         self.s_side = torch.cuda.Stream(device)
         ctx_main.set_stream(self.s_main.cuda_stream)
         ctx_side.set_stream(self.s_side.cuda_stream)
