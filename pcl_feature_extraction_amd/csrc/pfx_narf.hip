@@ -19,6 +19,8 @@
 #include <cstring>
 
 #include "pfx_device_math.h"
+#include <cstdio>
+
 #include "pfx_internal.h"
 
 namespace pfx {
@@ -34,13 +36,13 @@ enum {
 struct NarfState {
   int w = 0, h = 0;
   DevBuf direct, fill, pts, surf, svalid, sL, sR, sT, sB, uL, uR, uT, uB, shadow, traits, rawdir, dir, scs, scd,
-      interest, cand, counters, sat, work, fb1;
+      interest, cand, counters, rowp, sat, work, fb1;
   std::vector<float> h_interest, h_scs, h_range;
   std::vector<uint32_t> h_traits;
   bool have_debug = false;
   void release() {
     DevBuf* all[] = {&direct, &fill, &pts, &surf, &svalid, &sL, &sR, &sT, &sB, &uL, &uR, &uT, &uB, &shadow,
-                     &traits, &rawdir, &dir, &scs, &scd, &interest, &cand, &counters, &sat, &work, &fb1};
+                     &traits, &rawdir, &dir, &scs, &scd, &interest, &cand, &counters, &rowp, &sat, &work, &fb1};
     for (auto* b : all) b->release();
   }
 };
@@ -566,15 +568,26 @@ __global__ void k_contrib_rows(Img I, const float4* __restrict__ P, const uint32
   if (tid == 0) rowp[y * (I.w + 1)] = 0;
 }
 
-// wave-uniform: does the window hold a contributing pixel?
-__device__ __forceinline__ bool window_contributes(const Img& I, const int* __restrict__ rowp, int x0, int y0,
-                                                   int ww, int wh, int lane) {
-  bool any = false;
-  for (int r = lane; r < wh; r += 64) {
-    const int* row = rowp + (y0 + r) * (I.w + 1);
-    any |= row[x0 + ww] != row[x0];
+// Summed-area table of the contributing pixels: sat[y][x] = count in rows [0, y) x columns
+// [0, x), (h + 1) x (w + 1) ints, from the row prefixes (one thread per column).
+__global__ void k_contrib_sat(Img I, const int* __restrict__ rowp, int* __restrict__ sat) {
+  const int x = blockIdx.x * blockDim.x + threadIdx.x;
+  if (x > I.w) return;
+  int acc = 0;
+  sat[x] = 0;
+  for (int y = 0; y < I.h; ++y) {
+    acc += rowp[y * (I.w + 1) + x];
+    sat[(y + 1) * (I.w + 1) + x] = acc;
   }
-  return __ballot(any) != 0;
+}
+
+// does the window hold a contributing pixel?  (four table reads, the same in every lane)
+__device__ __forceinline__ bool window_contributes(const Img& I, const int* __restrict__ sat, int x0, int y0,
+                                                   int ww, int wh, int lane) {
+  (void)lane;
+  const int W = I.w + 1;
+  const int c = sat[(y0 + wh) * W + x0 + ww] - sat[y0 * W + x0 + ww] - sat[(y0 + wh) * W + x0] + sat[y0 * W + x0];
+  return c != 0;
 }
 
 // histogram cell of the direction angle: 0.5 * normAngle(2 acos(dvx)) (NarfKeypoint,
@@ -802,6 +815,15 @@ __device__ __forceinline__ void hdil(uint64_t lo, uint64_t hi, uint64_t& dlo, ui
   dhi = hi | (hi << 1) | (hi >> 1) | (lo >> 63);
 }
 
+#ifdef PFX_SHOT_PROFILE
+__device__ unsigned long long g_ff_prof[8];  // cycles: window test, masks, flood fill, contributions
+#define FF_T(v) const long long v = clock64()
+#define FF_ADD(i, a, b) if (lane == 0) atomicAdd(&g_ff_prof[i], (unsigned long long)((b) - (a)))
+#else
+#define FF_T(v)
+#define FF_ADD(i, a, b)
+#endif
+
 __global__ void __launch_bounds__(64) k_interest_ff(Img I, const float4* __restrict__ P,
                                                     const uint32_t* __restrict__ traits,
                                                     const float* __restrict__ scs, const float4* __restrict__ scd,
@@ -823,8 +845,12 @@ __global__ void __launch_bounds__(64) k_interest_ff(Img I, const float4* __restr
     }
     const int y = index / I.w, x = index - y * I.w;
     int x0, y0, ww, wh;
+    FF_T(q0);
     interest_window(I, point, x, y, ip.R, x0, y0, ww, wh);
-    if (!window_contributes(I, rowp, x0, y0, ww, wh, lane)) {  // nothing can contribute: interest 0
+    const bool contributes = window_contributes(I, rowp, x0, y0, ww, wh, lane);
+    FF_T(q1);
+    FF_ADD(0, q0, q1);
+    if (!contributes) {  // nothing can contribute: interest 0
       if (lane == 0) interest[index] = 0.0f;
       continue;
     }
@@ -873,6 +899,8 @@ __global__ void __launch_bounds__(64) k_interest_ff(Img I, const float4* __restr
         }
       }
     }
+    FF_T(q2);
+    FF_ADD(1, q1, q2);
     // 8-connected component of p in A
     Rows2 R;
     {
@@ -915,6 +943,8 @@ __global__ void __launch_bounds__(64) k_interest_ff(Img I, const float4* __restr
       if (x0 + ww < I.w) edge |= (((R.m00 | R.m10) & last0) | ((R.m01 | R.m11) & last1)) != 0;
       if (__ballot(edge) && lane == 0) atomicOr(err, 2);
     }
+    FF_T(q3);
+    FF_ADD(2, q2, q3);
     // contributions of the accepted contributing pixels
     f3 tmp0, tmp1, tmp2;
     viewer_frame(I, point, tmp0, tmp1, tmp2);
@@ -962,6 +992,8 @@ __global__ void __launch_bounds__(64) k_interest_ff(Img I, const float4* __restr
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
+    FF_T(q4);
+    FF_ADD(3, q3, q4);
     const int accepted = __popcll(R.m00) + __popcll(R.m01) + __popcll(R.m10) + __popcll(R.m11);
     int tot = accepted;
 #pragma unroll
@@ -1152,7 +1184,8 @@ int64_t narf_dev(pfx_ctx* ctx, const float* x, const float* y, const float* z, i
   ip.d180 = 180.0f * deg;
   ip.R = search_radius;
   PFX_HIP(hipMemsetAsync(counters, 0, 4 * sizeof(int), st));
-  int* sat = S.sat.as<int>((I.w + 1) * I.h);
+  int* rowp = S.rowp.as<int>((I.w + 1) * I.h);
+  int* sat = S.sat.as<int>((I.w + 1) * (I.h + 1));
   unsigned long long* work = S.work.as<unsigned long long>(4);
   PFX_HIP(hipMemsetAsync(work, 0, 4 * sizeof(unsigned long long), st));
   {
@@ -1163,7 +1196,8 @@ int64_t narf_dev(pfx_ctx* ctx, const float* x, const float* y, const float* z, i
     // changes no keypoint (NMS and selection only look at pixels >= min_interest_value).
     const float thr = p.calculate_sparse_interest_image
                           ? std::max(ip.min_scs, p.min_interest_value * 0.9999f) : ip.min_scs;
-    k_contrib_rows<<<I.h, 1024, 0, st>>>(I, P, traits, scs, thr, sat);
+    k_contrib_rows<<<I.h, 1024, 0, st>>>(I, P, traits, scs, thr, rowp);
+    k_contrib_sat<<<(unsigned)((I.w + 1 + 255) / 256), 256, 0, st>>>(I, rowp, sat);
     int* fb1 = S.fb1.as<int>(npx);
     k_interest_ff<<<256 * 16, 64, 0, st>>>(I, P, traits, scs, scd, sat, ip, interest, fb1, counters + 3,
                                             counters + 1, work);
@@ -1188,6 +1222,17 @@ int64_t narf_dev(pfx_ctx* ctx, const float* x, const float* y, const float* z, i
     k_nms<<<nblk(npx), 256, 0, st>>>(I, interest, p.min_interest_value, p.do_non_maximum_suppression, cand, counters);
     check_launch("k_nms");
   }
+#ifdef PFX_SHOT_PROFILE
+  {
+    unsigned long long pr[8];
+    PFX_HIP(hipStreamSynchronize(st));
+    PFX_HIP(hipMemcpyFromSymbol(pr, HIP_SYMBOL(g_ff_prof), sizeof(pr)));
+    fprintf(stderr, "narf ff cycles (summed over pixels): window test %llu masks %llu flood %llu contrib %llu\n", pr[0],
+            pr[1], pr[2], pr[3]);
+    const unsigned long long z[8] = {};
+    PFX_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_ff_prof), z, sizeof(z)));
+  }
+#endif
   int h_cnt[4];
   unsigned long long h_work[4];
   PFX_HIP(hipMemcpyAsync(h_cnt, counters, sizeof(h_cnt), hipMemcpyDeviceToHost, st));
