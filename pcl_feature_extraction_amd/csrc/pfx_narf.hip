@@ -36,13 +36,13 @@ enum {
 struct NarfState {
   int w = 0, h = 0;
   DevBuf direct, fill, pts, surf, svalid, sL, sR, sT, sB, uL, uR, uT, uB, shadow, traits, rawdir, dir, scs, scd,
-      interest, cand, counters, rowp, sat, work, fb1;
+      interest, cand, counters, rowp, sat, work, fb1, pk;
   std::vector<float> h_interest, h_scs, h_range;
   std::vector<uint32_t> h_traits;
   bool have_debug = false;
   void release() {
     DevBuf* all[] = {&direct, &fill, &pts, &surf, &svalid, &sL, &sR, &sT, &sB, &uL, &uR, &uT, &uB, &shadow,
-                     &traits, &rawdir, &dir, &scs, &scd, &interest, &cand, &counters, &rowp, &sat, &work, &fb1};
+                     &traits, &rawdir, &dir, &scs, &scd, &interest, &cand, &counters, &rowp, &sat, &work, &fb1, &pk};
     for (auto* b : all) b->release();
   }
 };
@@ -568,6 +568,18 @@ __global__ void k_contrib_rows(Img I, const float4* __restrict__ P, const uint32
   if (tid == 0) rowp[y * (I.w + 1)] = 0;
 }
 
+// Packed pixel for the flood-fill masks: (x, y, z, flags) with flags in the bits of w --
+// bit 0: valid and not shadow / veil (the grow may accept it), bit 1: scs >= min_scs.
+__global__ void k_pack_px(Img I, const float4* __restrict__ P, const uint32_t* __restrict__ traits,
+                          const float* __restrict__ scs, float min_scs, float4* __restrict__ pk) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= I.w * I.h) return;
+  const uint32_t skip = TB(T_SHADOW_BORDER) | TB(T_VEIL_POINT);
+  const float4 p = P[i];
+  const uint32_t f = ((isfinite(p.w) && !(traits[i] & skip)) ? 1u : 0u) | (scs[i] >= min_scs ? 2u : 0u);
+  pk[i] = make_float4(p.x, p.y, p.z, __uint_as_float(f));
+}
+
 // Summed-area table of the contributing pixels: sat[y][x] = count in rows [0, y) x columns
 // [0, x), (h + 1) x (w + 1) ints, from the row prefixes (one thread per column).
 __global__ void k_contrib_sat(Img I, const int* __restrict__ rowp, int* __restrict__ sat) {
@@ -824,7 +836,8 @@ __device__ unsigned long long g_ff_prof[8];  // cycles: window test, masks, floo
 #define FF_ADD(i, a, b)
 #endif
 
-__global__ void __launch_bounds__(64) k_interest_ff(Img I, const float4* __restrict__ P,
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) k_interest_ff(Img I, const float4* __restrict__ P,
+                                                    const float4* __restrict__ PK,
                                                     const uint32_t* __restrict__ traits,
                                                     const float* __restrict__ scs, const float4* __restrict__ scd,
                                                     const int* __restrict__ rowp, InterestParams ip,
@@ -866,15 +879,10 @@ __global__ void __launch_bounds__(64) k_interest_ff(Img I, const float4* __restr
         const int c = wd * 64 + lane;
         const bool col = c < ww;
         float4 p2[4];
-        uint32_t tr[4];
-        float sv[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
           const int rr = r0 + u < wh ? r0 + u : wh - 1;  // clamped: rows past the window are ignored
-          const int idx2 = (y0 + rr) * I.w + x0 + (col ? c : 0);
-          p2[u] = P[idx2];
-          tr[u] = traits[idx2];
-          sv[u] = scs[idx2];
+          p2[u] = PK[(y0 + rr) * I.w + x0 + (col ? c : 0)];
         }
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
@@ -882,11 +890,12 @@ __global__ void __launch_bounds__(64) k_interest_ff(Img I, const float4* __restr
           if (r >= wh) break;  // wave-uniform
           bool acc = false, con = false;
           if (col) {
-            acc = isfinite(p2[u].w) && !(tr[u] & skip);
+            const uint32_t f = __float_as_uint(p2[u].w);
+            acc = f & 1u;
             const float pd = (float)max(abs(x0 + c - x), abs(y0 + r - y));
             const float d2 = sq_dist(point, p2[u]);
             if (acc && pd > 2.0f && d2 > ip.radius_squared) acc = false;
-            con = acc && sv[u] >= ip.min_scs;
+            con = acc && (f & 2u);
           }
           const uint64_t ma = __ballot(acc), mc = __ballot(con);
           const bool mine = lane == (r & 63), hi = r >= 64;
@@ -975,7 +984,7 @@ __global__ void __launch_bounds__(64) k_interest_ff(Img I, const float4* __restr
           for (int wd = 0; wd < 2; ++wd) {
             const bool on = (mm[u][wd] >> lane) & 1ull;
             const int idx2 = on ? (y0 + 64 * half + rr[u]) * I.w + x0 + wd * 64 + lane : 0;
-            p2[u][wd] = on ? P[idx2] : make_float4(0.f, 0.f, 0.f, 0.f);
+            p2[u][wd] = on ? PK[idx2] : make_float4(0.f, 0.f, 0.f, 0.f);
             sv[u][wd] = on ? scs[idx2] : 0.f;
             dv[u][wd] = on ? scd[idx2] : make_float4(0.f, 0.f, 0.f, 0.f);
           }
@@ -1199,7 +1208,9 @@ int64_t narf_dev(pfx_ctx* ctx, const float* x, const float* y, const float* z, i
     k_contrib_rows<<<I.h, 1024, 0, st>>>(I, P, traits, scs, thr, rowp);
     k_contrib_sat<<<(unsigned)((I.w + 1 + 255) / 256), 256, 0, st>>>(I, rowp, sat);
     int* fb1 = S.fb1.as<int>(npx);
-    k_interest_ff<<<256 * 16, 64, 0, st>>>(I, P, traits, scs, scd, sat, ip, interest, fb1, counters + 3,
+    float4* pk = S.pk.as<float4>(npx);
+    k_pack_px<<<nblk(npx), 256, 0, st>>>(I, P, traits, scs, ip.min_scs, pk);
+    k_interest_ff<<<256 * 16, 64, 0, st>>>(I, P, pk, traits, scs, scd, sat, ip, interest, fb1, counters + 3,
                                             counters + 1, work);
     check_launch("k_interest_ff");
     // windows beyond the flood-fill masks: queue-based grow in a windowed LDS bitmap
