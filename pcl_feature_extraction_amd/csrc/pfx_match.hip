@@ -6,7 +6,8 @@
 // over the D dimensions (oracle/or_match.cpp).  The 1-NN over all pairs is a dense contraction,
 // so it runs on the matrix cores, and exactness is restored afterwards:
 //
-//   1. prep:   every row -> validity (all finite), fp32 squared norm, and a bf16 split
+//   1. prep:   every row -> validity (all finite), fp32 squared norm, and a bf16 split (rows
+//              padded to Dp = 32-multiple dims)
 //              a = a_hi + a_lo + O(2^-16 |a|), packed as [a_hi | a_hi | a_lo] (source) and
 //              [b_hi | b_lo | b_hi] (target), so ONE bf16 MFMA product over K = 3 Dp gives
 //              a_hi.b_hi + a_hi.b_lo + a_lo.b_hi (error <= 3.1 2^-16 |a||b|).
@@ -118,20 +119,58 @@ __global__ void __launch_bounds__(256) k_match_tiles(Side A, Side B, int D, int 
     for (int b = 0; b < 2; ++b)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
-  const uint16_t* pa0 = A.P + (r0 + l32) * KP + 8 * h;
-  const uint16_t* pa1 = pa0 + (int64_t)32 * KP;
-  const uint16_t* pb0 = B.P + (q0 + l32) * KP + 8 * h;
-  const uint16_t* pb1 = pb0 + (int64_t)32 * KP;
-  for (int k0 = 0; k0 < KP; k0 += 16) {
-    const bf16x8 fa0 = *reinterpret_cast<const bf16x8*>(pa0 + k0);
-    const bf16x8 fa1 = *reinterpret_cast<const bf16x8*>(pa1 + k0);
-    const bf16x8 fb0 = *reinterpret_cast<const bf16x8*>(pb0 + k0);
-    const bf16x8 fb1 = *reinterpret_cast<const bf16x8*>(pb1 + k0);
-    acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa0, fb0, acc[0][0], 0, 0, 0);
-    acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa0, fb1, acc[0][1], 0, 0, 0);
-    acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa1, fb0, acc[1][0], 0, 0, 0);
-    acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa1, fb1, acc[1][1], 0, 0, 0);
+  // K in chunks of KC = 32 (two MFMA k-steps): the workgroup's 128 A rows and 128 B rows of a
+  // chunk are staged in LDS (double buffer; rows padded to 80 B so the 32 rows a fragment read
+  // touches spread over the banks) and the next chunk's global loads are in flight while the
+  // current one is multiplied -- every fragment is read from L2 once per workgroup instead of
+  // once per wave.
+  constexpr int KC = 32, RS = KC + 8;
+  __shared__ __attribute__((aligned(16))) uint16_t sa[2][kTile * RS];
+  __shared__ __attribute__((aligned(16))) uint16_t sb[2][kTile * RS];
+  const int tid = threadIdx.x;
+  const int64_t ra0 = (int64_t)blockIdx.y * kTile, qb0 = (int64_t)blockIdx.x * kTile;
+  uint4 va0, va1, vb0, vb1;
+  // 128 rows x 64 B per operand = 512 16-B pieces: thread t moves pieces t and t + 256
+  const int row0 = tid >> 2, row1 = (tid + 256) >> 2, part = tid & 3;
+#define PFX_MATCH_GLOAD(k0)                                                                       \
+  va0 = *reinterpret_cast<const uint4*>(A.P + (ra0 + row0) * KP + (k0) + part * 8);               \
+  va1 = *reinterpret_cast<const uint4*>(A.P + (ra0 + row1) * KP + (k0) + part * 8);               \
+  vb0 = *reinterpret_cast<const uint4*>(B.P + (qb0 + row0) * KP + (k0) + part * 8);               \
+  vb1 = *reinterpret_cast<const uint4*>(B.P + (qb0 + row1) * KP + (k0) + part * 8)
+#define PFX_MATCH_SSTORE(buf)                                                                     \
+  *reinterpret_cast<uint4*>(&sa[buf][row0 * RS + part * 8]) = va0;                                \
+  *reinterpret_cast<uint4*>(&sa[buf][row1 * RS + part * 8]) = va1;                                \
+  *reinterpret_cast<uint4*>(&sb[buf][row0 * RS + part * 8]) = vb0;                                \
+  *reinterpret_cast<uint4*>(&sb[buf][row1 * RS + part * 8]) = vb1
+  const int nch = KP / KC;
+  const int ar = (wv >> 1) * 64 + l32, br = (wv & 1) * 64 + l32;
+  PFX_MATCH_GLOAD(0);
+  PFX_MATCH_SSTORE(0);
+  __syncthreads();
+  for (int c = 0; c < nch; ++c) {
+    const int buf = c & 1;
+    if (c + 1 < nch) {
+      PFX_MATCH_GLOAD((c + 1) * KC);
+    }
+#pragma unroll
+    for (int st = 0; st < 2; ++st) {
+      const int ko = 16 * st + 8 * h;
+      const bf16x8 fa0 = *reinterpret_cast<const bf16x8*>(&sa[buf][ar * RS + ko]);
+      const bf16x8 fa1 = *reinterpret_cast<const bf16x8*>(&sa[buf][(ar + 32) * RS + ko]);
+      const bf16x8 fb0 = *reinterpret_cast<const bf16x8*>(&sb[buf][br * RS + ko]);
+      const bf16x8 fb1 = *reinterpret_cast<const bf16x8*>(&sb[buf][(br + 32) * RS + ko]);
+      acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa0, fb0, acc[0][0], 0, 0, 0);
+      acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa0, fb1, acc[0][1], 0, 0, 0);
+      acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa1, fb0, acc[1][0], 0, 0, 0);
+      acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa1, fb1, acc[1][1], 0, 0, 0);
+    }
+    if (c + 1 < nch) {  // buf ^ 1 was last read before the previous barrier
+      PFX_MATCH_SSTORE(buf ^ 1);
+    }
+    __syncthreads();
   }
+#undef PFX_MATCH_GLOAD
+#undef PFX_MATCH_SSTORE
   // epilogue: C/D map of 32x32 tiles: col = lane & 31, row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5)
   float cn2[2], cnr[2];
   bool cval[2];
@@ -274,7 +313,7 @@ void match_nearest_dev(pfx_ctx* ctx, const float* src, int64_t ns, int64_t ss, c
     return;
   }
   TimeScope total(ctx, "match");
-  const int Dp = (D + 15) / 16 * 16;
+  const int Dp = (D + 31) / 32 * 32;  // K = 3 Dp: whole 32-deep LDS chunks
   const Prepared a = prep(ctx, "match_a", src, ns, ss, D, Dp, false);
   const Prepared b = prep(ctx, "match_b", tgt, nt, ts, D, Dp, true);
   uint32_t* Urow = ctx->buf("match_urow").as<uint32_t>(a.n_pad);
