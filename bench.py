@@ -200,6 +200,7 @@ def main():
     for c in (ctx, ctx_n):
         c.set_timing(False)
     neighbors = stat("normals_neighbors")
+    long_nb, long_q = stat("normals_long_neighbors"), stat("normals_long_queries")
     # the chain stage once more, alone on the GPU (after the timed region, not part of `value`):
     # in the timed step it shares the device with NARF on the other stream
     iso_ms = None
@@ -222,8 +223,10 @@ def main():
         # roofline of the neighbour-gather kernel: k_normals_chain reads every query's
         # FLANN-ordered neighbour list and gathers the neighbours' coordinates into the ordered
         # covariance chains.  Algorithmic bytes per launch = sum_q |N_0.05(q)| * 12 B (xyz) +
-        # N * 16 B (normal + curvature out); time = its HIP-event duration on the ctx stream.
-        algo_bytes = neighbors * 12 + N_POINTS * 16
+        # 16 B (normal + curvature out) over the queries these kernels own, i.e. every query but
+        # the lists longer than 1024 (k_normals_long's, reported beside); time = their HIP-event
+        # duration on the ctx stream.
+        algo_bytes = (neighbors - long_nb) * 12 + (N_POINTS - long_q) * 16
         # the chain stage is k_normals_chain (LDS-staged workgroups) + k_normals_chain_big (the
         # dense workgroups it defers to a 144 KB-LDS pass), run as two masked passes per step
         # (FPFH support points on the main stream, the rest on the side stream): its time per
@@ -243,7 +246,9 @@ def main():
         roofline = {"bound": "hbm", "kernel": "k_normals_chain + k_normals_chain_big", "achieved": round(achieved, 2),
                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
                     "traffic": traffic, "algorithmic_bytes_per_launch": int(algo_bytes),
-                    "chain_ms_per_step": round(chain_s * 1e3, 4), "neighbors_per_launch": int(neighbors),
+                    "chain_ms_per_step": round(chain_s * 1e3, 4), "neighbors_per_launch": int(neighbors - long_nb),
+                    "long_lists": {"kernel": "k_normals_long", "lists": int(long_q), "neighbors": int(long_nb),
+                                   "ms_per_step": round(timers["normals_long"][0] / args.steps, 4)},
                     "isolated": None if iso_ms is None else {
                         "chain_ms": round(iso_ms, 4), "achieved": round(algo_bytes / (iso_ms / 1e3) / 1e9, 2),
                         "frac": round(algo_bytes / (iso_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 5),
@@ -255,9 +260,21 @@ def main():
             shot_ms, shot_n = timers["shot"]
             shot_s = (shot_ms / max(shot_n, 1)) / 1e3
             sb = stat("shot_neighbors") * 24
-            roofline["shot"] = {"kernel": "k_shot", "avg_ms": round(shot_s * 1e3, 4),
-                                "algorithmic_bytes_per_launch": int(sb),
-                                "achieved": round(sb / shot_s / 1e9, 2) if shot_s > 0 else 0.0}
+            # k_shot is this workload's dominant kernel (the chains take 0.5 ms of a 7.6 ms step):
+            # it heads the roofline; the chain figures stay beside it.  On this dense cloud
+            # (k(0.05) ~ 390) the chain's per-neighbour gather model exceeds the HBM peak because
+            # the kernel stages coordinates once per workgroup in LDS; the PMC traffic file is
+            # the default workload's, so no `traffic` here.
+            chain = dict(roofline, kernel="k_normals_chain + k_normals_chain_big", traffic=None,
+                         note="algorithmic model = 12 B per neighbour gather; coordinates are read once "
+                              "per workgroup from HBM and reused from LDS")
+            chain.pop("bound")
+            shot_gbs = sb / shot_s / 1e9 if shot_s > 0 else 0.0
+            roofline = {"bound": "hbm", "kernel": "k_shot", "achieved": round(shot_gbs, 2), "peak": HBM_PEAK_GBS,
+                        "unit": "GB/s", "frac": round(shot_gbs / HBM_PEAK_GBS, 5), "traffic": None,
+                        "algorithmic_bytes_per_launch": int(sb), "avg_ms": round(shot_s * 1e3, 4),
+                        "note": "sum_q |N_0.08(q)| x 24 B (xyz + normal) per launch (SURVEY 8(d)); VALU/LDS-atomic "
+                                "bound, not HBM", "normals_chain": chain}
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             cb = cpu_baseline(x, y, z, args.workload, sample_np)

@@ -227,23 +227,27 @@ struct NeighborGrid {
     x = x_; y = y_; z = z_; n = n_;
     cell = r > 0 ? r : 1.0;
     inv = 1.0 / cell;
+    // non-finite points are not indexed (PCL's kd-tree skips them)
     ox = oy = oz = 0.0;
-    if (n > 0) {
-      ox = x[0]; oy = y[0]; oz = z[0];
-      for (i64 i = 1; i < n; ++i) {
-        ox = std::min(ox, (double)x[i]); oy = std::min(oy, (double)y[i]); oz = std::min(oz, (double)z[i]);
-      }
-    }
-    std::vector<std::pair<uint64_t, i64> > kv((size_t)n);
+    bool first = true;
     for (i64 i = 0; i < n; ++i) {
+      if (!finite3(x[i], y[i], z[i])) continue;
+      if (first) { ox = x[i]; oy = y[i]; oz = z[i]; first = false; }
+      ox = std::min(ox, (double)x[i]); oy = std::min(oy, (double)y[i]); oz = std::min(oz, (double)z[i]);
+    }
+    std::vector<std::pair<uint64_t, i64> > kv;
+    kv.reserve((size_t)n);
+    for (i64 i = 0; i < n; ++i) {
+      if (!finite3(x[i], y[i], z[i])) continue;
       i64 ix, iy, iz;
       cellOf(x[i], y[i], z[i], ix, iy, iz);
-      kv[(size_t)i] = std::make_pair(pack(ix, iy, iz), i);
+      kv.push_back(std::make_pair(pack(ix, iy, iz), i));
     }
     std::sort(kv.begin(), kv.end());
-    order.resize((size_t)n);
+    const i64 m = (i64)kv.size();
+    order.resize((size_t)m);
     keys.clear(); start.clear(); end.clear();
-    for (i64 i = 0; i < n; ++i) {
+    for (i64 i = 0; i < m; ++i) {
       order[(size_t)i] = kv[(size_t)i].second;
       if (i == 0 || kv[(size_t)i].first != kv[(size_t)i - 1].first) {
         keys.push_back(kv[(size_t)i].first);
@@ -251,13 +255,15 @@ struct NeighborGrid {
         if (i) end.push_back(i);
       }
     }
-    if (n) end.push_back(n);
+    if (m) end.push_back(m);
   }
+  static bool finite3(float a, float b, float c) { return std::isfinite(a) && std::isfinite(b) && std::isfinite(c); }
   // returns neighbours sorted by (d2, index)
   void radius(float qx, float qy, float qz, double r, std::vector<int>& idx,
               std::vector<float>& d2) const {
     idx.clear(); d2.clear();
     const float rr = (float)(r * r);
+    if (!finite3(qx, qy, qz)) return;
     i64 cx, cy, cz;
     cellOf(qx, qy, qz, cx, cy, cz);
     std::vector<std::pair<float, int> > hits;

@@ -25,6 +25,8 @@ __host__ __device__ __forceinline__ uint32_t entry_off(uint32_t e) { return e & 
 struct NbLists {
   int64_t nq = 0;            // number of queries
   int64_t total = 0;         // sum of cnt
+  int64_t long_total = 0;    // sum of cnt over the lists longer than kLongList
+  int64_t long_nq = 0;       // number of those lists
   int64_t slots = 0;         // list entries allocated (total + interleave padding)
   const int32_t* qpos = nullptr;   // [nq] sorted position of each query
   const int64_t* off = nullptr;    // [nq]
@@ -33,6 +35,9 @@ struct NbLists {
   const uint32_t* list = nullptr;  // [slots] run entries
   const uint32_t* skeys = nullptr; // cell key of each sorted position (the grid's)
 };
+
+// lists longer than this are handled by per-query kernels downstream (normals: k_normals_long)
+constexpr int kLongList = 1024;
 
 // mask (nullable): per *caller* index, queries are the masked points (in cell order).
 void build_lists(pfx_ctx* ctx, const Grid& g, const uint8_t* mask, double radius, bool sorted, NbLists& out,

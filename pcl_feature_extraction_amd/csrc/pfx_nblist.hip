@@ -114,7 +114,7 @@ struct ListOut {
   int32_t* cnt;
   uint8_t* lg;
   uint32_t* list;
-  unsigned long long* cursor;  // [0] slots allocated, [1] neighbours
+  unsigned long long* cursor;  // [0] slots allocated, [1] neighbours, [2] neighbours in long lists, [3] long lists
   unsigned long long cap;
 };
 
@@ -615,6 +615,10 @@ __global__ void __launch_bounds__(256) k_nb_query(GridView g, const int32_t* __r
     if (tid == 0) {
       s_base = k ? atomicAdd(out.cursor, (unsigned long long)k) : 0ull;
       if (k) atomicAdd(out.cursor + 1, (unsigned long long)k);
+      if (k > kLongList) {
+        atomicAdd(out.cursor + 2, (unsigned long long)k);
+        atomicAdd(out.cursor + 3, 1ull);
+      }
       out.off[j] = (int64_t)s_base;
       out.cnt[j] = k;
       out.lg[j] = 0;
@@ -667,7 +671,7 @@ void build_lists(pfx_ctx* ctx, const Grid& G, const uint8_t* mask, double radius
   // 5 / 7 sparse / dense tile queue heads, 6 per-query work queued by the classifier (restored
   // for a rerun), 8 / 9 per-query / huge work queue heads
   int* counters = B("counters").as<int>(10);
-  unsigned long long* cursor = B("cursor").as<unsigned long long>(2);
+  unsigned long long* cursor = B("cursor").as<unsigned long long>(4);
   size_t t1 = 0, t2 = 0, t3 = 0;
   PFX_HIP(rocprim::select(nullptr, t1, rocprim::counting_iterator<int32_t>(0), flags, qpos, d_nq, (size_t)n, st));
   PFX_HIP(rocprim::inclusive_scan(nullptr, t2, seg, seg, (size_t)n, rocprim::maximum<int32_t>(), st));
@@ -703,7 +707,7 @@ void build_lists(pfx_ctx* ctx, const Grid& G, const uint8_t* mask, double radius
   const int isort = sorted ? 1 : 0;
   for (int attempt = 0; attempt < 2; ++attempt) {
     ListOut lo{off, cnt, lgs, static_cast<uint32_t*>(lb.ptr), cursor, lb.bytes / sizeof(uint32_t)};
-    PFX_HIP(hipMemsetAsync(cursor, 0, 2 * sizeof(unsigned long long), st));
+    PFX_HIP(hipMemsetAsync(cursor, 0, 4 * sizeof(unsigned long long), st));
     if (attempt) {
       PFX_HIP(hipMemcpyAsync(counters + 2, counters + 6, sizeof(int), hipMemcpyDeviceToDevice, st));
       PFX_HIP(hipMemsetAsync(counters + 3, 0, 3 * sizeof(int), st));  // huge, max k, sparse queue
@@ -740,7 +744,7 @@ void build_lists(pfx_ctx* ctx, const Grid& G, const uint8_t* mask, double radius
       }
     }
     int64_t h_nq = 0;
-    unsigned long long h_cur[2] = {0, 0};
+    unsigned long long h_cur[4] = {0, 0, 0, 0};
     PFX_HIP(hipMemcpyAsync(&h_nq, d_nq, sizeof(int64_t), hipMemcpyDeviceToHost, st));
     PFX_HIP(hipMemcpyAsync(h_cur, cursor, sizeof(h_cur), hipMemcpyDeviceToHost, st));
     PFX_HIP(hipMemcpyAsync(h_cnt, counters, sizeof(h_cnt), hipMemcpyDeviceToHost, st));
@@ -755,6 +759,8 @@ void build_lists(pfx_ctx* ctx, const Grid& G, const uint8_t* mask, double radius
     }
     out.nq = h_nq;
     out.total = (int64_t)h_cur[1];
+    out.long_total = (int64_t)h_cur[2];
+    out.long_nq = (int64_t)h_cur[3];
     out.slots = (int64_t)h_cur[0];
     out.qpos = qpos;
     out.off = off;

@@ -26,7 +26,7 @@ namespace pfx {
 namespace {
 
 constexpr int kBatch = 8;      // neighbour entries per half-batch (two in flight)
-constexpr int kLaneMax = 1024;  // longer lists go to k_normals_long
+constexpr int kLaneMax = kLongList;  // longer lists go to k_normals_long
 
 __device__ __forceinline__ void chain_add(float a[9], float x, float y, float z) {
   a[0] = a[0] + x * x;
@@ -513,6 +513,8 @@ void normals_lists_dev(pfx_ctx* ctx, const float* x, const float* y, const float
   PFX_HIP(hipMemsetAsync(curv, 0xff, sizeof(float) * n, st));
   build_lists(ctx, ctx->grid_a, nullptr, r, true, ns.L, "normals");
   ctx->stats["normals_neighbors"] = ns.L.total;
+  ctx->stats["normals_long_neighbors"] = ns.L.long_total;
+  ctx->stats["normals_long_queries"] = ns.L.long_nq;
   ctx->stats["normals_queries"] = ns.L.nq;
   ns.ready = true;
 }
@@ -536,11 +538,13 @@ void normals_chains_dev(pfx_ctx* ctx, pfx_ctx* owner, const uint8_t* mask, int w
   {
     // natural block order = round-robin over the 8 XCDs: the dense (heavy) workgroups cluster in
     // space, so contiguous per-XCD slices would leave one XCD with ~1.4x the mean work
-    TimeScope ts(ctx, "normals_chain");
     int64_t* deferq = ctx->buf("normals_deferq").as<int64_t>(nb);
-    k_normals_chain<<<(unsigned)nb, 256, 0, st>>>(view(G), L, vp[0], vp[1], vp[2], nx, ny, nz, curv, longq, n_long,
-                                                  n_long + 1, deferq, mask, want);
-    check_launch("k_normals_chain");
+    {
+      TimeScope ts(ctx, "normals_chain");
+      k_normals_chain<<<(unsigned)nb, 256, 0, st>>>(view(G), L, vp[0], vp[1], vp[2], nx, ny, nz, curv, longq, n_long,
+                                                    n_long + 1, deferq, mask, want);
+      check_launch("k_normals_chain");
+    }
     static std::once_flag attr;  // contexts may run on several host threads
     hipError_t attr_err = hipSuccess;
     std::call_once(attr, [&] {
