@@ -31,6 +31,9 @@
  *                          KdTreeFLANN<FeatureT>::nearestKSearch(k = 1) per descriptor
  *   pfx_correspondences* <- Features<T>::findCorrespondences (features.h:224-253)
  *   pfx_pcd_*           <- pcl::io::loadPCDFile<PointXYZRGB> (evaluation.cpp:226-235)
+ *   pfx_cloud_resolution* <- Keypoints::computeCloudResolution (keypoints.h:401-428)
+ *   pfx_iss_keypoints*  <- ISSKeypoint3D<PointXYZRGB,PointXYZRGB>::compute as configured by
+ *                          Keypoints::compute's ISS branch (keypoints.h:177-189)
  * ===================================================================================== */
 #ifndef PFX_H_
 #define PFX_H_
@@ -247,6 +250,28 @@ pfx_status pfx_pcd_read_header(const char* path, pfx_pcd_header* out);
  * sensor pose, which NARF's range image uses: keypoints.h:207-210). */
 pfx_status pfx_pcd_load_xyz_dev(pfx_ctx* ctx, const char* path, float* d_x, float* d_y, float* d_z,
                                 int64_t cap, int64_t* n_out, pfx_pcd_header* hdr);
+
+/* ---- active-list keypoints ------------------------------------------ */
+/* Keypoints::computeCloudResolution: mean distance of every finite point to its nearest other
+ * point (FLANN kNN k = 2, the first hit being the point itself), 0 without such points. */
+pfx_status pfx_cloud_resolution_dev(pfx_ctx* ctx, const float* d_x, const float* d_y, const float* d_z, int64_t n,
+                                    double* resolution);
+pfx_status pfx_cloud_resolution(pfx_ctx* ctx, const float* x, const float* y, const float* z, int64_t n,
+                                double* resolution);
+/* ISSKeypoint3D::compute (PCL 1.7 iss_3d.hpp): setSalientRadius, setNonMaxRadius,
+ * setMinNeighbors, setThreshold21, setThreshold32 (keypoints.h:182-187; no border radius).
+ * Keypoint cloud indices in ascending order into idx[0..cap); *n_out = their number
+ * (PFX_ERR_CAPACITY, nothing written, when it exceeds cap).  third (nullable, n doubles): the
+ * per-point third eigenvalue map (0 where the point is not a candidate).  A parameter that
+ * PCL's initCompute rejects (radius, threshold or min neighbours <= 0) -> PFX_ERR_INVALID. */
+pfx_status pfx_iss_keypoints_dev(pfx_ctx* ctx, const float* d_x, const float* d_y, const float* d_z, int64_t n,
+                                 double salient_radius, double non_max_radius, int32_t min_neighbors,
+                                 double threshold21, double threshold32, int32_t* d_idx, int64_t cap,
+                                 int64_t* n_out, double* d_third);
+pfx_status pfx_iss_keypoints(pfx_ctx* ctx, const float* x, const float* y, const float* z, int64_t n,
+                             double salient_radius, double non_max_radius, int32_t min_neighbors,
+                             double threshold21, double threshold32, int32_t* idx, int64_t cap, int64_t* n_out,
+                             double* third);
 
 #ifdef __cplusplus
 } /* extern "C" */

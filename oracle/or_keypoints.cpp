@@ -1,0 +1,347 @@
+// =====================================================================================
+//  oracle/or_keypoints.cpp  --  TEST INFRASTRUCTURE ONLY (parity vs real PCL UNPINNED)
+//
+//  CPU restatement of the reference's active-list keypoint detectors:
+//
+//    Keypoints::computeCloudResolution           include/pcl_feature_extraction/keypoints.h:401-428
+//    Keypoints::compute, ISS branch               include/pcl_feature_extraction/keypoints.h:177-189
+//      -> pcl::ISSKeypoint3D<PointXYZRGB, PointXYZRGB>  (PCL 1.7 keypoints/impl/iss_3d.hpp),
+//         salient radius 6 res, non-max radius 4 res, min neighbours 5, gamma21 = gamma32 = 0.975,
+//         search::KdTree<PointXYZRGB> (sorted results), no border radius, no normals.
+//
+//  computeCloudResolution: mean over the points with a finite x of sqrt(d2 of the second
+//  nearest neighbour), where the first is the point itself (d2 = 0; a duplicate point gives
+//  0 as well).  `sqrt(squaredDistances[1])` takes a float under `using namespace std`
+//  (keypoints.h:33), so the term is std::sqrt(float) -- correctly rounded float -- and the sum
+//  is a sequential double accumulation in index order, divided by the count.
+//
+//  ISSKeypoint3D::detectKeypoints (PCL 1.7), per finite point i:
+//    getScatterMatrix: N = radiusSearch(i, salient) in FLANN order; if |N| < min_neighbors the
+//      matrix stays 0; else cov[a*3+b] += (p_a - c_a) * (p_b - c_b) in double, neighbour order;
+//    Eigen::SelfAdjointEigenSolver<Matrix3d>(cov) (Eigen 3.2.0, restated below);
+//    e1 >= e2 >= e3; skip (no value) when one is non-finite or e3 < 0;
+//    third[i] = e3 when e2/e1 < gamma21 and e3/e2 < gamma32, else 0;
+//  then i is a keypoint when third[i] > 0, |radiusSearch(i, non_max)| >= min_neighbors and no
+//  neighbour has a larger third value.  Output: the keypoints' cloud indices, ascending.
+//
+//  Restatement choices (documented in DESIGN.md, unpinned):
+//    * skipped points (non-finite or negative eigenvalues) have third = 0.  PCL leaves their
+//      prg_mem slot uninitialised (iss_3d.hpp `continue` before the copy) -- undefined;
+//    * the reference pushes keypoints from an OpenMP loop under `omp critical` (thread order);
+//      the restatement returns them in index order (the single-thread order);
+//    * computeCloudResolution skips points with any non-finite coordinate (the reference tests
+//      x only and queries the kd-tree with the NaN point otherwise: undefined).
+// =====================================================================================
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <cstdlib>
+#include <vector>
+
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+#include "or_common.h"
+
+using orc::i64;
+using orc::NeighborGrid;
+
+namespace {
+
+// ---- Eigen 3.2.0 SelfAdjointEigenSolver<Matrix3d>::compute, eigenvalues only -------------
+// (Eigenvalues/SelfAdjointEigenSolver.h, Eigenvalues/Tridiagonalization.h, Jacobi/Jacobi.h,
+// MathFunctions.h hypot_impl).  The eigenvector updates do not feed back into the values.
+
+double hypot_e(double x, double y) {  // internal::hypot_impl
+  const double ax = std::fabs(x), ay = std::fabs(y);
+  const double p = std::max(ax, ay);
+  if (p == 0.0) return 0.0;
+  const double q = std::min(ax, ay);
+  const double qp = q / p;
+  return p * std::sqrt(1.0 + qp * qp);
+}
+
+void make_givens(double p, double q, double& c, double& s) {  // JacobiRotation::makeGivens (real)
+  if (q == 0.0) {
+    c = p < 0.0 ? -1.0 : 1.0;
+    s = 0.0;
+  } else if (p == 0.0) {
+    c = 0.0;
+    s = q < 0.0 ? 1.0 : -1.0;
+  } else if (std::fabs(p) > std::fabs(q)) {
+    const double t = q / p;
+    double u = std::sqrt(1.0 + t * t);
+    if (p < 0.0) u = -u;
+    c = 1.0 / u;
+    s = -t * c;
+  } else {
+    const double t = p / q;
+    double u = std::sqrt(1.0 + t * t);
+    if (q < 0.0) u = -u;
+    s = -1.0 / u;
+    c = -t * s;
+  }
+}
+
+void tridiagonal_qr_step(double* diag, double* sub, int start, int end) {
+  const double td = (diag[end - 1] - diag[end]) * 0.5;
+  const double e = sub[end - 1];
+  double mu = diag[end];
+  if (td == 0.0) {
+    mu -= std::fabs(e);
+  } else {
+    const double e2 = e * e;
+    const double h = hypot_e(td, e);
+    if (e2 == 0.0)
+      mu -= (e / (td + (td > 0.0 ? 1.0 : -1.0))) * (e / h);
+    else
+      mu -= e2 / (td + (td > 0.0 ? h : -h));
+  }
+  double x = diag[start] - mu;
+  double z = sub[start];
+  for (int k = start; k < end; ++k) {
+    double c, s;
+    make_givens(x, z, c, s);
+    const double sdk = s * diag[k] + c * sub[k];
+    const double dkp1 = s * sub[k] + c * diag[k + 1];
+    diag[k] = c * (c * diag[k] - s * sub[k]) - s * (c * sub[k] - s * diag[k + 1]);
+    diag[k + 1] = s * sdk + c * dkp1;
+    sub[k] = c * sdk - s * dkp1;
+    if (k > start) sub[k - 1] = c * sub[k - 1] - s * z;
+    x = sub[k];
+    if (k < end - 1) {
+      z = -s * sub[k + 1];
+      sub[k + 1] = c * sub[k + 1];
+    }
+  }
+}
+
+// a: row-major symmetric 3x3 (the lower triangle is read, as Eigen does); ev ascending
+void selfadjoint_eigenvalues3(const double a[9], double ev[3]) {
+  double m[3][3] = {{a[0], 0.0, 0.0}, {a[3], a[4], 0.0}, {a[6], a[7], a[8]}};
+  double scale = 0.0;
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) scale = std::max(scale, std::fabs(m[i][j]));
+  if (scale == 0.0) scale = 1.0;
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j <= i; ++j) m[i][j] /= scale;
+  // tridiagonalization_inplace_selector<MatrixType, 3, false>::run
+  double diag[3], sub[2];
+  diag[0] = m[0][0];
+  const double v1norm2 = m[2][0] * m[2][0];
+  if (v1norm2 == 0.0) {
+    diag[1] = m[1][1];
+    diag[2] = m[2][2];
+    sub[0] = m[1][0];
+    sub[1] = m[2][1];
+  } else {
+    const double beta = std::sqrt(m[1][0] * m[1][0] + v1norm2);
+    const double inv_beta = 1.0 / beta;
+    const double m01 = m[1][0] * inv_beta;
+    const double m02 = m[2][0] * inv_beta;
+    const double q = 2.0 * m01 * m[2][1] + m02 * (m[2][2] - m[1][1]);
+    diag[1] = m[1][1] + m02 * q;
+    diag[2] = m[2][2] - m02 * q;
+    sub[0] = beta;
+    sub[1] = m[2][1] - m01 * q;
+  }
+  // implicit symmetric QR with Wilkinson shift (max 30 * n iterations)
+  int end = 2, start = 0, iter = 0;
+  while (end > 0) {
+    for (int i = start; i < end; ++i)
+      if (std::fabs(sub[i]) <= (std::fabs(diag[i]) + std::fabs(diag[i + 1])) * 1e-12) sub[i] = 0.0;
+    while (end > 0 && sub[end - 1] == 0.0) end--;
+    if (end <= 0) break;
+    iter++;
+    if (iter > 30 * 3) break;
+    start = end - 1;
+    while (start > 0 && sub[start - 1] != 0.0) start--;
+    tridiagonal_qr_step(diag, sub, start, end);
+  }
+  if (iter <= 30 * 3) {  // Success: selection sort, ascending (first minimum wins)
+    for (int i = 0; i < 2; ++i) {
+      int k = i;
+      for (int j = i + 1; j < 3; ++j)
+        if (diag[j] < diag[k]) k = j;
+      if (k != i) std::swap(diag[i], diag[k]);
+    }
+  }
+  for (int i = 0; i < 3; ++i) ev[i] = diag[i] * scale;
+}
+
+inline bool finite3(const float* x, const float* y, const float* z, i64 i) {
+  return std::isfinite(x[i]) && std::isfinite(y[i]) && std::isfinite(z[i]);
+}
+
+// d2 of the second nearest point of the cloud to point i (itself included, FLANN kNN k = 2);
+// +inf when the cloud has a single finite point.  Ring search on a grid of cell h.
+float second_nn_d2(const NeighborGrid& g, const float* x, const float* y, const float* z, i64 i) {
+  const float qx = x[i], qy = y[i], qz = z[i];
+  float b1 = INFINITY, b2 = INFINITY;
+  auto visit = [&](i64 p) {
+    const float dx = qx - x[p], dy = qy - y[p], dz = qz - z[p];
+    const float dd = ((0.0f + dx * dx) + dy * dy) + dz * dz;  // flann::L2_Simple
+    if (dd < b1) {
+      b2 = b1;
+      b1 = dd;
+    } else if (dd < b2) {
+      b2 = dd;
+    }
+  };
+  i64 cx, cy, cz;
+  g.cellOf(qx, qy, qz, cx, cy, cz);
+  for (i64 R = 1; R <= 4; ++R) {
+    b1 = b2 = INFINITY;
+    for (i64 ix = cx - R; ix <= cx + R; ++ix)
+      for (i64 iy = cy - R; iy <= cy + R; ++iy)
+        for (i64 iz = cz - R; iz <= cz + R; ++iz) {
+          if (ix < -NeighborGrid::OFF + 1 || iy < -NeighborGrid::OFF + 1 || iz < -NeighborGrid::OFF + 1 ||
+              ix >= NeighborGrid::OFF || iy >= NeighborGrid::OFF || iz >= NeighborGrid::OFF)
+            continue;
+          const uint64_t k = NeighborGrid::pack(ix, iy, iz);
+          std::vector<uint64_t>::const_iterator it = std::lower_bound(g.keys.begin(), g.keys.end(), k);
+          if (it == g.keys.end() || *it != k) continue;
+          const size_t c = (size_t)(it - g.keys.begin());
+          for (i64 s = g.start[c]; s < g.end[c]; ++s) visit(g.order[(size_t)s]);
+        }
+    // everything outside the block is at least R cells (R * cell) away
+    const double reach = (double)R * g.cell;
+    if ((double)b2 < reach * reach * (1.0 - 1e-6)) return b2;
+  }
+  b1 = b2 = INFINITY;  // isolated point: every indexed point
+  for (size_t s = 0; s < g.order.size(); ++s) visit(g.order[s]);
+  return b2;
+}
+
+}  // namespace
+
+extern "C" {
+
+// Eigen 3.2.0 SelfAdjointEigenSolver<Matrix3d> eigenvalues (ascending) of row-major symmetric
+// 3x3 matrices, for the tests of the restatement itself.
+int orc_eigen_selfadjoint3(const double* a, i64 n, double* ev) {
+  for (i64 i = 0; i < n; ++i) selfadjoint_eigenvalues3(a + 9 * i, ev + 3 * i);
+  return 0;
+}
+
+// Keypoints::computeCloudResolution (keypoints.h:401-428).  `terms` (nullable, n floats): the
+// per-point sqrt term, NaN where the point does not contribute.
+int orc_cloud_resolution(const float* x, const float* y, const float* z, i64 n, double* out, float* terms,
+                         int threads) {
+  *out = 0.0;
+  if (n <= 0) return 0;
+  // cell: the mean spacing of the bounding volume (any cell size gives the same answer)
+  double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+  i64 nf = 0;
+  for (i64 i = 0; i < n; ++i) {
+    if (!finite3(x, y, z, i)) continue;
+    const float p[3] = {x[i], y[i], z[i]};
+    for (int d = 0; d < 3; ++d) { lo[d] = std::min(lo[d], (double)p[d]); hi[d] = std::max(hi[d], (double)p[d]); }
+    ++nf;
+  }
+  std::vector<float> t((size_t)n, NAN);
+  if (nf >= 2) {
+    double ext = 0.0, vol = 1.0;
+    for (int d = 0; d < 3; ++d) ext = std::max(ext, hi[d] - lo[d]);
+    for (int d = 0; d < 3; ++d) vol *= std::max(hi[d] - lo[d], ext * 1e-3);
+    double h = ext > 0.0 ? 0.5 * std::cbrt(vol / (double)nf) : 1.0;
+    NeighborGrid g;
+    g.build(x, y, z, n, h);
+#ifdef _OPENMP
+    if (threads > 0) omp_set_num_threads(threads);
+#pragma omp parallel for schedule(dynamic, 256)
+#endif
+    for (i64 i = 0; i < n; ++i) {
+      if (!finite3(x, y, z, i)) continue;
+      t[(size_t)i] = std::sqrt(second_nn_d2(g, x, y, z, i));  // std::sqrt(float)
+    }
+  }
+  double resolution = 0.0;
+  i64 count = 0;
+  for (i64 i = 0; i < n; ++i) {
+    if (std::isnan(t[(size_t)i])) continue;
+    resolution += t[(size_t)i];
+    ++count;
+  }
+  if (count != 0) resolution /= count;
+  *out = resolution;
+  if (terms)
+    for (i64 i = 0; i < n; ++i) terms[i] = t[(size_t)i];
+  return 0;
+}
+
+// ISSKeypoint3D::compute as configured at keypoints.h:177-189.  idx: keypoint cloud indices
+// (ascending), third (nullable, n doubles): the per-point third eigenvalue map.
+// Returns 1 for parameters PCL's initCompute rejects (no output), 3 when cap is too small.
+int orc_iss_keypoints(const float* x, const float* y, const float* z, i64 n, double salient, double non_max,
+                      int min_neighbors, double gamma21, double gamma32, int32_t* idx, i64 cap, i64* n_out,
+                      double* third_out, int threads) {
+  *n_out = 0;
+  if (salient <= 0.0 || non_max <= 0.0 || gamma21 <= 0.0 || gamma32 <= 0.0 || min_neighbors <= 0) return 1;
+  if (n <= 0) return 0;
+  std::vector<double> third((size_t)n, 0.0);
+  std::vector<char> is_max((size_t)n, 0);
+#ifdef _OPENMP
+  if (threads > 0) omp_set_num_threads(threads);
+#endif
+  {
+    NeighborGrid gs;
+    gs.build(x, y, z, n, salient);
+#pragma omp parallel
+    {
+      std::vector<int> nb;
+      std::vector<float> dd;
+#pragma omp for schedule(dynamic, 256)
+      for (i64 i = 0; i < n; ++i) {
+        if (!finite3(x, y, z, i)) continue;
+        gs.radius(x[i], y[i], z[i], salient, nb, dd);
+        double cov[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+        if ((int)nb.size() >= min_neighbors) {
+          const double c[3] = {x[i], y[i], z[i]};
+          for (size_t m = 0; m < nb.size(); ++m) {
+            const double p[3] = {x[nb[m]], y[nb[m]], z[nb[m]]};
+            for (int a = 0; a < 3; ++a)
+              for (int b = 0; b < 3; ++b) cov[a * 3 + b] += (p[a] - c[a]) * (p[b] - c[b]);
+          }
+        }
+        double ev[3];
+        selfadjoint_eigenvalues3(cov, ev);
+        const double e1 = ev[2], e2 = ev[1], e3 = ev[0];
+        if (!std::isfinite(e1) || !std::isfinite(e2) || !std::isfinite(e3) || e3 < 0.0) continue;
+        if (e2 / e1 < gamma21 && e3 / e2 < gamma32) third[(size_t)i] = e3;
+      }
+    }
+  }
+  {
+    NeighborGrid gn;
+    gn.build(x, y, z, n, non_max);
+#pragma omp parallel
+    {
+      std::vector<int> nb;
+      std::vector<float> dd;
+#pragma omp for schedule(dynamic, 256)
+      for (i64 i = 0; i < n; ++i) {
+        if (!(third[(size_t)i] > 0.0) || !finite3(x, y, z, i)) continue;
+        gn.radius(x[i], y[i], z[i], non_max, nb, dd);
+        if ((int)nb.size() < min_neighbors) continue;
+        bool m = true;
+        for (size_t j = 0; j < nb.size(); ++j)
+          if (third[(size_t)i] < third[(size_t)nb[j]]) m = false;
+        is_max[(size_t)i] = m;
+      }
+    }
+  }
+  i64 k = 0;
+  for (i64 i = 0; i < n; ++i)
+    if (is_max[(size_t)i]) {
+      if (k < cap) idx[k] = (int32_t)i;
+      ++k;
+    }
+  *n_out = k;
+  if (third_out)
+    for (i64 i = 0; i < n; ++i) third_out[i] = third[(size_t)i];
+  return k > cap ? 3 : 0;
+}
+
+}  // extern "C"

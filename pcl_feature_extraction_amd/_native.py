@@ -115,6 +115,12 @@ _SIGS = {
                                         c_vp, c_vp, c_i64, c_i64p]),
     "pfx_correspondences": (c_int, [c_vp, c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, ctypes.c_int32,
                                     c_vp, c_vp, c_i64, c_i64p]),
+    "pfx_cloud_resolution_dev": (c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, ctypes.POINTER(ctypes.c_double)]),
+    "pfx_cloud_resolution": (c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, ctypes.POINTER(ctypes.c_double)]),
+    "pfx_iss_keypoints_dev": (c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, ctypes.c_double, ctypes.c_double,
+                                      ctypes.c_int32, ctypes.c_double, ctypes.c_double, c_vp, c_i64, c_i64p, c_vp]),
+    "pfx_iss_keypoints": (c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, ctypes.c_double, ctypes.c_double, ctypes.c_int32,
+                                  ctypes.c_double, ctypes.c_double, c_vp, c_i64, c_i64p, c_vp]),
 }
 
 _lib = None

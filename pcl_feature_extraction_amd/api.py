@@ -288,3 +288,43 @@ class Context:
                                                       query.numel(), ctypes.byref(n)))
         return n.value
 
+
+    # ---- active-list keypoints ------------------------------------------
+    def cloud_resolution(self, x, y, z):
+        """Keypoints::computeCloudResolution (keypoints.h:401-428), host arrays."""
+        x, y, z = map(_f32, (x, y, z))
+        out = ctypes.c_double()
+        self._check(self._lib.pfx_cloud_resolution(self.h, _ptr(x), _ptr(y), _ptr(z), len(x), ctypes.byref(out)))
+        return out.value
+
+    def cloud_resolution_dev(self, x, y, z):
+        """Keypoints::computeCloudResolution on device arrays (the value comes back to the host,
+        as the reference's return value)."""
+        out = ctypes.c_double()
+        self._check(self._lib.pfx_cloud_resolution_dev(self.h, _ptr(x), _ptr(y), _ptr(z), x.numel(),
+                                                       ctypes.byref(out)))
+        return out.value
+
+    def iss_keypoints(self, x, y, z, salient_radius, non_max_radius, min_neighbors=5, threshold21=0.975,
+                      threshold32=0.975, return_third=False):
+        """ISSKeypoint3D::compute (keypoints.h:177-189), host arrays: keypoint indices ascending
+        (and the per-point third eigenvalue map)."""
+        x, y, z = map(_f32, (x, y, z))
+        n = len(x)
+        idx = np.empty(max(n, 1), np.int32)
+        third = np.empty(max(n, 1), np.float64) if return_third else None
+        k = ctypes.c_int64()
+        self._check(self._lib.pfx_iss_keypoints(self.h, _ptr(x), _ptr(y), _ptr(z), n, salient_radius, non_max_radius,
+                                                min_neighbors, threshold21, threshold32, _ptr(idx), len(idx),
+                                                ctypes.byref(k), _ptr(third)))
+        out = idx[: k.value].copy()
+        return (out, third[:n].copy()) if return_third else out
+
+    def iss_keypoints_dev(self, x, y, z, salient_radius, non_max_radius, idx, min_neighbors=5, threshold21=0.975,
+                          threshold32=0.975, third=None):
+        """Device version: indices into `idx` (int32 tensor), returns their number."""
+        k = ctypes.c_int64()
+        self._check(self._lib.pfx_iss_keypoints_dev(self.h, _ptr(x), _ptr(y), _ptr(z), x.numel(), salient_radius,
+                                                    non_max_radius, min_neighbors, threshold21, threshold32,
+                                                    _ptr(idx), idx.numel(), ctypes.byref(k), _ptr(third)))
+        return k.value

@@ -113,6 +113,7 @@ void pfx_ctx_destroy(pfx_ctx* ctx) {
   (void)hipStreamSynchronize(ctx->stream);
   pfx::narf_release(ctx);
   pfx::normals_release(ctx);
+  pfx::keypoints_release(ctx);
   ctx->grid_a.release();
   ctx->grid_b.release();
   for (auto& kv : ctx->bufs) kv.second.release();
@@ -566,5 +567,78 @@ extern "C" pfx_status pfx_pcd_load_xyz_dev(pfx_ctx* ctx, const char* path, float
   const int64_t n = pfx::pcd_load_xyz_dev(ctx, path, d_x, d_y, d_z, cap, hdr);
   *n_out = n;
   if (n > cap) throw Error(PFX_ERR_CAPACITY, "pcd load: " + std::to_string(n) + " points > cap");
+  PFX_API_END(ctx)
+}
+
+namespace {
+void check_points(const float* x, const float* y, const float* z, int64_t n, const char* what) {
+  if (n < 0 || (n && (!x || !y || !z))) throw Error(PFX_ERR_INVALID, std::string(what) + ": invalid point arrays");
+}
+void check_iss(double sal, double nm, int32_t min_nb, double t21, double t32) {
+  if (!(sal > 0.0) || !(nm > 0.0) || min_nb <= 0 || !(t21 > 0.0) || !(t32 > 0.0))
+    throw Error(PFX_ERR_INVALID, "iss: radii, thresholds and min neighbours must be > 0 (ISSKeypoint3D::initCompute)");
+}
+}  // namespace
+
+extern "C" pfx_status pfx_cloud_resolution_dev(pfx_ctx* ctx, const float* d_x, const float* d_y, const float* d_z,
+                                               int64_t n, double* resolution) {
+  PFX_API_BEGIN
+  check_ctx(ctx);
+  check_points(d_x, d_y, d_z, n, "cloud_resolution");
+  if (!resolution) throw Error(PFX_ERR_INVALID, "cloud_resolution: null output");
+  *resolution = pfx::cloud_resolution_dev(ctx, d_x, d_y, d_z, n);
+  PFX_API_END(ctx)
+}
+
+extern "C" pfx_status pfx_cloud_resolution(pfx_ctx* ctx, const float* x, const float* y, const float* z, int64_t n,
+                                           double* resolution) {
+  PFX_API_BEGIN
+  check_ctx(ctx);
+  check_points(x, y, z, n, "cloud_resolution");
+  if (!resolution) throw Error(PFX_ERR_INVALID, "cloud_resolution: null output");
+  float* dx = stage_in(ctx, "in_x", x, n);
+  float* dy = stage_in(ctx, "in_y", y, n);
+  float* dz = stage_in(ctx, "in_z", z, n);
+  *resolution = pfx::cloud_resolution_dev(ctx, dx, dy, dz, n);
+  PFX_API_END(ctx)
+}
+
+extern "C" pfx_status pfx_iss_keypoints_dev(pfx_ctx* ctx, const float* d_x, const float* d_y, const float* d_z,
+                                            int64_t n, double salient_radius, double non_max_radius,
+                                            int32_t min_neighbors, double threshold21, double threshold32,
+                                            int32_t* d_idx, int64_t cap, int64_t* n_out, double* d_third) {
+  PFX_API_BEGIN
+  check_ctx(ctx);
+  check_points(d_x, d_y, d_z, n, "iss");
+  check_iss(salient_radius, non_max_radius, min_neighbors, threshold21, threshold32);
+  if (!n_out || cap < 0 || (cap && !d_idx)) throw Error(PFX_ERR_INVALID, "iss: invalid output arguments");
+  const int64_t k = pfx::iss_keypoints_dev(ctx, d_x, d_y, d_z, n, salient_radius, non_max_radius, min_neighbors,
+                                           threshold21, threshold32, d_idx, cap, d_third);
+  *n_out = k;
+  if (k > cap) throw Error(PFX_ERR_CAPACITY, "iss: " + std::to_string(k) + " keypoints > cap");
+  PFX_API_END(ctx)
+}
+
+extern "C" pfx_status pfx_iss_keypoints(pfx_ctx* ctx, const float* x, const float* y, const float* z, int64_t n,
+                                        double salient_radius, double non_max_radius, int32_t min_neighbors,
+                                        double threshold21, double threshold32, int32_t* idx, int64_t cap,
+                                        int64_t* n_out, double* third) {
+  PFX_API_BEGIN
+  check_ctx(ctx);
+  check_points(x, y, z, n, "iss");
+  check_iss(salient_radius, non_max_radius, min_neighbors, threshold21, threshold32);
+  if (!n_out || cap < 0 || (cap && !idx)) throw Error(PFX_ERR_INVALID, "iss: invalid output arguments");
+  float* dx = stage_in(ctx, "in_x", x, n);
+  float* dy = stage_in(ctx, "in_y", y, n);
+  float* dz = stage_in(ctx, "in_z", z, n);
+  int32_t* di = ctx->buf("out_iss_idx").as<int32_t>(n + 1);
+  double* dt = third ? ctx->buf("out_iss_third").as<double>(n + 1) : nullptr;
+  const int64_t k = pfx::iss_keypoints_dev(ctx, dx, dy, dz, n, salient_radius, non_max_radius, min_neighbors,
+                                           threshold21, threshold32, di, n, dt);
+  *n_out = k;
+  if (k > cap) throw Error(PFX_ERR_CAPACITY, "iss: " + std::to_string(k) + " keypoints > cap");
+  if (k) PFX_HIP(hipMemcpyAsync(idx, di, sizeof(int32_t) * k, hipMemcpyDeviceToHost, ctx->stream));
+  if (third && n) PFX_HIP(hipMemcpyAsync(third, dt, sizeof(double) * n, hipMemcpyDeviceToHost, ctx->stream));
+  PFX_HIP(hipStreamSynchronize(ctx->stream));
   PFX_API_END(ctx)
 }

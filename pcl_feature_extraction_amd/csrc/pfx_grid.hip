@@ -115,6 +115,26 @@ __global__ void __launch_bounds__(256) k_gather_sorted(const float* __restrict__
 
 }  // namespace
 
+void points_bbox(pfx_ctx* ctx, Grid& g, const float* d_x, const float* d_y, const float* d_z, int64_t n,
+                 double lo[3], double hi[3]) {
+  hipStream_t st = ctx->stream;
+  uint32_t* mm = g.b_minmax.as<uint32_t>(6);
+  uint32_t init[6] = {0xffffffffu, 0xffffffffu, 0xffffffffu, 0u, 0u, 0u};
+  PFX_HIP(hipMemcpyAsync(mm, init, sizeof(init), hipMemcpyHostToDevice, st));
+  if (n > 0) {
+    k_bbox<<<(int)std::min<int64_t>(ceil_div(n, 256), 256), 256, 0, st>>>(d_x, d_y, d_z, n, mm);
+    check_launch("k_bbox");
+  }
+  uint32_t h[6];
+  PFX_HIP(hipMemcpyAsync(h, mm, sizeof(h), hipMemcpyDeviceToHost, st));
+  PFX_HIP(hipStreamSynchronize(st));
+  const bool any = h[0] != 0xffffffffu && h[3] != 0u;
+  for (int d = 0; d < 3; ++d) {
+    lo[d] = any ? ord2f(h[d]) : 0.0;
+    hi[d] = any ? ord2f(h[3 + d]) : 0.0;
+  }
+}
+
 void build_grid(pfx_ctx* ctx, Grid& g, const float* d_x, const float* d_y, const float* d_z,
                 int64_t n, double radius) {
   PFX_CHECK(n >= 0 && n < (int64_t(1) << 31), "point count must be in [0, 2^31)");

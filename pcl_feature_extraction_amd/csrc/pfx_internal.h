@@ -95,6 +95,7 @@ struct GridView {
 
 struct NarfState;     // pfx_narf.hip
 struct NormalsState;  // pfx_normals.hip
+struct KeypointState;  // pfx_iss.hip
 
 }  // namespace pfx
 
@@ -114,6 +115,7 @@ struct pfx_ctx {
   std::map<std::string, pfx::DevBuf> bufs;  // named scratch
   pfx::NarfState* narf = nullptr;
   pfx::NormalsState* normals = nullptr;  // neighbour lists between the two normal phases
+  pfx::KeypointState* kp = nullptr;      // grids + lists of the keypoint detectors
   pfx::DevBuf& buf(const char* name) { return bufs[name]; }
 };
 
@@ -150,6 +152,9 @@ inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 // grid building (pfx_grid.hip)
 void build_grid(pfx_ctx* ctx, Grid& g, const float* d_x, const float* d_y, const float* d_z,
                 int64_t n, double radius);
+// bounding box of the finite points (0 when there are none), synchronous
+void points_bbox(pfx_ctx* ctx, Grid& g, const float* d_x, const float* d_y, const float* d_z, int64_t n,
+                 double lo[3], double hi[3]);
 inline GridView view(const Grid& g) {
   GridView v;
   v.sx = g.sx; v.sy = g.sy; v.sz = g.sz; v.sp = g.sp; v.perm = g.perm; v.cell_start = g.cell_start;
@@ -166,6 +171,11 @@ void normals_lists_dev(pfx_ctx* ctx, const float* x, const float* y, const float
 void normals_chains_dev(pfx_ctx* ctx, pfx_ctx* owner, const uint8_t* mask, int want, const float vp[3], float* nx,
                         float* ny, float* nz, float* curv);
 void normals_release(pfx_ctx* ctx);
+double cloud_resolution_dev(pfx_ctx* ctx, const float* x, const float* y, const float* z, int64_t n);
+int64_t iss_keypoints_dev(pfx_ctx* ctx, const float* x, const float* y, const float* z, int64_t n, double salient,
+                          double non_max, int min_nb, double g21, double g32, int32_t* out, int64_t cap,
+                          double* third_out);
+void keypoints_release(pfx_ctx* ctx);
 void fpfh_support_mask_dev(pfx_ctx* ctx, const float* sx, const float* sy, const float* sz, int64_t ns,
                            const float* qx, const float* qy, const float* qz, int64_t nq, double r, uint8_t* mask);
 void radius_search_dev(pfx_ctx* ctx, const float* x, const float* y, const float* z, int64_t n,

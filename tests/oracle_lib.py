@@ -177,3 +177,42 @@ def correspondences(src, tgt, threads=0):
                                    _p(m, _i32p), _i64(cap), ctypes.byref(n), ctypes.c_int(threads))
     assert rc == 0
     return q[: n.value].copy(), m[: n.value].copy()
+
+
+_f64p = ctypes.POINTER(ctypes.c_double)
+
+
+def eigen_selfadjoint3(mats):
+    """Eigen 3.2.0 SelfAdjointEigenSolver<Matrix3d> eigenvalues (ascending) of (n, 3, 3)."""
+    a = np.ascontiguousarray(mats, np.float64).reshape(-1, 9)
+    ev = np.empty((len(a), 3), np.float64)
+    assert lib().orc_eigen_selfadjoint3(_p(a, _f64p), _i64(len(a)), _p(ev, _f64p)) == 0
+    return ev
+
+
+def cloud_resolution(x, y, z, threads=0):
+    """Keypoints::computeCloudResolution (keypoints.h:401-428): (resolution, per-point terms)."""
+    x, y, z = map(_f32, (x, y, z))
+    out = ctypes.c_double()
+    terms = np.empty(len(x), np.float32)
+    assert lib().orc_cloud_resolution(_p(x), _p(y), _p(z), _i64(len(x)), ctypes.byref(out), _p(terms),
+                                      ctypes.c_int(threads)) == 0
+    return out.value, terms
+
+
+def iss_keypoints(x, y, z, salient_radius, non_max_radius, min_neighbors=5, gamma21=0.975, gamma32=0.975,
+                  threads=0):
+    """ISSKeypoint3D::compute (PCL 1.7) as keypoints.h:177-189 configures it: (indices, third)."""
+    x, y, z = map(_f32, (x, y, z))
+    n = len(x)
+    idx = np.empty(max(n, 1), np.int32)
+    third = np.empty(n, np.float64)
+    k = ctypes.c_int64()
+    rc = lib().orc_iss_keypoints(_p(x), _p(y), _p(z), _i64(n), ctypes.c_double(salient_radius),
+                                 ctypes.c_double(non_max_radius), ctypes.c_int(min_neighbors),
+                                 ctypes.c_double(gamma21), ctypes.c_double(gamma32), _p(idx, _i32p), _i64(len(idx)),
+                                 ctypes.byref(k), _p(third, _f64p), ctypes.c_int(threads))
+    if rc == 1:
+        return np.empty(0, np.int32), np.zeros(n)
+    assert rc == 0, rc
+    return idx[: k.value].copy(), third
