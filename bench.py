@@ -14,6 +14,8 @@ seabed, normals + SHOT-352 (r = 0.08) at the NARF keypoints and a fixed 10,000-p
 `--workload match` measures the next row of SURVEY 8(f) (F1, Features<T>::findCorrespondences,
 features.h:224-253): mutual 1-NN between the SHOT-352 descriptor sets of two such scans
 (descriptors computed before the timed region; one step = one correspondence search).
+`--workload iss` measures F3, the reference's active ISS keypoints (Keypoints::compute ISS
+branch, keypoints.h:177-189): one step = cloud resolution + ISSKeypoint3D over the 1M-point room.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--workload fpfh|shot] [--no-cpu-baseline]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
@@ -98,7 +100,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--workload", choices=["fpfh", "shot", "match"], default="fpfh")
+    ap.add_argument("--workload", choices=["fpfh", "shot", "match", "iss"], default="fpfh")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
     if os.environ.get("PFX_BENCH_VERBOSE"):
@@ -125,6 +127,8 @@ def main():
 
     if args.workload == "match":
         return bench_match(args, torch, dev, world, rank, local)
+    if args.workload == "iss":
+        return bench_iss(args, torch, dev, world, rank, local)
 
     shot = args.workload == "shot"
     if shot:  # configs[3]: seabed seed 3 (per-rank seeds 300 + rank at N > 1)
@@ -409,6 +413,89 @@ def bench_match(args, torch, dev, world, rank, local):
             rep = {nm: round(ctx.kernel_time(nm)[0] / args.steps, 4)
                    for nm in ("match", "match_bound", "match_filter", "match_exact")}
             print("per-step kernel ms:", json.dumps(rep), file=sys.stderr, flush=True)
+        print(json.dumps(line), flush=True)
+    ctx.close()
+
+
+def bench_iss(args, torch, dev, world, rank, local):
+    """Keypoints("ISS").compute over the 1M-point room scan (one per rank)."""
+    import numpy as np
+
+    from pcl_feature_extraction_amd import Context
+    from pcl_feature_extraction_amd.pipeline import keypoints_iss
+    from pcl_feature_extraction_amd.synth import synth_room
+
+    x, y, z, _ = synth_room(N_POINTS, 2 if world == 1 else 100 + rank)
+    ctx = Context(local)
+    ctx.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+    dx, dy, dz = (torch.from_numpy(a).to(dev) for a in (x, y, z))
+    idx = torch.empty(N_POINTS, dtype=torch.int32, device=dev)
+    k = 0
+    for _ in range(args.warmup):
+        k = keypoints_iss(ctx, dx, dy, dz, idx)
+    torch.cuda.synchronize(dev)
+    ctx.set_timing(True)
+    ctx.reset_timing()
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        k = keypoints_iss(ctx, dx, dy, dz, idx)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        torch.distributed.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        elapsed = float(t.item())
+    if rank == 0:
+        # the scatter kernel (k_iss_cov): every point's salient neighbours' coordinates and its
+        # third value; algorithmic bytes per launch = sum_q |N_6res(q)| x 12 B + N x 8 B
+        nb = ctx.stat("iss_neighbors")
+        ts, ns = ctx.kernel_time("iss_scatter")
+        scat_s = ts / max(ns, 1) / 1e3
+        algo = nb * 12 + N_POINTS * 8
+        achieved = algo / scat_s / 1e9 if scat_s > 0 else 0.0
+        stages = {nm: round(ctx.kernel_time(nm)[0] / args.steps, 4)
+                  for nm in ("resolution", "resolution_nn2", "resolution_brute", "resolution_sum", "iss",
+                             "iss_scatter", "iss_ordered", "iss_nms")}
+        res = ctx.cloud_resolution_dev(dx, dy, dz)
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline:
+            sys.path.insert(0, os.path.join(ROOT, "tests"))
+            import oracle_lib as O
+            threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
+            c0 = time.perf_counter()
+            ores, _ = O.cloud_resolution(x, y, z, threads=threads)
+            okp, _ = O.iss_keypoints(x, y, z, 6 * ores, 4 * ores, threads=threads)
+            csec = time.perf_counter() - c0
+            same = bool(ores == res and np.array_equal(okp, idx[:k].cpu().numpy()))
+            cpu = {"value": round(N_POINTS / csec / 1e6, 6), "unit": "Mpoints/s", "cores": threads, "kind": "port",
+                   "sample": (f"the same 1M-point scan through the CPU restatement (oracle/or_keypoints.cpp: grid "
+                              f"kNN + sequential double sum, OpenMP radius searches), {csec:.1f}s"),
+                   "parity": {"resolution": bool(ores == res), "keypoints": same}}
+        line = {
+            "metric": "Mpoints/s through ISS keypoints (Keypoints::compute ISS branch) on 1M-pt cloud",
+            "value": round(world * N_POINTS * args.steps / elapsed / 1e6, 4),
+            "unit": "Mpoints/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "f32 search, f64 scatter + eigen",
+            "data": "synthetic (synth_room: seeded pinhole room scan; see synth.py)",
+            "config": {"workload": "SURVEY 8(f) F3: computeCloudResolution + ISSKeypoint3D(6 res, 4 res, 5, 0.975, "
+                                   "0.975) on configs[2]'s 1M-pt room", "points_per_scan": N_POINTS,
+                       "resolution": res, "keypoints": int(k), "parallelism": f"scan-per-gpu x{world}"},
+            "roofline": {"bound": "hbm", "kernel": "k_iss_cov", "achieved": round(achieved, 2),
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
+                         "traffic": None, "algorithmic_bytes_per_launch": int(algo), "avg_ms": round(scat_s * 1e3, 4),
+                         "neighbors_per_launch": int(nb), "stages_ms_per_step": stages,
+                         "ordered_points": ctx.stat("iss_ordered"),
+                         "resolution_rounds": ctx.stat("resolution_rounds"),
+                         "resolution_brute": ctx.stat("resolution_brute"),
+                         "resolution_exact_sum": ctx.stat("resolution_exact_sum")},
+            "cpu_baseline": cpu,
+        }
         print(json.dumps(line), flush=True)
     ctx.close()
 

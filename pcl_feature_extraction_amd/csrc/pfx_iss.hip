@@ -15,9 +15,12 @@
 //     multiples of 2^L (L = ulp exponent of the smallest non-zero term); when the integer sum
 //     in units of 2^L stays below 2^53, every partial sum of PCL's sequential loop is exact and
 //     equals the order-free integer sum.  Otherwise one workgroup runs the sequential loop.
-//   scatter: FLANN-ordered lists at the salient radius (pfx_nblist), lane per query, the six
-//     distinct double covariance chains in list order, then Eigen 3.2.0's
-//     SelfAdjointEigenSolver<Matrix3d> restated per lane (tridiagonalisation + implicit QR).
+//   scatter: lane per point over its 3x3x3 block of the salient grid, the six distinct double
+//     covariance chains in scan order -- exact, hence equal to PCL's FLANN-order sums, whenever
+//     every partial sum is provably exact (k_iss_cov); the rest (coordinates near 0) sorted per
+//     wave into FLANN order (k_iss_ordered) or, beyond 512 neighbours, from FLANN-ordered lists
+//     (pfx_nblist).  Then Eigen 3.2.0's SelfAdjointEigenSolver<Matrix3d> restated per lane
+//     (tridiagonalisation + implicit QR).
 //   non-max suppression: lane per point on the non-max grid, third values gathered in that
 //     grid's order so candidate reads are contiguous; keypoints compacted in index order.
 #include <cstring>
@@ -98,99 +101,112 @@ __global__ void __launch_bounds__(256) k_nn2(GridView g, const int32_t* __restri
     failq[atomicAdd(n_fail, 1)] = i;
 }
 
-// exhaustive 2nd-nearest of the queued points: one workgroup per query over every finite point
+// exhaustive 2nd-nearest of the queued points: kParts workgroups per query, each over a slice
+// of every finite point, then one lane per query merges the slices
+constexpr int kParts = 64;
+
+__device__ __forceinline__ void top2_merge(float& a1, float& a2, float b1, float b2) {
+  const float n2 = fminf(fmaxf(a1, b1), fminf(a2, b2));
+  a1 = fminf(a1, b1);
+  a2 = n2;
+}
+
 __global__ void __launch_bounds__(256) k_nn2_brute(GridView g, const int32_t* __restrict__ queue,
-                                                   const int* __restrict__ n_queue, float* __restrict__ term) {
+                                                   float2* __restrict__ part) {
   __shared__ float s1[4], s2[4];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int nq = *n_queue;
+  const int q = blockIdx.x / kParts, pt = blockIdx.x % kParts;
   const int32_t nf = grid_nfinite(g);
-  for (int q = blockIdx.x; q < nq; q += gridDim.x) {
-    const int32_t i = queue[q];
-    const float qx = g.ux[i], qy = g.uy[i], qz = g.uz[i];
-    float b1 = INFINITY, b2 = INFINITY;
-    for (int32_t p = tid; p < nf; p += 256) {
-      const float4 c = g.sp[p];
-      top2(flann_d2(qx, qy, qz, c.x, c.y, c.z), b1, b2);
-    }
+  const int32_t chunk = (nf + kParts - 1) / kParts, p0 = pt * chunk, p1 = min(nf, p0 + chunk);
+  const int32_t i = queue[q];
+  const float qx = g.ux[i], qy = g.uy[i], qz = g.uz[i];
+  float b1 = INFINITY, b2 = INFINITY;
+  for (int32_t p = p0 + tid; p < p1; p += 256) {
+    const float4 c = g.sp[p];
+    top2(flann_d2(qx, qy, qz, c.x, c.y, c.z), b1, b2);
+  }
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      const float o1 = __shfl_xor(b1, o), o2 = __shfl_xor(b2, o);
-      const float n2 = fminf(fmaxf(b1, o1), fminf(b2, o2));
-      b1 = fminf(b1, o1);
-      b2 = n2;
-    }
-    if (lane == 0) {
-      s1[wv] = b1;
-      s2[wv] = b2;
-    }
-    __syncthreads();
-    if (tid == 0) {
-      float a1 = s1[0], a2 = s2[0];
-      for (int w = 1; w < 4; ++w) {
-        const float n2 = fminf(fmaxf(a1, s1[w]), fminf(a2, s2[w]));
-        a1 = fminf(a1, s1[w]);
-        a2 = n2;
-      }
-      term[i] = a2 < INFINITY ? sqrtf(a2) : __int_as_float(0x7fc00000);  // nres < 2: no term
-    }
-    __syncthreads();
+  for (int o = 32; o > 0; o >>= 1) top2_merge(b1, b2, __shfl_xor(b1, o), __shfl_xor(b2, o));
+  if (lane == 0) {
+    s1[wv] = b1;
+    s2[wv] = b2;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    for (int w = 1; w < 4; ++w) top2_merge(b1, b2, s1[w], s2[w]);
+    part[blockIdx.x] = make_float2(b1, b2);
   }
 }
 
-// [0] count, [1] min positive term bits, [2] max term bits, [3] term of a magnitude the fixed
-// point sum cannot hold, [4..5] u64 integer sum in units of 2^L, [6..7] double approximate sum
-struct ResAcc {
-  unsigned long long count;
-  unsigned int minbits, maxbits, overflow, pad;
-  unsigned long long isum;
-  double dsum;
-};
-
-__device__ __forceinline__ int term_ulp_exp(unsigned int bits) {  // exponent of the ulp of a float
-  return (int)((bits >> 23) & 0xff) - 127 - 23;
+__global__ void __launch_bounds__(64) k_nn2_brute_merge(const int32_t* __restrict__ queue, int nq,
+                                                        const float2* __restrict__ part, float* __restrict__ term) {
+  const int q = blockIdx.x * 64 + threadIdx.x;
+  if (q >= nq) return;
+  float b1 = INFINITY, b2 = INFINITY;
+  for (int k = 0; k < kParts; ++k) {
+    const float2 v = part[q * kParts + k];
+    top2_merge(b1, b2, v.x, v.y);
+  }
+  term[queue[q]] = b2 < INFINITY ? sqrtf(b2) : __int_as_float(0x7fc00000);  // nres < 2: no term
 }
 
-__global__ void __launch_bounds__(256) k_res_stats(const float* __restrict__ term, int64_t n, ResAcc* acc) {
+// Exact sum of the terms.  Per block: count, smallest positive term (its ulp exponent L_b) and
+// the integer sum in units of 2^L_b; the final pass rescales every block to the global L.
+struct ResPart {
+  unsigned long long count, isum;
+  double dsum;
+  unsigned int minbits, overflow;
+};
+struct ResAcc {
+  unsigned long long count, isum;
+  double dsum;
+  int L, exact;
+};
+
+__device__ __forceinline__ int ulp_exp(unsigned int bits) {  // exponent of the ulp of a normal float
+  return (int)((bits >> 23) & 0xff) - 150;
+}
+
+__global__ void __launch_bounds__(256) k_res_partial(const float* __restrict__ term, int64_t n,
+                                                     ResPart* __restrict__ part) {
+  __shared__ unsigned long long s_c[4], s_i[4];
+  __shared__ double s_d[4];
+  __shared__ unsigned int s_m[4], s_o[4];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int64_t stride = (int64_t)gridDim.x * 256;
   unsigned long long cnt = 0;
-  unsigned int mn = 0xffffffffu, mx = 0;
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+  unsigned int mn = 0xffffffffu;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + tid; i < n; i += stride) {
     const float t = term[i];
     if (isnan(t)) continue;
     ++cnt;
-    const unsigned int b = __float_as_uint(t);
-    if (t > 0.0f) mn = min(mn, b);
-    mx = max(mx, b);
+    if (t > 0.0f) mn = min(mn, __float_as_uint(t));
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
     cnt += __shfl_xor(cnt, o);
     mn = min(mn, (unsigned int)__shfl_xor((int)mn, o));
-    mx = max(mx, (unsigned int)__shfl_xor((int)mx, o));
   }
-  if ((threadIdx.x & 63) == 0) {
-    if (cnt) atomicAdd(&acc->count, cnt);
-    atomicMin(&acc->minbits, mn);
-    atomicMax(&acc->maxbits, mx);
+  if (lane == 0) {
+    s_c[wv] = cnt;
+    s_m[wv] = mn;
   }
-}
-
-__global__ void __launch_bounds__(256) k_res_fixed(const float* __restrict__ term, int64_t n, ResAcc* acc) {
-  const unsigned int mn = acc->minbits;
-  const int L = mn == 0xffffffffu ? 0 : term_ulp_exp(mn);
+  __syncthreads();
+  mn = min(min(s_m[0], s_m[1]), min(s_m[2], s_m[3]));
+  const int L = mn == 0xffffffffu ? 0 : ulp_exp(mn);
   unsigned long long is = 0;
   double ds = 0.0;
   unsigned int ovf = 0;
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + tid; i < n; i += stride) {
     const float t = term[i];
     if (!(t > 0.0f)) continue;  // NaN (no term) and zeros add nothing
-    const int sh = (int)((__float_as_uint(t) >> 23) & 0xff) - 127 - 23 - L;  // t = m * 2^(L + sh)
+    const unsigned int b = __float_as_uint(t);
+    const int sh = ulp_exp(b) - L;  // t = m * 2^(L + sh)
     if (sh > 39) {
       ovf = 1;
       continue;
     }
-    const unsigned long long m = (unsigned long long)((__float_as_uint(t) & 0x7fffffu) | 0x800000u);
-    is += m << sh;
+    is += (unsigned long long)((b & 0x7fffffu) | 0x800000u) << sh;
     ds += (double)t;
   }
 #pragma unroll
@@ -199,10 +215,61 @@ __global__ void __launch_bounds__(256) k_res_fixed(const float* __restrict__ ter
     ds += __shfl_xor(ds, o);
     ovf |= __shfl_xor(ovf, o);
   }
-  if ((threadIdx.x & 63) == 0) {
-    atomicAdd(&acc->isum, is);
-    atomicAdd(&acc->dsum, ds);
-    if (ovf) atomicOr(&acc->overflow, 1u);
+  if (lane == 0) {
+    s_i[wv] = is;
+    s_d[wv] = ds;
+    s_o[wv] = ovf;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    ResPart r;
+    r.count = s_c[0] + s_c[1] + s_c[2] + s_c[3];
+    r.isum = s_i[0] + s_i[1] + s_i[2] + s_i[3];  // < 2^63 each: a wrap shows in dsum below
+    r.dsum = (s_d[0] + s_d[1]) + (s_d[2] + s_d[3]);
+    r.minbits = mn;
+    r.overflow = s_o[0] | s_o[1] | s_o[2] | s_o[3];
+    part[blockIdx.x] = r;
+  }
+}
+
+// one wave: global L = min over blocks, then every block sum rescaled to 2^L (exactness checked)
+__global__ void __launch_bounds__(64) k_res_final(const ResPart* __restrict__ part, int nb, ResAcc* __restrict__ acc) {
+  const int lane = threadIdx.x;
+  unsigned int mn = 0xffffffffu;
+  for (int b = lane; b < nb; b += 64) mn = min(mn, part[b].minbits);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) mn = min(mn, (unsigned int)__shfl_xor((int)mn, o));
+  const int L = mn == 0xffffffffu ? 0 : ulp_exp(mn);
+  unsigned long long cnt = 0, is = 0;
+  double ds = 0.0;
+  int bad = 0;
+  for (int b = lane; b < nb; b += 64) {
+    const ResPart r = part[b];
+    cnt += r.count;
+    ds += r.dsum;
+    if (r.overflow) bad = 1;
+    if (r.isum == 0) continue;
+    const int sh = ulp_exp(r.minbits) - L;
+    // the block sum in units of 2^L must stay below 2^53 (and its own sum must not have wrapped)
+    if (r.dsum >= ldexp(1.0, ulp_exp(r.minbits) + 62) || sh > 52 || r.isum >= (1ull << (53 - sh))) {
+      bad = 1;
+      continue;
+    }
+    is += r.isum << sh;  // < 2^53 per block, <= 16 blocks per lane: no wrap
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    cnt += __shfl_xor(cnt, o);
+    is += __shfl_xor(is, o);
+    ds += __shfl_xor(ds, o);
+    bad |= __shfl_xor(bad, o);
+  }
+  if (lane == 0) {
+    acc->count = cnt;
+    acc->isum = is;
+    acc->dsum = ds;
+    acc->L = L;
+    acc->exact = (!bad && is < (1ull << 53)) ? 1 : 0;
   }
 }
 
@@ -350,6 +417,15 @@ __device__ void eigen_selfadjoint3(double a00, double a10, double a11, double a2
   ev[2] = d[2] * scale;
 }
 
+__device__ __forceinline__ double iss_third(double c00, double c01, double c02, double c11, double c12, double c22,
+                                            double g21, double g32) {
+  double ev[3];
+  eigen_selfadjoint3(c00, c01, c11, c02, c12, c22, ev);
+  const double e1 = ev[2], e2 = ev[1], e3 = ev[0];
+  if (isfinite(e1) && isfinite(e2) && isfinite(e3) && !(e3 < 0.0) && e2 / e1 < g21 && e3 / e2 < g32) return e3;
+  return 0.0;
+}
+
 // ISSKeypoint3D::getScatterMatrix + the eigenvalue tests, lane per query, from FLANN-ordered
 // lists: the six distinct double chains cov[a*3+b] += (p_a - c_a) * (p_b - c_b) in list order
 __global__ void __launch_bounds__(256) k_iss_scatter(GridView g, NbLists L, int min_nb, double g21, double g32,
@@ -397,12 +473,193 @@ __global__ void __launch_bounds__(256) k_iss_scatter(GridView g, NbLists L, int 
       }
     }
   }
-  double ev[3];
-  eigen_selfadjoint3(c00, c01, c11, c02, c12, c22, ev);
-  const double e1 = ev[2], e2 = ev[1], e3 = ev[0];
-  double t = 0.0;
-  if (isfinite(e1) && isfinite(e2) && isfinite(e3) && !(e3 < 0.0) && e2 / e1 < g21 && e3 / e2 < g32) t = e3;
-  third[i] = t;
+  third[i] = iss_third(c00, c01, c02, c11, c12, c22, g21, g32);
+}
+
+// ISSKeypoint3D::getScatterMatrix without neighbour lists: lane per finite point of the salient
+// grid, the block scanned in grid order.  PCL adds the terms (p_a - c_a)(p_b - c_b) in FLANN
+// order; every coordinate difference is a multiple of 2^(E - 23) (E = the smallest float
+// exponent among the coordinates involved), so every term is a multiple of 2^L, L = 2E - 46,
+// and with sum |term| <= k r^2 < 2^(L + 53) every partial sum in ANY order is exact: the scan
+// order gives PCL's result bit for bit.  Points that miss the bound (coordinates near 0) are
+// queued (oq) for k_iss_ordered.  part[block] = neighbours found (statistics).
+__global__ void __launch_bounds__(256) k_iss_cov(GridView g, float rr, int min_nb, double g21, double g32,
+                                                 double* __restrict__ third, int32_t* __restrict__ oq,
+                                                 int* __restrict__ n_mask, unsigned int* __restrict__ part) {
+  __shared__ unsigned int s_cnt[4];
+  const int tid = threadIdx.x;
+  const int64_t p = (int64_t)blockIdx.x * 256 + tid;
+  unsigned int cnt = 0;
+  if (p < grid_nfinite(g)) {
+    const float4 q = g.sp[p];
+    const int32_t i = g.perm[p];
+    const double qx = q.x, qy = q.y, qz = q.z;
+    Runs R;
+    query_runs(g, q.x, q.y, q.z, R);
+    double c00 = 0.0, c01 = 0.0, c02 = 0.0, c11 = 0.0, c12 = 0.0, c22 = 0.0;
+    unsigned int ex = (__float_as_uint(q.x) >> 23) & 0xffu, ey = (__float_as_uint(q.y) >> 23) & 0xffu,
+                 ez = (__float_as_uint(q.z) >> 23) & 0xffu;
+#pragma unroll
+    for (int r = 0; r < 9; ++r) {
+      const int32_t s = R.start[r], e = s + (R.pref[r + 1] - R.pref[r]);
+      for (int32_t c = s; c < e; ++c) {
+        const float4 v = g.sp[c];
+        if (flann_d2(q.x, q.y, q.z, v.x, v.y, v.z) < rr) {
+          ++cnt;
+          const double dx = (double)v.x - qx, dy = (double)v.y - qy, dz = (double)v.z - qz;
+          c00 += dx * dx;
+          c01 += dx * dy;
+          c02 += dx * dz;
+          c11 += dy * dy;
+          c12 += dy * dz;
+          c22 += dz * dz;
+          ex = min(ex, (__float_as_uint(v.x) >> 23) & 0xffu);
+          ey = min(ey, (__float_as_uint(v.y) >> 23) & 0xffu);
+          ez = min(ez, (__float_as_uint(v.z) >> 23) & 0xffu);
+        }
+      }
+    }
+    double t = 0.0;  // fewer than min_nb neighbours: PCL's zero matrix, NaN ratios, no value
+    if ((int)cnt >= min_nb) {
+      // per axis a: the differences are multiples of 2^(E_a - 23); chain (a, a) is exact when
+      // sum dx_a^2 < 2^(2 E_a + 7), and then chain (a, b) too (Cauchy-Schwarz)
+      const bool ok = c00 * 1.000001 < ldexp(1.0, 2 * ((int)ex - 127) + 7) &&
+                      c11 * 1.000001 < ldexp(1.0, 2 * ((int)ey - 127) + 7) &&
+                      c22 * 1.000001 < ldexp(1.0, 2 * ((int)ez - 127) + 7);
+      if (ok) {
+        t = iss_third(c00, c01, c02, c11, c12, c22, g21, g32);
+      } else {
+        oq[atomicAdd(n_mask, 1)] = (int32_t)p;
+      }
+    }
+    third[i] = t;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o);
+  if ((tid & 63) == 0) s_cnt[tid >> 6] = cnt;
+  __syncthreads();
+  if (tid == 0) part[blockIdx.x] = s_cnt[0] + s_cnt[1] + s_cnt[2] + s_cnt[3];
+}
+
+// The queued points in PCL's order: one wave per point gathers its salient neighbours as
+// (d2, index) keys into LDS, bitonic-sorts them (= FLANN's sorted result), stages their
+// coordinates, and one lane runs the sequential double chains.  More than kOrdCap neighbours:
+// the point is masked for the list path (pfx_nblist).
+constexpr int kOrdCap = 512;
+
+__global__ void __launch_bounds__(256) k_iss_ordered(GridView g, const int32_t* __restrict__ oq,
+                                                     int* __restrict__ n_oq, float rr, int min_nb, double g21,
+                                                     double g32, double* __restrict__ third,
+                                                     uint8_t* __restrict__ mask, int* __restrict__ n_over) {
+  __shared__ uint64_t s_key[4][kOrdCap];
+  __shared__ float s_c[4][3][kOrdCap];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int count = n_oq[0];
+  uint64_t* key = s_key[wv];
+  for (;;) {  // dynamic queue: the cost per point varies with the local density
+    int w = 0;
+    if (lane == 0) w = atomicAdd(n_oq + 4, 1);
+    w = __shfl(w, 0);
+    if (w >= count) break;
+    const int32_t p = oq[w];
+    const float4 q = g.sp[p];
+    const int32_t i = g.perm[p];
+    Runs R;
+    query_runs(g, q.x, q.y, q.z, R);
+    const int32_t T = R.pref[9];
+    int k = 0;
+    for (int32_t t0 = 0; t0 < T; t0 += 64) {
+      const int32_t t = t0 + lane;
+      bool hit = false;
+      uint64_t kv = 0;
+      if (t < T) {
+        const int32_t pos = run_pos(R, t);
+        const float4 v = g.sp[pos];
+        const float d2 = flann_d2(q.x, q.y, q.z, v.x, v.y, v.z);
+        hit = d2 < rr;
+        kv = nb_key(d2, g.perm[pos]);
+      }
+      const uint64_t m = __ballot(hit);
+      const int slot = k + __popcll(m & lanemask_lt());
+      if (hit && slot < kOrdCap) key[slot] = kv;
+      k += __popcll(m);
+    }
+    if (k > kOrdCap) {
+      if (lane == 0) {
+        mask[i] = 1;
+        atomicAdd(n_over, 1);
+      }
+      continue;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    if (k <= 64) {  // rank sort: lane l holds key l, its rank = keys below it (keys are distinct)
+      const uint64_t mine = lane < k ? key[lane] : ~0ull;
+      int rank = 0;
+      for (int m = 0; m < k; ++m) rank += key[m] < mine ? 1 : 0;
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      if (lane < k) key[rank] = mine;
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+    }
+    int P = 64;
+    while (P < k) P <<= 1;
+    for (int m = k + lane; m < P; m += 64) key[m] = ~0ull;
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    for (int size = 2; size <= (k <= 64 ? 1 : P); size <<= 1) {
+      for (int stride = size >> 1; stride > 0; stride >>= 1) {
+        for (int c = lane; c < (P >> 1); c += 64) {
+          const int a = 2 * stride * (c / stride) + (c % stride), b = a + stride;
+          const uint64_t ka = key[a], kb = key[b];
+          const bool asc = (a & size) == 0;
+          if ((ka > kb) == asc) {
+            key[a] = kb;
+            key[b] = ka;
+          }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+      }
+    }
+    for (int m = lane; m < k; m += 64) {
+      const int32_t j = key_idx(key[m]);
+      s_c[wv][0][m] = g.ux[j];
+      s_c[wv][1][m] = g.uy[j];
+      s_c[wv][2][m] = g.uz[j];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    if (lane == 0) {
+      const double qx = q.x, qy = q.y, qz = q.z;
+      double c00 = 0.0, c01 = 0.0, c02 = 0.0, c11 = 0.0, c12 = 0.0, c22 = 0.0;
+      for (int m = 0; m < k; ++m) {
+        const double dx = (double)s_c[wv][0][m] - qx, dy = (double)s_c[wv][1][m] - qy, dz = (double)s_c[wv][2][m] - qz;
+        c00 += dx * dx;
+        c01 += dx * dy;
+        c02 += dx * dz;
+        c11 += dy * dy;
+        c12 += dy * dz;
+        c22 += dz * dz;
+      }
+      third[i] = k >= min_nb ? iss_third(c00, c01, c02, c11, c12, c22, g21, g32) : 0.0;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();  // the LDS regions are rewritten by the next point
+  }
+}
+
+__global__ void __launch_bounds__(256) k_sum_u32(const unsigned int* __restrict__ v, int64_t n,
+                                                 unsigned long long* __restrict__ out) {
+  __shared__ unsigned long long s[4];
+  unsigned long long a = 0;
+  for (int64_t i = threadIdx.x; i < n; i += 256) a += v[i];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) a += __shfl_xor(a, o);
+  if ((threadIdx.x & 63) == 0) s[threadIdx.x >> 6] = a;
+  __syncthreads();
+  if (threadIdx.x == 0) *out = s[0] + s[1] + s[2] + s[3];
 }
 
 __global__ void __launch_bounds__(256) k_gather_third(GridView g, const double* __restrict__ third,
@@ -490,7 +747,9 @@ double cloud_resolution_dev(pfx_ctx* ctx, const float* x, const float* y, const 
     if (h_fail <= kBruteMax || rounds >= 8) {
       brute = h_fail;
       TimeScope ts(ctx, "resolution_brute");
-      k_nn2_brute<<<(unsigned)std::min(h_fail, 1024), 256, 0, st>>>(view(G), fail, nq, term);
+      float2* part = ctx->buf("res_brute").as<float2>((size_t)h_fail * kParts);
+      k_nn2_brute<<<(unsigned)(h_fail * kParts), 256, 0, st>>>(view(G), fail, part);
+      k_nn2_brute_merge<<<(unsigned)ceil_div(h_fail, 64), 64, 0, st>>>(fail, h_fail, part, term);
       check_launch("k_nn2_brute");
       break;
     }
@@ -498,22 +757,22 @@ double cloud_resolution_dev(pfx_ctx* ctx, const float* x, const float* y, const 
     fail = fail == qa ? qb : qa;
     h *= 2.0;
   }
+  const int nblk = (int)std::min<int64_t>(ceil_div(n, 256), 1024);
+  ResPart* part = ctx->buf("res_part").as<ResPart>(nblk);
   ResAcc* acc = ctx->buf("res_acc").as<ResAcc>(1);
-  ResAcc init{};
-  init.minbits = 0xffffffffu;
-  PFX_HIP(hipMemcpyAsync(acc, &init, sizeof(init), hipMemcpyHostToDevice, st));
-  const unsigned blocks = (unsigned)std::min<int64_t>(ceil_div(n, 256), 1024);
-  k_res_stats<<<blocks, 256, 0, st>>>(term, n, acc);
-  k_res_fixed<<<blocks, 256, 0, st>>>(term, n, acc);
-  check_launch("k_res_sum");
+  {
+    TimeScope ts(ctx, "resolution_sum");
+    k_res_partial<<<nblk, 256, 0, st>>>(term, n, part);
+    k_res_final<<<1, 64, 0, st>>>(part, nblk, acc);
+    check_launch("k_res_sum");
+  }
   ResAcc h_acc;
   PFX_HIP(hipMemcpyAsync(&h_acc, acc, sizeof(h_acc), hipMemcpyDeviceToHost, st));
   PFX_HIP(hipStreamSynchronize(st));
   double sum = 0.0;
-  const int L = h_acc.minbits == 0xffffffffu ? 0 : (int)((h_acc.minbits >> 23) & 0xff) - 150;
-  const bool exact = !h_acc.overflow && h_acc.dsum < std::ldexp(1.0, L + 62) && h_acc.isum < (1ull << 53);
+  const bool exact = h_acc.exact != 0;
   if (exact) {
-    sum = std::ldexp((double)h_acc.isum, L);
+    sum = std::ldexp((double)h_acc.isum, h_acc.L);
   } else {
     double* d = ctx->buf("res_seq").as<double>(1);
     k_res_sequential<<<1, 256, 0, st>>>(term, n, d);
@@ -540,20 +799,51 @@ int64_t iss_keypoints_dev(pfx_ctx* ctx, const float* x, const float* y, const fl
   double* third = third_out ? third_out : ctx->buf("iss_third").as<double>(n);
   PFX_HIP(hipMemsetAsync(third, 0, sizeof(double) * n, st));
   build_grid(ctx, K.sal, x, y, z, n, salient);
-  build_lists(ctx, K.sal, nullptr, salient, true, K.L, "iss");
-  if (K.L.nq > 0) {
+  const unsigned nb = (unsigned)ceil_div(n, 256);
+  uint8_t* mask = ctx->buf("iss_mask").as<uint8_t>(n);
+  int32_t* oq = ctx->buf("iss_oq").as<int32_t>(n);
+  // [0] queued for the ordered scatter, [1] of those beyond kOrdCap, [2..3] u64 neighbour count,
+  // [4] queue head of k_iss_ordered
+  int* n_mask = ctx->buf("iss_nmask").as<int>(6);
+  unsigned int* part = ctx->buf("iss_part").as<unsigned int>(nb);
+  PFX_HIP(hipMemsetAsync(n_mask, 0, 6 * sizeof(int), st));
+  {
     TimeScope ts(ctx, "iss_scatter");
-    k_iss_scatter<<<(unsigned)ceil_div(K.L.nq, 256), 256, 0, st>>>(view(K.sal), K.L, min_nb, g21, g32, third);
-    check_launch("k_iss_scatter");
+    k_iss_cov<<<nb, 256, 0, st>>>(view(K.sal), (float)(salient * salient), min_nb, g21, g32, third, oq, n_mask,
+                                  part);
+    k_sum_u32<<<1, 256, 0, st>>>(part, nb, reinterpret_cast<unsigned long long*>(n_mask + 2));
+    check_launch("k_iss_cov");
   }
-  ctx->stats["iss_neighbors"] = K.L.total;
+  {
+    TimeScope ts(ctx, "iss_ordered");
+    PFX_HIP(hipMemsetAsync(mask, 0, n, st));
+    // persistent: the queue length stays on the device
+    k_iss_ordered<<<1024, 256, 0, st>>>(view(K.sal), oq, n_mask, (float)(salient * salient), min_nb, g21, g32,
+                                        third, mask, n_mask + 1);
+    check_launch("k_iss_ordered");
+  }
+  int h_nm[4];
+  PFX_HIP(hipMemcpyAsync(h_nm, n_mask, sizeof(h_nm), hipMemcpyDeviceToHost, st));
+  PFX_HIP(hipStreamSynchronize(st));
+  int64_t nbrs = 0;
+  std::memcpy(&nbrs, h_nm + 2, sizeof(nbrs));
+  ctx->stats["iss_neighbors"] = nbrs;
+  ctx->stats["iss_ordered"] = h_nm[0];
+  ctx->stats["iss_ordered_lists"] = h_nm[1];
+  if (h_nm[1] > 0) {  // ordered points with more than kOrdCap neighbours: masked FLANN-ordered lists
+    TimeScope ts(ctx, "iss_ordered_lists");
+    build_lists(ctx, K.sal, mask, salient, true, K.L, "iss");
+    if (K.L.nq > 0) {
+      k_iss_scatter<<<(unsigned)ceil_div(K.L.nq, 256), 256, 0, st>>>(view(K.sal), K.L, min_nb, g21, g32, third);
+      check_launch("k_iss_scatter");
+    }
+  }
   build_grid(ctx, K.nms, x, y, z, n, non_max);
   double* tn = ctx->buf("iss_tn").as<double>(n);
   uint8_t* flag = ctx->buf("iss_flag").as<uint8_t>(n);
   PFX_HIP(hipMemsetAsync(flag, 0, n, st));
   {
     TimeScope ts(ctx, "iss_nms");
-    const unsigned nb = (unsigned)ceil_div(n, 256);
     k_gather_third<<<nb, 256, 0, st>>>(view(K.nms), third, tn);
     k_iss_nms<<<nb, 256, 0, st>>>(view(K.nms), tn, (float)(non_max * non_max), min_nb, flag);
     check_launch("k_iss_nms");

@@ -133,3 +133,16 @@ def narf_shot(ctx: Context, b: ScanBuffers, s: ShotBuffers, sample, normal_radiu
     ctx.shot_dev(b.x, b.y, b.z, b.nx, b.ny, b.nz, s.qx[:rows], s.qy[:rows], s.qz[:rows], feat_radius,
                  s.desc[:rows], s.rf[:rows])
     return rows
+
+
+def keypoints_iss(ctx: Context, x, y, z, idx, third=None) -> int:
+    """Keypoints("ISS").compute (keypoints.h:177-189): resolution = computeCloudResolution
+    (keypoints.h:401-428), then ISSKeypoint3D with salient radius 6 res, non-max radius 4 res,
+    min neighbours 5, thresholds 0.975 / 0.975.  Keypoint cloud indices (ascending) into `idx`;
+    returns their number (0 for a cloud without two finite points: the reference's ISS then
+    rejects the zero radius in initCompute and leaves the output empty)."""
+    res = ctx.cloud_resolution_dev(x, y, z)
+    if res <= 0.0:
+        return 0
+    return ctx.iss_keypoints_dev(x, y, z, 6 * res, 4 * res, idx, min_neighbors=5, threshold21=0.975,
+                                 threshold32=0.975, third=third)

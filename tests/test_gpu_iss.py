@@ -70,6 +70,8 @@ def test_surface_with_nan_and_duplicates(ctx):
     z[5::101] = np.inf
     x[1000:1300], y[1000:1300], z[1000:1300] = x[2000:2300], y[2000:2300], z[2000:2300]
     assert _check_cloud(ctx, x, y, z) > 0
+    # points within ~1 cm of the x = 0 / y = 0 planes take the FLANN-ordered list path
+    assert 0 < ctx.stat("iss_ordered") < len(x) // 4
 
 
 def test_outliers_take_the_exhaustive_path(ctx):
@@ -143,3 +145,16 @@ def test_rejected_parameters_and_capacity(ctx):
     with pytest.raises(PfxError) as e:
         ctx.iss_keypoints_dev(dx, dy, dz, 6 * res, 4 * res, small)
     assert e.value.code == 3
+
+
+def test_dense_cluster_at_origin_takes_the_list_path(ctx):
+    # a 1 mm blob of 1500 points at the origin inside a sparse surface: its points need PCL's
+    # order (coordinates near 0) and have more neighbours than the wave sort holds
+    x, y, z = _surface(20000, 7)
+    rng = np.random.default_rng(8)
+    b = (rng.random((3, 1500)) * 1e-3).astype(np.float32)
+    x = np.concatenate([x, b[0]])
+    y = np.concatenate([y, b[1]])
+    z = np.concatenate([z, b[2]])
+    _check_cloud(ctx, x, y, z)
+    assert ctx.stat("iss_ordered_lists") > 0
