@@ -520,6 +520,74 @@ class NarfKeypoint {
   Parameters parameters_;
 };
 
+// ---- ISS keypoints (keypoints.h:177-189) ------------------------------------------------------
+// ISSKeypoint3D<In, Out, NormalT>: the reference's setters, compute() -> the keypoints' xyz in
+// index order (pfx_iss_keypoints; PCL pushes them from an OpenMP loop).  A
+// parameter initCompute rejects (radius, threshold or min neighbours <= 0) -> PCL_ERROR and an
+// empty output.  Border radius / normals are not on the accelerated path (the reference sets
+// neither).
+template <typename PointInT, typename PointOutT, typename NormalT = Normal>
+class ISSKeypoint3D {
+ public:
+  typedef typename PointCloud<PointInT>::ConstPtr PointCloudInConstPtr;
+  typedef typename search::KdTree<PointInT>::Ptr KdTreePtr;
+  explicit ISSKeypoint3D(double salient_radius = 0.0001) : salient_radius_(salient_radius) {}
+  void setInputCloud(const PointCloudInConstPtr& cloud) { input_ = cloud; }
+  void setSearchMethod(const KdTreePtr& tree) { tree_ = tree; }
+  void setSalientRadius(double r) { salient_radius_ = r; }
+  void setNonMaxRadius(double r) { non_max_radius_ = r; }
+  void setMinNeighbors(int k) { min_neighbors_ = k; }
+  void setThreshold21(double t) { gamma_21_ = t; }
+  void setThreshold32(double t) { gamma_32_ = t; }
+  const std::vector<int>& getKeypointsIndices() const { return indices_; }
+  void compute(PointCloud<PointOutT>& output) {
+    output.clear();
+    indices_.clear();
+    if (!input_) {
+      PCL_ERROR("[pcl::ISSKeypoint3D::compute] no input cloud\n");
+      return;
+    }
+    if (!detail::context()) return;
+    const detail::SoA c = detail::soa_xyz(*input_);
+    std::vector<int32_t> idx(c.x.size() + 1);
+    int64_t k = 0;
+    if (!detail::ok(pfx_iss_keypoints(detail::context(), c.x.data(), c.y.data(), c.z.data(), (int64_t)c.x.size(),
+                                      salient_radius_, non_max_radius_, min_neighbors_, gamma_21_, gamma_32_,
+                                      idx.data(), (int64_t)idx.size(), &k, nullptr),
+                    "ISSKeypoint3D"))
+      return;
+    for (int64_t j = 0; j < k; ++j) {
+      PointOutT p;
+      p.x = input_->points[idx[j]].x;
+      p.y = input_->points[idx[j]].y;
+      p.z = input_->points[idx[j]].z;
+      output.push_back(p);
+      indices_.push_back(idx[j]);
+    }
+  }
+
+ private:
+  PointCloudInConstPtr input_;
+  KdTreePtr tree_;
+  double salient_radius_, non_max_radius_ = 0.0, gamma_21_ = 0.975, gamma_32_ = 0.975;
+  int min_neighbors_ = 5;
+  std::vector<int> indices_;
+};
+
+// Keypoints::computeCloudResolution (keypoints.h:401-428) is the reference's own helper; its
+// body becomes this call (same value: see DESIGN.md, F3)
+template <typename PointT>
+inline double cloudResolution(const typename PointCloud<PointT>::ConstPtr& cloud) {
+  if (!cloud || !detail::context()) return 0.0;
+  const detail::SoA c = detail::soa_xyz(*cloud);
+  double res = 0.0;
+  if (!detail::ok(pfx_cloud_resolution(detail::context(), c.x.data(), c.y.data(), c.z.data(), (int64_t)c.x.size(),
+                                       &res),
+                  "computeCloudResolution"))
+    return 0.0;
+  return res;
+}
+
 // ---- descriptor matching (features.h:224-273) ------------------------------------------------
 struct Correspondence {
   int index_query = 0;

@@ -170,6 +170,26 @@ static PointCloudRGB::Ptr narf_keypoints(const PointCloudRGB::Ptr& cloud, PointC
   return cloud_keypoints;
 }
 
+// keypoints.h:401-428, Keypoints::computeCloudResolution: the reference's own helper, its body
+// replaced by the libpfx call
+static double computeCloudResolution(const PointCloudRGB::Ptr& cloud) { return cloudResolution<PointRGB>(cloud); }
+
+// keypoints.h:177-189 (ISS branch), verbatim
+static void iss_keypoints(const PointCloudRGB::Ptr& cloud, PointCloudRGB::Ptr& cloud_keypoints) {
+  cloud_keypoints.reset(new PointCloudRGB);
+    ISSKeypoint3D<PointRGB, PointRGB> detector;
+    detector.setInputCloud(cloud);
+    search::KdTree<PointRGB>::Ptr kdtree(new search::KdTree<PointRGB>);
+    detector.setSearchMethod(kdtree);
+    double resolution = computeCloudResolution(cloud);
+    detector.setSalientRadius(6 * resolution);
+    detector.setNonMaxRadius(4 * resolution);
+    detector.setMinNeighbors(5);
+    detector.setThreshold21(0.975);
+    detector.setThreshold32(0.975);
+    detector.compute(*cloud_keypoints);
+}
+
 int main(int argc, char** argv) {
   if (argc < 3) {
     std::fprintf(stderr, "usage: %s cloud.pcd out_dir\n", argv[0]);
@@ -208,6 +228,20 @@ int main(int argc, char** argv) {
   dump(out + "/shot_rf.f32", rf.data(), rf.size());
   std::printf("points %zu keypoints %zu fpfh %zu shot %zu\n", cloud->size(), keypoints->size(), fdesc->size(),
               sdesc->size());
+
+  // ---- keypoints.h:177-189 (ISS, the reference's active list) ----
+  PointCloudRGB::Ptr iss_kp;
+  iss_keypoints(cloud, iss_kp);
+  std::vector<float> iss_xyz;
+  for (const PointRGB& p : iss_kp->points) {
+    iss_xyz.push_back(p.x);
+    iss_xyz.push_back(p.y);
+    iss_xyz.push_back(p.z);
+  }
+  dump(out + "/iss_xyz.f32", iss_xyz.data(), iss_xyz.size());
+  const double res = computeCloudResolution(cloud);
+  dump(out + "/resolution.f64", &res, 1);
+  std::printf("iss keypoints %zu\n", iss_kp->size());
 
   // ---- evaluation.cpp:342 (feat.findCorrespondences) between this cloud and a target ----
   if (argc > 3) {

@@ -63,3 +63,11 @@ def test_facade_matches_c_abi(ctx, tmp_path):
     import oracle_lib as O
     oq, om = O.correspondences(fp, tf)
     assert np.array_equal(q, oq) and np.array_equal(m, om) and len(q) > 0
+
+    # keypoints.h:177-189 (ISS branch) verbatim against the facade
+    res = np.fromfile(tmp_path / "resolution.f64", np.float64)[0]
+    ores, _ = O.cloud_resolution(x, y, z)
+    assert res == ores
+    okp, _ = O.iss_keypoints(x, y, z, 6 * ores, 4 * ores)
+    ixyz = np.fromfile(tmp_path / "iss_xyz.f32", np.float32).reshape(-1, 3)
+    assert len(okp) > 0 and np.array_equal(ixyz, np.stack([x[okp], y[okp], z[okp]], 1))
