@@ -247,16 +247,27 @@ def main():
         if os.path.exists(pmc):  # FETCH_SIZE x2 + WRITE_SIZE of k_normals_chain (scripts/gpu_pmc.sh)
             with open(pmc) as f:
                 traffic = json.load(f).get("hbm_bytes_per_launch")
-        roofline = {"bound": "hbm", "kernel": "k_normals_chain + k_normals_chain_big", "achieved": round(achieved, 2),
-                    "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
+        # basis of `achieved`: the chain kernels' own launch durations, i.e. the isolated launches
+        # (normal estimation alone on the device, right after the timed region).  Inside the step
+        # the two masked chain passes run on two streams next to NARF's kernels, so their event
+        # durations include the CU time those share; that in-step figure is reported beside it.
+        in_step = {"chain_ms_per_step": round(chain_s * 1e3, 4), "achieved": round(achieved, 2),
+                   "frac": round(achieved / HBM_PEAK_GBS, 5),
+                   "note": "sum of the two masked passes' event durations inside the timed step (concurrent "
+                           "with NARF on the other stream)"}
+        if iso_ms is not None:
+            basis_ms, basis = iso_ms, "isolated launches after the timed region (normal estimation alone)"
+        else:
+            basis_ms, basis = chain_s * 1e3, "in-step launches"
+        basis_gbs = algo_bytes / (basis_ms / 1e3) / 1e9 if basis_ms > 0 else 0.0
+        roofline = {"bound": "hbm", "kernel": "k_normals_chain + k_normals_chain_big", "achieved": round(basis_gbs, 2),
+                    "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(basis_gbs / HBM_PEAK_GBS, 5),
                     "traffic": traffic, "algorithmic_bytes_per_launch": int(algo_bytes),
-                    "chain_ms_per_step": round(chain_s * 1e3, 4), "neighbors_per_launch": int(neighbors - long_nb),
+                    "chain_ms": round(basis_ms, 4), "basis": basis,
+                    "neighbors_per_launch": int(neighbors - long_nb),
                     "long_lists": {"kernel": "k_normals_long", "lists": int(long_q), "neighbors": int(long_nb),
                                    "ms_per_step": round(timers["normals_long"][0] / args.steps, 4)},
-                    "isolated": None if iso_ms is None else {
-                        "chain_ms": round(iso_ms, 4), "achieved": round(algo_bytes / (iso_ms / 1e3) / 1e9, 2),
-                        "frac": round(algo_bytes / (iso_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 5),
-                        "note": "same kernels, normal estimation alone on the device after the timed region"},
+                    "in_step": in_step,
                     "stage": {"name": "normals: grid + FLANN-ordered lists + chains",
                               "avg_ms": round(stage_s * 1e3, 4), "achieved": round(stage_gbs, 2),
                               "frac": round(stage_gbs / HBM_PEAK_GBS, 5)}}
