@@ -16,6 +16,8 @@ features.h:224-253): mutual 1-NN between the SHOT-352 descriptor sets of two suc
 (descriptors computed before the timed region; one step = one correspondence search).
 `--workload iss` measures F3, the reference's active ISS keypoints (Keypoints::compute ISS
 branch, keypoints.h:177-189): one step = cloud resolution + ISSKeypoint3D over the 1M-point room.
+`--workload harris`: F3's Harris3D branch (keypoints.h:150-162 + getKeypointsCloud) over the same
+room: normals (r 0.01) + response + suppression + corner refinement + snap.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--workload fpfh|shot] [--no-cpu-baseline]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
@@ -100,7 +102,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--workload", choices=["fpfh", "shot", "match", "iss"], default="fpfh")
+    ap.add_argument("--workload", choices=["fpfh", "shot", "match", "iss", "harris"], default="fpfh")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
     if os.environ.get("PFX_BENCH_VERBOSE"):
@@ -129,6 +131,8 @@ def main():
         return bench_match(args, torch, dev, world, rank, local)
     if args.workload == "iss":
         return bench_iss(args, torch, dev, world, rank, local)
+    if args.workload == "harris":
+        return bench_harris(args, torch, dev, world, rank, local)
 
     shot = args.workload == "shot"
     if shot:  # configs[3]: seabed seed 3 (per-rank seeds 300 + rank at N > 1)
@@ -505,6 +509,85 @@ def bench_iss(args, torch, dev, world, rank, local):
                          "resolution_rounds": ctx.stat("resolution_rounds"),
                          "resolution_brute": ctx.stat("resolution_brute"),
                          "resolution_exact_sum": ctx.stat("resolution_exact_sum")},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    ctx.close()
+
+
+def bench_harris(args, torch, dev, world, rank, local):
+    """Keypoints("Harris3D").compute over the 1M-point room scan (one per rank)."""
+    import numpy as np
+
+    from pcl_feature_extraction_amd import Context
+    from pcl_feature_extraction_amd.pipeline import keypoints_harris3d
+    from pcl_feature_extraction_amd.synth import synth_room
+
+    x, y, z, _ = synth_room(N_POINTS, 2 if world == 1 else 100 + rank)
+    ctx = Context(local)
+    ctx.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+    dx, dy, dz = (torch.from_numpy(a).to(dev) for a in (x, y, z))
+    idx = torch.empty(N_POINTS, dtype=torch.int32, device=dev)
+    k = 0
+    for _ in range(args.warmup):
+        k = keypoints_harris3d(ctx, dx, dy, dz, idx)
+    torch.cuda.synchronize(dev)
+    ctx.set_timing(True)
+    ctx.reset_timing()
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        k = keypoints_harris3d(ctx, dx, dy, dz, idx)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        torch.distributed.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        elapsed = float(t.item())
+    if rank == 0:
+        # the response kernel: every query's FLANN-ordered list (4 B entries) and its neighbours'
+        # normals; algorithmic bytes per launch = sum_q |N_0.01(q)| x (4 + 12) B + N x 4 B
+        nb = ctx.stat("normals_neighbors")
+        tr, nr = ctx.kernel_time("harris3d_response")
+        resp_s = tr / max(nr, 1) / 1e3
+        algo = nb * 16 + N_POINTS * 4
+        achieved = algo / resp_s / 1e9 if resp_s > 0 else 0.0
+        stages = {nm: round(ctx.kernel_time(nm)[0] / args.steps, 4)
+                  for nm in ("harris3d", "normals_lists_phase", "grid_bbox", "grid_build", "normals_tiles",
+                             "normals_lists_sparse", "normals_lists_dense", "normals_lists_query", "normals_chain",
+                             "normals_chain_big", "normals_long", "harris3d_response", "harris3d_refine")}
+        corners = ctx.stat("harris3d_corners")
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline:
+            sys.path.insert(0, os.path.join(ROOT, "tests"))
+            import oracle_lib as O
+            threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
+            c0 = time.perf_counter()
+            okp, _, _ = O.harris3d(x, y, z, 0.01, 1e-6, True, threads=threads)
+            csec = time.perf_counter() - c0
+            same = bool(np.array_equal(okp, idx[:k].cpu().numpy()))
+            cpu = {"value": round(N_POINTS / csec / 1e6, 6), "unit": "Mpoints/s", "cores": threads, "kind": "port",
+                   "sample": (f"the same 1M-point scan through the CPU restatement (oracle/or_keypoints.cpp "
+                              f"orc_harris3d: OpenMP normals, responses, suppression, refinement), {csec:.1f}s"),
+                   "parity": {"keypoints": same}}
+        line = {
+            "metric": "Mpoints/s through Harris3D keypoints (Keypoints::compute HARRIS_3D branch) on 1M-pt cloud",
+            "value": round(world * N_POINTS * args.steps / elapsed / 1e6, 4),
+            "unit": "Mpoints/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic (synth_room: seeded pinhole room scan; see synth.py)",
+            "config": {"workload": "SURVEY 8(f) F3: HarrisKeypoint3D(HARRIS, r 0.01, nms, threshold 1e-6, refine) + "
+                                   "getKeypointsCloud on configs[2]'s 1M-pt room", "points_per_scan": N_POINTS,
+                       "corners": int(corners), "keypoints": int(k), "parallelism": f"scan-per-gpu x{world}"},
+            "roofline": {"bound": "hbm", "kernel": "k_harris_response + k_harris_nms", "achieved": round(achieved, 2),
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
+                         "traffic": None, "algorithmic_bytes_per_launch": int(algo), "avg_ms": round(resp_s * 1e3, 4),
+                         "neighbors_per_launch": int(nb), "stages_ms_per_step": stages},
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

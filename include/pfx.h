@@ -34,6 +34,8 @@
  *   pfx_cloud_resolution* <- Keypoints::computeCloudResolution (keypoints.h:401-428)
  *   pfx_iss_keypoints*  <- ISSKeypoint3D<PointXYZRGB,PointXYZRGB>::compute as configured by
  *                          Keypoints::compute's ISS branch (keypoints.h:177-189)
+ *   pfx_harris3d_keypoints* <- HarrisKeypoint3D<PointXYZRGB,PointXYZI>::compute + getKeypointsCloud
+ *                          (Keypoints::compute's HARRIS_3D branch, keypoints.h:150-162, 365-395)
  * ===================================================================================== */
 #ifndef PFX_H_
 #define PFX_H_
@@ -272,6 +274,22 @@ pfx_status pfx_iss_keypoints(pfx_ctx* ctx, const float* x, const float* y, const
                              double salient_radius, double non_max_radius, int32_t min_neighbors,
                              double threshold21, double threshold32, int32_t* idx, int64_t cap, int64_t* n_out,
                              double* third);
+
+/* HarrisKeypoint3D (method HARRIS) + Keypoints::getKeypointsCloud: response over the normals of
+ * the radius ball (NormalEstimation at the same radius, viewpoint 0), non-maximum suppression
+ * above `threshold`, corner refinement (refine != 0, PCL's default), then every corner snapped
+ * to its nearest cloud point when d2 < 0.0001.  idx[0..cap): those cloud indices in corner
+ * (= index) order, *n_out their number (PFX_ERR_CAPACITY when it or the corner count exceeds
+ * cap).  response (nullable, n floats): per-point intensity; corners (nullable, 3 * cap floats)
+ * and n_corners (nullable): the refined corners.  non_max == 0 -> PFX_ERR_UNSUPPORTED (not used
+ * by the reference: keypoints.h:155). */
+pfx_status pfx_harris3d_keypoints_dev(pfx_ctx* ctx, const float* d_x, const float* d_y, const float* d_z, int64_t n,
+                                      double radius, float threshold, int32_t non_max, int32_t refine,
+                                      int32_t* d_idx, int64_t cap, int64_t* n_out, float* d_response,
+                                      float* d_corners, int64_t* n_corners);
+pfx_status pfx_harris3d_keypoints(pfx_ctx* ctx, const float* x, const float* y, const float* z, int64_t n,
+                                  double radius, float threshold, int32_t non_max, int32_t refine, int32_t* idx,
+                                  int64_t cap, int64_t* n_out, float* response, float* corners, int64_t* n_corners);
 
 #ifdef __cplusplus
 } /* extern "C" */

@@ -345,3 +345,218 @@ int orc_iss_keypoints(const float* x, const float* y, const float* z, i64 n, dou
 }
 
 }  // extern "C"
+
+// =====================================================================================
+//  Harris3D: Keypoints::compute HARRIS_3D branch, keypoints.h:150-162
+//    HarrisKeypoint3D<PointXYZRGB, PointXYZI> (PCL 1.7 keypoints/impl/harris_3d.hpp), method
+//    HARRIS, radius 0.01 (constructor default), setNonMaxSupression(true), setThreshold(1e-6),
+//    refine (default true); then Keypoints::getKeypointsCloud (keypoints.h:365-395) snaps each
+//    refined corner to its nearest cloud point when that is closer than d2 < 0.0001.
+//  Per finite point i (radius r):
+//    normals: NormalEstimation at r, viewpoint 0 (the orc_normals restatement);
+//    covariance (calculateNormalCovar, SSE branch): over the neighbours with a finite normal,
+//      sequential float sums of nx*nx, ny*nx, nz*nx, ny*ny, nz*ny, nz*nz, each divided by
+//      float(count) (0 matrix without such neighbours);
+//    response: trace = (c00 + c11) + c22; when trace != 0,
+//      det = c00*c11*c22 + 2*c01*c02*c12 - c02*c02*c11 - c01*c01*c22 - c12*c12*c00 (left to right)
+//      intensity = 0.04f + det - 0.04f * trace * trace, else 0;
+//  non-maximum suppression: finite intensity >= threshold and no neighbour within r larger;
+//  refineCorners: up to 10 times, over the corner's current r-ball (finite normals),
+//    NNT += n n^T, NNTp += (n n^T) p (Matrix3f * Vector3f: ((m0 p0 + m1 p1) + m2 p2)),
+//    invert3x3SymMatrix (common/eigen.hpp: adjugate / det, det != 0), corner = NNTInv * NNTp,
+//    until |corner - previous|^2 <= 1e-6.
+//  Restatement choices (unpinned): neighbour order = FLANN's sorted (d2, index) order -- PCL's
+//  NormalEstimation and HarrisKeypoint3D search an unsorted search::KdTree(false), i.e. the
+//  kd-tree traversal order, which changes float sums in the last bits; corners in index order
+//  (PCL: omp critical order); nearest-point ties -> lowest index (FLANN: first visited).
+// =====================================================================================
+extern "C" int orc_normals(const float* x, const float* y, const float* z, i64 n, double r, float vpx, float vpy,
+                           float vpz, float* nx, float* ny, float* nz, float* curv, int nthreads);
+
+namespace {
+
+struct M3 { float m[9]; };  // column-major, as Eigen's Matrix3f coeff(k)
+
+// pcl::invert3x3SymMatrix (common/impl/eigen.hpp)
+float invert3x3Sym(const M3& a, M3& inv) {
+  const float* c = a.m;
+  const float fd_ee = c[4] * c[8] - c[7] * c[5];
+  const float ce_bf = c[2] * c[5] - c[1] * c[8];
+  const float be_cd = c[1] * c[5] - c[2] * c[4];
+  const float det = c[0] * fd_ee + c[1] * ce_bf + c[2] * be_cd;
+  if (det != 0.0f) {
+    inv.m[0] = fd_ee;
+    inv.m[1] = inv.m[3] = ce_bf;
+    inv.m[2] = inv.m[6] = be_cd;
+    inv.m[4] = c[0] * c[8] - c[2] * c[2];
+    inv.m[5] = inv.m[7] = c[1] * c[2] - c[0] * c[5];
+    inv.m[8] = c[0] * c[4] - c[1] * c[1];
+    for (int k = 0; k < 9; ++k) inv.m[k] /= det;
+  }
+  return det;
+}
+
+// Matrix3f (column-major) * Vector3f, Eigen's coefficient-based product order
+inline void mat_vec(const M3& a, const float v[3], float out[3]) {
+  for (int r = 0; r < 3; ++r) out[r] = (a.m[r] * v[0] + a.m[3 + r] * v[1]) + a.m[6 + r] * v[2];
+}
+
+float harris_response(const std::vector<int>& nb, const float* nx, const float* ny, const float* nz) {
+  float sxx = 0.f, sxy = 0.f, sxz = 0.f, syy = 0.f, syz = 0.f, szz = 0.f;
+  unsigned count = 0;
+  for (size_t m = 0; m < nb.size(); ++m) {
+    const int j = nb[m];
+    if (!std::isfinite(nx[j])) continue;
+    sxx += nx[j] * nx[j];
+    sxy += ny[j] * nx[j];
+    sxz += nz[j] * nx[j];
+    syy += ny[j] * ny[j];
+    syz += nz[j] * ny[j];
+    szz += nz[j] * nz[j];
+    ++count;
+  }
+  float c[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (count > 0) {
+    const float f = (float)count;
+    c[0] = sxx / f; c[1] = sxy / f; c[2] = sxz / f;
+    c[5] = syy / f; c[6] = syz / f; c[7] = szz / f;
+  }
+  const float trace = c[0] + c[5] + c[7];
+  if (trace == 0.0f) return 0.0f;
+  const float det = c[0] * c[5] * c[7] + 2.0f * c[1] * c[2] * c[6] - c[2] * c[2] * c[5] - c[1] * c[1] * c[7] -
+                    c[6] * c[6] * c[0];
+  return 0.04f + det - 0.04f * trace * trace;
+}
+
+}  // namespace
+
+extern "C" {
+
+// resp (nullable, n), corners (nullable, 3 * cap floats: refined xyz in corner order),
+// idx[0..cap): snapped cloud indices (getKeypointsCloud), *n_out their number, *n_corners the
+// number of corners.  Returns 3 when cap is too small.
+int orc_harris3d(const float* x, const float* y, const float* z, i64 n, double radius, float threshold, int refine,
+                 int32_t* idx, i64 cap, i64* n_out, i64* n_corners, float* resp_out, float* corners_out,
+                 int threads) {
+  *n_out = 0;
+  *n_corners = 0;
+  if (n <= 0) return 0;
+  std::vector<float> nx((size_t)n), ny((size_t)n), nz((size_t)n), cv((size_t)n), resp((size_t)n, 0.0f);
+  orc_normals(x, y, z, n, radius, 0.f, 0.f, 0.f, nx.data(), ny.data(), nz.data(), cv.data(), threads);
+  NeighborGrid g;
+  g.build(x, y, z, n, radius);
+#ifdef _OPENMP
+  if (threads > 0) omp_set_num_threads(threads);
+#endif
+#pragma omp parallel
+  {
+    std::vector<int> nb;
+    std::vector<float> dd;
+#pragma omp for schedule(dynamic, 256)
+    for (i64 i = 0; i < n; ++i) {
+      if (!finite3(x, y, z, i)) continue;
+      g.radius(x[i], y[i], z[i], radius, nb, dd);
+      resp[(size_t)i] = harris_response(nb, nx.data(), ny.data(), nz.data());
+    }
+  }
+  std::vector<char> is_max((size_t)n, 0);
+#pragma omp parallel
+  {
+    std::vector<int> nb;
+    std::vector<float> dd;
+#pragma omp for schedule(dynamic, 256)
+    for (i64 i = 0; i < n; ++i) {
+      const float v = resp[(size_t)i];
+      if (!finite3(x, y, z, i) || !std::isfinite(v) || v < threshold) continue;
+      g.radius(x[i], y[i], z[i], radius, nb, dd);
+      bool m = true;
+      for (size_t k = 0; k < nb.size() && m; ++k)
+        if (v < resp[(size_t)nb[k]]) m = false;
+      is_max[(size_t)i] = m;
+    }
+  }
+  std::vector<i64> corner_of;
+  for (i64 i = 0; i < n; ++i)
+    if (is_max[(size_t)i]) corner_of.push_back(i);
+  const i64 nc = (i64)corner_of.size();
+  std::vector<float> cx((size_t)nc), cy((size_t)nc), cz((size_t)nc);
+  for (i64 c = 0; c < nc; ++c) {
+    cx[(size_t)c] = x[corner_of[(size_t)c]];
+    cy[(size_t)c] = y[corner_of[(size_t)c]];
+    cz[(size_t)c] = z[corner_of[(size_t)c]];
+  }
+  if (refine) {
+#pragma omp parallel
+    {
+      std::vector<int> nb;
+      std::vector<float> dd;
+#pragma omp for schedule(dynamic, 16)
+      for (i64 c = 0; c < nc; ++c) {
+        float px = cx[(size_t)c], py = cy[(size_t)c], pz = cz[(size_t)c];
+        unsigned iterations = 0;
+        float diff;
+        do {
+          M3 NNT, inv;
+          float NNTp[3] = {0.f, 0.f, 0.f};
+          for (int k = 0; k < 9; ++k) NNT.m[k] = 0.f;
+          const float ox = px, oy = py, oz = pz;
+          g.radius(px, py, pz, radius, nb, dd);
+          for (size_t k = 0; k < nb.size(); ++k) {
+            const int j = nb[k];
+            if (!std::isfinite(nx[j])) continue;
+            const float nv[3] = {nx[j], ny[j], nz[j]};
+            M3 nnT;
+            for (int col = 0; col < 3; ++col)
+              for (int row = 0; row < 3; ++row) nnT.m[3 * col + row] = nv[row] * nv[col];
+            for (int e = 0; e < 9; ++e) NNT.m[e] += nnT.m[e];
+            const float p[3] = {x[j], y[j], z[j]};
+            float t[3];
+            mat_vec(nnT, p, t);
+            for (int e = 0; e < 3; ++e) NNTp[e] += t[e];
+          }
+          if (invert3x3Sym(NNT, inv) != 0.0f) {
+            float q[3];
+            mat_vec(inv, NNTp, q);
+            px = q[0]; py = q[1]; pz = q[2];
+          }
+          const float dx = px - ox, dy = py - oy, dz = pz - oz;
+          diff = (dx * dx + dy * dy) + dz * dz;
+        } while (diff > 1e-6 && ++iterations < 10);
+        cx[(size_t)c] = px; cy[(size_t)c] = py; cz[(size_t)c] = pz;
+      }
+    }
+  }
+  // getKeypointsCloud: nearest cloud point of each corner, kept when d2 < 0.0001
+  std::vector<int32_t> snap((size_t)nc, -1);
+#pragma omp parallel
+  {
+    std::vector<int> nb;
+    std::vector<float> dd;
+#pragma omp for schedule(dynamic, 64)
+    for (i64 c = 0; c < nc; ++c) {
+      const float px = cx[(size_t)c], py = cy[(size_t)c], pz = cz[(size_t)c];
+      if (!std::isfinite(px) || !std::isfinite(py) || !std::isfinite(pz)) continue;
+      g.radius(px, py, pz, radius * 1.00001, nb, dd);  // (d2, index) order: nb[0] is the nearest
+      if (!nb.empty() && (double)dd[0] < 0.0001) snap[(size_t)c] = nb[0];
+    }
+  }
+  i64 k = 0;
+  for (i64 c = 0; c < nc; ++c)
+    if (snap[(size_t)c] >= 0) {
+      if (k < cap) idx[k] = snap[(size_t)c];
+      ++k;
+    }
+  *n_out = k;
+  *n_corners = nc;
+  if (resp_out)
+    for (i64 i = 0; i < n; ++i) resp_out[i] = resp[(size_t)i];
+  if (corners_out)
+    for (i64 c = 0; c < nc && c < cap; ++c) {
+      corners_out[3 * c] = cx[(size_t)c];
+      corners_out[3 * c + 1] = cy[(size_t)c];
+      corners_out[3 * c + 2] = cz[(size_t)c];
+    }
+  return (k > cap || nc > cap) ? 3 : 0;
+}
+
+}  // extern "C"

@@ -328,3 +328,30 @@ class Context:
                                                     non_max_radius, min_neighbors, threshold21, threshold32,
                                                     _ptr(idx), idx.numel(), ctypes.byref(k), _ptr(third)))
         return k.value
+
+    def harris3d_keypoints(self, x, y, z, radius=0.01, threshold=1e-6, refine=True, non_max=True, details=False):
+        """HarrisKeypoint3D + getKeypointsCloud (keypoints.h:150-162, 365-395), host arrays: the
+        snapped cloud indices in corner order (details: and the per-point response and the
+        refined corners)."""
+        x, y, z = map(_f32, (x, y, z))
+        n = len(x)
+        cap = max(n, 1)
+        idx = np.empty(cap, np.int32)
+        resp = np.empty(cap, np.float32) if details else None
+        corners = np.empty((cap, 3), np.float32) if details else None
+        k, nc = ctypes.c_int64(), ctypes.c_int64()
+        self._check(self._lib.pfx_harris3d_keypoints(self.h, _ptr(x), _ptr(y), _ptr(z), n, radius, threshold,
+                                                     1 if non_max else 0, 1 if refine else 0, _ptr(idx), cap,
+                                                     ctypes.byref(k), _ptr(resp), _ptr(corners), ctypes.byref(nc)))
+        out = idx[: k.value].copy()
+        return (out, resp[:n].copy(), corners[: nc.value].copy()) if details else out
+
+    def harris3d_keypoints_dev(self, x, y, z, idx, radius=0.01, threshold=1e-6, refine=True, response=None,
+                               corners=None):
+        """Device version: snapped indices into `idx` (int32 tensor); returns (count, corners)."""
+        k, nc = ctypes.c_int64(), ctypes.c_int64()
+        self._check(self._lib.pfx_harris3d_keypoints_dev(self.h, _ptr(x), _ptr(y), _ptr(z), x.numel(), radius,
+                                                         threshold, 1, 1 if refine else 0, _ptr(idx), idx.numel(),
+                                                         ctypes.byref(k), _ptr(response), _ptr(corners),
+                                                         ctypes.byref(nc)))
+        return k.value, nc.value

@@ -176,6 +176,9 @@ int64_t iss_keypoints_dev(pfx_ctx* ctx, const float* x, const float* y, const fl
                           double non_max, int min_nb, double g21, double g32, int32_t* out, int64_t cap,
                           double* third_out);
 void keypoints_release(pfx_ctx* ctx);
+int64_t harris3d_dev(pfx_ctx* ctx, const float* x, const float* y, const float* z, int64_t n, double radius,
+                     float threshold, int refine, int32_t* out, int64_t cap, float* resp_out, float* corners_out,
+                     int64_t* n_corners);
 void fpfh_support_mask_dev(pfx_ctx* ctx, const float* sx, const float* sy, const float* sz, int64_t ns,
                            const float* qx, const float* qy, const float* qz, int64_t nq, double r, uint8_t* mask);
 void radius_search_dev(pfx_ctx* ctx, const float* x, const float* y, const float* z, int64_t n,

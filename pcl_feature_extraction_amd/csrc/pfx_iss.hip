@@ -31,6 +31,7 @@
 #include "pfx_internal.h"
 #include "pfx_nblist.h"
 #include "pfx_neighbors.h"
+#include "pfx_wave_sort.h"
 
 namespace pfx {
 
@@ -545,7 +546,7 @@ __global__ void __launch_bounds__(256) k_iss_cov(GridView g, float rr, int min_n
 // (d2, index) keys into LDS, bitonic-sorts them (= FLANN's sorted result), stages their
 // coordinates, and one lane runs the sequential double chains.  More than kOrdCap neighbours:
 // the point is masked for the list path (pfx_nblist).
-constexpr int kOrdCap = 512;
+constexpr int kOrdCap = kWaveSortCap;
 
 __global__ void __launch_bounds__(256) k_iss_ordered(GridView g, const int32_t* __restrict__ oq,
                                                      int* __restrict__ n_oq, float rr, int min_nb, double g21,
@@ -591,38 +592,7 @@ __global__ void __launch_bounds__(256) k_iss_ordered(GridView g, const int32_t* 
       }
       continue;
     }
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    if (k <= 64) {  // rank sort: lane l holds key l, its rank = keys below it (keys are distinct)
-      const uint64_t mine = lane < k ? key[lane] : ~0ull;
-      int rank = 0;
-      for (int m = 0; m < k; ++m) rank += key[m] < mine ? 1 : 0;
-      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      if (lane < k) key[rank] = mine;
-      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-    }
-    int P = 64;
-    while (P < k) P <<= 1;
-    for (int m = k + lane; m < P; m += 64) key[m] = ~0ull;
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    for (int size = 2; size <= (k <= 64 ? 1 : P); size <<= 1) {
-      for (int stride = size >> 1; stride > 0; stride >>= 1) {
-        for (int c = lane; c < (P >> 1); c += 64) {
-          const int a = 2 * stride * (c / stride) + (c % stride), b = a + stride;
-          const uint64_t ka = key[a], kb = key[b];
-          const bool asc = (a & size) == 0;
-          if ((ka > kb) == asc) {
-            key[a] = kb;
-            key[b] = ka;
-          }
-        }
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-      }
-    }
+    wave_sort_keys(key, k, lane);  // = FLANN's sorted result
     for (int m = lane; m < k; m += 64) {
       const int32_t j = key_idx(key[m]);
       s_c[wv][0][m] = g.ux[j];

@@ -39,6 +39,14 @@ struct NbLists {
 // lists longer than this are handled by per-query kernels downstream (normals: k_normals_long)
 constexpr int kLongList = 1024;
 
+// neighbour lists kept between the two normal-estimation phases (pfx_normals.hip) and reused
+// by the detectors that search at the normal radius (pfx_harris.hip)
+struct NormalsState {
+  NbLists L;
+  int64_t n = 0;
+  bool ready = false;
+};
+
 // mask (nullable): per *caller* index, queries are the masked points (in cell order).
 void build_lists(pfx_ctx* ctx, const Grid& g, const uint8_t* mask, double radius, bool sorted, NbLists& out,
                  const char* tag);

@@ -328,11 +328,34 @@ __device__ __forceinline__ void wave_sort(uint16_t* L, int k, float qx, float qy
   TPROF_ADD(11, w3, w4);
 }
 
+// k <= 64: one entry per lane, rank = entries with a smaller (d2, caller index) key, counted
+// over register shuffles (no buckets, no LDS scan)
+template <class Cand>
+__device__ __forceinline__ void wave_rank_sort(uint16_t* L, int k, float qx, float qy, float qz, const Cand& cand,
+                                               const GridView& g, const Runs& R, int lane) {
+  const bool in = lane < k;
+  const int t = in ? L[lane] : 0;
+  float px, py, pz;
+  cand.get(t, px, py, pz);
+  const uint32_t d = in ? __float_as_uint(flann_d2(qx, qy, qz, px, py, pz)) : 0xffffffffu;
+  const int32_t id = in ? g.perm[run_pos(R, t)] : 0x7fffffff;
+  int rank = 0;
+  for (int m = 0; m < k; ++m) {
+    const uint32_t dm = (uint32_t)__shfl((int)d, m);
+    const int32_t im = __shfl(id, m);
+    rank += (dm < d || (dm == d && im < id)) ? 1 : 0;
+  }
+  wave_sync();
+  if (in) L[rank] = (uint16_t)t;
+  wave_sync();
+}
+
 template <int NB, class Cand>
 __device__ __forceinline__ void sort_list(uint16_t* L, int k, float qx, float qy, float qz, const Cand& cand,
                                           float bscale, uint32_t* Sd, uint16_t* St, int* bcount, int* bpos,
                                           const GridView& g, const Runs& R, int lane) {
-  if (k <= 128) wave_sort_regs<NB, 2>(L, k, qx, qy, qz, cand, bscale, Sd, St, bcount, bpos, g, R, lane);
+  if (k <= 64) wave_rank_sort(L, k, qx, qy, qz, cand, g, R, lane);
+  else if (k <= 128) wave_sort_regs<NB, 2>(L, k, qx, qy, qz, cand, bscale, Sd, St, bcount, bpos, g, R, lane);
   else if (k <= 256) wave_sort_regs<NB, 4>(L, k, qx, qy, qz, cand, bscale, Sd, St, bcount, bpos, g, R, lane);
   else if (k <= 512) wave_sort_regs<NB, 8>(L, k, qx, qy, qz, cand, bscale, Sd, St, bcount, bpos, g, R, lane);
   else if (k <= 1024) wave_sort_regs<NB, 16>(L, k, qx, qy, qz, cand, bscale, Sd, St, bcount, bpos, g, R, lane);

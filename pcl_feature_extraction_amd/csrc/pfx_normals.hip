@@ -478,11 +478,6 @@ __global__ void __launch_bounds__(256) k_normals_long(GridView g, NbLists L, con
 
 }  // namespace
 
-struct NormalsState {
-  NbLists L;
-  int64_t n = 0;
-  bool ready = false;
-};
 
 void normals_release(pfx_ctx* ctx) {
   delete ctx->normals;

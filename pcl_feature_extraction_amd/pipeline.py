@@ -146,3 +146,12 @@ def keypoints_iss(ctx: Context, x, y, z, idx, third=None) -> int:
         return 0
     return ctx.iss_keypoints_dev(x, y, z, 6 * res, 4 * res, idx, min_neighbors=5, threshold21=0.975,
                                  threshold32=0.975, third=third)
+
+
+def keypoints_harris3d(ctx: Context, x, y, z, idx) -> int:
+    """Keypoints("Harris3D").compute (keypoints.h:150-162): HarrisKeypoint3D<PointXYZRGB,
+    PointXYZI> with non-maximum suppression, threshold 1e-6, radius 0.01 (the constructor's
+    default) and corner refinement, then getKeypointsCloud (keypoints.h:365-395): the snapped
+    cloud indices into `idx`; returns their number."""
+    k, _ = ctx.harris3d_keypoints_dev(x, y, z, idx, radius=0.01, threshold=1e-6, refine=True)
+    return k

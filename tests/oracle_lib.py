@@ -216,3 +216,20 @@ def iss_keypoints(x, y, z, salient_radius, non_max_radius, min_neighbors=5, gamm
         return np.empty(0, np.int32), np.zeros(n)
     assert rc == 0, rc
     return idx[: k.value].copy(), third
+
+
+def harris3d(x, y, z, radius=0.01, threshold=1e-6, refine=True, threads=0):
+    """HarrisKeypoint3D (keypoints.h:150-162) + getKeypointsCloud (keypoints.h:365-395):
+    (snapped cloud indices, per-point response, refined corners (nc, 3))."""
+    x, y, z = map(_f32, (x, y, z))
+    n = len(x)
+    cap = max(n, 1)
+    idx = np.empty(cap, np.int32)
+    resp = np.empty(max(n, 1), np.float32)
+    corners = np.empty((cap, 3), np.float32)
+    k, nc = ctypes.c_int64(), ctypes.c_int64()
+    rc = lib().orc_harris3d(_p(x), _p(y), _p(z), _i64(n), ctypes.c_double(radius), ctypes.c_float(threshold),
+                            ctypes.c_int(1 if refine else 0), _p(idx, _i32p), _i64(cap), ctypes.byref(k),
+                            ctypes.byref(nc), _p(resp), _p(corners), ctypes.c_int(threads))
+    assert rc == 0, rc
+    return idx[: k.value].copy(), resp[:n].copy(), corners[: nc.value].copy()

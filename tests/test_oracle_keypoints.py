@@ -157,3 +157,61 @@ def test_iss_rejected_parameters():
     x = np.zeros(3, np.float32)
     kp, third = O.iss_keypoints(x, x, x, 0.0, 0.1)
     assert len(kp) == 0
+
+
+def _corner_scene(n, seed):
+    rng = np.random.default_rng(seed)
+    m = n // 4
+    pts = []
+    for axis in range(3):
+        p = rng.random((m, 3)).astype(np.float32) * 0.3
+        p[:, axis] = 0.0
+        pts.append(p)
+    u, v = rng.random((2, n - 3 * m)).astype(np.float32) * 0.6
+    w = (0.01 * np.sin(40 * u) * np.cos(30 * v)).astype(np.float32) - 0.05
+    pts.append(np.stack([u, v, w], 1))
+    P = np.concatenate(pts).astype(np.float32) + rng.normal(0, 1e-4, (n, 3)).astype(np.float32)
+    return P[:, 0].copy(), P[:, 1].copy(), P[:, 2].copy()
+
+
+def test_harris3d_response_nms_and_snap():
+    """Harris3D restatement (keypoints.h:150-162, 365-395) against numpy: the response formula
+    in float32 over FLANN-ordered neighbours' normals (sampled points), the suppression rule on
+    every point, and the snap of every corner to its nearest cloud point."""
+    x, y, z = _corner_scene(3000, 6)
+    r = 0.03  # a denser ball than the reference's 0.01 on this small scene
+    kp, resp, corners = O.harris3d(x, y, z, radius=r)
+    nx, ny, nz, _ = O.normals(x, y, z, r)
+    P = np.stack([x, y, z], 1)
+    d = _flann_d2(P, P)
+    rr = np.float32(r * r)
+    f32 = np.float32
+    for i in range(0, len(x), 11):
+        nb = np.nonzero(d[i] < rr)[0]
+        nb = nb[np.lexsort((nb, d[i, nb]))]
+        s = [f32(0)] * 6
+        cnt = 0
+        for j in nb:
+            if not np.isfinite(nx[j]):
+                continue
+            a, b, c = nx[j], ny[j], nz[j]
+            s = [s[0] + a * a, s[1] + b * a, s[2] + c * a, s[3] + b * b, s[4] + c * b, s[5] + c * c]
+            cnt += 1
+        c0, c1, c2, c5, c6, c7 = [v / f32(cnt) for v in s] if cnt else [f32(0)] * 6
+        tr = c0 + c5 + c7
+        want = f32(0)
+        if tr != 0:
+            det = c0 * c5 * c7 + f32(2) * c1 * c2 * c6 - c2 * c2 * c5 - c1 * c1 * c7 - c6 * c6 * c0
+            want = f32(0.04) + det - f32(0.04) * tr * tr
+        assert np.float32(resp[i]).view(np.uint32) == np.float32(want).view(np.uint32), i
+    # suppression: corners = points with resp >= 1e-6 and no larger neighbour, in index order
+    is_max = [bool(resp[i] >= np.float32(1e-6) and not np.any(resp[d[i] < rr] > resp[i])) for i in range(len(x))]
+    assert len(corners) == sum(is_max)
+    # snap: nearest cloud point of each refined corner, kept when d2 < 1e-4
+    snapped = []
+    for c in corners:
+        dc = _flann_d2(P, c[None, :].astype(np.float32))[0]
+        j = int(np.lexsort((np.arange(len(x)), dc))[0])
+        if float(dc[j]) < 1e-4:
+            snapped.append(j)
+    assert np.array_equal(kp, np.asarray(snapped, np.int32))
