@@ -38,7 +38,8 @@ BF16_PEAK_TFLOPS = 2500.0  # dense bf16 MFMA (MI355X_MICROARCH.md: ~2.5 PF dense
 N_POINTS = 1_000_000
 SHOT_SAMPLE = 10_000
 
-VERBOSE_TIMERS = ["grid_bbox", "grid_build", "normals", "normals_lists_phase", "normals_tiles", "normals_lists", "normals_lists_sparse",
+VERBOSE_TIMERS = ["grid_bbox", "grid_build", "normals", "normals_lists_phase", "normals_tiles", "normals_lists",
+                  "normals_lists_small", "normals_lists_sparse",
                   "normals_lists_dense", "normals_lists_query", "normals_chain", "normals_chain_big", "normals_long", "range_image",
                   "narf_border", "narf_interest", "narf_nms", "narf_gather", "fpfh_mark", "fpfh_spfh",
                   "fpfh_support", "fpfh_weight", "shot"]
@@ -558,7 +559,7 @@ def bench_harris(args, torch, dev, world, rank, local):
         achieved = algo / resp_s / 1e9 if resp_s > 0 else 0.0
         stages = {nm: round(ctx.kernel_time(nm)[0] / args.steps, 4)
                   for nm in ("harris3d", "normals_lists_phase", "grid_bbox", "grid_build", "normals_tiles",
-                             "normals_lists_sparse", "normals_lists_dense", "normals_lists_query", "normals_chain",
+                             "normals_lists_small", "normals_lists_sparse", "normals_lists_dense", "normals_lists_query", "normals_chain",
                              "normals_chain_big", "normals_long", "harris3d_response", "harris3d_refine")}
         corners = ctx.stat("harris3d_corners")
         cpu = None

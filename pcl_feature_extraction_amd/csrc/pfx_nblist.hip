@@ -11,6 +11,7 @@
 // Queries of larger blocks and overflowing lists go to k_nb_query (one 256-thread workgroup per
 // query, candidates streamed from L2/HBM, <= 4096 neighbours sorted in LDS); beyond that the
 // same kernel runs with its sort arrays in global scratch (<= 262144 neighbours).
+#include <cstdlib>
 #include <cstring>
 #include <rocprim/rocprim.hpp>
 
@@ -21,6 +22,7 @@ namespace pfx {
 namespace {
 
 constexpr int kQ = 16;  // tile: consecutive queries of one cell
+constexpr int kArena = 4096;    // list entries per arena reservation of a tile workgroup
 constexpr int kTcapSparse = 1280, kTcapDense = 8000;
 constexpr int kCapQuery = 4096, kBucketsQuery = 1024;
 constexpr int kCapHuge = 1 << 18, kBucketsHuge = 4096, kHugeBlocks = 32;
@@ -370,7 +372,7 @@ __global__ void __launch_bounds__(256, STAGE ? 3 : 2) k_nb_tile(GridView g, cons
                                                  const uint32_t* __restrict__ tiles, const int* __restrict__ ntiles_ptr,
                                                  float rr, float bscale, int sorted, ListOut out,
                                                  int32_t* __restrict__ single, int* __restrict__ n_single,
-                                                 int* __restrict__ next_tile) {
+                                                 int* __restrict__ next_tile, int chunk) {
   constexpr int Q = kQ, QW = Q / 4;  // queries per tile / per wave
   __shared__ float cx[STAGE ? TCAP : 1], cy[STAGE ? TCAP : 1], cz[STAGE ? TCAP : 1];
   __shared__ uint16_t lists[Q][LCAP + 2];  // +2: odd dword row stride (no bank conflicts)
@@ -382,12 +384,20 @@ __global__ void __launch_bounds__(256, STAGE ? 3 : 2) k_nb_tile(GridView g, cons
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   __shared__ int s_tile;
   const int ntiles = *ntiles_ptr;
-  // dynamic tile queue: tile costs vary by orders of magnitude with the local density
-  for (;;) {
-    if (tid == 0) s_tile = atomicAdd(next_tile, 1);
-    __syncthreads();
-    const int64_t tile = s_tile;
-    __syncthreads();  // every thread holds `tile` before thread 0 may fetch the next one
+  // dynamic tile queue: tile costs vary by orders of magnitude with the local density.  Tiles
+  // are fetched kTileChunk at a time and the neighbour total is added once per workgroup: one
+  // queue atomic per tile made the counter's address the bottleneck when tiles are cheap (small
+  // radii); `chunk` tiles per fetch
+  unsigned long long wg_total = 0, arena_base = 0, arena_left = 0;  // thread 0's
+  int64_t tile = 0, tile_end = 0;
+  for (;; ++tile) {
+    if (tile == tile_end) {
+      if (tid == 0) s_tile = atomicAdd(next_tile, chunk);
+      __syncthreads();
+      tile = s_tile;
+      tile_end = tile + chunk;
+      __syncthreads();  // every thread holds `tile` before thread 0 may fetch the next chunk
+    }
     if (tile >= ntiles) break;
     TPROF_T(p0);
     const uint32_t te = tiles[tile];
@@ -464,10 +474,18 @@ __global__ void __launch_bounds__(256, STAGE ? 3 : 2) k_nb_tile(GridView g, cons
       maxk = (k <= LCAP && k > maxk) ? k : maxk;
     }
     if (tid == 0) {
-      s_base = maxk ? atomicAdd(out.cursor, (unsigned long long)maxk << lg) : 0ull;
-      unsigned long long sum = 0;
-      for (int j = 0; j < qn; ++j) sum += s_k[j] <= LCAP ? (unsigned long long)s_k[j] : 0ull;
-      if (sum) atomicAdd(out.cursor + 1, sum);
+      // list slots come from a per-workgroup arena reserved kArena entries at a time (one
+      // cursor atomic per arena, not per tile); unused arena tails are never read
+      const unsigned long long need = (unsigned long long)maxk << lg;
+      if (need > arena_left) {
+        const unsigned long long res = need > (unsigned long long)kArena ? need : (unsigned long long)kArena;
+        arena_base = atomicAdd(out.cursor, res);
+        arena_left = res;
+      }
+      s_base = arena_base;
+      arena_base += need;
+      arena_left -= need;
+      for (int j = 0; j < qn; ++j) wg_total += s_k[j] <= LCAP ? (unsigned long long)s_k[j] : 0ull;
     }
     if (tid < qn) {
       const int k = s_k[tid];
@@ -516,6 +534,7 @@ __global__ void __launch_bounds__(256, STAGE ? 3 : 2) k_nb_tile(GridView g, cons
     TPROF_T(p4);
     TPROF_ADD(STAGE ? 3 : 7, p3, p4);
   }
+  if (tid == 0 && wg_total) atomicAdd(out.cursor + 1, wg_total);
 }
 
 // One 256-thread workgroup per query: candidates streamed from L2/HBM, the list bucket-sorted
@@ -728,6 +747,9 @@ void build_lists(pfx_ctx* ctx, const Grid& G, const uint8_t* mask, double radius
   DevBuf& lb = B("list");
   if (!lb.ptr) lb.get(sizeof(uint32_t) * 64 * (size_t)(n + 1));
   const int isort = sorted ? 1 : 0;
+  // tiles per queue fetch (measured: 4 beats 1 at r = 0.05 too; PFX_TILE_CHUNK overrides)
+  static const char* chunk_env = getenv("PFX_TILE_CHUNK");
+  const int chunk = chunk_env ? std::max(1, atoi(chunk_env)) : 4;
   for (int attempt = 0; attempt < 2; ++attempt) {
     ListOut lo{off, cnt, lgs, static_cast<uint32_t*>(lb.ptr), cursor, lb.bytes / sizeof(uint32_t)};
     PFX_HIP(hipMemsetAsync(cursor, 0, 4 * sizeof(unsigned long long), st));
@@ -742,12 +764,12 @@ void build_lists(pfx_ctx* ctx, const Grid& G, const uint8_t* mask, double radius
       {
         TimeScope t1(ctx, std::string(tag) + "_lists_sparse");
         k_nb_tile<512, 256, kTcapSparse, true><<<256 * 3 * 4, 256, 0, st>>>(
-            g, qpos, G.skeys, sparse, counters + 0, rr, 256.0f / rr, isort, lo, single, counters + 2, counters + 5);
+            g, qpos, G.skeys, sparse, counters + 0, rr, 256.0f / rr, isort, lo, single, counters + 2, counters + 5, chunk);
       }
       {
         TimeScope t2(ctx, std::string(tag) + "_lists_dense");
         k_nb_tile<1024, 256, kTcapDense, false><<<256 * 2 * 4, 256, 0, st>>>(
-            g, qpos, G.skeys, dense, counters + 1, rr, 256.0f / rr, isort, lo, single, counters + 2, counters + 7);
+            g, qpos, G.skeys, dense, counters + 1, rr, 256.0f / rr, isort, lo, single, counters + 2, counters + 7, chunk);
       }
       {
         TimeScope t3(ctx, std::string(tag) + "_lists_query");
