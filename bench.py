@@ -101,8 +101,8 @@ def full_size_parity(outputs, kp, b, desc, rows, shot):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", choices=["fpfh", "shot", "match", "iss", "harris"], default="fpfh")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
