@@ -289,6 +289,9 @@ __global__ void __launch_bounds__(256) k_fpfh_spfh(GridView g, const float4* __r
                                                    const int64_t* __restrict__ count_ptr, float rr,
                                                    float* __restrict__ spfh, unsigned long long* __restrict__ pairs) {
   __shared__ uint32_t queue[4][128];
+  // pairs the fast path cannot bin with certainty, deferred so the (double precision, divergent)
+  // exact path runs on full waves of such pairs instead of whenever one lane of a batch needs it
+  __shared__ uint32_t slowq[4][128];
   // 16 copies of each wave's counters (lane & 15): pairs of a planar patch pile into a few bins,
   // and same-address LDS atomics serialise
   __shared__ int hist[4][kHistCopies][kDesc];
@@ -302,28 +305,52 @@ __global__ void __launch_bounds__(256) k_fpfh_spfh(GridView g, const float4* __r
     for (int i = lane; i < kHistCopies * kDesc; i += 64) (&hist[wv][0][0])[i] = 0;
     Runs R;
     query_runs(g, pc.x, pc.y, pc.z, R);
-    int k = 0, qn = 0;
-    auto process = [&](int nvalid) {
+    int k = 0, qn = 0, ns = 0;
+    // the exact path over the first nvalid deferred pairs (whole wave, one divergent call)
+    auto process_slow = [&](int nvalid) {
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
       __builtin_amdgcn_wave_barrier();
       if (lane < nvalid) {
-        const uint32_t q = queue[wv][lane];
+        const uint32_t q = slowq[wv][lane];
+        const float4 qc = g.sp[q], qnv = snp[q];
+        const int hb = pair_bins_exact(pp.x, pp.y, pp.z, pn.x, pn.y, pn.z, qc.x, qc.y, qc.z, qnv.x, qnv.y, qnv.z);
+        int* hc = hist[wv][lane & (kHistCopies - 1)];
+        atomicAdd(&hc[hb & 0xff], 1);
+        atomicAdd(&hc[kBins + ((hb >> 8) & 0xff)], 1);
+        atomicAdd(&hc[2 * kBins + (hb >> 16)], 1);
+      }
+      if (lane == 0 && nvalid > 0) atomicAdd(pairs + 1, (unsigned long long)nvalid);
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+    };
+    auto process = [&](int nvalid) {
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      bool fast = true;
+      uint32_t q = 0;
+      if (lane < nvalid) {
+        q = queue[wv][lane];
         const float4 qc = g.sp[q], qnv = snp[q];
         int h1, h2, h3;
         const f3 qp = mk3(qc.x, qc.y, qc.z), qn3 = mk3(qnv.x, qnv.y, qnv.z);
-        const bool fast = pair_bins_fast(pp, pn, qp, qn3, h1, h2, h3);
-        const uint64_t slow = __ballot(!fast);
-        if (lane == 0 && slow) atomicAdd(pairs + 1, (unsigned long long)__popcll(slow));
-        if (!fast) {
-          const int hb = pair_bins_exact(pp.x, pp.y, pp.z, pn.x, pn.y, pn.z, qp.x, qp.y, qp.z, qn3.x, qn3.y, qn3.z);
-          h1 = hb & 0xff;
-          h2 = (hb >> 8) & 0xff;
-          h3 = hb >> 16;
+        fast = pair_bins_fast(pp, pn, qp, qn3, h1, h2, h3);
+        if (fast) {
+          int* hc = hist[wv][lane & (kHistCopies - 1)];
+          atomicAdd(&hc[h1], 1);
+          atomicAdd(&hc[kBins + h2], 1);
+          atomicAdd(&hc[2 * kBins + h3], 1);
         }
-        int* hc = hist[wv][lane & (kHistCopies - 1)];
-        atomicAdd(&hc[h1], 1);
-        atomicAdd(&hc[kBins + h2], 1);
-        atomicAdd(&hc[2 * kBins + h3], 1);
+      }
+      const uint64_t m = __ballot(!fast);
+      if (!fast) slowq[wv][ns + __popcll(m & lanemask_lt())] = q;
+      ns += __popcll(m);
+      if (ns >= 64) {
+        process_slow(64);
+        const uint32_t rest = (lane + 64 < ns) ? slowq[wv][lane + 64] : 0u;
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        if (lane + 64 < ns) slowq[wv][lane] = rest;
+        ns -= 64;
       }
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
       __builtin_amdgcn_wave_barrier();
@@ -356,6 +383,7 @@ __global__ void __launch_bounds__(256) k_fpfh_spfh(GridView g, const float4* __r
     }
     }
     process(qn);
+    process_slow(ns);
     if (lane < kDesc) {
       int c = 0;
       for (int j = 0; j < kHistCopies; ++j) c += hist[wv][j][lane];
