@@ -36,6 +36,8 @@
  *                          Keypoints::compute's ISS branch (keypoints.h:177-189)
  *   pfx_harris3d_keypoints* <- HarrisKeypoint3D<PointXYZRGB,PointXYZI>::compute + getKeypointsCloud
  *                          (Keypoints::compute's HARRIS_3D branch, keypoints.h:150-162, 365-395)
+ *   pfx_ransac_rejector <- registration::CorrespondenceRejectorSampleConsensus<PointXYZRGB> in
+ *                          Features<T>::filterCorrespondences (features.h:282-297)
  * ===================================================================================== */
 #ifndef PFX_H_
 #define PFX_H_
@@ -290,6 +292,18 @@ pfx_status pfx_harris3d_keypoints_dev(pfx_ctx* ctx, const float* d_x, const floa
 pfx_status pfx_harris3d_keypoints(pfx_ctx* ctx, const float* x, const float* y, const float* z, int64_t n,
                                   double radius, float threshold, int32_t non_max, int32_t refine, int32_t* idx,
                                   int64_t cap, int64_t* n_out, float* response, float* corners, int64_t* n_corners);
+
+/* ---- RANSAC correspondence rejection --------------------------------- */
+/* CorrespondenceRejectorSampleConsensus::getCorrespondences + getBestTransformation (host
+ * arrays: the two keypoint clouds and the n correspondences index_query -> index_match):
+ * setInlierThreshold(threshold), setMaximumIterations(max_iterations).  keep[0..*n_keep) =
+ * positions of the remaining correspondences in input order (all of them when RANSAC finds no
+ * model or fewer than 3 inliers, as PCL), transformation = the best model, row-major 4x4
+ * (identity in those cases). */
+pfx_status pfx_ransac_rejector(pfx_ctx* ctx, const float* sx, const float* sy, const float* sz, int64_t ns,
+                               const float* tx, const float* ty, const float* tz, int64_t nt, const int32_t* query,
+                               const int32_t* match, int64_t n, double threshold, int32_t max_iterations,
+                               int32_t* keep, int64_t* n_keep, float* transformation);
 
 #ifdef __cplusplus
 } /* extern "C" */

@@ -355,3 +355,22 @@ class Context:
                                                          ctypes.byref(k), _ptr(response), _ptr(corners),
                                                          ctypes.byref(nc)))
         return k.value, nc.value
+
+    # ---- RANSAC correspondence rejection -----------------------------------
+    def ransac_rejector(self, src, tgt, query, match, threshold=0.015, max_iterations=1000):
+        """Features::filterCorrespondences (features.h:282-297): (kept correspondence positions in
+        input order, best 4x4 transformation).  src / tgt: (n, 3) keypoint clouds (host)."""
+        src = np.ascontiguousarray(src, np.float32)
+        tgt = np.ascontiguousarray(tgt, np.float32)
+        sx, sy, sz = (np.ascontiguousarray(src[:, i]) for i in range(3))
+        tx, ty, tz = (np.ascontiguousarray(tgt[:, i]) for i in range(3))
+        query = np.ascontiguousarray(query, np.int32)
+        match = np.ascontiguousarray(match, np.int32)
+        n = len(query)
+        keep = np.empty(max(n, 1), np.int32)
+        T = np.empty(16, np.float32)
+        nk = ctypes.c_int64()
+        self._check(self._lib.pfx_ransac_rejector(self.h, _ptr(sx), _ptr(sy), _ptr(sz), len(sx), _ptr(tx), _ptr(ty),
+                                                  _ptr(tz), len(tx), _ptr(query), _ptr(match), n, threshold,
+                                                  max_iterations, _ptr(keep), ctypes.byref(nk), _ptr(T)))
+        return keep[: nk.value].copy(), T.reshape(4, 4)

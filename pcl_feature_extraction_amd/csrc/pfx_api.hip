@@ -696,3 +696,22 @@ extern "C" pfx_status pfx_harris3d_keypoints(pfx_ctx* ctx, const float* x, const
   PFX_HIP(hipStreamSynchronize(ctx->stream));
   PFX_API_END(ctx)
 }
+
+extern "C" pfx_status pfx_ransac_rejector(pfx_ctx* ctx, const float* sx, const float* sy, const float* sz, int64_t ns,
+                                          const float* tx, const float* ty, const float* tz, int64_t nt,
+                                          const int32_t* query, const int32_t* match, int64_t n, double threshold,
+                                          int32_t max_iterations, int32_t* keep, int64_t* n_keep,
+                                          float* transformation) {
+  PFX_API_BEGIN
+  check_ctx(ctx);
+  check_points(sx, sy, sz, ns, "ransac");
+  check_points(tx, ty, tz, nt, "ransac");
+  if (n < 0 || (n && (!query || !match || !keep)) || !n_keep || !transformation || !(threshold > 0.0) ||
+      max_iterations < 0)
+    throw Error(PFX_ERR_INVALID, "ransac: invalid arguments");
+  int64_t iters = 0;
+  *n_keep = pfx::ransac_rejector(ctx, sx, sy, sz, ns, tx, ty, tz, nt, query, match, n, threshold, max_iterations,
+                                 keep, transformation, &iters);
+  ctx->stats["ransac_iterations"] = iters;
+  PFX_API_END(ctx)
+}

@@ -176,6 +176,10 @@ int64_t iss_keypoints_dev(pfx_ctx* ctx, const float* x, const float* y, const fl
                           double non_max, int min_nb, double g21, double g32, int32_t* out, int64_t cap,
                           double* third_out);
 void keypoints_release(pfx_ctx* ctx);
+int64_t ransac_rejector(pfx_ctx* ctx, const float* sx, const float* sy, const float* sz, int64_t ns,
+                        const float* tx, const float* ty, const float* tz, int64_t nt, const int32_t* query,
+                        const int32_t* match, int64_t n, double threshold, int max_iterations, int32_t* keep_out,
+                        float* T_out, int64_t* iters_out);
 int64_t harris3d_dev(pfx_ctx* ctx, const float* x, const float* y, const float* z, int64_t n, double radius,
                      float threshold, int refine, int32_t* out, int64_t cap, float* resp_out, float* corners_out,
                      int64_t* n_corners);

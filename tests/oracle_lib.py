@@ -233,3 +233,23 @@ def harris3d(x, y, z, radius=0.01, threshold=1e-6, refine=True, threads=0):
                             ctypes.byref(nc), _p(resp), _p(corners), ctypes.c_int(threads))
     assert rc == 0, rc
     return idx[: k.value].copy(), resp[:n].copy(), corners[: nc.value].copy()
+
+
+def ransac_rejector(src, tgt, query, match, threshold=0.015, max_iterations=1000):
+    """Features::filterCorrespondences (features.h:282-297): (kept correspondence positions,
+    4x4 best transformation, models evaluated).  src / tgt: (n, 3) keypoint clouds."""
+    src = np.ascontiguousarray(src, np.float32)
+    tgt = np.ascontiguousarray(tgt, np.float32)
+    sx, sy, sz = (np.ascontiguousarray(src[:, i]) for i in range(3))
+    tx, ty, tz = (np.ascontiguousarray(tgt[:, i]) for i in range(3))
+    query = np.ascontiguousarray(query, np.int32)
+    match = np.ascontiguousarray(match, np.int32)
+    n = len(query)
+    keep = np.empty(max(n, 1), np.int32)
+    nk, it = ctypes.c_int64(), ctypes.c_int64()
+    T = np.empty(16, np.float32)
+    assert lib().orc_ransac_rejector(_p(sx), _p(sy), _p(sz), _i64(len(sx)), _p(tx), _p(ty), _p(tz), _i64(len(tx)),
+                                     _p(query, _i32p), _p(match, _i32p), _i64(n), ctypes.c_double(threshold),
+                                     ctypes.c_int(max_iterations), _p(keep, _i32p), ctypes.byref(nk), _p(T),
+                                     ctypes.byref(it)) == 0
+    return keep[: nk.value].copy(), T.reshape(4, 4), it.value
