@@ -23,7 +23,7 @@ namespace {
 
 constexpr int kQ = 16;  // tile: consecutive queries of one cell
 constexpr int kArena = 4096;    // list entries per arena reservation of a tile workgroup
-constexpr int kTcapSparse = 1280, kTcapDense = 8000;
+constexpr int kTcapSmall = 384, kTcapSparse = 1280, kTcapDense = 8000;
 constexpr int kCapQuery = 4096, kBucketsQuery = 1024;
 constexpr int kCapHuge = 1 << 18, kBucketsHuge = 4096, kHugeBlocks = 32;
 
@@ -73,7 +73,8 @@ __global__ void __launch_bounds__(256) k_tile_class(GridView g, const int32_t* _
                                                     const int32_t* __restrict__ tiles,
                                                     const int64_t* __restrict__ ntiles_ptr,
                                                     uint32_t* __restrict__ sparse, uint32_t* __restrict__ dense,
-                                                    int32_t* __restrict__ single, int* __restrict__ counts) {
+                                                    uint32_t* __restrict__ small, int32_t* __restrict__ single,
+                                                    int* __restrict__ counts) {
   const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   const int64_t ntiles = *ntiles_ptr;
   const int lane = threadIdx.x & 63;
@@ -85,16 +86,20 @@ __global__ void __launch_bounds__(256) k_tile_class(GridView g, const int32_t* _
     qn = (int)(next - start < kQ ? next - start : kQ);
     Runs R;
     const int T = block_runs(g, skeys[qpos[start]], R);
-    cls = T <= kTcapSparse ? 0 : (T <= kTcapDense ? 1 : 2);
+    // 3: small tiles (<= kTcapSmall candidates, so no list can exceed them: a low-LDS kernel
+    // with more workgroups per CU), 0: sparse, 1: dense, 2: per query
+    cls = T <= kTcapSmall ? 3 : (T <= kTcapSparse ? 0 : (T <= kTcapDense ? 1 : 2));
   }
 #pragma unroll
-  for (int c = 0; c < 2; ++c) {
+  for (int c = 0; c < 4; ++c) {
+    if (c == 2) continue;
     const uint64_t m = __ballot(cls == c);
     if (!m) continue;
     int base = 0;
-    if (lane == __builtin_ctzll(m)) base = atomicAdd(&counts[c], __popcll(m));
+    const int ci = c == 3 ? 10 : c;
+    if (lane == __builtin_ctzll(m)) base = atomicAdd(&counts[ci], __popcll(m));
     base = __shfl(base, __builtin_ctzll(m));
-    if (cls == c) (c ? dense : sparse)[base + __popcll(m & lanemask_lt())] = tile_pack(start, qn);
+    if (cls == c) (c == 3 ? small : (c ? dense : sparse))[base + __popcll(m & lanemask_lt())] = tile_pack(start, qn);
   }
   int v = cls == 2 ? qn : 0, inc = v;
 #pragma unroll
@@ -352,11 +357,12 @@ __device__ __forceinline__ void wave_rank_sort(uint16_t* L, int k, float qx, flo
   wave_sync();
 }
 
-template <int NB, class Cand>
+template <int NB, class Cand, bool SMALL = false>
 __device__ __forceinline__ void sort_list(uint16_t* L, int k, float qx, float qy, float qz, const Cand& cand,
                                           float bscale, uint32_t* Sd, uint16_t* St, int* bcount, int* bpos,
                                           const GridView& g, const Runs& R, int lane) {
   if (k <= 64) wave_rank_sort(L, k, qx, qy, qz, cand, g, R, lane);
+  else if (SMALL && k > 128) wave_sort<NB>(L, k, qx, qy, qz, cand, bscale, Sd, St, bcount, bpos, g, R, lane);
   else if (k <= 128) wave_sort_regs<NB, 2>(L, k, qx, qy, qz, cand, bscale, Sd, St, bcount, bpos, g, R, lane);
   else if (k <= 256) wave_sort_regs<NB, 4>(L, k, qx, qy, qz, cand, bscale, Sd, St, bcount, bpos, g, R, lane);
   else if (k <= 512) wave_sort_regs<NB, 8>(L, k, qx, qy, qz, cand, bscale, Sd, St, bcount, bpos, g, R, lane);
@@ -367,7 +373,7 @@ __device__ __forceinline__ void sort_list(uint16_t* L, int k, float qx, float qy
 // STAGE: candidates staged in LDS (sparse tiles); otherwise read from L2 (dense tiles, where
 // staging 8000 candidates would cap the kernel at one workgroup per CU)
 template <int LCAP, int NB, int TCAP, bool STAGE>
-__global__ void __launch_bounds__(256, STAGE ? 3 : 2) k_nb_tile(GridView g, const int32_t* __restrict__ qpos,
+__global__ void __launch_bounds__(256, TCAP <= kTcapSmall ? 4 : (STAGE ? 3 : 2)) k_nb_tile(GridView g, const int32_t* __restrict__ qpos,
                                                  const uint32_t* __restrict__ skeys,
                                                  const uint32_t* __restrict__ tiles, const int* __restrict__ ntiles_ptr,
                                                  float rr, float bscale, int sorted, ListOut out,
@@ -504,8 +510,8 @@ __global__ void __launch_bounds__(256, STAGE ? 3 : 2) k_nb_tile(GridView g, cons
         if (j < qn && k <= LCAP && k > 1) {  // wave-uniform
           if (STAGE) {
             const CandLds cand{cx, cy, cz};
-            sort_list<NB>(lists[j], k, qx[u], qy[u], qz[u], cand, bscale, sd[wv], stt[wv], bcount[wv], bpos[wv],
-                          g, R, lane);
+            sort_list<NB, CandLds, (TCAP <= kTcapSmall)>(lists[j], k, qx[u], qy[u], qz[u], cand, bscale, sd[wv],
+                                                         stt[wv], bcount[wv], bpos[wv], g, R, lane);
           } else {
             const CandGlobal cand{g.sp, &R};
             sort_list<NB>(lists[j], k, qx[u], qy[u], qz[u], cand, bscale, sd[wv], stt[wv], bcount[wv], bpos[wv],
@@ -704,6 +710,7 @@ void build_lists(pfx_ctx* ctx, const Grid& G, const uint8_t* mask, double radius
   int64_t* d_ntiles = B("ntiles").as<int64_t>(1);
   uint32_t* sparse = B("sparse").as<uint32_t>(n);
   uint32_t* dense = B("dense").as<uint32_t>(n);
+  uint32_t* small = B("small").as<uint32_t>(n);
   int32_t* single = B("single").as<int32_t>(n);
   int32_t* huge = B("huge").as<int32_t>(n);
   int64_t* off = B("off").as<int64_t>(n);
@@ -711,8 +718,8 @@ void build_lists(pfx_ctx* ctx, const Grid& G, const uint8_t* mask, double radius
   uint8_t* lgs = B("lg").as<uint8_t>(n);
   // counters: 0 sparse tiles, 1 dense tiles, 2 per-query work, 3 huge work, 4 max k over cap,
   // 5 / 7 sparse / dense tile queue heads, 6 per-query work queued by the classifier (restored
-  // for a rerun), 8 / 9 per-query / huge work queue heads
-  int* counters = B("counters").as<int>(10);
+  // for a rerun), 8 / 9 per-query / huge work queue heads, 10 small tiles, 11 their queue head
+  int* counters = B("counters").as<int>(12);
   unsigned long long* cursor = B("cursor").as<unsigned long long>(4);
   size_t t1 = 0, t2 = 0, t3 = 0;
   PFX_HIP(rocprim::select(nullptr, t1, rocprim::counting_iterator<int32_t>(0), flags, qpos, d_nq, (size_t)n, st));
@@ -720,7 +727,7 @@ void build_lists(pfx_ctx* ctx, const Grid& G, const uint8_t* mask, double radius
   PFX_HIP(rocprim::select(nullptr, t3, rocprim::counting_iterator<int32_t>(0), flags, tiles, d_ntiles, (size_t)n,
                           st));
   void* tmp = B("tmp").get(std::max(t1, std::max(t2, t3)) + 16);
-  PFX_HIP(hipMemsetAsync(counters, 0, 10 * sizeof(int), st));
+  PFX_HIP(hipMemsetAsync(counters, 0, 12 * sizeof(int), st));
   const unsigned nb = (unsigned)ceil_div(n, 256);
   {
     TimeScope ts(ctx, std::string(tag) + "_tiles");
@@ -737,7 +744,8 @@ void build_lists(pfx_ctx* ctx, const Grid& G, const uint8_t* mask, double radius
     PFX_HIP(rocprim::inclusive_scan(tmp, t2, seg, seg, (size_t)n, rocprim::maximum<int32_t>(), st));
     k_tile_flags<<<nb, 256, 0, st>>>(seg, d_nq, flags, n);
     PFX_HIP(rocprim::select(tmp, t3, rocprim::counting_iterator<int32_t>(0), flags, tiles, d_ntiles, (size_t)n, st));
-    k_tile_class<<<nb, 256, 0, st>>>(g, qpos, G.skeys, d_nq, tiles, d_ntiles, sparse, dense, single, counters);
+    k_tile_class<<<nb, 256, 0, st>>>(g, qpos, G.skeys, d_nq, tiles, d_ntiles, sparse, dense, small, single,
+                                     counters);
     check_launch("nblist tiles");
     PFX_HIP(hipMemcpyAsync(counters + 6, counters + 2, sizeof(int), hipMemcpyDeviceToDevice, st));
   }
@@ -757,10 +765,17 @@ void build_lists(pfx_ctx* ctx, const Grid& G, const uint8_t* mask, double radius
       PFX_HIP(hipMemcpyAsync(counters + 2, counters + 6, sizeof(int), hipMemcpyDeviceToDevice, st));
       PFX_HIP(hipMemsetAsync(counters + 3, 0, 3 * sizeof(int), st));  // huge, max k, sparse queue
       PFX_HIP(hipMemsetAsync(counters + 7, 0, 3 * sizeof(int), st));  // dense, query, huge queues
+      PFX_HIP(hipMemsetAsync(counters + 11, 0, sizeof(int), st));      // small queue
     }
     int h_cnt[8];
     {
       TimeScope ts(ctx, std::string(tag) + "_lists");
+      {
+        TimeScope t0(ctx, std::string(tag) + "_lists_small");
+        k_nb_tile<kTcapSmall, 64, kTcapSmall, true><<<256 * 4 * 2, 256, 0, st>>>(
+            g, qpos, G.skeys, small, counters + 10, rr, 64.0f / rr, isort, lo, single, counters + 2, counters + 11,
+            chunk);
+      }
       {
         TimeScope t1(ctx, std::string(tag) + "_lists_sparse");
         k_nb_tile<512, 256, kTcapSparse, true><<<256 * 3 * 4, 256, 0, st>>>(
