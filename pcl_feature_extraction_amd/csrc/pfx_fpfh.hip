@@ -95,8 +95,8 @@ __device__ __forceinline__ void pair_bins(f3 p1, f3 n1, f3 p2, f3 n2, int& h1, i
 
 // c sequential float additions of incr starting from 0 (PCL's hist_incr loop), in O(binades):
 // inside a binade of s every step adds the same multiple of ulp(s) (incr's position between two
-// grid points does not depend on s) unless incr is an exact half-way case, which falls back to
-// the loop; steps that would reach the next binade are taken one by one.
+// grid points does not depend on s; an exact half-way case needs one step first, see below);
+// steps that would reach the next binade are taken one by one.
 __device__ __forceinline__ float repeated_add(float incr, int c) {
   float s = 0.0f;
   int rem = c;
@@ -107,9 +107,13 @@ __device__ __forceinline__ float repeated_add(float incr, int c) {
     const int e = ilogbf(s);
     const double ulp = ldexp(1.0, e - 23), top = ldexp(1.0, e + 1);
     const double t = (double)incr / ulp;
-    if (t - floor(t) == 0.5) {  // tie: the step depends on the parity of s
-      for (; rem > 0; --rem) s = s + incr;
-      break;
+    if (t - floor(t) == 0.5) {
+      // tie: s + incr rounds to even, so one more step leaves s an even multiple of ulp, and from
+      // there every step inside this binade adds the same amount (checked against the plain loop
+      // for 100 / (k - 1), k < 6000, and random increments)
+      s = s + incr;
+      --rem;
+      if (rem == 0 || ilogbf(s) != e) continue;
     }
     const double delta = (double)(s + incr) - (double)s;
     if (delta <= 0.0) {  // s no longer changes
@@ -282,16 +286,21 @@ __global__ void k_all_finite(const uint32_t* __restrict__ skeys, int64_t n, uint
   if (i < n) flags[i] = (uint64_t)skeys[i] < ncells;
 }
 
-// One wave per S point (sorted position): candidates tested in runs, hits other than the point
-// itself compacted into a wave-private LDS queue and evaluated 64 pairs at a time.
-__global__ void __launch_bounds__(256) k_fpfh_spfh(GridView g, const float4* __restrict__ snp,
-                                                   const int32_t* __restrict__ slist,
-                                                   const int64_t* __restrict__ count_ptr, float rr,
-                                                   float* __restrict__ spfh, unsigned long long* __restrict__ pairs) {
+// One wave per S point (sorted position, slist[w]): candidates tested in runs, hits other than
+// the point itself compacted into a wave-private LDS queue and binned 64 pairs at a time by the
+// fast path.  Pairs the fast path cannot bin with certainty go to a global queue for
+// k_fpfh_exact (no call to the double-precision path here: fewer registers, more waves); the
+// integer bin counts and |N| go to hcount / kcount, k_fpfh_finalize turns them into PCL's floats.
+#ifndef PFX_SPFH_WPE
+#define PFX_SPFH_WPE 8
+#endif
+__global__ void __launch_bounds__(256, PFX_SPFH_WPE) k_fpfh_spfh(GridView g, const float4* __restrict__ snp,
+                                                      const int32_t* __restrict__ slist,
+                                                      const int64_t* __restrict__ count_ptr, float rr,
+                                                      int* __restrict__ hcount, int* __restrict__ kcount,
+                                                      int2* __restrict__ slowq, unsigned* __restrict__ n_slow,
+                                                      unsigned slow_cap, unsigned long long* __restrict__ pairs) {
   __shared__ uint32_t queue[4][128];
-  // pairs the fast path cannot bin with certainty, deferred so the (double precision, divergent)
-  // exact path runs on full waves of such pairs instead of whenever one lane of a batch needs it
-  __shared__ uint32_t slowq[4][128];
   // 16 copies of each wave's counters (lane & 15): pairs of a planar patch pile into a few bins,
   // and same-address LDS atomics serialise
   __shared__ int hist[4][kHistCopies][kDesc];
@@ -305,24 +314,7 @@ __global__ void __launch_bounds__(256) k_fpfh_spfh(GridView g, const float4* __r
     for (int i = lane; i < kHistCopies * kDesc; i += 64) (&hist[wv][0][0])[i] = 0;
     Runs R;
     query_runs(g, pc.x, pc.y, pc.z, R);
-    int k = 0, qn = 0, ns = 0;
-    // the exact path over the first nvalid deferred pairs (whole wave, one divergent call)
-    auto process_slow = [&](int nvalid) {
-      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      if (lane < nvalid) {
-        const uint32_t q = slowq[wv][lane];
-        const float4 qc = g.sp[q], qnv = snp[q];
-        const int hb = pair_bins_exact(pp.x, pp.y, pp.z, pn.x, pn.y, pn.z, qc.x, qc.y, qc.z, qnv.x, qnv.y, qnv.z);
-        int* hc = hist[wv][lane & (kHistCopies - 1)];
-        atomicAdd(&hc[hb & 0xff], 1);
-        atomicAdd(&hc[kBins + ((hb >> 8) & 0xff)], 1);
-        atomicAdd(&hc[2 * kBins + (hb >> 16)], 1);
-      }
-      if (lane == 0 && nvalid > 0) atomicAdd(pairs + 1, (unsigned long long)nvalid);
-      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-    };
+    int k = 0, qn = 0;
     auto process = [&](int nvalid) {
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
       __builtin_amdgcn_wave_barrier();
@@ -342,15 +334,12 @@ __global__ void __launch_bounds__(256) k_fpfh_spfh(GridView g, const float4* __r
         }
       }
       const uint64_t m = __ballot(!fast);
-      if (!fast) slowq[wv][ns + __popcll(m & lanemask_lt())] = q;
-      ns += __popcll(m);
-      if (ns >= 64) {
-        process_slow(64);
-        const uint32_t rest = (lane + 64 < ns) ? slowq[wv][lane + 64] : 0u;
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        if (lane + 64 < ns) slowq[wv][lane] = rest;
-        ns -= 64;
+      if (m) {
+        unsigned base = 0;
+        if (lane == 0) base = atomicAdd(n_slow, (unsigned)__popcll(m));
+        base = __shfl(base, 0);
+        const unsigned slot = base + __popcll(m & lanemask_lt());
+        if (!fast && slot < slow_cap) slowq[slot] = make_int2((int)w, (int)q);
       }
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
       __builtin_amdgcn_wave_barrier();
@@ -359,40 +348,76 @@ __global__ void __launch_bounds__(256) k_fpfh_spfh(GridView g, const float4* __r
 #pragma unroll
     for (int r = 0; r < 9; ++r) {
       const int32_t rs = R.start[r], rn = R.pref[r + 1] - R.pref[r];
-    for (int32_t t0 = 0; t0 < rn; t0 += 64) {
-      const int32_t t = t0 + lane;
-      bool hit = false;
-      const int32_t pos = rs + t;
-      if (t < rn) {
-        const float4 c = g.sp[pos];
-        hit = flann_d2(pc.x, pc.y, pc.z, c.x, c.y, c.z) < rr;
+      for (int32_t t0 = 0; t0 < rn; t0 += 64) {
+        const int32_t t = t0 + lane;
+        bool hit = false;
+        const int32_t pos = rs + t;
+        if (t < rn) {
+          const float4 c = g.sp[pos];
+          hit = flann_d2(pc.x, pc.y, pc.z, c.x, c.y, c.z) < rr;
+        }
+        k += __popcll(__ballot(hit));
+        const bool push = hit && pos != s;
+        const uint64_t m = __ballot(push);
+        if (push) queue[wv][qn + __popcll(m & lanemask_lt())] = (uint32_t)pos;
+        qn += __popcll(m);
+        if (qn >= 64) {
+          process(64);
+          const uint32_t rest = (lane + 64 < qn) ? queue[wv][lane + 64] : 0u;
+          __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+          __builtin_amdgcn_wave_barrier();
+          if (lane + 64 < qn) queue[wv][lane] = rest;
+          qn -= 64;
+        }
       }
-      k += __popcll(__ballot(hit));
-      const bool push = hit && pos != s;
-      const uint64_t m = __ballot(push);
-      if (push) queue[wv][qn + __popcll(m & lanemask_lt())] = (uint32_t)pos;
-      qn += __popcll(m);
-      if (qn >= 64) {
-        process(64);
-        const uint32_t rest = (lane + 64 < qn) ? queue[wv][lane + 64] : 0u;
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        if (lane + 64 < qn) queue[wv][lane] = rest;
-        qn -= 64;
-      }
-    }
     }
     process(qn);
-    process_slow(ns);
     if (lane < kDesc) {
       int c = 0;
       for (int j = 0; j < kHistCopies; ++j) c += hist[wv][j][lane];
-      const float incr = 100.0f / (float)(k - 1);
-      spfh[(int64_t)g.perm[s] * kDesc + lane] = repeated_add(incr, c);
+      hcount[w * kDesc + lane] = c;
     }
-    if (lane == 0) atomicAdd(pairs, (unsigned long long)(k - 1));
+    if (lane == 0) {
+      kcount[w] = k;
+      atomicAdd(pairs, (unsigned long long)(k - 1));
+    }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
+  }
+}
+
+// the deferred pairs through the exact path (double precision), one lane each
+__global__ void __launch_bounds__(256) k_fpfh_exact(GridView g, const float4* __restrict__ snp,
+                                                    const int32_t* __restrict__ slist,
+                                                    const int2* __restrict__ slowq, const unsigned* __restrict__ n_slow,
+                                                    unsigned slow_cap, int* __restrict__ hcount,
+                                                    unsigned long long* __restrict__ pairs) {
+  const unsigned n = min(*n_slow, slow_cap);  // over capacity: the host reruns with a larger queue
+  const unsigned i = blockIdx.x * 256 + threadIdx.x;
+  if (i == 0) atomicAdd(pairs + 1, (unsigned long long)n);
+  for (unsigned j = i; j < n; j += gridDim.x * 256) {
+    const int2 e = slowq[j];
+    const int32_t s = slist[e.x];
+    const float4 pc = g.sp[s], pnc = snp[s], qc = g.sp[e.y], qnv = snp[e.y];
+    const int hb = pair_bins_exact(pc.x, pc.y, pc.z, pnc.x, pnc.y, pnc.z, qc.x, qc.y, qc.z, qnv.x, qnv.y, qnv.z);
+    int* hc = hcount + (int64_t)e.x * kDesc;
+    atomicAdd(&hc[hb & 0xff], 1);
+    atomicAdd(&hc[kBins + ((hb >> 8) & 0xff)], 1);
+    atomicAdd(&hc[2 * kBins + (hb >> 16)], 1);
+  }
+}
+
+// PCL's float histogram: hist[b] += 100 / (|N| - 1) once per pair (repeated_add), per S point
+__global__ void __launch_bounds__(256) k_fpfh_finalize(GridView g, const int32_t* __restrict__ slist,
+                                                       const int64_t* __restrict__ count_ptr,
+                                                       const int* __restrict__ hcount,
+                                                       const int* __restrict__ kcount, float* __restrict__ spfh) {
+  const int64_t count = *count_ptr;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < count * kDesc; e += (int64_t)gridDim.x * 256) {
+    const int64_t w = e / kDesc;
+    const int b = (int)(e - w * kDesc);
+    const float incr = 100.0f / (float)(kcount[w] - 1);
+    spfh[(int64_t)g.perm[slist[w]] * kDesc + b] = repeated_add(incr, hcount[e]);
   }
 }
 
@@ -626,30 +651,47 @@ void fpfh_dev(pfx_ctx* ctx, const float* sx, const float* sy, const float* sz, c
     PFX_HIP(rocprim::select(tmp, tmp_bytes, rocprim::counting_iterator<int32_t>(0), flags, slist, d_sel,
                             (size_t)ns, st));
   }
-  int* err = ctx->buf("fpfh_err").as<int>(8);  // [0] k over capacity, [1] max k, [2] inexact sums, [4..5] pairs
-  PFX_HIP(hipMemsetAsync(err, 0, 8 * sizeof(int), st));
+  int* err = ctx->buf("fpfh_err").as<int>(8);  // [0] k over capacity, [1] max k, [2] inexact sums, [3] deferred pairs, [4..7] pairs
   unsigned long long* d_pairs = reinterpret_cast<unsigned long long*>(err + 4);
-  {
-    // the S count stays on the device: a grid-stride launch sized for the worst case
-    TimeScope ts(ctx, "fpfh_spfh");
-    const int64_t waves = std::min<int64_t>(ns, 256 * 4 * 20);  // up to 20 waves per CU in flight
-    k_fpfh_spfh<<<(unsigned)std::max<int64_t>(8, ceil_div(waves, 4) & ~7), 256, 0, st>>>(g, snp, slist, d_sel, rr,
-                                                                                          spfh, d_pairs);
-    check_launch("k_fpfh_spfh");
-  }
-  {
-    TimeScope ts(ctx, "fpfh_weight");
-    const size_t lds = sizeof(uint64_t) * kCapW;
-    PFX_HIP(hipFuncSetAttribute((const void*)k_fpfh_weight, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    const unsigned blocks = (unsigned)std::min<int64_t>(nq, 256 * 2);
-    k_fpfh_weight<<<blocks, kWT, lds, st>>>(g, qx, qy, qz, nq, rr, spfh, out, err);
-    check_launch("k_fpfh_weight");
-  }
+  unsigned* n_slow = reinterpret_cast<unsigned*>(err + 3);
+  int* hcount = ctx->buf("fpfh_hcount").as<int>(ns * kDesc);
+  int* kcount = ctx->buf("fpfh_kcount").as<int>(ns);
   int h[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   int64_t count = 0;
-  PFX_HIP(hipMemcpyAsync(h, err, sizeof(h), hipMemcpyDeviceToHost, st));
-  PFX_HIP(hipMemcpyAsync(&count, d_sel, sizeof(int64_t), hipMemcpyDeviceToHost, st));
-  PFX_HIP(hipStreamSynchronize(st));
+  // deferred pairs are rare (cancellation near bin edges); a cloud that overflows the queue is
+  // run once more with a queue of the size it reported
+  int64_t reruns = 0;
+  const char* cap_env = getenv("PFX_FPFH_SLOW_CAP");  // test hook: forces the rerun path
+  for (unsigned slow_cap = cap_env ? (unsigned)std::max(1, atoi(cap_env)) : 1u << 20;;) {
+    PFX_HIP(hipMemsetAsync(err, 0, 8 * sizeof(int), st));
+    int2* slowq = ctx->buf("fpfh_slowq").as<int2>(slow_cap);
+    {
+      // the S count stays on the device: grid-stride launches sized for the worst case
+      TimeScope ts(ctx, "fpfh_spfh");
+      const int64_t waves = std::min<int64_t>(ns, 256 * 4 * 32);  // up to 32 waves per CU in flight
+      k_fpfh_spfh<<<(unsigned)std::max<int64_t>(8, ceil_div(waves, 4) & ~7), 256, 0, st>>>(
+          g, snp, slist, d_sel, rr, hcount, kcount, slowq, n_slow, slow_cap, d_pairs);
+      k_fpfh_exact<<<256, 256, 0, st>>>(g, snp, slist, slowq, n_slow, slow_cap, hcount, d_pairs);
+      k_fpfh_finalize<<<(unsigned)std::min<int64_t>(ceil_div(ns * kDesc, 256), 4096), 256, 0, st>>>(
+          g, slist, d_sel, hcount, kcount, spfh);
+      check_launch("k_fpfh_spfh");
+    }
+    {
+      TimeScope ts(ctx, "fpfh_weight");
+      const size_t lds = sizeof(uint64_t) * kCapW;
+      PFX_HIP(hipFuncSetAttribute((const void*)k_fpfh_weight, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+      const unsigned blocks = (unsigned)std::min<int64_t>(nq, 256 * 2);
+      k_fpfh_weight<<<blocks, kWT, lds, st>>>(g, qx, qy, qz, nq, rr, spfh, out, err);
+      check_launch("k_fpfh_weight");
+    }
+    PFX_HIP(hipMemcpyAsync(h, err, sizeof(h), hipMemcpyDeviceToHost, st));
+    PFX_HIP(hipMemcpyAsync(&count, d_sel, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+    PFX_HIP(hipStreamSynchronize(st));
+    if ((unsigned)h[3] <= slow_cap) break;
+    slow_cap = (unsigned)h[3];
+    ++reruns;
+  }
+  ctx->stats["fpfh_spfh_reruns"] = reruns;
   ctx->stats["fpfh_spfh_points"] = count;
   {
     unsigned long long pr;

@@ -170,3 +170,19 @@ def test_config1_normals_fpfh_all_points():
         d = c.fpfh(x, y, z, g[0], g[1], g[2], None, None, None, 0.05, same_as_surface=True)
     od = O.fpfh(x, y, z, o[0], o[1], o[2], x, y, z, 0.05, same_as_surface=True, threads=8)
     assert _nan_aware_equal(d, od)
+
+
+def test_fpfh_deferred_pair_queue_overflow(ctx, monkeypatch):
+    """Pairs the fast binning path cannot certify are queued for the exact path; a queue too
+    small for the cloud makes fpfh_dev rerun with the reported size -- same descriptors."""
+    x, y, z = _cloud("indoor_source")
+    nx, ny, nz, _ = O.normals(x, y, z, 0.05)
+    rng = np.random.default_rng(6)
+    q = np.sort(rng.choice(len(x), 400, replace=False))
+    base = ctx.fpfh(x, y, z, nx, ny, nz, x[q], y[q], z[q], 0.08)
+    assert ctx.stat("fpfh_spfh_exact_pairs") > 4 and ctx.stat("fpfh_spfh_reruns") == 0
+    monkeypatch.setenv("PFX_FPFH_SLOW_CAP", "4")
+    g = ctx.fpfh(x, y, z, nx, ny, nz, x[q], y[q], z[q], 0.08)
+    assert ctx.stat("fpfh_spfh_reruns") == 1
+    assert _nan_aware_equal(g, base)
+    assert _nan_aware_equal(g, O.fpfh(x, y, z, nx, ny, nz, x[q], y[q], z[q], 0.08))
