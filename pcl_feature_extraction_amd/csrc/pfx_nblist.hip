@@ -546,6 +546,15 @@ __global__ void __launch_bounds__(256, TCAP <= kTcapSmall ? 4 : (STAGE ? 3 : 2))
 // One 256-thread workgroup per query: candidates streamed from L2/HBM, the list bucket-sorted
 // in LDS (GLOBAL = false) or in a per-workgroup global scratch slice (GLOBAL = true).
 // Lists longer than CAP go to `over` (or raise err when over == nullptr).
+// list entry of grid position p: (run << 28) | offset in the run
+__device__ __forceinline__ uint32_t pos_entry(const Runs& R, int32_t p) {
+  uint32_t e = 0;
+#pragma unroll
+  for (int r = 0; r < 9; ++r)
+    if (p >= R.start[r] && p < R.start[r] + (R.pref[r + 1] - R.pref[r])) e = ((uint32_t)r << 28) | (uint32_t)(p - R.start[r]);
+  return e;
+}
+
 template <int CAP, int NB, bool GLOBAL>
 __global__ void __launch_bounds__(256) k_nb_query(GridView g, const int32_t* __restrict__ qpos,
                                                   const uint32_t* __restrict__ skeys,
@@ -561,7 +570,7 @@ __global__ void __launch_bounds__(256) k_nb_query(GridView g, const int32_t* __r
   uint32_t* base_arr = GLOBAL ? scratch + (size_t)blockIdx.x * 4 * CAP : smem;
   uint32_t* hits = base_arr;        // positions, then the sorted list
   uint32_t* hd = base_arr + CAP;    // d2 bits of hits
-  uint32_t* sdv = base_arr + 2 * CAP;
+  uint32_t* sdv = base_arr + 2 * CAP;  // (GLOBAL: bucket-ordered copies)
   uint32_t* spv = base_arr + 3 * CAP;
   const int tid = threadIdx.x;
   const int count = *n_ptr;
@@ -616,6 +625,17 @@ __global__ void __launch_bounds__(256) k_nb_query(GridView g, const int32_t* __r
       __syncthreads();
       continue;
     }
+    if (tid == 0) {
+      s_base = k ? atomicAdd(out.cursor, (unsigned long long)k) : 0ull;
+      if (k) atomicAdd(out.cursor + 1, (unsigned long long)k);
+      if (k > kLongList) {
+        atomicAdd(out.cursor + 2, (unsigned long long)k);
+        atomicAdd(out.cursor + 3, 1ull);
+      }
+      out.off[j] = (int64_t)s_base;
+      out.cnt[j] = k;
+      out.lg[j] = 0;
+    }
     if (sorted && k > 1) {
       for (int e = tid; e < k; e += 256) {
         const int b = (int)(__uint_as_float(hd[e]) * bscale);
@@ -636,53 +656,75 @@ __global__ void __launch_bounds__(256) k_nb_query(GridView g, const int32_t* __r
         for (int v = 0; v < PER; ++v) { bpos[tid * PER + v] = ex; ex += bcount[tid * PER + v]; }
       }
       __syncthreads();
-      for (int e = tid; e < k; e += 256) {
-        const uint32_t d = hd[e];
-        int b = (int)(__uint_as_float(d) * bscale);
-        b = b < NB ? b : NB - 1;
-        const int slot = atomicAdd(&bpos[b], 1);
-        sdv[slot] = d;
-        spv[slot] = hits[e];
-      }
-      __syncthreads();
-      for (int s = tid; s < k; s += 256) {
-        const uint32_t d = sdv[s], p = spv[s];
-        int b = (int)(__uint_as_float(d) * bscale);
-        b = b < NB ? b : NB - 1;
-        const int en = bpos[b], st = en - bcount[b];
-        int rank = 0;
-        for (int v = st; v < en; ++v) {
-          const uint32_t dv = sdv[v];
-          if (dv < d) ++rank;
-          else if (dv == d && v != s && g.perm[spv[v]] < g.perm[p]) ++rank;
+      if constexpr (!GLOBAL) {
+        // bucket scatter in place through registers (8 B of LDS per entry: 4 workgroups per CU)
+        constexpr int PT = CAP / 256;
+        uint32_t rp[PT], rd[PT];
+#pragma unroll
+        for (int u = 0; u < PT; ++u) {
+          const int e = tid + u * 256;
+          rp[u] = e < k ? hits[e] : 0u;
+          rd[u] = e < k ? hd[e] : 0u;
         }
-        hits[st + rank] = p;
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < PT; ++u) {
+          if (tid + u * 256 < k) {
+            int b = (int)(__uint_as_float(rd[u]) * bscale);
+            b = b < NB ? b : NB - 1;
+            const int slot = atomicAdd(&bpos[b], 1);
+            hd[slot] = rd[u];
+            hits[slot] = rp[u];
+          }
+        }
+        __syncthreads();
+        const int64_t off = (int64_t)s_base;
+        const bool fits = (unsigned long long)(off + k) <= out.cap;
+        // exact (d2, caller index) rank inside the bucket, written straight to the list
+        for (int s = tid; s < k; s += 256) {
+          const uint32_t d = hd[s], p = hits[s];
+          int b = (int)(__uint_as_float(d) * bscale);
+          b = b < NB ? b : NB - 1;
+          const int en = bpos[b], st = en - bcount[b];
+          int rank = 0;
+          for (int v = st; v < en; ++v) {
+            const uint32_t dv = hd[v];
+            if (dv < d) ++rank;
+            else if (dv == d && v != s && g.perm[hits[v]] < g.perm[p]) ++rank;
+          }
+          if (fits) out.list[off + st + rank] = pos_entry(R, (int32_t)p);
+        }
+        __syncthreads();
+        continue;
+      } else {
+        for (int e = tid; e < k; e += 256) {
+          const uint32_t d = hd[e];
+          int b = (int)(__uint_as_float(d) * bscale);
+          b = b < NB ? b : NB - 1;
+          const int slot = atomicAdd(&bpos[b], 1);
+          sdv[slot] = d;
+          spv[slot] = hits[e];
+        }
+        __syncthreads();
+        for (int s = tid; s < k; s += 256) {
+          const uint32_t d = sdv[s], p = spv[s];
+          int b = (int)(__uint_as_float(d) * bscale);
+          b = b < NB ? b : NB - 1;
+          const int en = bpos[b], st = en - bcount[b];
+          int rank = 0;
+          for (int v = st; v < en; ++v) {
+            const uint32_t dv = sdv[v];
+            if (dv < d) ++rank;
+            else if (dv == d && v != s && g.perm[spv[v]] < g.perm[p]) ++rank;
+          }
+          hits[st + rank] = p;
+        }
       }
-      __syncthreads();
-    }
-    if (tid == 0) {
-      s_base = k ? atomicAdd(out.cursor, (unsigned long long)k) : 0ull;
-      if (k) atomicAdd(out.cursor + 1, (unsigned long long)k);
-      if (k > kLongList) {
-        atomicAdd(out.cursor + 2, (unsigned long long)k);
-        atomicAdd(out.cursor + 3, 1ull);
-      }
-      out.off[j] = (int64_t)s_base;
-      out.cnt[j] = k;
-      out.lg[j] = 0;
     }
     __syncthreads();
     const int64_t off = (int64_t)s_base;
     if ((unsigned long long)(off + k) <= out.cap)
-      for (int m = tid; m < k; m += 256) {
-        const int32_t p = (int32_t)hits[m];
-        uint32_t e = 0;
-#pragma unroll
-        for (int r = 0; r < 9; ++r)
-          if (p >= R.start[r] && p < R.start[r] + (R.pref[r + 1] - R.pref[r]))
-            e = ((uint32_t)r << 28) | (uint32_t)(p - R.start[r]);
-        out.list[off + m] = e;
-      }
+      for (int m = tid; m < k; m += 256) out.list[off + m] = pos_entry(R, (int32_t)hits[m]);
     __syncthreads();
   }
 }
@@ -749,7 +791,7 @@ void build_lists(pfx_ctx* ctx, const Grid& G, const uint8_t* mask, double radius
     check_launch("nblist tiles");
     PFX_HIP(hipMemcpyAsync(counters + 6, counters + 2, sizeof(int), hipMemcpyDeviceToDevice, st));
   }
-  const size_t lds_q = sizeof(uint32_t) * 4 * kCapQuery;
+  const size_t lds_q = sizeof(uint32_t) * 2 * kCapQuery;
   PFX_HIP(hipFuncSetAttribute((const void*)k_nb_query<kCapQuery, kBucketsQuery, false>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_q));
   DevBuf& lb = B("list");
