@@ -131,6 +131,10 @@ __device__ __forceinline__ float repeated_add(float incr, int c) {
   return s;
 }
 
+__device__ __forceinline__ float uniformf(float v) {
+  return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v)));
+}
+
 // ---- fast path of pair_bins ----
 // The same float operations as pair_bins up to the first division; then approximate quotients
 // (v_rcp / v_rsq), a polynomial atan2 and the bin maps, each feature checked against its bin
@@ -304,16 +308,24 @@ __global__ void __launch_bounds__(256, PFX_SPFH_WPE) k_fpfh_spfh(GridView g, con
   // 16 copies of each wave's counters (lane & 15): pairs of a planar patch pile into a few bins,
   // and same-address LDS atomics serialise
   __shared__ int hist[4][kHistCopies][kDesc];
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  // wave-uniform values pinned to SGPRs (readfirstlane): the pair path needs the VGPRs
+  const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int64_t count = *count_ptr;
   const int64_t stride = (int64_t)gridDim.x * 4;
   for (int64_t w = xcd_block(blockIdx.x, gridDim.x) * 4 + wv; w < count; w += stride) {
-    const int32_t s = slist[w];
-    const float4 pc = g.sp[s], pnc = snp[s];
+    const int32_t s = __builtin_amdgcn_readfirstlane(slist[w]);
+    float4 pc = g.sp[s], pnc = snp[s];
+    pc.x = uniformf(pc.x); pc.y = uniformf(pc.y); pc.z = uniformf(pc.z);
+    pnc.x = uniformf(pnc.x); pnc.y = uniformf(pnc.y); pnc.z = uniformf(pnc.z);
     const f3 pp = mk3(pc.x, pc.y, pc.z), pn = mk3(pnc.x, pnc.y, pnc.z);
     for (int i = lane; i < kHistCopies * kDesc; i += 64) (&hist[wv][0][0])[i] = 0;
     Runs R;
     query_runs(g, pc.x, pc.y, pc.z, R);
+#pragma unroll
+    for (int r = 0; r < 9; ++r) {
+      R.start[r] = __builtin_amdgcn_readfirstlane(R.start[r]);
+      R.pref[r + 1] = __builtin_amdgcn_readfirstlane(R.pref[r + 1]);
+    }
     int k = 0, qn = 0;
     auto process = [&](int nvalid) {
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
