@@ -131,10 +131,6 @@ __device__ __forceinline__ float repeated_add(float incr, int c) {
   return s;
 }
 
-__device__ __forceinline__ float uniformf(float v) {
-  return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v)));
-}
-
 // ---- fast path of pair_bins ----
 // The same float operations as pair_bins up to the first division; then approximate quotients
 // (v_rcp / v_rsq), a polynomial atan2 and the bin maps, each feature checked against its bin

@@ -13,6 +13,12 @@ __device__ __forceinline__ uint64_t nb_key(float d2, int32_t idx) {
 __device__ __forceinline__ float key_d2(uint64_t k) { return __uint_as_float((uint32_t)(k >> 32)); }
 __device__ __forceinline__ int32_t key_idx(uint64_t k) { return (int32_t)(uint32_t)(k & 0xffffffffu); }
 
+// a wave-uniform float kept in an SGPR (the compiler cannot prove values loaded through LDS or
+// indexed by threadIdx >> 6 uniform)
+__device__ __forceinline__ float uniformf(float v) {
+  return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v)));
+}
+
 __device__ __forceinline__ uint64_t lanemask_lt() {
   const int lane = threadIdx.x & 63;
   return lane == 0 ? 0ull : (~0ull >> (64 - lane));
