@@ -23,6 +23,7 @@ namespace {
 
 constexpr int kQ = 16;  // tile: consecutive queries of one cell
 constexpr int kArena = 4096;    // list entries per arena reservation of a tile workgroup
+constexpr int kArenaQuery = 16384;  // ... of a per-query workgroup (lists of 1k-4k entries)
 constexpr int kTcapSmall = 384, kTcapSparse = 1280, kTcapDense = 8000;
 constexpr int kCapQuery = 4096, kBucketsQuery = 1024;
 constexpr int kCapHuge = 1 << 18, kBucketsHuge = 4096, kHugeBlocks = 32;
@@ -575,6 +576,9 @@ __global__ void __launch_bounds__(256) k_nb_query(GridView g, const int32_t* __r
   const int tid = threadIdx.x;
   const int count = *n_ptr;
   __shared__ int s_w;
+  // thread 0's: list slots from a per-workgroup arena and the totals added once per workgroup
+  // (one same-address atomic per query made the cursors the bottleneck of this kernel)
+  unsigned long long wg_total = 0, wg_long = 0, wg_long_n = 0, arena_base = 0, arena_left = 0;
   for (;;) {  // dynamic queue: list lengths (and costs) differ by orders of magnitude
     if (tid == 0) s_w = atomicAdd(next_work, 1);
     __syncthreads();
@@ -626,11 +630,19 @@ __global__ void __launch_bounds__(256) k_nb_query(GridView g, const int32_t* __r
       continue;
     }
     if (tid == 0) {
-      s_base = k ? atomicAdd(out.cursor, (unsigned long long)k) : 0ull;
-      if (k) atomicAdd(out.cursor + 1, (unsigned long long)k);
+      const unsigned long long need = (unsigned long long)k;
+      if (need > arena_left) {
+        const unsigned long long res = need > (unsigned long long)kArenaQuery ? need : (unsigned long long)kArenaQuery;
+        arena_base = atomicAdd(out.cursor, res);
+        arena_left = res;
+      }
+      s_base = arena_base;
+      arena_base += need;
+      arena_left -= need;
+      wg_total += need;
       if (k > kLongList) {
-        atomicAdd(out.cursor + 2, (unsigned long long)k);
-        atomicAdd(out.cursor + 3, 1ull);
+        wg_long += need;
+        ++wg_long_n;
       }
       out.off[j] = (int64_t)s_base;
       out.cnt[j] = k;
@@ -726,6 +738,13 @@ __global__ void __launch_bounds__(256) k_nb_query(GridView g, const int32_t* __r
     if ((unsigned long long)(off + k) <= out.cap)
       for (int m = tid; m < k; m += 256) out.list[off + m] = pos_entry(R, (int32_t)hits[m]);
     __syncthreads();
+  }
+  if (tid == 0) {
+    if (wg_total) atomicAdd(out.cursor + 1, wg_total);
+    if (wg_long_n) {
+      atomicAdd(out.cursor + 2, wg_long);
+      atomicAdd(out.cursor + 3, wg_long_n);
+    }
   }
 }
 
@@ -855,8 +874,8 @@ void build_lists(pfx_ctx* ctx, const Grid& G, const uint8_t* mask, double radius
       throw Error(PFX_ERR_CAPACITY, std::string(tag) + ": a query has " + std::to_string(h_cnt[4]) +
                                         " neighbours (> " + std::to_string(kCapHuge) + " supported)");
     if (h_cur[0] > lo.cap) {  // list buffer too small: grow (no copy needed) and rebuild once
-      lb.release();
-      lb.get(sizeof(uint32_t) * (size_t)h_cur[0]);
+      lb.release();  // headroom: arena tails vary from run to run
+      lb.get(sizeof(uint32_t) * ((size_t)h_cur[0] + (size_t)h_cur[0] / 8 + ((size_t)1 << 22)));
       continue;
     }
     out.nq = h_nq;
