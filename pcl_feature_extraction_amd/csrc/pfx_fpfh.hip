@@ -308,6 +308,7 @@ __global__ void __launch_bounds__(256, PFX_SPFH_WPE) k_fpfh_spfh(GridView g, con
   const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int64_t count = *count_ptr;
   const int64_t stride = (int64_t)gridDim.x * 4;
+  unsigned long long wpairs = 0;
   for (int64_t w = xcd_block(blockIdx.x, gridDim.x) * 4 + wv; w < count; w += stride) {
     const int32_t s = __builtin_amdgcn_readfirstlane(slist[w]);
     float4 pc = g.sp[s], pnc = snp[s];
@@ -385,13 +386,12 @@ __global__ void __launch_bounds__(256, PFX_SPFH_WPE) k_fpfh_spfh(GridView g, con
       for (int j = 0; j < kHistCopies; ++j) c += hist[wv][j][lane];
       hcount[w * kDesc + lane] = c;
     }
-    if (lane == 0) {
-      kcount[w] = k;
-      atomicAdd(pairs, (unsigned long long)(k - 1));
-    }
+    if (lane == 0) kcount[w] = k;
+    wpairs += (unsigned long long)(k - 1);
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
   }
+  if (lane == 0 && wpairs) atomicAdd(pairs, wpairs);  // once per wave (same-address atomics serialise)
 }
 
 // the deferred pairs through the exact path (double precision), one lane each

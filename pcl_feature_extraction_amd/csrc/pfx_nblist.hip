@@ -497,7 +497,7 @@ __global__ void __launch_bounds__(256, TCAP <= kTcapSmall ? 4 : (STAGE ? 3 : 2))
     if (tid < qn) {
       const int k = s_k[tid];
       if (k > LCAP) {
-        single[atomicAdd(n_single, 1)] = start + tid;  // the per-query path writes its descriptor
+        single[wave_push_slot(n_single)] = start + tid;  // the per-query path writes its descriptor
       } else {
         out.cnt[start + tid] = k;
         out.lg[start + tid] = (uint8_t)lg;

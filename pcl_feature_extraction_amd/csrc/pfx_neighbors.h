@@ -24,6 +24,17 @@ __device__ __forceinline__ uint64_t lanemask_lt() {
   return lane == 0 ? 0ull : (~0ull >> (64 - lane));
 }
 
+// slot for each calling lane in an array filled through `counter`: one atomic per wave, not per
+// lane (same-address atomics serialise at the L2)
+__device__ __forceinline__ int wave_push_slot(int* counter) {
+  const uint64_t m = __ballot(1);
+  const int leader = __builtin_ctzll(m);
+  int base = 0;
+  if ((int)(threadIdx.x & 63) == leader) base = atomicAdd(counter, __popcll(m));
+  base = __shfl(base, leader);
+  return base + __popcll(m & lanemask_lt());
+}
+
 // XCD-aware block remap: blocks b and b+8 share an XCD (observed round-robin placement);
 // give each XCD a contiguous slice of the (spatially sorted) work so its L2 sees one region.
 __device__ __forceinline__ int64_t xcd_block(int64_t b, int64_t nblocks) {

@@ -337,7 +337,7 @@ __device__ __forceinline__ void chain_wg(ChainLds<CAP>& S, const GridView& g, co
 #endif
   if (!active) return;
   if (k > kLaneMax) {
-    longq[atomicAdd(n_long, 1)] = (int32_t)j;
+    longq[wave_push_slot(n_long)] = (int32_t)j;
     return;
   }
   const uint32_t* lst = L.list + L.off[j];
