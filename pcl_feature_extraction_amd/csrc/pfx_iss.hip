@@ -530,7 +530,7 @@ __global__ void __launch_bounds__(256) k_iss_cov(GridView g, float rr, int min_n
       if (ok) {
         t = iss_third(c00, c01, c02, c11, c12, c22, g21, g32);
       } else {
-        oq[atomicAdd(n_mask, 1)] = (int32_t)p;
+        oq[wave_push_slot(n_mask)] = (int32_t)p;
       }
     }
     third[i] = t;
