@@ -1,13 +1,16 @@
 #!/usr/bin/env python3
-"""Headline benchmark: Mpoints/s through NARF keypoints + FPFH descriptors on a 1M-point cloud
-(BASELINE.json metric; configs[2] at N = 1, configs[4] = one 1M-point scan per GPU at N > 1).
+"""Headline benchmark: Mpoints/s through NARF keypoint + FPFH descriptor on 1M-pt clouds
+(BASELINE.json metric; configs[2] at --gpus 1, configs[4] = the fixed batch of 8 1M-pt scans
+round-robin over the GPUs at N > 1).
 
-One step = the reference's (Narf, FPFH) pass over one scan (pcl_feature_extraction_amd/pipeline.py):
+One scan = the reference's (Narf, FPFH) pass (pcl_feature_extraction_amd/pipeline.py):
 range image -> border extraction -> NARF interest + NMS + greedy selection -> keypoint mapping ->
-normals of the whole cloud (r = 0.05) -> FPFH at the keypoints (r = 0.08), inputs resident in HBM.
-At N > 1 every rank processes its own scan and the descriptor matrices are gathered on every rank
-over RCCL (dist.gather_descriptors: all_gather of the counts and of the padded K x 33 blocks)
-inside the step.
+normals of the whole cloud (r = 0.05) -> FPFH at the keypoints (r = 0.08), inputs resident in HBM
+(`value`); the same step with H2D of the scan and D2H of the descriptors inside it is reported
+beside it (`end_to_end_h2d_d2h`).  At N > 1 every rank processes its scans (8/N each) and the
+K_s x 33 descriptor matrices + K_s indices are gathered on rank 0 over RCCL (grouped
+send/recv, dist.gather_to_root) inside the step.  `bench.py --gpus N` without an external
+launcher starts its N ranks itself (launch.py) before touching a GPU.
 
 `--workload shot` measures configs[3] instead (secondary line): a 1M-point underwater-style
 seabed, normals + SHOT-352 (r = 0.08) at the NARF keypoints and a fixed 10,000-point sample.
@@ -19,8 +22,8 @@ branch, keypoints.h:177-189): one step = cloud resolution + ISSKeypoint3D over t
 `--workload harris`: F3's Harris3D branch (keypoints.h:150-162 + getKeypointsCloud) over the same
 room: normals (r 0.01) + response + suppression + corner refinement + snap.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload fpfh|shot] [--no-cpu-baseline]
-    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload fpfh|shot|...] [--scans S]
+                    [--no-cpu-baseline] [--no-e2e]
 """
 from __future__ import annotations
 
@@ -51,32 +54,65 @@ VERBOSE_STATS = ["normals_neighbors", "normals_queries", "normals_tiles_sparse",
                  "shot_neighbors"]
 
 
-def cpu_baseline(x, y, z, workload, sample=None):
+def host_info():
+    """CPU model, logical CPUs of the machine and of this process's affinity mask."""
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except AttributeError:
+        affinity = os.cpu_count() or 1
+    return {"cpu_model": model, "nproc": os.cpu_count() or 1, "affinity_cpus": affinity}
+
+
+def cpu_baseline(x, y, z, workload, sample=None, reps=5):
     """The CPU restatement (oracle/, test infrastructure) on the same scan, threads as PCL:
     NARF and FPFH single-threaded (PCL 1.7 defaults, non-OMP FPFHEstimation), normals and SHOT
-    OpenMP (NormalEstimationOMP / SHOTEstimationOMP)."""
+    OpenMP (NormalEstimationOMP / SHOTEstimationOMP).  SURVEY 8(d): one warm-up run (on a
+    1/10 subsample of the scan: pages the code and the allocator in) + the median of `reps`
+    full runs."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import numpy as np
     import oracle_lib as O
     threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
-    t0 = time.perf_counter()
-    kp = O.narf_keypoints(x, y, z, threads=1)
-    t1 = time.perf_counter()
-    nx, ny, nz, _ = O.normals(x, y, z, 0.05, threads=threads)
-    t2 = time.perf_counter()
-    rows = kp[kp < len(x)]
-    if workload == "fpfh":
-        desc = O.fpfh(x, y, z, nx, ny, nz, x[rows], y[rows], z[rows], 0.08, threads=1)
-        feat = "FPFH 1 thread"
-    else:
-        rows = np.r_[rows, sample]
-        desc = O.shot(x, y, z, nx, ny, nz, x[rows], y[rows], z[rows], 0.08, threads=threads)
-        feat = f"SHOT {threads} threads"
-    t3 = time.perf_counter()
-    return dict(seconds=t3 - t0, threads=threads, outputs=(kp, (nx, ny, nz), desc),
-                sample=(f"the same 1M-point scan through the CPU restatement (oracle/): NARF 1 thread "
-                        f"{t1 - t0:.1f}s, normals {threads} threads {t2 - t1:.1f}s, {feat} {t3 - t2:.1f}s at "
-                        f"{len(rows)} rows; real PCL is not available anywhere in this pipeline"))
+
+    def once(cx, cy, cz, samp):
+        t0 = time.perf_counter()
+        kp = O.narf_keypoints(cx, cy, cz, threads=1)
+        t1 = time.perf_counter()
+        nx, ny, nz, _ = O.normals(cx, cy, cz, 0.05, threads=threads)
+        t2 = time.perf_counter()
+        rows = kp[kp < len(cx)]
+        if workload == "fpfh":
+            desc = O.fpfh(cx, cy, cz, nx, ny, nz, cx[rows], cy[rows], cz[rows], 0.08, threads=1)
+        else:
+            rows = np.r_[rows, samp]
+            desc = O.shot(cx, cy, cz, nx, ny, nz, cx[rows], cy[rows], cz[rows], 0.08, threads=threads)
+        t3 = time.perf_counter()
+        return (t1 - t0, t2 - t1, t3 - t2), (kp, (nx, ny, nz), desc), len(rows)
+
+    sub = slice(None, None, 10)
+    once(x[sub], y[sub], z[sub], None if sample is None else sample[sample < len(x[sub])])
+    times, outputs, nrows = [], None, 0
+    for _ in range(reps):
+        t, outputs, nrows = once(x, y, z, sample)
+        times.append(t)
+    tot = sorted(sum(t) for t in times)
+    med = tot[len(tot) // 2]
+    stage_med = [sorted(t[i] for t in times)[len(times) // 2] for i in range(3)]
+    feat = "FPFH 1 thread" if workload == "fpfh" else f"SHOT {threads} threads"
+    return dict(seconds=med, threads=threads, outputs=outputs, runs=[round(v, 3) for v in tot],
+                sample=(f"the same 1M-point scan through the CPU restatement (oracle/), 1 warm-up (1/10 subsample) + "
+                        f"median of {reps} full runs: NARF 1 thread {stage_med[0]:.2f}s, normals {threads} threads "
+                        f"{stage_med[1]:.2f}s, {feat} {stage_med[2]:.2f}s at {nrows} rows; real PCL is not available "
+                        f"anywhere in this pipeline"))
 
 
 def full_size_parity(outputs, kp, b, desc, rows, shot):
@@ -98,94 +134,160 @@ def full_size_parity(outputs, kp, b, desc, rows, shot):
     return res
 
 
+def load_pmc(name):
+    """Committed PMC summary (scripts/gpu_pmc.sh -> scripts/pmc_summary.py), or None."""
+    path = os.path.join(ROOT, "profiles", name)
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        return json.load(f)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", choices=["fpfh", "shot", "match", "iss", "harris"], default="fpfh")
+    ap.add_argument("--scans", type=int, default=0,
+                    help="fpfh workload: scans per step (default 1 = configs[2] at --gpus 1, 8 = configs[4] at N > 1)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the host-buffer (H2D/D2H inside the step) leg")
     args = ap.parse_args()
+
+    # driver-style `bench.py --gpus N` without an external launcher: start the N ranks as a child
+    # torch.distributed.run BEFORE anything here touches a GPU, and exit with its code
+    from pcl_feature_extraction_amd import launch
+    if launch.needs_spawn(args.gpus):
+        sys.exit(launch.spawn(args.gpus, os.path.abspath(__file__), sys.argv[1:]))
+
     if os.environ.get("PFX_BENCH_VERBOSE"):
         os.environ["PFX_VERBOSE_STATS"] = "1"  # libpfx diagnostics (extra host syncs): verbose runs only
 
-    import numpy as np
     import torch
     import torch.distributed as dist
-
-    from pcl_feature_extraction_amd import Context
-    from pcl_feature_extraction_amd.dist import gather_descriptors
-    from pcl_feature_extraction_amd.pipeline import OverlappedNarfFpfh, alloc, alloc_shot, narf_shot
-    from pcl_feature_extraction_amd.synth import synth_room, synth_seabed
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
-        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch N > 1 with torch.distributed.run")
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
-
-    if args.workload == "match":
-        return bench_match(args, torch, dev, world, rank, local)
-    if args.workload == "iss":
-        return bench_iss(args, torch, dev, world, rank, local)
-    if args.workload == "harris":
-        return bench_harris(args, torch, dev, world, rank, local)
-
-    shot = args.workload == "shot"
-    if shot:  # configs[3]: seabed seed 3 (per-rank seeds 300 + rank at N > 1)
-        x, y, z, _ = synth_seabed(N_POINTS, 3 if world == 1 else 300 + rank)
-    else:     # configs[2] (seed 2) / configs[4] (seeds 100..107)
-        x, y, z, _ = synth_room(N_POINTS, 2 if world == 1 else 100 + rank)
-    ctx = Context(local)
-    ctx.set_stream(torch.cuda.current_stream(dev).cuda_stream)
-    ctx_n = Context(local)  # normal estimation overlapped with NARF on a second stream
-    run_fpfh = OverlappedNarfFpfh(torch, ctx, ctx_n, dev)
-    b = alloc(torch, N_POINTS, dev)
-    b.x.copy_(torch.from_numpy(x))
-    b.y.copy_(torch.from_numpy(y))
-    b.z.copy_(torch.from_numpy(z))
-    sample_np = np.sort(np.random.default_rng(10).choice(N_POINTS, SHOT_SAMPLE, replace=False))
-    if shot:
-        s = alloc_shot(torch, 1 << 16, dev)
-        sample = torch.from_numpy(sample_np.astype(np.int64)).to(dev)
-    gathered = None
-    last_kp = None
-
-    def step():
-        nonlocal gathered, last_kp
-        if shot:
-            rows = narf_shot(ctx, b, s, sample)
-            desc = s.desc
-        else:
-            last_kp, rows = run_fpfh(b)
-            desc = b.desc
+    try:
+        if args.workload == "match":
+            return bench_match(args, torch, dev, world, rank, local)
+        if args.workload == "iss":
+            return bench_iss(args, torch, dev, world, rank, local)
+        if args.workload == "harris":
+            return bench_harris(args, torch, dev, world, rank, local)
+        return bench_scans(args, torch, dist, dev, world, rank, local)
+    finally:
         if world > 1:
-            gathered = gather_descriptors(torch, dist, desc, rows)
-        return rows
+            dist.destroy_process_group()
 
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize(dev)
-    for c in (ctx, ctx_n):
-        c.set_timing(True)
-        c.reset_timing()
+
+def timed(torch, dist, dev, world, steps, fn):
+    """Barrier + synchronize on both sides of exactly `steps` calls; max over ranks (seconds)."""
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        rows = step()
+    for _ in range(steps):
+        fn()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    def merged(nm):  # a stage runs on one of the two contexts (grids on both)
-        a, b_ = ctx.kernel_time(nm), ctx_n.kernel_time(nm)
-        return a[0] + b_[0], a[1] + b_[1]
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    return elapsed
+
+
+def bench_scans(args, torch, dist, dev, world, rank, local):
+    """The headline (fpfh) and the configs[3] (shot) workloads.
+
+    fpfh: a step = every scan of the batch through Keypoints("Narf") + Features<FPFH> on the rank
+    that owns it (scans dealt round-robin, dist.owned_scans), then the gather of every scan's
+    K_s x 33 descriptors + K_s cloud indices to rank 0 (dist.gather_to_root: RCCL grouped
+    send/recv).  --gpus 1: one scan (configs[2], seed 2).  N > 1: configs[4], the fixed batch of
+    8 scans (seeds 100..107), 8/N per GPU -- total work fixed, so "scaling": "strong".
+    shot: configs[3], one seabed scan per rank (replicas)."""
+    import numpy as np
+
+    from pcl_feature_extraction_amd import Context
+    from pcl_feature_extraction_amd.dist import gather_to_root, in_scan_order, owned_scans
+    from pcl_feature_extraction_amd.pipeline import (OverlappedNarfFpfh, alloc, alloc_shot, keypoint_rows,
+                                                     narf_shot)
+    from pcl_feature_extraction_amd.synth import synth_room, synth_seabed
+
+    shot = args.workload == "shot"
+    if shot:
+        n_scans, seeds = world, [3] if world == 1 else [300 + r for r in range(world)]
+    else:
+        n_scans = args.scans or (1 if world == 1 else 8)
+        seeds = [2] if (n_scans == 1 and world == 1) else [100 + i for i in range(n_scans)]
+    mine = owned_scans(n_scans, world, rank)
+    per_rank_max = -(-n_scans // world)
+    ctx = Context(local)
+    ctx.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+    ctx_n = Context(local)  # normal estimation overlapped with NARF on a second stream
+    run_fpfh = OverlappedNarfFpfh(torch, ctx, ctx_n, dev)
+    scans, host = [], []
+    for s in mine:
+        x, y, z, _ = (synth_seabed if shot else synth_room)(N_POINTS, seeds[s])
+        b = alloc(torch, N_POINTS, dev)
+        for t, a in zip((b.x, b.y, b.z), (x, y, z)):
+            t.copy_(torch.from_numpy(a))
+        scans.append(b)
+        host.append((x, y, z))
+    sample_np = np.sort(np.random.default_rng(10).choice(N_POINTS, SHOT_SAMPLE, replace=False))
+    if shot:
+        sb = alloc_shot(torch, 1 << 16, dev)
+        sample = torch.from_numpy(sample_np.astype(np.int64)).to(dev)
+    state = {"kp": None, "rows": 0, "gathered": None}
+
+    def one_scan(b):
+        if shot:
+            rows = narf_shot(ctx, b, sb, sample)
+            return sb.desc[:rows], None
+        kp, k = run_fpfh(b)
+        state["kp"] = kp
+        idx = torch.from_numpy(keypoint_rows(kp, N_POINTS).astype(np.int32)).to(dev, non_blocking=True)
+        return b.desc[:k], idx
+
+    def step():
+        blocks = [one_scan(b) for b in scans]
+        state["rows"] = int(blocks[-1][0].shape[0]) if blocks else 0
+        if world > 1 and not shot:
+            state["gathered"] = gather_to_root(torch, dist, blocks, 33, dev, per_rank_max)
+        return blocks
+
+    # warm-up; per-scan neighbour counts of the normal estimation (for the algorithmic bytes)
+    nb_scan, long_scan = [], []
+    for w in range(max(args.warmup, 1)):
+        blocks = []
+        for b in scans:
+            blocks.append(one_scan(b))
+            if w == 0:
+                c = ctx if shot else ctx_n
+                nb_scan.append(c.stat("normals_neighbors"))
+                long_scan.append((c.stat("normals_long_neighbors"), c.stat("normals_long_queries")))
+        if world > 1 and not shot:
+            gather_to_root(torch, dist, blocks, 33, dev, per_rank_max)
+    torch.cuda.synchronize(dev)
+    for c in (ctx, ctx_n):
+        c.set_timing(True)
+        c.reset_timing()
+    elapsed = timed(torch, dist, dev, world, args.steps, step)
+    timers = {nm: (ctx.kernel_time(nm)[0] + ctx_n.kernel_time(nm)[0], ctx.kernel_time(nm)[1] + ctx_n.kernel_time(nm)[1])
+              for nm in VERBOSE_TIMERS}
+    for c in (ctx, ctx_n):
+        c.set_timing(False)
 
     def stat(nm):
         for c in (ctx_n, ctx) if nm.startswith("normals") else (ctx, ctx_n):
@@ -195,7 +297,6 @@ def main():
                 pass
         raise KeyError(nm)
 
-    timers = {nm: merged(nm) for nm in VERBOSE_TIMERS}
     if os.environ.get("PFX_BENCH_VERBOSE"):
         rep = {nm: round(ms / args.steps, 3) for nm, (ms, _) in timers.items() if ms > 0}
         print("per-step kernel ms:", json.dumps(rep), file=sys.stderr, flush=True)
@@ -206,136 +307,158 @@ def main():
             except Exception:
                 pass
         print("stats:", json.dumps(stats), file=sys.stderr, flush=True)
-    for c in (ctx, ctx_n):
-        c.set_timing(False)
-    neighbors = stat("normals_neighbors")
-    long_nb, long_q = stat("normals_long_neighbors"), stat("normals_long_queries")
-    # the chain stage once more, alone on the GPU (after the timed region, not part of `value`):
-    # in the timed step it shares the device with NARF on the other stream
-    iso_ms = None
+
+    # gathered batch on rank 0: scan order, sizes (the descriptors themselves stay on the device)
+    batch = None
+    if world > 1 and not shot and rank == 0:
+        ordered = in_scan_order(state["gathered"], n_scans, world)
+        batch = {"scans": n_scans, "rows_per_scan": [int(d.shape[0]) for d, _ in ordered],
+                 "matrix_rows": int(sum(d.shape[0] for d, _ in ordered)),
+                 "finite": bool(all(torch.isfinite(d).all().item() for d, _ in ordered if d.numel()))}
+
+    # the host-buffer leg (SURVEY 8(d) "H2D/D2H included"): each scan's xyz copied from pinned
+    # host memory inside the step, descriptors + indices copied back; reported beside `value`
+    e2e = None
+    if not args.no_e2e and not shot:
+        hx = [[torch.from_numpy(a).pin_memory() for a in h] for h in host]
+        hd = [torch.empty((1 << 16, 33), dtype=torch.float32).pin_memory() for _ in scans]
+        hi = [torch.empty((1 << 16,), dtype=torch.int32).pin_memory() for _ in scans]
+
+        def step_e2e():
+            blocks = []
+            for j, b in enumerate(scans):
+                for t, a in zip((b.x, b.y, b.z), hx[j]):
+                    t.copy_(a, non_blocking=True)
+                d, i = one_scan(b)
+                k = int(d.shape[0])
+                hd[j][:k].copy_(d, non_blocking=True)
+                hi[j][:k].copy_(i, non_blocking=True)
+                blocks.append((d, i))
+            if world > 1:
+                gather_to_root(torch, dist, blocks, 33, dev, per_rank_max)
+        step_e2e()
+        e_el = timed(torch, dist, dev, world, args.steps, step_e2e)
+        e2e = {"value": round(n_scans * N_POINTS * args.steps / e_el / 1e6, 4), "unit": "Mpoints/s",
+               "ms_per_step": round(e_el / args.steps * 1e3, 4),
+               "note": ("host-pointer semantics: per scan 12 MB xyz H2D from pinned memory + K x 33 descriptors and "
+                        "K indices D2H inside the timed step (SURVEY 8(d) definition); `value` is the same step with "
+                        "the scan already resident in HBM")}
+
+    # the same normal-estimation stage alone on the device (after the timed region, not part of
+    # `value`): inside the step it shares the CUs with NARF on the other stream
+    iso = None
     if rank == 0 and not shot:
+        b = scans[0]
         ctx_n.set_timing(True)
         ctx_n.reset_timing()
         for _ in range(3):
             ctx_n.normals_dev(b.x, b.y, b.z, 0.05, b.nx, b.ny, b.nz, b.curv)
         torch.cuda.synchronize(dev)
-        iso_ms = (ctx_n.kernel_time("normals_chain")[0] + ctx_n.kernel_time("normals_chain_big")[0]) / 3
+        iso = {nm: ctx_n.kernel_time(nm)[0] / 3 for nm in VERBOSE_TIMERS}
         ctx_n.set_timing(False)
-    if world > 1:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
 
     if rank == 0:
-        ms_per_step = elapsed / args.steps * 1e3
-        value = world * N_POINTS * args.steps / elapsed / 1e6
-        # roofline of the neighbour-gather kernel: k_normals_chain reads every query's
-        # FLANN-ordered neighbour list and gathers the neighbours' coordinates into the ordered
-        # covariance chains.  Algorithmic bytes per launch = sum_q |N_0.05(q)| * 12 B (xyz) +
-        # 16 B (normal + curvature out) over the queries these kernels own, i.e. every query but
-        # the lists longer than 1024 (k_normals_long's, reported beside); time = their HIP-event
-        # duration on the ctx stream.
-        algo_bytes = (neighbors - long_nb) * 12 + (N_POINTS - long_q) * 16
-        # the chain stage is k_normals_chain (LDS-staged workgroups) + k_normals_chain_big (the
-        # dense workgroups it defers to a 144 KB-LDS pass), run as two masked passes per step
-        # (FPFH support points on the main stream, the rest on the side stream): its time per
-        # step is the sum over both contexts' launches
-        chain_ms = timers["normals_chain"][0] + timers["normals_chain_big"][0]
-        stage_ms = timers["normals"][0] or sum(timers[nm][0] for nm in ("normals_lists_phase", "normals_chain",
-                                                                          "normals_chain_big", "normals_long"))
-        chain_s = chain_ms / args.steps / 1e3
-        stage_s = stage_ms / args.steps / 1e3
-        achieved = algo_bytes / chain_s / 1e9 if chain_s > 0 else 0.0
-        stage_gbs = algo_bytes / stage_s / 1e9 if stage_s > 0 else 0.0
-        traffic = None
-        pmc = os.path.join(ROOT, "profiles", "pmc_normals_chain.json")
-        if os.path.exists(pmc):  # FETCH_SIZE x2 + WRITE_SIZE of k_normals_chain (scripts/gpu_pmc.sh)
-            with open(pmc) as f:
-                traffic = json.load(f).get("hbm_bytes_per_launch")
-        # basis of `achieved`: the chain kernels' own launch durations, i.e. the isolated launches
-        # (normal estimation alone on the device, right after the timed region).  Inside the step
-        # the two masked chain passes run on two streams next to NARF's kernels, so their event
-        # durations include the CU time those share; that in-step figure is reported beside it.
-        in_step = {"chain_ms_per_step": round(chain_s * 1e3, 4), "achieved": round(achieved, 2),
-                   "frac": round(achieved / HBM_PEAK_GBS, 5),
-                   "note": "sum of the two masked passes' event durations inside the timed step (concurrent "
-                           "with NARF on the other stream)"}
-        if iso_ms is not None:
-            basis_ms, basis = iso_ms, "isolated launches after the timed region (normal estimation alone)"
-        else:
-            basis_ms, basis = chain_s * 1e3, "in-step launches"
-        basis_gbs = algo_bytes / (basis_ms / 1e3) / 1e9 if basis_ms > 0 else 0.0
-        roofline = {"bound": "hbm", "kernel": "k_normals_chain + k_normals_chain_big", "achieved": round(basis_gbs, 2),
-                    "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(basis_gbs / HBM_PEAK_GBS, 5),
-                    "traffic": traffic, "algorithmic_bytes_per_launch": int(algo_bytes),
-                    "chain_ms": round(basis_ms, 4), "basis": basis,
-                    "neighbors_per_launch": int(neighbors - long_nb),
-                    "long_lists": {"kernel": "k_normals_long", "lists": int(long_q), "neighbors": int(long_nb),
-                                   "ms_per_step": round(timers["normals_long"][0] / args.steps, 4)},
-                    "in_step": in_step,
-                    "stage": {"name": "normals: grid + FLANN-ordered lists + chains",
-                              "avg_ms": round(stage_s * 1e3, 4), "achieved": round(stage_gbs, 2),
-                              "frac": round(stage_gbs / HBM_PEAK_GBS, 5)}}
-        if shot:  # SHOT kernel: sum_q |N(q)| x 24 B (xyz + normal) per launch
-            shot_ms, shot_n = timers["shot"]
-            shot_s = (shot_ms / max(shot_n, 1)) / 1e3
-            sb = stat("shot_neighbors") * 24
-            # k_shot is this workload's dominant kernel (the chains take 0.5 ms of a 7.6 ms step):
-            # it heads the roofline; the chain figures stay beside it.  On this dense cloud
-            # (k(0.05) ~ 390) the chain's per-neighbour gather model exceeds the HBM peak because
-            # the kernel stages coordinates once per workgroup in LDS; the PMC traffic file is
-            # the default workload's, so no `traffic` here.
-            chain = dict(roofline, kernel="k_normals_chain + k_normals_chain_big", traffic=None,
-                         note="algorithmic model = 12 B per neighbour gather; coordinates are read once "
-                              "per workgroup from HBM and reused from LDS")
-            chain.pop("bound")
-            shot_gbs = sb / shot_s / 1e9 if shot_s > 0 else 0.0
-            roofline = {"bound": "hbm", "kernel": "k_shot", "achieved": round(shot_gbs, 2), "peak": HBM_PEAK_GBS,
-                        "unit": "GB/s", "frac": round(shot_gbs / HBM_PEAK_GBS, 5), "traffic": None,
-                        "algorithmic_bytes_per_launch": int(sb), "avg_ms": round(shot_s * 1e3, 4),
-                        "note": "sum_q |N_0.08(q)| x 24 B (xyz + normal) per launch (SURVEY 8(d)); VALU/LDS-atomic "
-                                "bound, not HBM", "normals_chain": chain}
+        line = scans_line(args, world, n_scans, mine, shot, elapsed, timers, iso, nb_scan, long_scan, stat)
+        line["config"]["descriptor_rows"] = state["rows"]
+        if batch is not None:
+            line["config"]["gathered_on_rank0"] = batch
+            line["config"]["ranks_seen_by_rccl"] = dist.get_world_size()
+            line["config"]["backend"] = dist.get_backend()
+        line["end_to_end_h2d_d2h"] = e2e
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
+            x, y, z = host[0]
             cb = cpu_baseline(x, y, z, args.workload, sample_np)
             cpu = {"value": round(N_POINTS / cb["seconds"] / 1e6, 6), "unit": "Mpoints/s",
-                   "cores": cb["threads"], "kind": "port", "sample": cb["sample"],
-                   "parity": full_size_parity(cb["outputs"], last_kp, b, s.desc if shot else b.desc, rows, shot)}
-        if shot:
-            metric = "Mpoints/s through NARF keypoint + normals + SHOT-352 descriptor on 1M-pt underwater-style cloud"
-            workload = (f"configs[3] 1M-pt synthetic seabed, NARF(support 0.2) + normals(r 0.05) + SHOT-352(r 0.08) "
-                        f"at the keypoints + a fixed {SHOT_SAMPLE}-point sample")
-            data = "synthetic (synth_seabed: seeded fBm height field under a pinhole camera, k(0.08)~1000)"
-        else:
-            metric = "Mpoints/s through NARF keypoint + FPFH descriptor on 1M-pt cloud"
-            workload = ("configs[2] 1M-pt synthetic room, NARF(support 0.2) + normals(r 0.05) + FPFH(r 0.08) at "
-                        "the keypoints" if world == 1 else
-                        "configs[4] one 1M-pt room scan per GPU + RCCL all_gather of K x 33 descriptors")
-            data = "synthetic (synth_room: seeded pinhole room scan, k(0.05)~230; see synth.py)"
-        line = {
-            "metric": metric,
-            "value": round(value, 4),
-            "unit": "Mpoints/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(ms_per_step, 4),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "f32",
-            "data": data,
-            "config": {"workload": workload, "points_per_scan": N_POINTS, "descriptor_rows": int(rows),
-                       "image": "640x480", "parallelism": f"scan-per-gpu x{world}"},
-            "roofline": roofline,
-            "cpu_baseline": cpu,
-        }
+                   "cores": cb["threads"], "kind": "port", "sample": cb["sample"], "runs_s": cb["runs"],
+                   **host_info(),
+                   "parity": full_size_parity(cb["outputs"], state["kp"], scans[0], sb.desc if shot else scans[0].desc,
+                                              state["rows"], shot)}
+        line["cpu_baseline"] = cpu
         print(json.dumps(line), flush=True)
     run_fpfh.close()
     ctx.close()
     ctx_n.close()
-    if world > 1:
-        dist.destroy_process_group()
+
+
+def scans_line(args, world, n_scans, mine, shot, elapsed, timers, iso, nb_scan, long_scan, stat):
+    """The contract line of bench_scans (rank 0), roofline over the neighbour-gather stage."""
+    per_scan_calls = args.steps * len(mine)
+    ms_per_step = elapsed / args.steps * 1e3
+    value = n_scans * N_POINTS * args.steps / elapsed / 1e6
+    nb = sum(nb_scan) / len(nb_scan)
+    long_nb = sum(l[0] for l in long_scan) / len(long_scan)
+    long_q = sum(l[1] for l in long_scan) / len(long_scan)
+    # SURVEY 8(d): neighbour-gather bytes per scan = sum_q |N_0.05(q)| x 12 B + N x 16 B, over
+    # the WHOLE stage that produces them: grid build + FLANN-ordered list builders + ordered
+    # covariance chains + long lists (timer "normals": HIP events around pfx_normals_dev on its
+    # stream, inside the timed step, averaged per scan)
+    algo = nb * 12 + N_POINTS * 16
+    stage_ms = timers["normals"][0] / max(per_scan_calls, 1)
+    stage_gbs = algo / (stage_ms / 1e3) / 1e9 if stage_ms > 0 else 0.0
+    parts = ("grid_bbox", "grid_build", "normals_lists_small", "normals_lists_sparse", "normals_lists_dense",
+             "normals_lists_query", "normals_chain", "normals_chain_big", "normals_long")
+    kernels = {nm: round(timers[nm][0] / max(per_scan_calls, 1), 4) for nm in parts}
+    chain_algo = (nb - long_nb) * 12 + (N_POINTS - long_q) * 16
+    chain_ms = kernels["normals_chain"] + kernels["normals_chain_big"]
+    chain = {"kernel": "k_normals_chain + k_normals_chain_big",
+             "algorithmic_bytes_per_launch": int(chain_algo), "ms": chain_ms,
+             "achieved": round(chain_algo / (chain_ms / 1e3) / 1e9, 2) if chain_ms > 0 else None}
+    chain["frac"] = round(chain["achieved"] / HBM_PEAK_GBS, 5) if chain["achieved"] else None
+    pmc = load_pmc("pmc_normals_stage.json") or {}
+    roofline = {"bound": "hbm", "kernel": "normals stage: grid + k_nb_tile/k_nb_query list builders + "
+                                          "k_normals_chain(_big) + k_normals_long",
+                "achieved": round(stage_gbs, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(stage_gbs / HBM_PEAK_GBS, 5), "traffic": pmc.get("stage_hbm_bytes_per_launch"),
+                "algorithmic_bytes_per_launch": int(algo), "avg_ms": round(stage_ms, 4),
+                "neighbors_per_launch": int(nb),
+                "basis": "HIP events on the normal-estimation stream over the timed region, per scan (concurrent "
+                         "with NARF on the other stream)",
+                "kernels_ms_per_scan": kernels, "chain": chain,
+                "pmc": pmc.get("kernels")}
+    if iso is not None:
+        iso_stage = iso["normals"]
+        roofline["isolated"] = {"avg_ms": round(iso_stage, 4),
+                                "achieved": round(algo / (iso_stage / 1e3) / 1e9, 2) if iso_stage > 0 else None,
+                                "frac": round(algo / (iso_stage / 1e3) / 1e9 / HBM_PEAK_GBS, 5) if iso_stage > 0 else None,
+                                "kernels_ms": {nm: round(iso[nm], 4) for nm in parts},
+                                "note": "pfx_normals_dev alone on the device after the timed region (not `value`)"}
+    if shot:  # configs[3]: k_shot heads the line (the dominant kernel of that step)
+        shot_ms, shot_n = timers["shot"]
+        shot_s = (shot_ms / max(shot_n, 1)) / 1e3
+        sbytes = stat("shot_neighbors") * 24
+        shot_gbs = sbytes / shot_s / 1e9 if shot_s > 0 else 0.0
+        stage = roofline
+        stage.pop("bound")
+        roofline = {"bound": "hbm", "kernel": "k_shot", "achieved": round(shot_gbs, 2), "peak": HBM_PEAK_GBS,
+                    "unit": "GB/s", "frac": round(shot_gbs / HBM_PEAK_GBS, 5), "traffic": None,
+                    "algorithmic_bytes_per_launch": int(sbytes), "avg_ms": round(shot_s * 1e3, 4),
+                    "note": "sum_q |N_0.08(q)| x 24 B (xyz + normal) per launch (SURVEY 8(d)); VALU/LDS-atomic "
+                            "bound, not HBM", "normals_stage": stage}
+        metric = "Mpoints/s through NARF keypoint + normals + SHOT-352 descriptor on 1M-pt underwater-style cloud"
+        workload = (f"configs[3] 1M-pt synthetic seabed, NARF(support 0.2) + normals(r 0.05) + SHOT-352(r 0.08) at "
+                    f"the keypoints + a fixed {SHOT_SAMPLE}-point sample" + ("" if world == 1 else ", one scan per GPU"))
+        data = "synthetic (synth_seabed: seeded fBm height field under a pinhole camera, k(0.08)~1000)"
+        scaling = "weak"
+    else:
+        metric = "Mpoints/s through NARF keypoint + FPFH descriptor on 1M-pt cloud"
+        if n_scans == 1:
+            workload = ("configs[2] 1M-pt synthetic room, NARF(support 0.2) + normals(r 0.05) + FPFH(r 0.08) at "
+                        "the keypoints")
+        else:
+            workload = (f"configs[4] batch of {n_scans} 1M-pt room scans (seeds 100..{99 + n_scans}) round-robin over "
+                        f"{world} GPU(s), configs[2] work per scan, K_s x 33 descriptors + indices gathered to rank 0 "
+                        f"(RCCL grouped send/recv)")
+        data = "synthetic (synth_room: seeded pinhole room scan, k(0.05)~230; see synth.py)"
+        scaling = "strong" if n_scans > 1 else "weak"
+    return {
+        "metric": metric, "value": round(value, 4), "unit": "Mpoints/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
+        "higher_is_better": True, "scaling": scaling, "vs_baseline": None, "dtype": "f32", "data": data,
+        "config": {"workload": workload, "points_per_scan": N_POINTS, "scans_per_step": n_scans,
+                   "image": "640x480", "parallelism": f"scan-per-gpu x{world}"},
+        "roofline": roofline,
+    }
 
 
 def bench_match(args, torch, dev, world, rank, local):
