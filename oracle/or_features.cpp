@@ -38,8 +38,9 @@ void pointNormal(const float* x, const float* y, const float* z, const std::vect
     accu[7] += y[p];
     accu[8] += z[p];
   }
-  const float cnt = (float)nb.size();
-  for (int i = 0; i < 9; ++i) accu[i] /= cnt;
+  // `accu /= static_cast<Scalar> (point_count)`: Eigen 3.2 multiplies by the reciprocal
+  const float inv = 1.0f / (float)nb.size();
+  for (int i = 0; i < 9; ++i) accu[i] *= inv;
   float C[3][3];
   C[0][0] = accu[0] - accu[6] * accu[6];
   C[0][1] = accu[1] - accu[6] * accu[7];
@@ -79,10 +80,10 @@ void pairFeatures(V3 p1, V3 n1, V3 p2, V3 n2, float& f1, float& f2, float& f3, f
   V3 v = cross(dp, n1c);
   float v_norm = std::sqrt(sqn4(v));
   if (v_norm == 0.0f) { f1 = f2 = f3 = f4 = 0.0f; return; }
-  v = divs(v, v_norm);
+  v = mul(v, 1.0f / v_norm);  // `v /= v_norm` (Eigen 3.2: times the reciprocal)
   V3 w = cross(n1c, v);
   f2 = dot4(v, n2c);
-  f1 = atan2f_cr(dot4(w, n2c), dot4(n1c, n2c));
+  f1 = atan2f_glibc(dot4(w, n2c), dot4(n1c, n2c));
 }
 
 inline int clampBin(double v, int nbins) {
@@ -100,6 +101,53 @@ inline int clampBin(double v, int nbins) {
 extern "C" {
 
 int orc_version() { return 1; }
+
+// PCL 1.7 computeMeanAndCovarianceMatrix (dense branch) over cloud[idx[0..n)]: the covariance
+// entries (c00, c01, c02, c11, c12, c22) as pointNormal forms them (tests: the Eigen 3.2
+// reciprocal form of `accu /= n`)
+void orc_point_covariance(const float* x, const float* y, const float* z, const int32_t* idx, i64 n, float* out6) {
+  float accu[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+  for (i64 i = 0; i < n; ++i) {
+    const int p = idx[i];
+    accu[0] += x[p] * x[p]; accu[1] += x[p] * y[p]; accu[2] += x[p] * z[p];
+    accu[3] += y[p] * y[p]; accu[4] += y[p] * z[p]; accu[5] += z[p] * z[p];
+    accu[6] += x[p]; accu[7] += y[p]; accu[8] += z[p];
+  }
+  const float inv = 1.0f / (float)n;
+  for (int i = 0; i < 9; ++i) accu[i] *= inv;
+  out6[0] = accu[0] - accu[6] * accu[6]; out6[1] = accu[1] - accu[6] * accu[7];
+  out6[2] = accu[2] - accu[6] * accu[8]; out6[3] = accu[3] - accu[7] * accu[7];
+  out6[4] = accu[4] - accu[7] * accu[8]; out6[5] = accu[5] - accu[8] * accu[8];
+}
+
+// Pins the glibc float restatements of or_common.h against the host libm (tests only):
+// which = 0: atan2f on n pairs (even i: uniform in [-1, 1]^2, odd i: random bit patterns),
+// which = 1: acosf on every stride-th float of [-1, 1] (stride = n).  Returns the number of
+// results whose bits differ (NaN == NaN).
+i64 orc_libm_mismatches(int which, i64 n, uint64_t seed) {
+  uint64_t s = seed ? seed : 88172645463325252ull;
+  auto next = [&s]() { s ^= s << 13; s ^= s >> 7; s ^= s << 17; return s; };
+  auto uni = [&]() { return (float)((double)(next() >> 11) / 9007199254740992.0 * 2.0 - 1.0); };
+  i64 bad = 0;
+  if (which == 0) {
+    for (i64 i = 0; i < n; ++i) {
+      float y, x;
+      if (i % 2 == 0) { y = uni(); x = uni(); }
+      else { y = w2f((int32_t)next()); x = w2f((int32_t)next()); }
+      const float a = ::atan2f(y, x), b = atan2f_glibc(y, x);
+      if (f2w(a) != f2w(b) && !(a != a && b != b)) ++bad;
+    }
+  } else {
+    const int64_t stride = n > 0 ? n : 1;
+    for (int sg = 0; sg < 2; ++sg)
+      for (int64_t u = 0; u <= 0x3f800000; u += stride) {
+        const float x = w2f((int32_t)((uint32_t)u | (sg ? 0x80000000u : 0u)));
+        const float a = ::acosf(x), b = acosf_glibc(x);
+        if (f2w(a) != f2w(b) && !(a != a && b != b)) ++bad;
+      }
+  }
+  return bad;
+}
 
 // Radius search (FLANN order).  counts[nq]; if idx != NULL, writes up to cap entries per
 // query row-major (row stride = cap) of indices and squared distances.

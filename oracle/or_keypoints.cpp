@@ -49,126 +49,9 @@ using orc::NeighborGrid;
 
 namespace {
 
-// ---- Eigen 3.2.0 SelfAdjointEigenSolver<Matrix3d>::compute, eigenvalues only -------------
-// (Eigenvalues/SelfAdjointEigenSolver.h, Eigenvalues/Tridiagonalization.h, Jacobi/Jacobi.h,
-// MathFunctions.h hypot_impl).  The eigenvector updates do not feed back into the values.
-
-double hypot_e(double x, double y) {  // internal::hypot_impl
-  const double ax = std::fabs(x), ay = std::fabs(y);
-  const double p = std::max(ax, ay);
-  if (p == 0.0) return 0.0;
-  const double q = std::min(ax, ay);
-  const double qp = q / p;
-  return p * std::sqrt(1.0 + qp * qp);
-}
-
-void make_givens(double p, double q, double& c, double& s) {  // JacobiRotation::makeGivens (real)
-  if (q == 0.0) {
-    c = p < 0.0 ? -1.0 : 1.0;
-    s = 0.0;
-  } else if (p == 0.0) {
-    c = 0.0;
-    s = q < 0.0 ? 1.0 : -1.0;
-  } else if (std::fabs(p) > std::fabs(q)) {
-    const double t = q / p;
-    double u = std::sqrt(1.0 + t * t);
-    if (p < 0.0) u = -u;
-    c = 1.0 / u;
-    s = -t * c;
-  } else {
-    const double t = p / q;
-    double u = std::sqrt(1.0 + t * t);
-    if (q < 0.0) u = -u;
-    s = -1.0 / u;
-    c = -t * s;
-  }
-}
-
-void tridiagonal_qr_step(double* diag, double* sub, int start, int end) {
-  const double td = (diag[end - 1] - diag[end]) * 0.5;
-  const double e = sub[end - 1];
-  double mu = diag[end];
-  if (td == 0.0) {
-    mu -= std::fabs(e);
-  } else {
-    const double e2 = e * e;
-    const double h = hypot_e(td, e);
-    if (e2 == 0.0)
-      mu -= (e / (td + (td > 0.0 ? 1.0 : -1.0))) * (e / h);
-    else
-      mu -= e2 / (td + (td > 0.0 ? h : -h));
-  }
-  double x = diag[start] - mu;
-  double z = sub[start];
-  for (int k = start; k < end; ++k) {
-    double c, s;
-    make_givens(x, z, c, s);
-    const double sdk = s * diag[k] + c * sub[k];
-    const double dkp1 = s * sub[k] + c * diag[k + 1];
-    diag[k] = c * (c * diag[k] - s * sub[k]) - s * (c * sub[k] - s * diag[k + 1]);
-    diag[k + 1] = s * sdk + c * dkp1;
-    sub[k] = c * sdk - s * dkp1;
-    if (k > start) sub[k - 1] = c * sub[k - 1] - s * z;
-    x = sub[k];
-    if (k < end - 1) {
-      z = -s * sub[k + 1];
-      sub[k + 1] = c * sub[k + 1];
-    }
-  }
-}
-
-// a: row-major symmetric 3x3 (the lower triangle is read, as Eigen does); ev ascending
-void selfadjoint_eigenvalues3(const double a[9], double ev[3]) {
-  double m[3][3] = {{a[0], 0.0, 0.0}, {a[3], a[4], 0.0}, {a[6], a[7], a[8]}};
-  double scale = 0.0;
-  for (int i = 0; i < 3; ++i)
-    for (int j = 0; j < 3; ++j) scale = std::max(scale, std::fabs(m[i][j]));
-  if (scale == 0.0) scale = 1.0;
-  for (int i = 0; i < 3; ++i)
-    for (int j = 0; j <= i; ++j) m[i][j] /= scale;
-  // tridiagonalization_inplace_selector<MatrixType, 3, false>::run
-  double diag[3], sub[2];
-  diag[0] = m[0][0];
-  const double v1norm2 = m[2][0] * m[2][0];
-  if (v1norm2 == 0.0) {
-    diag[1] = m[1][1];
-    diag[2] = m[2][2];
-    sub[0] = m[1][0];
-    sub[1] = m[2][1];
-  } else {
-    const double beta = std::sqrt(m[1][0] * m[1][0] + v1norm2);
-    const double inv_beta = 1.0 / beta;
-    const double m01 = m[1][0] * inv_beta;
-    const double m02 = m[2][0] * inv_beta;
-    const double q = 2.0 * m01 * m[2][1] + m02 * (m[2][2] - m[1][1]);
-    diag[1] = m[1][1] + m02 * q;
-    diag[2] = m[2][2] - m02 * q;
-    sub[0] = beta;
-    sub[1] = m[2][1] - m01 * q;
-  }
-  // implicit symmetric QR with Wilkinson shift (max 30 * n iterations)
-  int end = 2, start = 0, iter = 0;
-  while (end > 0) {
-    for (int i = start; i < end; ++i)
-      if (std::fabs(sub[i]) <= (std::fabs(diag[i]) + std::fabs(diag[i + 1])) * 1e-12) sub[i] = 0.0;
-    while (end > 0 && sub[end - 1] == 0.0) end--;
-    if (end <= 0) break;
-    iter++;
-    if (iter > 30 * 3) break;
-    start = end - 1;
-    while (start > 0 && sub[start - 1] != 0.0) start--;
-    tridiagonal_qr_step(diag, sub, start, end);
-  }
-  if (iter <= 30 * 3) {  // Success: selection sort, ascending (first minimum wins)
-    for (int i = 0; i < 2; ++i) {
-      int k = i;
-      for (int j = i + 1; j < 3; ++j)
-        if (diag[j] < diag[k]) k = j;
-      if (k != i) std::swap(diag[i], diag[k]);
-    }
-  }
-  for (int i = 0; i < 3; ++i) ev[i] = diag[i] * scale;
-}
+// Eigen 3.2.0 SelfAdjointEigenSolver<Matrix3d>: orc::selfadjoint_eigen3 (or_common.h)
+using orc::selfadjoint_eigen3;
+inline void selfadjoint_eigenvalues3(const double a[9], double ev[3]) { selfadjoint_eigen3(a, ev, 0); }
 
 inline bool finite3(const float* x, const float* y, const float* z, i64 i) {
   return std::isfinite(x[i]) && std::isfinite(y[i]) && std::isfinite(z[i]);
@@ -222,6 +105,12 @@ extern "C" {
 // 3x3 matrices, for the tests of the restatement itself.
 int orc_eigen_selfadjoint3(const double* a, i64 n, double* ev) {
   for (i64 i = 0; i < n; ++i) selfadjoint_eigenvalues3(a + 9 * i, ev + 3 * i);
+  return 0;
+}
+
+// the same with eigenvectors: vec[9 i + 3 k + r] = component r of the eigenvector of ev[3 i + k]
+int orc_eigen_selfadjoint3_vectors(const double* a, i64 n, double* ev, double* vec) {
+  for (i64 i = 0; i < n; ++i) selfadjoint_eigen3(a + 9 * i, ev + 3 * i, (double(*)[3])(vec + 9 * i));
   return 0;
 }
 

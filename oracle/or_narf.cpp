@@ -463,7 +463,7 @@ struct Border {
     } else {
       direction = sub(nbp, pt);
     }
-    direction = normalized3(direction);
+    direction = normalize3(direction);  // `direction.normalize ()`
     return true;
   }
 
@@ -502,7 +502,7 @@ struct Border {
             ws += 1.0f;
           }
         if (std::lrint(ws) < min_weight) continue;
-        dir[i] = normalized3(avg);
+        dir[i] = normalize3(avg);  // `average_border_direction->normalize ()`
         dir_valid[i] = 1;
       }
   }
@@ -645,8 +645,8 @@ void interestImage(const RangeImage& ri, const Border& B, const Params& P, std::
           // nkdGetDirectionAngle
           V3 rot = v3(0.0f + dot3(tmp0, dir), 0.0f + dot3(tmp1, dir), 0.0f + dot3(tmp2, dir));
           float inv = std::sqrt(rot.x * rot.x + rot.y * rot.y);
-          float dvx = rot.x / inv;
-          float angle = 0.5f * normAngle(2.0f * acosf_cr(dvx));
+          float dvx = rot.x * (1.0f / inv);  // Vector2f::normalize (): times the reciprocal
+          float angle = 0.5f * normAngle(2.0f * acosf_glibc(dvx));
           float cellf = std::floor((angle + d90) / d180 * hist_size);
           int cell;
           if (!(cellf == cellf)) cell = 0;  // NaN -> lrint -> INT_MIN -> (int) 0

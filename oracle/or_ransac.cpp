@@ -193,7 +193,8 @@ double orc_ransac_sample_threshold(const float* x, const float* y, const float* 
     accu[3] += py * py; accu[4] += py * pz; accu[5] += pz * pz;
     accu[6] += px; accu[7] += py; accu[8] += pz;
   }
-  for (int k = 0; k < 9; ++k) accu[k] /= (float)n;
+  const float inv = 1.0f / (float)n;  // computeMeanAndCovarianceMatrix: `accu /= n` (Eigen 3.2)
+  for (int k = 0; k < 9; ++k) accu[k] *= inv;
   float C[3][3];
   C[0][0] = accu[0] - accu[6] * accu[6];
   C[0][1] = accu[1] - accu[6] * accu[7];

@@ -7,10 +7,10 @@
 //    SHOTEstimation::computePointSHOT / createBinDistanceShape / interpolateSingleChannel /
 //    normalizeHistogram                               (features/impl/shot.hpp)
 //  Restatement choices (DESIGN.md "SHOT"):
-//    * Eigen's SelfAdjointEigenSolver<Matrix3d> is restated by a cyclic Jacobi solver in
-//      double (same eigenpairs to ~1e-16; the rf is cast to float, and the eigenvector sign is
-//      re-chosen by PCL's disambiguation, so the float rf agrees except for ill-conditioned
-//      (near-degenerate) covariances -- unpinned vs PCL, bit-identical to the HIP kernel);
+//    * Eigen 3.2.0's SelfAdjointEigenSolver<Matrix3d> (values AND vectors: the closed-form 3x3
+//      Householder Q times the Givens rotations of the implicit QR steps) is restated operation
+//      for operation (or_common.h selfadjoint_eigen3), `cov_m /= sum` as Eigen 3.2's
+//      multiplication by the reciprocal;
 //    * unqualified sqrt/acos/atan2 on float/double arguments resolve to the C double functions.
 // =====================================================================================
 #include "or_common.h"
@@ -28,57 +28,6 @@ const double PST_RAD_45 = 0.78539816339744830961566084581988;
 const double PST_RAD_90 = 1.5707963267948966192313216916398;
 const double PST_RAD_135 = 2.3561944901923449288469825374596;
 const double PST_RAD_PI_7_8 = 2.7488935718910690836548129603691;
-
-// Cyclic Jacobi eigen-decomposition of a symmetric 3x3 double matrix.  Eigenvalues ascending,
-// V[:,k] the eigenvector of evals[k].  Deterministic operation sequence (restated identically
-// in pcl_feature_extraction_amd/csrc/pfx_shot.hip).
-void jacobi3(const double A_in[3][3], double evals[3], double V[3][3]) {
-  double a[3][3];
-  for (int i = 0; i < 3; ++i)
-    for (int j = 0; j < 3; ++j) { a[i][j] = A_in[i][j]; V[i][j] = (i == j) ? 1.0 : 0.0; }
-  for (int sweep = 0; sweep < 50; ++sweep) {
-    double off = (a[0][1] * a[0][1] + a[0][2] * a[0][2]) + a[1][2] * a[1][2];
-    double diag = (a[0][0] * a[0][0] + a[1][1] * a[1][1]) + a[2][2] * a[2][2];
-    if (off == 0.0 || off <= 1e-36 * diag) break;
-    for (int pq = 0; pq < 3; ++pq) {
-      const int p = (pq == 2) ? 1 : 0, q = (pq == 0) ? 1 : 2;
-      const double apq = a[p][q];
-      if (apq == 0.0) continue;
-      const double theta = (a[q][q] - a[p][p]) / (2.0 * apq);
-      double t;
-      if (std::fabs(theta) > 1e150) t = 0.5 / theta;
-      else t = (theta >= 0.0 ? 1.0 : -1.0) / (std::fabs(theta) + std::sqrt(theta * theta + 1.0));
-      const double c = 1.0 / std::sqrt(t * t + 1.0), s = t * c;
-      const double tau = s / (1.0 + c);
-      a[p][p] = a[p][p] - t * apq;
-      a[q][q] = a[q][q] + t * apq;
-      a[p][q] = a[q][p] = 0.0;
-      const int r = 3 - p - q;
-      const double arp = a[r][p], arq = a[r][q];
-      a[r][p] = a[p][r] = arp - s * (arq + tau * arp);
-      a[r][q] = a[q][r] = arq + s * (arp - tau * arq);
-      for (int k = 0; k < 3; ++k) {
-        const double vkp = V[k][p], vkq = V[k][q];
-        V[k][p] = vkp - s * (vkq + tau * vkp);
-        V[k][q] = vkq + s * (vkp - tau * vkq);
-      }
-    }
-  }
-  double ev[3] = {a[0][0], a[1][1], a[2][2]};
-  int ord[3] = {0, 1, 2};
-  // stable ascending order of the diagonal
-  for (int i = 1; i < 3; ++i) {
-    int v = ord[i], j = i;
-    while (j > 0 && ev[v] < ev[ord[j - 1]]) { ord[j] = ord[j - 1]; --j; }
-    ord[j] = v;
-  }
-  double Vs[3][3];
-  for (int k = 0; k < 3; ++k) {
-    evals[k] = ev[ord[k]];
-    for (int i = 0; i < 3; ++i) Vs[i][k] = V[i][ord[k]];
-  }
-  std::memcpy(V, Vs, sizeof(Vs));
-}
 
 // SHOTLocalReferenceFrameEstimation::getLocalRF; returns false (rf = NaN) on failure
 bool localRF(const float* sx, const float* sy, const float* sz, float cx, float cy, float cz,
@@ -102,15 +51,18 @@ bool localRF(const float* sx, const float* sy, const float* sz, float cx, float 
     for (int k = 0; k < 9; ++k) rf[k] = kNaN;
     return false;
   }
+  // `cov_m /= sum` (Eigen 3.2: times the reciprocal), then SelfAdjointEigenSolver<Matrix3d>
+  const double inv_sum = 1.0 / sum;
+  double covr[9];
   for (int a = 0; a < 3; ++a)
-    for (int b = 0; b < 3; ++b) cov[a][b] /= sum;
-  double ev[3], V[3][3];
-  jacobi3(cov, ev, V);
+    for (int b = 0; b < 3; ++b) covr[3 * a + b] = cov[a][b] * inv_sum;
+  double ev[3], V[3][3];  // V[k]: eigenvector of ev[k]
+  selfadjoint_eigen3(covr, ev, V);
   if (!std::isfinite(ev[0]) || !std::isfinite(ev[1]) || !std::isfinite(ev[2])) {
     for (int k = 0; k < 9; ++k) rf[k] = kNaN;
     return false;
   }
-  double v1[3] = {V[0][2], V[1][2], V[2][2]}, v3[3] = {V[0][0], V[1][0], V[2][0]};
+  double v1[3] = {V[2][0], V[2][1], V[2][2]}, v3[3] = {V[0][0], V[0][1], V[0][2]};
   // vij.row(ne).dot(v) on a column-major Dynamic x 4 matrix row: ((x + y) + z) + 0
   auto dotv = [&](int ne, const double* v) { return ((vx[ne] * v[0] + vy[ne] * v[1]) + vz[ne] * v[2]) + 0.0; };
   int plusT = 0, plusN = 0;

@@ -6,8 +6,10 @@
 //     (v_div_fixup / corrected v_sqrt sequences), f32 denormals on;
 //   * Eigen fixed-size Vector3f reductions: (x + y) + z; aligned Vector4f (SSE2 predux):
 //     (x + z) + (y + w);
-//   * float transcendentals (atan2f, cosf, sinf, acosf) as the correctly rounded result,
-//     evaluated in f64 (ocml) and rounded once.
+//   * atan2f / acosf: glibc's fdlibm float routines (e_atan2f.c, s_atanf.c, e_acosf.c) restated
+//     operation for operation (the oracle's are pinned bit for bit against the host libm);
+//     cosf / sinf as the correctly rounded result, evaluated in f64 (ocml) and rounded once;
+//   * Eigen 3.2 `v /= s` and `v.normalize()` multiply by the reciprocal 1/s.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -30,10 +32,117 @@ __device__ __forceinline__ f3 cross3(f3 a, f3 b) {
 }
 __device__ __forceinline__ f3 normalized3(f3 a) { return div3(a, sqrtf(sqn3(a))); }
 
-__device__ __forceinline__ float atan2f_cr(float y, float x) { return (float)atan2((double)y, (double)x); }
+// Eigen 3.2 normalize() in place: v * (1 / sqrt(squaredNorm))
+__device__ __forceinline__ f3 normalize3(f3 a) { return scale3(a, 1.0f / sqrtf(sqn3(a))); }
+
 __device__ __forceinline__ float cosf_cr(float t) { return (float)cos((double)t); }
 __device__ __forceinline__ float sinf_cr(float t) { return (float)sin((double)t); }
-__device__ __forceinline__ float acosf_cr(float t) { return (float)acos((double)t); }
+
+// glibc __atanf (s_atanf.c, fdlibm)
+__device__ __forceinline__ float atanf_glibc(float x) {
+  const int32_t hx = __float_as_int(x), ix = hx & 0x7fffffff;
+  int id;
+  if (ix >= 0x4c000000) {  // |x| >= 2^25
+    if (ix > 0x7f800000) return x + x;
+    return hx > 0 ? 1.5707962513e+00f + 7.5497894159e-08f : -1.5707962513e+00f - 7.5497894159e-08f;
+  }
+  float hi = 0.0f, lo = 0.0f;
+  if (ix < 0x3ee00000) {  // |x| < 0.4375
+    if (ix < 0x31000000) return x;
+    id = -1;
+  } else {
+    x = fabsf(x);
+    if (ix < 0x3f980000) {
+      if (ix < 0x3f300000) { id = 0; x = (2.0f * x - 1.0f) / (2.0f + x); hi = 4.6364760399e-01f; lo = 5.0121582440e-09f; }
+      else { id = 1; x = (x - 1.0f) / (x + 1.0f); hi = 7.8539812565e-01f; lo = 3.7748947079e-08f; }
+    } else {
+      if (ix < 0x401c0000) { id = 2; x = (x - 1.5f) / (1.0f + 1.5f * x); hi = 9.8279368877e-01f; lo = 3.4473217170e-08f; }
+      else { id = 3; x = -1.0f / x; hi = 1.5707962513e+00f; lo = 7.5497894159e-08f; }
+    }
+  }
+  const float z = x * x, w = z * z;
+  const float s1 = z * (3.3333334327e-01f +
+                        w * (1.4285714924e-01f + w * (9.0908870101e-02f + w * (6.6610731184e-02f +
+                        w * (4.9768779427e-02f + w * 1.6285819933e-02f)))));
+  const float s2 = w * (-2.0000000298e-01f + w * (-1.1111110449e-01f + w * (-7.6918758452e-02f +
+                        w * (-5.8335702866e-02f + w * -3.6531571299e-02f))));
+  if (id < 0) return x - x * (s1 + s2);
+  const float r = hi - ((x * (s1 + s2) - lo) - x);
+  return hx < 0 ? -r : r;
+}
+
+// glibc __ieee754_atan2f (e_atan2f.c, fdlibm)
+__device__ __forceinline__ float atan2f_glibc(float y, float x) {
+  const float tiny = 1.0e-30f, pi_o_4 = 7.8539818525e-01f, pi_o_2 = 1.5707963705e+00f, pi = 3.1415927410e+00f,
+              pi_lo = -8.7422776573e-08f;
+  const int32_t hx = __float_as_int(x), ix = hx & 0x7fffffff, hy = __float_as_int(y), iy = hy & 0x7fffffff;
+  if (ix > 0x7f800000 || iy > 0x7f800000) return x + y;
+  if (hx == 0x3f800000) return atanf_glibc(y);
+  const int m = ((hy >> 31) & 1) | ((hx >> 30) & 2);
+  if (iy == 0) {
+    if (m <= 1) return y;
+    return m == 2 ? pi + tiny : -pi - tiny;
+  }
+  if (ix == 0) return hy < 0 ? -pi_o_2 - tiny : pi_o_2 + tiny;
+  if (ix == 0x7f800000) {
+    if (iy == 0x7f800000) {
+      if (m == 0) return pi_o_4 + tiny;
+      if (m == 1) return -pi_o_4 - tiny;
+      if (m == 2) return 3.0f * pi_o_4 + tiny;
+      return -3.0f * pi_o_4 - tiny;
+    }
+    if (m == 0) return 0.0f;
+    if (m == 1) return -0.0f;
+    return m == 2 ? pi + tiny : -pi - tiny;
+  }
+  if (iy == 0x7f800000) return hy < 0 ? -pi_o_2 - tiny : pi_o_2 + tiny;
+  const int32_t k = (iy - ix) >> 23;
+  float z;
+  if (k > 60) z = pi_o_2 + 0.5f * pi_lo;
+  else if (hx < 0 && k < -60) z = 0.0f;
+  else z = atanf_glibc(fabsf(y / x));
+  if (m == 0) return z;
+  if (m == 1) return __int_as_float(__float_as_int(z) ^ (int32_t)0x80000000);
+  if (m == 2) return pi - (z - pi_lo);
+  return (z - pi_lo) - pi;
+}
+
+// glibc __ieee754_acosf (e_acosf.c, fdlibm)
+__device__ __forceinline__ float acosf_glibc(float x) {
+  const float one = 1.0f, pi = 3.1415925026e+00f, pio2_hi = 1.5707962513e+00f, pio2_lo = 7.5497894159e-08f,
+              pS0 = 1.6666667163e-01f, pS1 = -3.2556581497e-01f, pS2 = 2.0121252537e-01f, pS3 = -4.0055535734e-02f,
+              pS4 = 7.9153501429e-04f, pS5 = 3.4793309169e-05f, qS1 = -2.4033949375e+00f, qS2 = 2.0209457874e+00f,
+              qS3 = -6.8828397989e-01f, qS4 = 7.7038154006e-02f;
+  const int32_t hx = __float_as_int(x), ix = hx & 0x7fffffff;
+  if (ix == 0x3f800000) return hx > 0 ? 0.0f : pi + 2.0f * pio2_lo;
+  if (ix > 0x3f800000) return (x - x) / (x - x);
+  if (ix < 0x3f000000) {
+    if (ix <= 0x32800000) return pio2_hi + pio2_lo;
+    const float z = x * x;
+    const float p = z * (pS0 + z * (pS1 + z * (pS2 + z * (pS3 + z * (pS4 + z * pS5)))));
+    const float q = one + z * (qS1 + z * (qS2 + z * (qS3 + z * qS4)));
+    const float r = p / q;
+    return pio2_hi - (x - (pio2_lo - x * r));
+  }
+  if (hx < 0) {
+    const float z = (one + x) * 0.5f;
+    const float p = z * (pS0 + z * (pS1 + z * (pS2 + z * (pS3 + z * (pS4 + z * pS5)))));
+    const float q = one + z * (qS1 + z * (qS2 + z * (qS3 + z * qS4)));
+    const float s = sqrtf(z);
+    const float r = p / q;
+    const float w = r * s - pio2_lo;
+    return pi - 2.0f * (s + w);
+  }
+  const float z = (one - x) * 0.5f;
+  const float s = sqrtf(z);
+  const float df = __int_as_float(__float_as_int(s) & (int32_t)0xfffff000);
+  const float c = (z - df * df) / (s + df);
+  const float p = z * (pS0 + z * (pS1 + z * (pS2 + z * (pS3 + z * (pS4 + z * pS5)))));
+  const float q = one + z * (qS1 + z * (qS2 + z * (qS3 + z * qS4)));
+  const float r = p / q;
+  const float w = r * s + c;
+  return 2.0f * (df + w);
+}
 __device__ __forceinline__ float pow3f_cr(float x) { double d = (double)x; return (float)(d * d * d); }
 
 // squared distance exactly as FLANN L2_Simple: ((0 + dx^2) + dy^2) + dz^2, dx = q - p
@@ -72,7 +181,7 @@ __device__ __forceinline__ void computeRoots(float m00, float m01, float m02, fl
   float q = half_b * half_b + a_over_3 * a_over_3 * a_over_3;
   if (q > 0.0f) q = 0.0f;
   float rho = sqrtf(-a_over_3);
-  float theta = atan2f_cr(sqrtf(-q), half_b) * s_inv3;
+  float theta = atan2f_glibc(sqrtf(-q), half_b) * s_inv3;
   float ct = cosf_cr(theta), st = sinf_cr(theta);
   r[0] = c2_over_3 + 2.0f * rho * ct;
   r[1] = c2_over_3 - rho * (ct + s_sqrt3 * st);

@@ -49,12 +49,12 @@ __device__ __forceinline__ double f1_scaled(double f1) {
   return (double)kBins * ((f1 + 3.14159265358979323846) * (double)d_pi);
 }
 
-// bin of f1 = atan2 correctly rounded to float (PCL: atan2f == (float)atan2 in glibc's
-// double-evaluated form).  The float atan2 is within a few ulp (< 1e-5 rad) of it,
-// and the bin map is monotone, so when both ends of that interval fall in one bin the bin is
-// exact; otherwise (a bin edge within 1e-5 rad) the correctly rounded value is computed.
+// bin of f1 = glibc's atan2f (PCL: `atan2f (w.dot (n2), n1.dot (n2))`, the fdlibm float routine,
+// pfx_device_math.h).  The hardware float atan2 and glibc's are both within a few ulp (< 1e-5 rad)
+// of the true value and the bin map is monotone, so when both ends of that interval fall in one
+// bin the bin is exact; otherwise (a bin edge within 1e-5 rad) glibc's value is computed.
 __device__ __attribute__((noinline)) int bin_f1_exact(float y, float x) {
-  return bin_of(f1_scaled((double)atan2f_cr(y, x)));
+  return bin_of(f1_scaled((double)atan2f_glibc(y, x)));
 }
 
 __device__ __forceinline__ int bin_f1(float y, float x) {
@@ -85,7 +85,7 @@ __device__ __forceinline__ void pair_bins(f3 p1, f3 n1, f3 p2, f3 n2, int& h1, i
   f3 v = cross3(dp, n1c);
   const float v_norm = sqrtf(sqn4(v));
   if (v_norm == 0.0f) { h1 = b_zero_f1; h2 = h3 = b_zero; return; }
-  v = div3(v, v_norm);
+  v = scale3(v, 1.0f / v_norm);  // `v /= v_norm`: Eigen 3.2 multiplies by the reciprocal
   const f3 w = cross3(n1c, v);
   const float f2 = dot4(v, n2c);
   h1 = bin_f1(dot4(w, n2c), dot4(n1c, n2c));

@@ -28,6 +28,7 @@
 #include <cmath>
 #include <rocprim/rocprim.hpp>
 
+#include "pfx_eigen3.h"
 #include "pfx_internal.h"
 #include "pfx_nblist.h"
 #include "pfx_neighbors.h"
@@ -294,134 +295,12 @@ __global__ void __launch_bounds__(256) k_res_sequential(const float* __restrict_
   if (threadIdx.x == 0) *out = sum;
 }
 
-// ---- Eigen 3.2.0 SelfAdjointEigenSolver<Matrix3d>, eigenvalues (ascending) ----------------
-__device__ __forceinline__ double hypot_e(double x, double y) {  // internal::hypot_impl
-  const double ax = fabs(x), ay = fabs(y);
-  const double p = ax > ay ? ax : ay;
-  if (p == 0.0) return 0.0;
-  const double q = ax > ay ? ay : ax;
-  const double qp = q / p;
-  return p * sqrt(1.0 + qp * qp);
-}
-
-__device__ __forceinline__ void make_givens(double p, double q, double& c, double& s) {
-  if (q == 0.0) {
-    c = p < 0.0 ? -1.0 : 1.0;
-    s = 0.0;
-  } else if (p == 0.0) {
-    c = 0.0;
-    s = q < 0.0 ? 1.0 : -1.0;
-  } else if (fabs(p) > fabs(q)) {
-    const double t = q / p;
-    double u = sqrt(1.0 + t * t);
-    if (p < 0.0) u = -u;
-    c = 1.0 / u;
-    s = -t * c;
-  } else {
-    const double t = p / q;
-    double u = sqrt(1.0 + t * t);
-    if (q < 0.0) u = -u;
-    s = -1.0 / u;
-    c = -t * s;
-  }
-}
-
-// one implicit QR step on the unreduced block [start, end] of a 3x3 tridiagonal
-__device__ void qr_step(double d[3], double e[2], int start, int end) {
-  const double td = (d[end - 1] - d[end]) * 0.5;
-  const double ee = e[end - 1];
-  double mu = d[end];
-  if (td == 0.0) {
-    mu -= fabs(ee);
-  } else {
-    const double e2 = ee * ee;
-    const double h = hypot_e(td, ee);
-    if (e2 == 0.0)
-      mu -= (ee / (td + (td > 0.0 ? 1.0 : -1.0))) * (ee / h);
-    else
-      mu -= e2 / (td + (td > 0.0 ? h : -h));
-  }
-  double x = d[start] - mu;
-  double z = e[start];
-  for (int k = start; k < end; ++k) {
-    double c, s;
-    make_givens(x, z, c, s);
-    const double sdk = s * d[k] + c * e[k];
-    const double dkp1 = s * e[k] + c * d[k + 1];
-    d[k] = c * (c * d[k] - s * e[k]) - s * (c * e[k] - s * d[k + 1]);
-    d[k + 1] = s * sdk + c * dkp1;
-    e[k] = c * sdk - s * dkp1;
-    if (k > start) e[k - 1] = c * e[k - 1] - s * z;
-    x = e[k];
-    if (k < end - 1) {
-      z = -s * e[k + 1];
-      e[k + 1] = c * e[k + 1];
-    }
-  }
-}
-
-// lower triangle a00, a10, a11, a20, a21, a22 of a symmetric matrix -> ev ascending
-__device__ void eigen_selfadjoint3(double a00, double a10, double a11, double a20, double a21, double a22,
-                                   double ev[3]) {
-  double scale = fmax(fmax(fmax(fabs(a00), fabs(a10)), fmax(fabs(a11), fabs(a20))), fmax(fabs(a21), fabs(a22)));
-  if (scale == 0.0) scale = 1.0;
-  a00 /= scale;
-  a10 /= scale;
-  a11 /= scale;
-  a20 /= scale;
-  a21 /= scale;
-  a22 /= scale;
-  double d[3], e[2];
-  d[0] = a00;
-  const double v1norm2 = a20 * a20;
-  if (v1norm2 == 0.0) {
-    d[1] = a11;
-    d[2] = a22;
-    e[0] = a10;
-    e[1] = a21;
-  } else {
-    const double beta = sqrt(a10 * a10 + v1norm2);
-    const double inv_beta = 1.0 / beta;
-    const double m01 = a10 * inv_beta;
-    const double m02 = a20 * inv_beta;
-    const double q = 2.0 * m01 * a21 + m02 * (a22 - a11);
-    d[1] = a11 + m02 * q;
-    d[2] = a22 - m02 * q;
-    e[0] = beta;
-    e[1] = a21 - m01 * q;
-  }
-  int end = 2, start = 0, iter = 0;
-  while (end > 0) {
-    for (int i = start; i < end; ++i)
-      if (fabs(e[i]) <= (fabs(d[i]) + fabs(d[i + 1])) * 1e-12) e[i] = 0.0;
-    while (end > 0 && e[end - 1] == 0.0) end--;
-    if (end <= 0) break;
-    if (++iter > 90) break;
-    start = end - 1;
-    while (start > 0 && e[start - 1] != 0.0) start--;
-    qr_step(d, e, start, end);
-  }
-  if (iter <= 90) {
-    for (int i = 0; i < 2; ++i) {
-      int k = i;
-      for (int j = i + 1; j < 3; ++j)
-        if (d[j] < d[k]) k = j;
-      if (k != i) {
-        const double t = d[i];
-        d[i] = d[k];
-        d[k] = t;
-      }
-    }
-  }
-  ev[0] = d[0] * scale;
-  ev[1] = d[1] * scale;
-  ev[2] = d[2] * scale;
-}
+// Eigen 3.2.0 SelfAdjointEigenSolver<Matrix3d> eigenvalues: pfx_eigen3.h
 
 __device__ __forceinline__ double iss_third(double c00, double c01, double c02, double c11, double c12, double c22,
                                             double g21, double g32) {
   double ev[3];
-  eigen_selfadjoint3(c00, c01, c11, c02, c12, c22, ev);
+  eigen_selfadjoint3<false>(c00, c01, c11, c02, c12, c22, ev, nullptr);
   const double e1 = ev[2], e2 = ev[1], e3 = ev[0];
   if (isfinite(e1) && isfinite(e2) && isfinite(e3) && !(e3 < 0.0) && e2 / e1 < g21 && e3 / e2 < g32) return e3;
   return 0.0;

@@ -431,7 +431,7 @@ __global__ void k_border_dir_raw(Img I, const float4* __restrict__ P, const floa
       } else {
         d = sub3(nbp, pt);
       }
-      d = normalized3(d);
+      d = normalize3(d);  // get3dDirection: `direction.normalize ()`
       out = make_float4(d.x, d.y, d.z, 1.0f);
     }
   }
@@ -466,7 +466,7 @@ __global__ void k_border_dir_avg(Img I, const float4* __restrict__ P, const floa
         ws += 1.0f;
       }
     if ((int)rintf(ws) >= radius + 1) {
-      f3 d = normalized3(avg);
+      f3 d = normalize3(avg);  // `average_border_direction->normalize ()`
       out = make_float4(d.x, d.y, d.z, 1.0f);
     }
   }
@@ -602,10 +602,10 @@ __device__ __forceinline__ bool window_contributes(const Img& I, const int* __re
   return c != 0;
 }
 
-// histogram cell of the direction angle: 0.5 * normAngle(2 acos(dvx)) (NarfKeypoint,
-// nkdGetDirectionAngle) with acos correctly rounded to float.  The float acosf is within 1e-5 of
-// it; the map is monotone on each side of acos = pi/2 (where normAngle wraps), so equal cells at
-// both ends of the interval (same side) are exact, otherwise the correctly rounded value is used.
+// histogram cell of the direction angle: 0.5 * normAngle(2 acosf(dvx)) (NarfKeypoint,
+// nkdGetDirectionAngle) with glibc's acosf.  The hardware acosf is within 1e-5 of it; the map is
+// monotone on each side of acos = pi/2 (where normAngle wraps), so equal cells at both ends of the
+// interval (same side) are exact, otherwise glibc's value (pfx_device_math.h) is used.
 __device__ __forceinline__ int angle_cell_of(float ac, float d90, float d180) {
   const float angle = 0.5f * norm_angle(2.0f * ac);
   const float cellf = floorf((angle + d90) / d180 * 18);
@@ -615,7 +615,7 @@ __device__ __forceinline__ int angle_cell_of(float ac, float d90, float d180) {
 }
 
 __device__ __attribute__((noinline)) int angle_cell_exact(float dvx, float d90, float d180) {
-  return angle_cell_of(acosf_cr(dvx), d90, d180);
+  return angle_cell_of(acosf_glibc(dvx), d90, d180);
 }
 
 __device__ __forceinline__ int angle_cell(float dvx, float d90, float d180) {
@@ -665,7 +665,7 @@ __device__ __forceinline__ void contribute(const InterestParams& ip, float sc, f
   const float pos = (pd < 2.0f) ? sc : sc * (1.0f - df);
   const f3 rot = mk3(0.0f + dot3(tmp0, dir), 0.0f + dot3(tmp1, dir), 0.0f + dot3(tmp2, dir));
   const float nrm = sqrtf(rot.x * rot.x + rot.y * rot.y);
-  const float dvx = rot.x / nrm;
+  const float dvx = rot.x * (1.0f / nrm);  // Vector2f::normalize (): times the reciprocal
   const int cell = angle_cell(dvx, ip.d90, ip.d180);
   if (pos > 0.0f) atomicMax(&hist[cell], __float_as_uint(pos));
   if (neg < 1.0f) atomicMin(neg_bits, __float_as_uint(neg));

@@ -1,6 +1,6 @@
 // pfx_normal_math.h -- PCL's per-point normal from the ordered neighbour sums:
 //   accu = sequential float sums {x^2, xy, xz, y^2, yz, z^2, x, y, z} in FLANN order
-//   C    = accu/|N| - mean mean^T;  (lambda, n) = pcl::eigen33(C);  curvature = |lambda / tr C|
+//   C    = accu * (1/|N|) - mean mean^T  (Eigen 3.2 `accu /= n`);  (lambda, n) = pcl::eigen33(C);  curvature = |lambda / tr C|
 //   flip n towards the viewpoint;  |N| < 3 -> NaN
 #pragma once
 #include "pfx_device_math.h"
@@ -21,9 +21,9 @@ __device__ __forceinline__ void finish_normal(const float accu_in[9], int k, flo
     return;
   }
   float a[9];
-  const float cnt = (float)k;
+  const float inv = 1.0f / (float)k;  // `accu /= n`: Eigen 3.2 multiplies by the reciprocal
 #pragma unroll
-  for (int i = 0; i < 9; ++i) a[i] = accu_in[i] / cnt;
+  for (int i = 0; i < 9; ++i) a[i] = accu_in[i] * inv;
   Sym3 C;
   C.a00 = a[0] - a[6] * a[6];
   C.a01 = a[1] - a[6] * a[7];

@@ -185,7 +185,8 @@ __global__ void k_ransac_threshold(const float* __restrict__ x, const float* __r
     a[3] += py * py; a[4] += py * pz; a[5] += pz * pz;
     a[6] += px; a[7] += py; a[8] += pz;
   }
-  for (int k = 0; k < 9; ++k) a[k] /= (float)n;
+  const float inv = 1.0f / (float)n;  // computeMeanAndCovarianceMatrix `accu /= n` (Eigen 3.2)
+  for (int k = 0; k < 9; ++k) a[k] *= inv;
   const float c00 = a[0] - a[6] * a[6], c01 = a[1] - a[6] * a[7], c02 = a[2] - a[6] * a[8];
   const float c11 = a[3] - a[7] * a[7], c12 = a[4] - a[7] * a[8], c22 = a[5] - a[8] * a[8];
   float scale = fmaxf(fmaxf(fmaxf(fabsf(c00), fabsf(c01)), fmaxf(fabsf(c02), fabsf(c11))),

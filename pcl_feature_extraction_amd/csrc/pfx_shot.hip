@@ -5,12 +5,14 @@
 //   1. radius neighbours in FLANN order (bitonic sort of (d2, caller index) keys in LDS);
 //   2. SHOTLocalReferenceFrameEstimation::getLocalRF: the weighted double covariance is a set of
 //      strictly ordered double chains (one lane per matrix entry + one for the weight sum) over
-//      LDS-staged neighbour chunks; cyclic Jacobi eigen solver (the oracle's operation
-//      sequence, double); sign disambiguation counts reduced over the block;
+//      LDS-staged neighbour chunks; Eigen 3.2.0's SelfAdjointEigenSolver<Matrix3d> with
+//      eigenvectors (pfx_eigen3.h, the oracle's operation sequence); sign disambiguation counts
+//      reduced over the block;
 //   3. SHOT: every neighbour's (up to) five interpolated bin updates are computed in parallel and
 //      applied per bin in PCL's sequential order (each wave owns a quarter of the bins; lanes
 //      that collide on a bin are serialised lowest-first); normalizeHistogram by one lane (double accumulation, as PCL).
 // Descriptors and reference frames are bit-exact against the restatement.
+#include "pfx_eigen3.h"
 #include "pfx_neighbors.h"
 
 namespace pfx {
@@ -24,55 +26,6 @@ constexpr double kRad45 = 0.78539816339744830961566084581988;
 constexpr double kRad90 = 1.5707963267948966192313216916398;
 constexpr double kRad135 = 2.3561944901923449288469825374596;
 constexpr double kRadPi78 = 2.7488935718910690836548129603691;
-
-// oracle jacobi3 (or_shot.cpp): same operation sequence
-__device__ __attribute__((noinline)) void jacobi3(double a[3][3], double evals[3], double V[3][3]) {
-  for (int i = 0; i < 3; ++i)
-    for (int j = 0; j < 3; ++j) V[i][j] = (i == j) ? 1.0 : 0.0;
-  for (int sweep = 0; sweep < 50; ++sweep) {
-    const double off = (a[0][1] * a[0][1] + a[0][2] * a[0][2]) + a[1][2] * a[1][2];
-    const double diag = (a[0][0] * a[0][0] + a[1][1] * a[1][1]) + a[2][2] * a[2][2];
-    if (off == 0.0 || off <= 1e-36 * diag) break;
-    for (int pq = 0; pq < 3; ++pq) {
-      const int p = (pq == 2) ? 1 : 0, q = (pq == 0) ? 1 : 2;
-      const double apq = a[p][q];
-      if (apq == 0.0) continue;
-      const double theta = (a[q][q] - a[p][p]) / (2.0 * apq);
-      double t;
-      if (fabs(theta) > 1e150) t = 0.5 / theta;
-      else t = (theta >= 0.0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
-      const double c = 1.0 / sqrt(t * t + 1.0), s = t * c;
-      const double tau = s / (1.0 + c);
-      a[p][p] = a[p][p] - t * apq;
-      a[q][q] = a[q][q] + t * apq;
-      a[p][q] = a[q][p] = 0.0;
-      const int r = 3 - p - q;
-      const double arp = a[r][p], arq = a[r][q];
-      a[r][p] = a[p][r] = arp - s * (arq + tau * arp);
-      a[r][q] = a[q][r] = arq + s * (arp - tau * arq);
-      for (int k = 0; k < 3; ++k) {
-        const double vkp = V[k][p], vkq = V[k][q];
-        V[k][p] = vkp - s * (vkq + tau * vkp);
-        V[k][q] = vkq + s * (vkp - tau * vkq);
-      }
-    }
-  }
-  const double ev[3] = {a[0][0], a[1][1], a[2][2]};
-  int ord[3] = {0, 1, 2};
-  for (int i = 1; i < 3; ++i) {
-    const int v = ord[i];
-    int j = i;
-    while (j > 0 && ev[v] < ev[ord[j - 1]]) { ord[j] = ord[j - 1]; --j; }
-    ord[j] = v;
-  }
-  double Vs[3][3];
-  for (int k = 0; k < 3; ++k) {
-    evals[k] = ev[ord[k]];
-    for (int i = 0; i < 3; ++i) Vs[i][k] = V[i][ord[k]];
-  }
-  for (int i = 0; i < 3; ++i)
-    for (int k = 0; k < 3; ++k) V[i][k] = Vs[i][k];
-}
 
 // the five (bin, value) updates of one neighbour (SHOTEstimation::interpolateSingleChannel with
 // the bin distance of createBinDistanceShape); bin -1 = no update.  Order = PCL's order.
@@ -292,14 +245,14 @@ __global__ void __launch_bounds__(256) k_shot(GridView g, const float* __restric
     if (tid == 0) {
       S.ok = 0;
       if (valid >= 5) {
-        double A[3][3], ev[3], V[3][3];
-        const double sum = S.cov[9];
-        for (int a = 0; a < 3; ++a)
-          for (int b = 0; b < 3; ++b) A[a][b] = S.cov[3 * a + b] / sum;
-        jacobi3(A, ev, V);
+        // `cov_m /= sum` (Eigen 3.2: times the reciprocal), SelfAdjointEigenSolver<Matrix3d>
+        double ev[3], V[3][3];
+        const double inv = 1.0 / S.cov[9];
+        eigen_selfadjoint3<true>(S.cov[0] * inv, S.cov[3] * inv, S.cov[4] * inv, S.cov[6] * inv, S.cov[7] * inv,
+                                 S.cov[8] * inv, ev, V);
         if (isfinite(ev[0]) && isfinite(ev[1]) && isfinite(ev[2])) {
           S.ok = 1;
-          for (int i = 0; i < 3; ++i) { S.axes[i] = V[i][2]; S.axes[3 + i] = V[i][0]; }
+          for (int i = 0; i < 3; ++i) { S.axes[i] = V[2][i]; S.axes[3 + i] = V[0][i]; }
         }
       }
     }

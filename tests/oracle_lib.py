@@ -39,6 +39,22 @@ def lib():
     return _lib
 
 
+def libm_mismatches(which, n, seed=0):
+    """Bits where the oracle's glibc restatement differs from the host libm (0: atan2f on n
+    pairs, 1: acosf on every n-th float of [-1, 1])."""
+    f = lib().orc_libm_mismatches
+    f.restype = ctypes.c_int64
+    return int(f(ctypes.c_int(which), _i64(n), ctypes.c_uint64(seed)))
+
+
+def point_covariance(x, y, z, idx):
+    x, y, z = map(_f32, (x, y, z))
+    idx = np.ascontiguousarray(idx, dtype=np.int32)
+    out = np.zeros(6, np.float32)
+    lib().orc_point_covariance(_p(x), _p(y), _p(z), _p(idx, _i32p), _i64(len(idx)), _p(out))
+    return out
+
+
 def _p(a, t=_f32p):
     return a.ctypes.data_as(t) if a is not None else None
 
@@ -188,6 +204,16 @@ def eigen_selfadjoint3(mats):
     ev = np.empty((len(a), 3), np.float64)
     assert lib().orc_eigen_selfadjoint3(_p(a, _f64p), _i64(len(a)), _p(ev, _f64p)) == 0
     return ev
+
+
+def eigen_selfadjoint3_vectors(mats):
+    """Eigen 3.2.0 SelfAdjointEigenSolver<Matrix3d> values (n, 3) and vectors (n, 3, 3):
+    vec[i, k] = eigenvector of value k (Eigen's eigenvectors().col(k))."""
+    a = np.ascontiguousarray(mats, np.float64).reshape(-1, 9)
+    ev = np.empty((len(a), 3), np.float64)
+    vec = np.empty((len(a), 3, 3), np.float64)
+    assert lib().orc_eigen_selfadjoint3_vectors(_p(a, _f64p), _i64(len(a)), _p(ev, _f64p), _p(vec, _f64p)) == 0
+    return ev, vec
 
 
 def cloud_resolution(x, y, z, threads=0):

@@ -36,9 +36,11 @@ def test_normals_plane_and_viewpoint_flip():
     g = np.stack(np.meshgrid(np.arange(20), np.arange(20)), -1).reshape(-1, 2).astype(np.float32) * 0.01
     x, y, z = g[:, 0].copy(), g[:, 1].copy(), np.full(len(g), 2.0, np.float32)
     nx, ny, nz, cv = O.normals(x, y, z, 0.05)
-    assert np.allclose(nx, 0, atol=1e-6) and np.allclose(ny, 0, atol=1e-6)
+    # float noise: E[z^2] - E[z]^2 with sums times rnd(1/n) (Eigen 3.2's reciprocal) leaves c22
+    # ~1e-7 instead of 0 against c00 ~ 2e-4: tilts of <= 2e-4 and curvature <= 1e-3 (as PCL)
+    assert np.allclose(nx, 0, atol=5e-4) and np.allclose(ny, 0, atol=5e-4)
     assert np.allclose(nz, -1.0, atol=1e-6)  # flipped towards the viewpoint at the origin
-    assert np.allclose(cv, 0.0, atol=1e-6)
+    assert np.allclose(cv, 0.0, atol=1e-3)
     nx, ny, nz, _ = O.normals(x, y, z, 0.05, vp=(0.0, 0.0, 10.0))
     assert np.allclose(nz, 1.0, atol=1e-6)
 
@@ -157,3 +159,39 @@ def test_golden_fixtures_reproduce(name):
     wn = np.isnan(want) if isf else np.zeros(want.shape, bool)
     assert np.array_equal(gn, wn)
     assert np.array_equal(np.asarray(got)[~gn], np.asarray(want)[~wn])
+
+
+def test_glibc_float_transcendentals_pinned_to_libm():
+    """The oracle's atan2f / acosf restate glibc's fdlibm float routines (e_atan2f.c, s_atanf.c,
+    e_acosf.c); pinned bit for bit against this host's libm, which still ships them (they are
+    NOT correctly rounded: the CR value differs on ~19 % of random atan2f pairs)."""
+    assert O.libm_mismatches(0, 4_000_000, seed=12345) == 0
+    assert O.libm_mismatches(1, 7) == 0   # every 7th float of [-1, 1], both signs
+
+
+def test_covariance_uses_eigen32_reciprocal_division():
+    """computeMeanAndCovarianceMatrix's `accu /= n` is `accu *= 1/n` under Eigen 3.2
+    (SelfCwiseBinaryOp.h, DenseBase::operator/=); a neighbourhood where the two forms differ."""
+    rng = np.random.default_rng(3)
+    found = 0
+    for trial in range(200):
+        n = int(rng.integers(3, 40))
+        x, y, z = (rng.normal(size=n).astype(np.float32) * np.float32(0.03) + np.float32(c)
+                   for c in (1.3, -0.4, 2.2))
+        idx = np.arange(n, dtype=np.int32)
+        acc = np.zeros(9, np.float32)
+        for p in idx:   # sequential float32 sums, FLANN order = index order here
+            terms = (x[p] * x[p], x[p] * y[p], x[p] * z[p], y[p] * y[p], y[p] * z[p], z[p] * z[p], x[p], y[p], z[p])
+            for i, t in enumerate(terms):
+                acc[i] = np.float32(acc[i] + np.float32(t))
+        recip = acc * np.float32(np.float32(1.0) / np.float32(n))
+        quot = acc / np.float32(n)
+
+        def cov(a):
+            return np.array([a[0] - a[6] * a[6], a[1] - a[6] * a[7], a[2] - a[6] * a[8],
+                             a[3] - a[7] * a[7], a[4] - a[7] * a[8], a[5] - a[8] * a[8]], np.float32)
+        got = O.point_covariance(x, y, z, idx)
+        assert np.array_equal(got.view(np.uint32), cov(recip).view(np.uint32))
+        if not np.array_equal(cov(recip).view(np.uint32), cov(quot).view(np.uint32)):
+            found += 1
+    assert found > 10   # the forms do differ on these inputs, so the check is not vacuous

@@ -37,6 +37,35 @@ def test_eigen_random_vs_lapack():
     assert np.all(np.diff(ev, axis=1) >= 0)  # ascending
 
 
+def test_eigen_vectors_random_vs_lapack():
+    """The eigenvector half (Householder Q x Givens rotations) used by SHOT's LRF: orthonormal,
+    A v = lambda v, equal to LAPACK's up to sign where the spectrum is separated, and the
+    values bit-identical to the values-only path (the vectors never feed back)."""
+    rng = np.random.default_rng(5)
+    A = rng.normal(size=(3000, 3, 3)) * rng.uniform(1e-6, 1e3, size=(3000, 1, 1))
+    A = A + A.transpose(0, 2, 1)
+    ev, vec = O.eigen_selfadjoint3_vectors(A)
+    assert np.array_equal(ev, O.eigen_selfadjoint3(A))
+    scale = np.abs(ev).max(axis=1)
+    for i in range(len(A)):
+        V = vec[i].T   # columns = eigenvectors
+        assert np.allclose(V.T @ V, np.eye(3), atol=1e-13)
+        assert np.allclose(A[i] @ V, V * ev[i], atol=1e-12 * scale[i])
+    w, U = np.linalg.eigh(A)
+    gap = np.minimum(np.diff(w, axis=2 - 1)[:, 0], np.diff(w, axis=1)[:, 1]) / scale
+    sep = gap > 1e-3
+    for i in np.nonzero(sep)[0][:500]:
+        for k in range(3):
+            assert abs(abs(np.dot(vec[i, k], U[i][:, k])) - 1.0) < 1e-9
+
+
+def test_eigen_vectors_special_matrices():
+    ev, vec = O.eigen_selfadjoint3_vectors(np.array([np.diag([3.0, 1.0, 2.0]), np.eye(3) * 5.0]))
+    assert np.array_equal(ev[0], [1.0, 2.0, 3.0])
+    assert np.array_equal(np.abs(vec[0]), [[0, 1, 0], [0, 0, 1], [1, 0, 0]])
+    assert np.array_equal(vec[1], np.eye(3))
+
+
 def test_eigen_special_matrices():
     M = np.array([np.diag([3.0, 1.0, 2.0]), np.zeros((3, 3)), np.eye(3) * 5.0,
                   [[1.0, 1.0, 0.0], [1.0, 1.0, 0.0], [0.0, 0.0, 0.0]]])
