@@ -206,10 +206,11 @@ pfx_status pfx_narf_debug_image(pfx_ctx* ctx, const char* which, void* out, int6
 /* ---- the reference's keypoint -> cloud mapping (keypoints.h:227-229) ----------------- */
 /* k_xyz[i] = cloud[idx[i]] for 0 <= idx[i] < n (the reference indexes the cloud with pixel
  * indices; out-of-range indices are an out-of-bounds read there and are skipped here).
- * Returns the number of points written to d_kx/d_ky/d_kz. */
+ * d_kx/d_ky/d_kz hold `cap` floats each; more in-range indices than `cap` -> PFX_ERR_CAPACITY
+ * (nothing written).  Returns the number of points written in *n_out. */
 pfx_status pfx_gather_points_dev(pfx_ctx* ctx, const float* d_x, const float* d_y,
                                  const float* d_z, int64_t n, const int32_t* idx, int64_t k,
-                                 float* d_kx, float* d_ky, float* d_kz, int64_t* n_out);
+                                 float* d_kx, float* d_ky, float* d_kz, int64_t cap, int64_t* n_out);
 
 /* Descriptor matching.  Rows are `dim` floats, `*_stride` floats apart
  * (FPFHSignature33: dim 33, stride 33; PointCloud<SHOT352> read in place: dim 352, stride 361).

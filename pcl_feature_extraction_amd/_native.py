@@ -104,7 +104,7 @@ _SIGS = {
                                        ctypes.POINTER(NarfParams), c_vp, c_i64, c_i64p]),
     "pfx_narf_debug_image": (c_int, [c_vp, ctypes.c_char_p, c_vp, c_i64]),
     "pfx_gather_points_dev": (c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_i64, c_vp, c_vp, c_vp,
-                                      c_i64p]),
+                                      c_i64, c_i64p]),
     "pfx_nearest_descriptors_dev": (c_int, [c_vp, c_vp, c_i64, c_i64, c_vp, c_i64, c_i64, ctypes.c_int32,
                                             c_vp, c_vp, c_vp, c_vp]),
     "pfx_pcd_read_header": (c_int, [ctypes.c_char_p, ctypes.POINTER(PcdHeader)]),

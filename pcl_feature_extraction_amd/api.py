@@ -232,7 +232,8 @@ class Context:
         idx = np.ascontiguousarray(idx_np, dtype=np.int32)
         nout = ctypes.c_int64()
         self._check(self._lib.pfx_gather_points_dev(self.h, _ptr(x), _ptr(y), _ptr(z), x.numel(), _ptr(idx),
-                                                    len(idx), _ptr(kx), _ptr(ky), _ptr(kz), ctypes.byref(nout)))
+                                                    len(idx), _ptr(kx), _ptr(ky), _ptr(kz),
+                                                    min(kx.numel(), ky.numel(), kz.numel()), ctypes.byref(nout)))
         return nout.value
 
     # ---- PCD input: pcl::io::loadPCDFile<PointXYZRGB> (evaluation.cpp:226-235) -------------

@@ -445,16 +445,19 @@ __global__ void k_gather_points(const float* __restrict__ x, const float* __rest
 
 extern "C" pfx_status pfx_gather_points_dev(pfx_ctx* ctx, const float* d_x, const float* d_y, const float* d_z,
                                             int64_t n, const int32_t* idx, int64_t k, float* d_kx, float* d_ky,
-                                            float* d_kz, int64_t* n_out) {
+                                            float* d_kz, int64_t cap, int64_t* n_out) {
   PFX_API_BEGIN
   check_ctx(ctx);
-  if (!n_out || k < 0 || (k && !idx)) throw Error(PFX_ERR_INVALID, "gather_points: invalid arguments");
+  if (!n_out || k < 0 || cap < 0 || (k && !idx)) throw Error(PFX_ERR_INVALID, "gather_points: invalid arguments");
   // the reference reads cloud->points[pixel_index] unchecked (out of bounds when the index is
   // >= cloud size); the guarded mapping keeps only in-range indices, in order
   std::vector<int32_t> keep;
   keep.reserve((size_t)k);
   for (int64_t i = 0; i < k; ++i)
     if (idx[i] >= 0 && idx[i] < n) keep.push_back(idx[i]);
+  if ((int64_t)keep.size() > cap)
+    throw Error(PFX_ERR_CAPACITY, "gather_points: " + std::to_string(keep.size()) + " in-range keypoints, output holds " +
+                                      std::to_string(cap));
   *n_out = (int64_t)keep.size();
   if (keep.empty()) return PFX_OK;
   int32_t* d_idx = ctx->buf("gather_idx").as<int32_t>(keep.size());

@@ -874,8 +874,12 @@ void build_lists(pfx_ctx* ctx, const Grid& G, const uint8_t* mask, double radius
       throw Error(PFX_ERR_CAPACITY, std::string(tag) + ": a query has " + std::to_string(h_cnt[4]) +
                                         " neighbours (> " + std::to_string(kCapHuge) + " supported)");
     if (h_cur[0] > lo.cap) {  // list buffer too small: grow (no copy needed) and rebuild once
-      lb.release();  // headroom: arena tails vary from run to run
-      lb.get(sizeof(uint32_t) * ((size_t)h_cur[0] + (size_t)h_cur[0] / 8 + ((size_t)1 << 22)));
+      // The slot demand of a run is the entries + interleave padding (fixed by the input) + the
+      // unused arena tails (scheduling-dependent, at most one arena per launched workgroup), so
+      // this run's demand plus the tail bound always fits the rebuild.
+      const size_t tails = (size_t)(256 * 4 * 2 + 256 * 3 * 4 + 256 * 2 * 4) * kArena + (size_t)(256 * 4 + kHugeBlocks) * kArenaQuery;
+      lb.release();
+      lb.get(sizeof(uint32_t) * ((size_t)h_cur[0] + tails + ((size_t)1 << 20)));
       continue;
     }
     out.nq = h_nq;
