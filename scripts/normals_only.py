@@ -30,7 +30,7 @@ for name, gen, seed in (("room", synth_room, 2), ("seabed", synth_seabed, 3)):
         for _ in range(steps):
             ctx.normals_dev(b.x, b.y, b.z, 0.05, b.nx, b.ny, b.nz, b.curv)
         torch.cuda.synchronize()
-        names = ["grid_build", "normals", "normals_lists_sparse", "normals_lists_dense", "normals_lists_query",
+        names = ["grid_build", "normals", "normals_lists_small", "normals_lists_sparse", "normals_lists_dense", "normals_lists_query",
                  "normals_chain", "normals_chain_big", "normals_long"]
         t = {n: round(ctx.kernel_time(n)[0] / steps, 4) for n in names}
         nb = ctx.stat("normals_neighbors")
