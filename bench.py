@@ -21,6 +21,8 @@ features.h:224-253): mutual 1-NN between the SHOT-352 descriptor sets of two suc
 branch, keypoints.h:177-189): one step = cloud resolution + ISSKeypoint3D over the 1M-point room.
 `--workload harris`: F3's Harris3D branch (keypoints.h:150-162 + getKeypointsCloud) over the same
 room: normals (r 0.01) + response + suppression + corner refinement + snap.
+`--workload harris6d`: F3's Harris6D branch (keypoints.h:164-176) over the same room with a
+procedural colour texture: normals + intensity gradients + 6x6 response + the Harris3D tail.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--workload fpfh|shot|...] [--scans S]
                     [--no-cpu-baseline] [--no-e2e]
@@ -148,7 +150,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", choices=["fpfh", "shot", "match", "iss", "harris"], default="fpfh")
+    ap.add_argument("--workload", choices=["fpfh", "shot", "match", "iss", "harris", "harris6d"], default="fpfh")
     ap.add_argument("--scans", type=int, default=0,
                     help="fpfh workload: scans per step (default 1 = configs[2] at --gpus 1, 8 = configs[4] at N > 1)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -181,8 +183,8 @@ def main():
             return bench_match(args, torch, dev, world, rank, local)
         if args.workload == "iss":
             return bench_iss(args, torch, dev, world, rank, local)
-        if args.workload == "harris":
-            return bench_harris(args, torch, dev, world, rank, local)
+        if args.workload in ("harris", "harris6d"):
+            return bench_harris(args, torch, dev, world, rank, local, six=args.workload == "harris6d")
         return bench_scans(args, torch, dist, dev, world, rank, local)
     finally:
         if world > 1:
@@ -639,22 +641,32 @@ def bench_iss(args, torch, dev, world, rank, local):
     ctx.close()
 
 
-def bench_harris(args, torch, dev, world, rank, local):
-    """Keypoints("Harris3D").compute over the 1M-point room scan (one per rank)."""
+def bench_harris(args, torch, dev, world, rank, local, six=False):
+    """Keypoints("Harris3D" / "Harris6D").compute over the 1M-point room scan (one
+    per rank); Harris6D reads the scan's colours (synth.texture_rgb: a smooth procedural texture)."""
     import numpy as np
 
     from pcl_feature_extraction_amd import Context
-    from pcl_feature_extraction_amd.pipeline import keypoints_harris3d
-    from pcl_feature_extraction_amd.synth import synth_room
+    from pcl_feature_extraction_amd.pipeline import keypoints_harris3d, keypoints_harris6d
+    from pcl_feature_extraction_amd.synth import synth_room, texture_rgb
 
-    x, y, z, _ = synth_room(N_POINTS, 2 if world == 1 else 100 + rank)
+    seed = 2 if world == 1 else 100 + rank
+    x, y, z, _ = synth_room(N_POINTS, seed)
+    rgb = texture_rgb(x, y, z, seed)
     ctx = Context(local)
     ctx.set_stream(torch.cuda.current_stream(dev).cuda_stream)
     dx, dy, dz = (torch.from_numpy(a).to(dev) for a in (x, y, z))
+    drgb = torch.from_numpy(rgb.view(np.int32)).to(dev)
     idx = torch.empty(N_POINTS, dtype=torch.int32, device=dev)
+    tag = "harris6d" if six else "harris3d"
+
+    def step():
+        if six:
+            return keypoints_harris6d(ctx, dx, dy, dz, drgb, idx)
+        return keypoints_harris3d(ctx, dx, dy, dz, idx)
     k = 0
     for _ in range(args.warmup):
-        k = keypoints_harris3d(ctx, dx, dy, dz, idx)
+        k = step()
     torch.cuda.synchronize(dev)
     ctx.set_timing(True)
     ctx.reset_timing()
@@ -663,7 +675,7 @@ def bench_harris(args, torch, dev, world, rank, local):
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        k = keypoints_harris3d(ctx, dx, dy, dz, idx)
+        k = step()
     torch.cuda.synchronize(dev)
     if world > 1:
         torch.distributed.barrier()
@@ -673,42 +685,63 @@ def bench_harris(args, torch, dev, world, rank, local):
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         elapsed = float(t.item())
     if rank == 0:
-        # the response kernel: every query's FLANN-ordered list (4 B entries) and its neighbours'
-        # normals; algorithmic bytes per launch = sum_q |N_0.01(q)| x (4 + 12) B + N x 4 B
         nb = ctx.stat("normals_neighbors")
-        tr, nr = ctx.kernel_time("harris3d_response")
-        resp_s = tr / max(nr, 1) / 1e3
-        algo = nb * 16 + N_POINTS * 4
+        if six:
+            # gradient (two passes: list entry 4 B + xyz 12 B + rgb 4 B per neighbour, normal in and
+            # gradient out 24 B per point) + response (entry 4 B + normal 12 B + gradient 12 B per
+            # neighbour, 4 B out): sum_q |N_0.01(q)| x 68 B + N x 28 B
+            tg, ng = ctx.kernel_time("harris6d_gradient")
+            tr, nr = ctx.kernel_time("harris6d_response")
+            resp_s = (tg / max(ng, 1) + tr / max(nr, 1)) / 1e3
+            algo = nb * 68 + N_POINTS * 28
+            kname = "k_intensity_gradient + k_harris6d_response"
+        else:
+            # the response kernel: every query's FLANN-ordered list (4 B entries) and its neighbours'
+            # normals; algorithmic bytes per launch = sum_q |N_0.01(q)| x (4 + 12) B + N x 4 B
+            tr, nr = ctx.kernel_time("harris3d_response")
+            resp_s = tr / max(nr, 1) / 1e3
+            algo = nb * 16 + N_POINTS * 4
+            kname = "k_harris_response + k_harris_nms"
         achieved = algo / resp_s / 1e9 if resp_s > 0 else 0.0
-        stages = {nm: round(ctx.kernel_time(nm)[0] / args.steps, 4)
-                  for nm in ("harris3d", "normals_lists_phase", "grid_bbox", "grid_build", "normals_tiles",
-                             "normals_lists_small", "normals_lists_sparse", "normals_lists_dense", "normals_lists_query", "normals_chain",
-                             "normals_chain_big", "normals_long", "harris3d_response", "harris3d_refine")}
-        corners = ctx.stat("harris3d_corners")
+        names = (tag, "normals_lists_phase", "grid_bbox", "grid_build", "normals_tiles", "normals_lists_small",
+                 "normals_lists_sparse", "normals_lists_dense", "normals_lists_query", "normals_chain",
+                 "normals_chain_big", "normals_long", tag + "_refine")
+        names += ("harris6d_gradient", "harris6d_response") if six else ("harris3d_response",)
+        stages = {nm: round(ctx.kernel_time(nm)[0] / args.steps, 4) for nm in names}
+        corners = ctx.stat(tag + "_corners")
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             sys.path.insert(0, os.path.join(ROOT, "tests"))
             import oracle_lib as O
             threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
-            c0 = time.perf_counter()
-            okp, _, _ = O.harris3d(x, y, z, 0.01, 1e-6, True, threads=threads)
-            csec = time.perf_counter() - c0
+            runs = []
+            for _ in range(2):  # 1 warm-up + 1 timed: the OpenMP restatement takes seconds per scan
+                c0 = time.perf_counter()
+                okp = (O.harris6d(x, y, z, rgb, 0.01, 1e-6, True, threads=threads)[0] if six
+                       else O.harris3d(x, y, z, 0.01, 1e-6, True, threads=threads)[0])
+                runs.append(time.perf_counter() - c0)
+            csec = runs[-1]
             same = bool(np.array_equal(okp, idx[:k].cpu().numpy()))
             cpu = {"value": round(N_POINTS / csec / 1e6, 6), "unit": "Mpoints/s", "cores": threads, "kind": "port",
                    "sample": (f"the same 1M-point scan through the CPU restatement (oracle/or_keypoints.cpp "
-                              f"orc_harris3d: OpenMP normals, responses, suppression, refinement), {csec:.1f}s"),
+                              f"orc_{tag}: OpenMP normals, {'gradients, ' if six else ''}responses, suppression, "
+                              f"refinement), 1 warm-up + 1 timed run: {csec:.1f}s"),
                    "parity": {"keypoints": same}}
+        label = "HARRIS_6D" if six else "HARRIS_3D"
         line = {
-            "metric": "Mpoints/s through Harris3D keypoints (Keypoints::compute HARRIS_3D branch) on 1M-pt cloud",
+            "metric": f"Mpoints/s through {'Harris6D' if six else 'Harris3D'} keypoints (Keypoints::compute "
+                      f"{label} branch) on 1M-pt cloud",
             "value": round(world * N_POINTS * args.steps / elapsed / 1e6, 4),
             "unit": "Mpoints/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "f32",
-            "data": "synthetic (synth_room: seeded pinhole room scan; see synth.py)",
-            "config": {"workload": "SURVEY 8(f) F3: HarrisKeypoint3D(HARRIS, r 0.01, nms, threshold 1e-6, refine) + "
-                                   "getKeypointsCloud on configs[2]'s 1M-pt room", "points_per_scan": N_POINTS,
+            "data": ("synthetic (synth_room: seeded pinhole room scan" +
+                     (", colours from synth.texture_rgb" if six else "") + "; see synth.py)"),
+            "config": {"workload": (f"SURVEY 8(f) F3: HarrisKeypoint{'6D' if six else '3D(HARRIS'}"
+                                    f"{'(' if six else ', '}r 0.01, nms, threshold 1e-6, refine) + "
+                                    "getKeypointsCloud on configs[2]'s 1M-pt room"), "points_per_scan": N_POINTS,
                        "corners": int(corners), "keypoints": int(k), "parallelism": f"scan-per-gpu x{world}"},
-            "roofline": {"bound": "hbm", "kernel": "k_harris_response + k_harris_nms", "achieved": round(achieved, 2),
+            "roofline": {"bound": "hbm", "kernel": kname, "achieved": round(achieved, 2),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5),
                          "traffic": None, "algorithmic_bytes_per_launch": int(algo), "avg_ms": round(resp_s * 1e3, 4),
                          "neighbors_per_launch": int(nb), "stages_ms_per_step": stages},

@@ -35,6 +35,7 @@
  *   pfx_iss_keypoints*  <- ISSKeypoint3D<PointXYZRGB,PointXYZRGB>::compute as configured by
  *                          Keypoints::compute's ISS branch (keypoints.h:177-189)
  *   pfx_harris3d_keypoints* <- HarrisKeypoint3D<PointXYZRGB,PointXYZI>::compute + getKeypointsCloud
+ *   pfx_harris6d_keypoints* <- HarrisKeypoint6D<PointXYZRGB,PointXYZI>::compute + getKeypointsCloud
  *                          (Keypoints::compute's HARRIS_3D branch, keypoints.h:150-162, 365-395)
  *   pfx_ransac_rejector <- registration::CorrespondenceRejectorSampleConsensus<PointXYZRGB> in
  *                          Features<T>::filterCorrespondences (features.h:282-297)
@@ -293,6 +294,23 @@ pfx_status pfx_harris3d_keypoints_dev(pfx_ctx* ctx, const float* d_x, const floa
 pfx_status pfx_harris3d_keypoints(pfx_ctx* ctx, const float* x, const float* y, const float* z, int64_t n,
                                   double radius, float threshold, int32_t non_max, int32_t refine, int32_t* idx,
                                   int64_t cap, int64_t* n_out, float* response, float* corners, int64_t* n_corners);
+
+/* HarrisKeypoint6D (keypoints.h:164-176) + Keypoints::getKeypointsCloud: normals at the radius
+ * (viewpoint 0), IntensityGradientEstimation at the radius over the colour intensity
+ * float(299 r + 587 g + 114 b) * 0.001f (IntensityFieldAccessor<PointXYZRGB>), gradients of
+ * squared length > 200 scaled to unit length, the 6x6 covariance of (normal, gradient) over the
+ * radius ball and its fourth eigenvalue as the response (responseTomasi), non-maximum
+ * suppression above `threshold`, corner refinement, snap -- outputs as the Harris3D entry.
+ * rgb: one packed 0x00RRGGBB word per point (the bits of PointXYZRGB::rgb).  grad (nullable,
+ * 3 n floats): the normalised gradient of every point (NaN where PCL writes NaN). */
+pfx_status pfx_harris6d_keypoints_dev(pfx_ctx* ctx, const float* d_x, const float* d_y, const float* d_z,
+                                      const uint32_t* d_rgb, int64_t n, double radius, float threshold,
+                                      int32_t non_max, int32_t refine, int32_t* d_idx, int64_t cap, int64_t* n_out,
+                                      float* d_response, float* d_corners, int64_t* n_corners, float* d_grad);
+pfx_status pfx_harris6d_keypoints(pfx_ctx* ctx, const float* x, const float* y, const float* z, const uint32_t* rgb,
+                                  int64_t n, double radius, float threshold, int32_t non_max, int32_t refine,
+                                  int32_t* idx, int64_t cap, int64_t* n_out, float* response, float* corners,
+                                  int64_t* n_corners, float* grad);
 
 /* ---- RANSAC correspondence rejection --------------------------------- */
 /* CorrespondenceRejectorSampleConsensus::getCorrespondences + getBestTransformation (host

@@ -280,7 +280,8 @@ float invert3x3Sym(const M3& a, M3& inv) {
     inv.m[4] = c[0] * c[8] - c[2] * c[2];
     inv.m[5] = inv.m[7] = c[1] * c[2] - c[0] * c[5];
     inv.m[8] = c[0] * c[4] - c[1] * c[1];
-    for (int k = 0; k < 9; ++k) inv.m[k] /= det;
+    const float rdet = 1.0f / det;  // `inverse /= det`: Eigen 3.2 multiplies by the reciprocal
+    for (int k = 0; k < 9; ++k) inv.m[k] *= rdet;
   }
   return det;
 }
@@ -317,6 +318,11 @@ float harris_response(const std::vector<int>& nb, const float* nx, const float* 
   return 0.04f + det - 0.04f * trace * trace;
 }
 
+int harris_finish(const float* x, const float* y, const float* z, i64 n, double radius, float threshold, int refine,
+                  const NeighborGrid& g, const std::vector<float>& nx, const std::vector<float>& ny,
+                  const std::vector<float>& nz, const std::vector<float>& resp, int32_t* idx, i64 cap, i64* n_out,
+                  i64* n_corners, float* resp_out, float* corners_out);
+
 }  // namespace
 
 extern "C" {
@@ -348,6 +354,20 @@ int orc_harris3d(const float* x, const float* y, const float* z, i64 n, double r
       resp[(size_t)i] = harris_response(nb, nx.data(), ny.data(), nz.data());
     }
   }
+  return harris_finish(x, y, z, n, radius, threshold, refine, g, nx, ny, nz, resp, idx, cap, n_out, n_corners,
+                       resp_out, corners_out);
+}
+
+}  // extern "C"
+
+namespace {
+
+// HarrisKeypoint3D/6D::detectKeypoints after the response: non-maximum suppression, refineCorners
+// (harris_3d.hpp / harris_6d.hpp: the same loop), then Keypoints::getKeypointsCloud
+int harris_finish(const float* x, const float* y, const float* z, i64 n, double radius, float threshold, int refine,
+                  const NeighborGrid& g, const std::vector<float>& nx, const std::vector<float>& ny,
+                  const std::vector<float>& nz, const std::vector<float>& resp, int32_t* idx, i64 cap, i64* n_out,
+                  i64* n_corners, float* resp_out, float* corners_out) {
   std::vector<char> is_max((size_t)n, 0);
 #pragma omp parallel
   {
@@ -448,4 +468,486 @@ int orc_harris3d(const float* x, const float* y, const float* z, i64 n, double r
   return (k > cap || nc > cap) ? 3 : 0;
 }
 
+}  // namespace
+
+// =====================================================================================
+//  Harris6D: Keypoints::compute HARRIS_6D branch, keypoints.h:164-176
+//    HarrisKeypoint6D<PointXYZRGB, PointXYZI> (PCL 1.7 keypoints/impl/harris_6d.hpp): radius
+//    0.01 (constructor default), setNonMaxSupression(true), setThreshold(1e-6), refine (default
+//    true); then Keypoints::getKeypointsCloud (keypoints.h:365-395) as for Harris3D.
+//  detectKeypoints:
+//    normals: NormalEstimation<PointXYZRGB, Normal> at r (orc_normals, viewpoint 0);
+//    IntensityGradientEstimation<PointXYZRGB, Normal, IntensityGradient> at r
+//      (features/impl/intensity_gradient.hpp) with IntensityFieldAccessor<PointXYZRGB>
+//      (common/intensity.h): I(p) = float(299 r + 587 g + 114 b) * 0.001f.  Per point, over its
+//      neighbours N in FLANN order: centroid = sum of xyz (Vector3f +=) then `/= float(|N|)`
+//      (Eigen 3.2: * (1/|N|)); mean = sum of I (float) / float(|N|);
+//      computePointIntensityGradient(centroid, mean, normal): |N| < 3 -> NaN; over N:
+//        p -= centroid; demean(p, mean) writes I(p) - mean back into the colour
+//        (r = u8(I' * 3.34448160535f), g = u8(I' * 1.70357751278f), b = u8(I' * 8.77192982456f),
+//        u8 = the low byte of cvttss2si, gcc's x86-64 code for static_cast<uint8_t>(float)),
+//        then A += (p p^T) upper, b += p * I(p) with the re-read I;
+//        x = A.colPivHouseholderQr().solve(b) (restated below); gradient = (I3 - n n^T) x;
+//    normalisation: len = |g|^2 (float); len > 200 -> g *= float(1.0 / sqrt(double(len)));
+//    responseTomasi: per finite point, over N with a finite normal_x and finite gradient[0], the
+//      21 float sums of v v^T with v = (nx, ny, nz, gx, gy, gz) (no normalisation); intensity =
+//      eigenvalues()[3] of SelfAdjointEigenSolver<Matrix<float,6,6>> (restated below); 0 for a
+//      non-finite point;
+//    non-maximum suppression, refineCorners and the snap: harris_finish (as Harris3D).
+//  Eigen 3.2 evaluation orders (SSE2 build): a fixed-size non-vectorisable sum (Matrix3f column)
+//  is tree-unrolled (Redux.h redux_novec_unroller: x0 + (x1 + x2)); a dynamic-size sum is left
+//  to right unless its operand has packet access (Matrix<float,6,6> blocks), where the first 4*j
+//  terms go through the 4-wide SSE predux ((t0 + t2) + (t1 + t3)) and the rest follow in order;
+//  SelfadjointMatrixVector.h takes its scalar path below 8 rows; `v / s` divides, `v /= s`
+//  multiplies by 1/s except TriangularView::operator/= (= m_matrix / s, divides).
+//  Restatement choices (unpinned): FLANN's sorted order (PCL: unsorted kd-trees, as Harris3D);
+//  corners in index order (PCL: omp critical); sqrt(float) as glibc's double sqrt (GCC 4.8's
+//  <cmath> has no global float overload); NaN responses are not corners.
+// =====================================================================================
+namespace {
+
+inline float h6_intensity(uint32_t rgb) {
+  const int r = (int)((rgb >> 16) & 255u), g = (int)((rgb >> 8) & 255u), b = (int)(rgb & 255u);
+  return (float)(299 * r + 587 * g + 114 * b) * 0.001f;
+}
+// static_cast<uint8_t>(float) as x86-64 gcc emits it: cvttss2si (truncation, INT_MIN when out
+// of range or NaN), low byte
+inline int h6_u8(float v) {
+  const int32_t i = (v > -2147483648.0f && v < 2147483648.0f) ? (int32_t)v : INT32_MIN;
+  return i & 255;
+}
+// IntensityFieldAccessor<PointXYZRGB>::demean followed by operator()
+inline float h6_demeaned(uint32_t rgb, float mean) {
+  const float iv = h6_intensity(rgb) - mean;
+  const int r = h6_u8(iv * 3.34448160535f), g = h6_u8(iv * 1.70357751278f), b = h6_u8(iv * 8.77192982456f);
+  return (float)(299 * r + 587 * g + 114 * b) * 0.001f;
+}
+
+// Eigen 3.2 ColPivHouseholderQR<Matrix3f>::compute(A).solve(rhs) (QR/ColPivHouseholderQR.h,
+// Householder/Householder.h).  a: column-major (a[3 c + r]).
+void colpiv_solve3(const float a[9], const float rhs[3], float x[3]) {
+  float qr[9], hc[3] = {0.f, 0.f, 0.f}, colsq[3];
+  int transp[3] = {0, 1, 2};
+  for (int e = 0; e < 9; ++e) qr[e] = a[e];
+  for (int c = 0; c < 3; ++c)  // Matrix3f column: fixed size 3, tree-unrolled
+    colsq[c] = qr[3 * c] * qr[3 * c] + (qr[3 * c + 1] * qr[3 * c + 1] + qr[3 * c + 2] * qr[3 * c + 2]);
+  const float eps = std::numeric_limits<float>::epsilon();
+  const float maxc = std::max(colsq[0], std::max(colsq[1], colsq[2]));
+  const float thr = maxc * (eps * eps) / 3.0f;
+  int nz = 3;
+  for (int k = 0; k < 3; ++k) {
+    int bi = k;
+    for (int j = k + 1; j < 3; ++j)
+      if (colsq[j] > colsq[bi]) bi = j;  // maxCoeff(&index): first maximum
+    float bv = qr[3 * bi + k] * qr[3 * bi + k];  // tail(rows - k) of a column: left to right
+    for (int r = k + 1; r < 3; ++r) bv = bv + qr[3 * bi + r] * qr[3 * bi + r];
+    colsq[bi] = bv;
+    if (bv < thr * (float)(3 - k)) {
+      nz = k;
+      for (int j = k; j < 3; ++j) hc[j] = 0.f;
+      for (int c = k; c < 3; ++c)
+        for (int r = c + 1; r < 3; ++r) qr[3 * c + r] = 0.f;
+      break;
+    }
+    transp[k] = bi;
+    if (k != bi) {
+      for (int r = 0; r < 3; ++r) std::swap(qr[3 * k + r], qr[3 * bi + r]);
+      std::swap(colsq[k], colsq[bi]);
+    }
+    // makeHouseholderInPlace on qr(k..2, k)
+    const float c0 = qr[3 * k + k];
+    float tailsq = 0.f;
+    if (k < 2) {
+      tailsq = qr[3 * k + k + 1] * qr[3 * k + k + 1];
+      for (int r = k + 2; r < 3; ++r) tailsq = tailsq + qr[3 * k + r] * qr[3 * k + r];
+    }
+    float tau, beta;
+    if (tailsq == 0.f) {
+      tau = 0.f;
+      beta = c0;
+      for (int r = k + 1; r < 3; ++r) qr[3 * k + r] = 0.f;
+    } else {
+      beta = std::sqrt(c0 * c0 + tailsq);
+      if (c0 >= 0.f) beta = -beta;
+      const float den = c0 - beta;
+      for (int r = k + 1; r < 3; ++r) qr[3 * k + r] = qr[3 * k + r] / den;
+      tau = (beta - c0) / beta;
+    }
+    qr[3 * k + k] = beta;
+    hc[k] = tau;
+    // applyHouseholderOnTheLeft(essential = qr(k+1..2, k), tau) on qr(k..2, k+1..2)
+    for (int c = k + 1; c < 3; ++c) {
+      if (k == 2) break;
+      float tmp = qr[3 * k + k + 1] * qr[3 * c + k + 1];
+      for (int r = k + 2; r < 3; ++r) tmp = tmp + qr[3 * k + r] * qr[3 * c + r];
+      tmp = tmp + qr[3 * c + k];
+      qr[3 * c + k] = qr[3 * c + k] - tau * tmp;
+      for (int r = k + 1; r < 3; ++r) qr[3 * c + r] = qr[3 * c + r] - (tau * qr[3 * k + r]) * tmp;
+    }
+    for (int c = k + 1; c < 3; ++c) colsq[c] = colsq[c] - qr[3 * c + k] * qr[3 * c + k];
+  }
+  if (nz == 0) {
+    x[0] = x[1] = x[2] = 0.f;
+    return;
+  }
+  // c = Q^T rhs: H_0 first, rows k..2 (a one-row block is scaled by 1 - tau)
+  float cv[3] = {rhs[0], rhs[1], rhs[2]};
+  for (int k = 0; k < nz; ++k) {
+    if (k == 2) {
+      cv[2] = cv[2] * (1.0f - hc[2]);
+      continue;
+    }
+    float tmp = qr[3 * k + k + 1] * cv[k + 1];
+    for (int r = k + 2; r < 3; ++r) tmp = tmp + qr[3 * k + r] * cv[r];
+    tmp = tmp + cv[k];
+    cv[k] = cv[k] - hc[k] * tmp;
+    for (int r = k + 1; r < 3; ++r) cv[r] = cv[r] - (hc[k] * qr[3 * k + r]) * tmp;
+  }
+  // R(0..nz) upper-triangular solve in place (triangular_solve_vector, column-major Upper)
+  for (int i = nz - 1; i >= 0; --i) {
+    if (cv[i] != 0.f) {
+      cv[i] /= qr[3 * i + i];
+      for (int j = 0; j < i; ++j) cv[j] = cv[j] - cv[i] * qr[3 * i + j];
+    }
+  }
+  int perm[3] = {0, 1, 2};
+  for (int k = 0; k < nz; ++k) std::swap(perm[k], perm[transp[k]]);
+  x[0] = x[1] = x[2] = 0.f;
+  for (int i = 0; i < nz; ++i) x[perm[i]] = cv[i];
+}
+
+// sum of the squares of v[0..m) as Eigen 3.2 reduces a dynamic-size block of a packet-capable
+// matrix: the first 4 j terms through the SSE predux, the rest in order (m < 4: in order)
+inline float h6_sqsum(const float* v, int m) {
+  if (m < 4) {
+    float s = v[0] * v[0];
+    for (int i = 1; i < m; ++i) s = s + v[i] * v[i];
+    return s;
+  }
+  float p0 = v[0] * v[0], p1 = v[1] * v[1], p2 = v[2] * v[2], p3 = v[3] * v[3];
+  int i = 4;
+  if (m >= 8) {
+    float q0 = v[4] * v[4], q1 = v[5] * v[5], q2 = v[6] * v[6], q3 = v[7] * v[7];
+    p0 = p0 + q0; p1 = p1 + q1; p2 = p2 + q2; p3 = p3 + q3;
+    i = 8;
+  }
+  float s = (p0 + p2) + (p1 + p3);
+  for (; i < m; ++i) s = s + v[i] * v[i];
+  return s;
+}
+
+inline float h6_hypot(float x, float y) {  // internal::hypot_impl<float>
+  const float ax = std::fabs(x), ay = std::fabs(y);
+  const float p = std::max(ax, ay);
+  if (p == 0.f) return 0.f;
+  const float q = std::min(ax, ay);
+  const float qp = q / p;
+  return p * std::sqrt(1.0f + qp * qp);
+}
+
+inline void h6_givens(float p, float q, float& c, float& s) {  // JacobiRotation::makeGivens (real)
+  if (q == 0.f) {
+    c = p < 0.f ? -1.f : 1.f;
+    s = 0.f;
+  } else if (p == 0.f) {
+    c = 0.f;
+    s = q < 0.f ? 1.f : -1.f;
+  } else if (std::fabs(p) > std::fabs(q)) {
+    const float t = q / p;
+    float u = std::sqrt(1.0f + t * t);
+    if (p < 0.f) u = -u;
+    c = 1.0f / u;
+    s = -t * c;
+  } else {
+    const float t = p / q;
+    float u = std::sqrt(1.0f + t * t);
+    if (q < 0.f) u = -u;
+    s = -1.0f / u;
+    c = -t * s;
+  }
+}
+
+// Eigen 3.2 SelfAdjointEigenSolver<Matrix<float,6,6>>::compute(A).eigenvalues() (A: lower
+// triangle read, column-major m[6 c + r]); returns false when the QR iteration does not converge
+// (then the values are unsorted, as Eigen leaves them)
+bool eigen_selfadjoint6f(const float A[36], float ev[6]) {
+  const int n = 6;
+  float m[36];
+  for (int c = 0; c < n; ++c)
+    for (int r = 0; r < n; ++r) m[6 * c + r] = r >= c ? A[6 * c + r] : 0.f;
+  float scale = 0.f;
+  for (int e = 0; e < 36; ++e) scale = std::max(scale, std::fabs(m[e]));  // cwiseAbs().maxCoeff()
+  if (scale == 0.f) scale = 1.f;
+  for (int c = 0; c < n; ++c)
+    for (int r = c; r < n; ++r) m[6 * c + r] = m[6 * c + r] / scale;  // TriangularView /= : divides
+  // Tridiagonalization.h tridiagonalization_inplace (generic selector), lower triangle
+  float hco[5];
+  for (int i = 0; i < n - 1; ++i) {
+    const int rs = n - i - 1;  // remaining size
+    float* v = m + 6 * i + i + 1;  // column i, rows i+1..n-1
+    // makeHouseholderInPlace(h, beta): c0 = v[0], tail = v[1..rs)
+    const float c0 = v[0];
+    const float tailsq = rs == 1 ? 0.f : h6_sqsum(v + 1, rs - 1);
+    float h, beta;
+    if (tailsq == 0.f) {
+      h = 0.f;
+      beta = c0;
+      for (int r = 1; r < rs; ++r) v[r] = 0.f;
+    } else {
+      beta = std::sqrt(c0 * c0 + tailsq);
+      if (c0 >= 0.f) beta = -beta;
+      const float den = c0 - beta;
+      for (int r = 1; r < rs; ++r) v[r] = v[r] / den;
+      h = (beta - c0) / beta;
+    }
+    v[0] = 1.f;
+    // hco(i..) = h * (B v), B = bottom-right rs x rs lower view (selfadjoint_matrix_vector_product,
+    // scalar path, alpha = h extracted from the rhs expression, rhs = v)
+    float res[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
+    const float* B = m + 6 * (i + 1) + (i + 1);  // B(r, c) = B[6 c + r]
+    for (int j = 0; j < rs; ++j) {
+      const float t1 = h * v[j];
+      float t2 = 0.f;
+      res[j] += B[6 * j + j] * t1;
+      for (int r = j + 1; r < rs; ++r) {
+        res[r] += B[6 * j + r] * t1;
+        t2 += B[6 * j + r] * v[r];
+      }
+      res[j] += h * t2;
+    }
+    // += (h * -0.5 * (hco . v)) v   (dot: CwiseBinaryOp of a 5-vector block, no packets: in order)
+    float dot = res[0] * v[0];
+    for (int r = 1; r < rs; ++r) dot = dot + res[r] * v[r];
+    const float sc = (h * -0.5f) * dot;
+    for (int r = 0; r < rs; ++r) res[r] = res[r] + sc * v[r];
+    // rankUpdate(v, res, -1): column j of the lower view: B(j.., j) += (-v_j) res(j..) + (-res_j) v(j..)
+    float* Bw = m + 6 * (i + 1) + (i + 1);
+    for (int j = 0; j < rs; ++j) {
+      const float a1 = -1.0f * v[j], a2 = -1.0f * res[j];
+      for (int r = j; r < rs; ++r) Bw[6 * j + r] = Bw[6 * j + r] + (a1 * res[r] + a2 * v[r]);
+    }
+    v[0] = beta;
+    hco[i] = h;
+  }
+  float d[6], e[5];
+  for (int k = 0; k < n; ++k) d[k] = m[6 * k + k];
+  for (int k = 0; k < n - 1; ++k) e[k] = m[6 * k + k + 1];
+  (void)hco;
+  int end = n - 1, start = 0, iter = 0;
+  const int maxit = 30 * n;
+  while (end > 0) {
+    for (int i = start; i < end; ++i)
+      if (std::fabs(e[i]) <= (std::fabs(d[i]) + std::fabs(d[i + 1])) * 1e-5f) e[i] = 0.f;  // isMuchSmallerThan
+    while (end > 0 && e[end - 1] == 0.f) end--;
+    if (end <= 0) break;
+    if (++iter > maxit) break;
+    start = end - 1;
+    while (start > 0 && e[start - 1] != 0.f) start--;
+    // tridiagonal_qr_step
+    const float td = (d[end - 1] - d[end]) * 0.5f;
+    const float ee = e[end - 1];
+    float mu = d[end];
+    if (td == 0.f) {
+      mu -= std::fabs(ee);
+    } else {
+      const float e2 = ee * ee;
+      const float hh = h6_hypot(td, ee);
+      if (e2 == 0.f) mu -= (ee / (td + (td > 0.f ? 1.f : -1.f))) * (ee / hh);
+      else mu -= e2 / (td + (td > 0.f ? hh : -hh));
+    }
+    float x = d[start] - mu, z = e[start];
+    for (int k = start; k < end; ++k) {
+      float c, s;
+      h6_givens(x, z, c, s);
+      const float sdk = s * d[k] + c * e[k];
+      const float dkp1 = s * e[k] + c * d[k + 1];
+      d[k] = c * (c * d[k] - s * e[k]) - s * (c * e[k] - s * d[k + 1]);
+      d[k + 1] = s * sdk + c * dkp1;
+      e[k] = c * sdk - s * dkp1;
+      if (k > start) e[k - 1] = c * e[k - 1] - s * z;
+      x = e[k];
+      if (k < end - 1) {
+        z = -s * e[k + 1];
+        e[k + 1] = c * e[k + 1];
+      }
+    }
+  }
+  const bool ok = iter <= maxit;
+  if (ok)
+    for (int i = 0; i < n - 1; ++i) {
+      int k = i;
+      for (int j = i + 1; j < n; ++j)
+        if (d[j] < d[k]) k = j;
+      if (k != i) std::swap(d[i], d[k]);
+    }
+  for (int k = 0; k < n; ++k) ev[k] = d[k] * scale;
+  return ok;
+}
+
+// IntensityGradientEstimation::computeFeature + computePointIntensityGradient for point i over
+// its FLANN-ordered neighbours nb
+void h6_gradient(const float* x, const float* y, const float* z, const uint32_t* rgb, const std::vector<int>& nb,
+                 float nxi, float nyi, float nzi, float g[3]) {
+  const size_t k = nb.size();
+  float cx = 0.f, cy = 0.f, cz = 0.f, mi = 0.f;
+  for (size_t m = 0; m < k; ++m) {
+    const int j = nb[m];
+    cx += x[j];
+    cy += y[j];
+    cz += z[j];
+    mi += h6_intensity(rgb[j]);
+  }
+  const float rk = 1.0f / (float)k;  // centroid /= float(k): Eigen 3.2 reciprocal
+  cx *= rk;
+  cy *= rk;
+  cz *= rk;
+  mi /= (float)k;
+  if (k < 3) {
+    g[0] = g[1] = g[2] = orc::kNaN;
+    return;
+  }
+  float A00 = 0.f, A01 = 0.f, A02 = 0.f, A11 = 0.f, A12 = 0.f, A22 = 0.f, b0 = 0.f, b1 = 0.f, b2 = 0.f;
+  for (size_t m = 0; m < k; ++m) {
+    const int j = nb[m];
+    const float px = x[j] - cx, py = y[j] - cy, pz = z[j] - cz;
+    const float iv = h6_demeaned(rgb[j], mi);
+    A00 += px * px;
+    A01 += px * py;
+    A02 += px * pz;
+    A11 += py * py;
+    A12 += py * pz;
+    A22 += pz * pz;
+    b0 += px * iv;
+    b1 += py * iv;
+    b2 += pz * iv;
+  }
+  const float A[9] = {A00, A01, A02, A01, A11, A12, A02, A12, A22};
+  const float bv[3] = {b0, b1, b2};
+  float xs[3];
+  colpiv_solve3(A, bv, xs);
+  // (Identity - n n^T) * x: Matrix3f * Vector3f, ((m0 x0 + m1 x1) + m2 x2)
+  const float nv[3] = {nxi, nyi, nzi};
+  float P[9];
+  for (int c = 0; c < 3; ++c)
+    for (int r = 0; r < 3; ++r) P[3 * c + r] = (r == c ? 1.0f : 0.0f) - nv[r] * nv[c];
+  for (int r = 0; r < 3; ++r) g[r] = (P[r] * xs[0] + P[3 + r] * xs[1]) + P[6 + r] * xs[2];
+}
+
+void h6_normalise(float g[3]) {  // HarrisKeypoint6D::detectKeypoints, "remove this magic number"
+  float len = (g[0] * g[0] + g[1] * g[1]) + g[2] * g[2];
+  if (len > 200.0) {
+    len = (float)(1.0 / std::sqrt((double)len));
+    g[0] = g[0] * len;
+    g[1] = g[1] * len;
+    g[2] = g[2] * len;
+  }
+}
+
+float h6_response(const std::vector<int>& nb, const float* nx, const float* ny, const float* nz, const float* gx,
+                  const float* gy, const float* gz) {
+  float cv[21];
+  for (int e = 0; e < 21; ++e) cv[e] = 0.f;
+  for (size_t m = 0; m < nb.size(); ++m) {
+    const int j = nb[m];
+    if (!std::isfinite(nx[j]) || !std::isfinite(gx[j])) continue;
+    const float v[6] = {nx[j], ny[j], nz[j], gx[j], gy[j], gz[j]};
+    int e = 0;
+    for (int a = 0; a < 6; ++a)
+      for (int b = a; b < 6; ++b) cv[e++] += v[a] * v[b];
+  }
+  float A[36];
+  int e = 0;
+  for (int a = 0; a < 6; ++a)
+    for (int b = a; b < 6; ++b, ++e) {
+      A[6 * a + b] = cv[e];  // (row b, column a): lower triangle
+      A[6 * b + a] = cv[e];
+    }
+  float ev[6];
+  eigen_selfadjoint6f(A, ev);
+  return ev[3];
+}
+
+}  // namespace
+
+extern "C" {
+
+// Eigen restatements exposed for the tests
+int orc_eigen_selfadjoint6f(const float* a, i64 n, float* ev) {
+  int bad = 0;
+  for (i64 i = 0; i < n; ++i) bad += eigen_selfadjoint6f(a + 36 * i, ev + 6 * i) ? 0 : 1;
+  return bad;
+}
+int orc_colpiv_solve3f(const float* a, const float* b, i64 n, float* x) {
+  for (i64 i = 0; i < n; ++i) colpiv_solve3(a + 9 * i, b + 3 * i, x + 3 * i);
+  return 0;
+}
+
+// rgb: packed 0x00RRGGBB (PointXYZRGB's float rgb field as bits).  grad_out (nullable, 3 n
+// floats): the normalised intensity gradients; the rest as orc_harris3d.
+int orc_harris6d(const float* x, const float* y, const float* z, const uint32_t* rgb, i64 n, double radius,
+                 float threshold, int refine, int32_t* idx, i64 cap, i64* n_out, i64* n_corners, float* resp_out,
+                 float* corners_out, float* grad_out, int threads) {
+  *n_out = 0;
+  *n_corners = 0;
+  if (n <= 0) return 0;
+  std::vector<float> nx((size_t)n), ny((size_t)n), nz((size_t)n), cv((size_t)n), resp((size_t)n, 0.0f);
+  std::vector<float> gx((size_t)n, orc::kNaN), gy((size_t)n, orc::kNaN), gz((size_t)n, orc::kNaN);
+  orc_normals(x, y, z, n, radius, 0.f, 0.f, 0.f, nx.data(), ny.data(), nz.data(), cv.data(), threads);
+  NeighborGrid g;
+  g.build(x, y, z, n, radius);
+#ifdef _OPENMP
+  if (threads > 0) omp_set_num_threads(threads);
+#endif
+#pragma omp parallel
+  {
+    std::vector<int> nb;
+    std::vector<float> dd;
+#pragma omp for schedule(dynamic, 256)
+    for (i64 i = 0; i < n; ++i) {
+      if (!finite3(x, y, z, i)) continue;  // the dense branch never sees these; not a neighbour either
+      g.radius(x[i], y[i], z[i], radius, nb, dd);
+      float gr[3];
+      h6_gradient(x, y, z, rgb, nb, nx[(size_t)i], ny[(size_t)i], nz[(size_t)i], gr);
+      h6_normalise(gr);
+      gx[(size_t)i] = gr[0];
+      gy[(size_t)i] = gr[1];
+      gz[(size_t)i] = gr[2];
+    }
+  }
+#pragma omp parallel
+  {
+    std::vector<int> nb;
+    std::vector<float> dd;
+#pragma omp for schedule(dynamic, 256)
+    for (i64 i = 0; i < n; ++i) {
+      if (!finite3(x, y, z, i)) continue;
+      g.radius(x[i], y[i], z[i], radius, nb, dd);
+      resp[(size_t)i] = h6_response(nb, nx.data(), ny.data(), nz.data(), gx.data(), gy.data(), gz.data());
+    }
+  }
+  if (grad_out)
+    for (i64 i = 0; i < n; ++i) {
+      grad_out[3 * i] = gx[(size_t)i];
+      grad_out[3 * i + 1] = gy[(size_t)i];
+      grad_out[3 * i + 2] = gz[(size_t)i];
+    }
+  return harris_finish(x, y, z, n, radius, threshold, refine, g, nx, ny, nz, resp, idx, cap, n_out, n_corners,
+                       resp_out, corners_out);
+}
+
+}  // extern "C"
+
+extern "C" {
+// the u8 model above vs the host compiler's own code for static_cast<uint8_t>(float) (the cast
+// is undefined for negative values in C++; x86-64 gcc emits cvttss2si and keeps the low byte):
+// test-only pin of the model
+int orc_u8_cast_model(const float* v, i64 n, int32_t* out) {
+  for (i64 i = 0; i < n; ++i) out[i] = h6_u8(v[i]);
+  return 0;
+}
+__attribute__((noinline)) static uint8_t native_u8(volatile float v) { return static_cast<uint8_t>(v); }
+int orc_u8_cast_native(const float* v, i64 n, int32_t* out) {
+  for (i64 i = 0; i < n; ++i) out[i] = native_u8(v[i]);
+  return 0;
+}
 }  // extern "C"

@@ -357,6 +357,40 @@ class Context:
                                                          ctypes.byref(nc)))
         return k.value, nc.value
 
+    def harris6d_keypoints(self, x, y, z, rgb, radius=0.01, threshold=1e-6, refine=True, non_max=True,
+                           details=False):
+        """HarrisKeypoint6D + getKeypointsCloud (keypoints.h:164-176, 365-395), host arrays (rgb:
+        packed 0x00RRGGBB per point): the snapped cloud indices in corner order (details: and the
+        per-point response, the refined corners and the normalised intensity gradients (n, 3))."""
+        x, y, z = map(_f32, (x, y, z))
+        rgb = np.ascontiguousarray(rgb, dtype=np.uint32)
+        n = len(x)
+        if len(rgb) != n:
+            raise ValueError("harris6d: one rgb word per point")
+        cap = max(n, 1)
+        idx = np.empty(cap, np.int32)
+        resp = np.empty(cap, np.float32) if details else None
+        corners = np.empty((cap, 3), np.float32) if details else None
+        grad = np.empty((cap, 3), np.float32) if details else None
+        k, nc = ctypes.c_int64(), ctypes.c_int64()
+        self._check(self._lib.pfx_harris6d_keypoints(self.h, _ptr(x), _ptr(y), _ptr(z), _ptr(rgb), n, radius,
+                                                     threshold, 1 if non_max else 0, 1 if refine else 0, _ptr(idx),
+                                                     cap, ctypes.byref(k), _ptr(resp), _ptr(corners), ctypes.byref(nc),
+                                                     _ptr(grad)))
+        out = idx[: k.value].copy()
+        return (out, resp[:n].copy(), corners[: nc.value].copy(), grad[:n].copy()) if details else out
+
+    def harris6d_keypoints_dev(self, x, y, z, rgb, idx, radius=0.01, threshold=1e-6, refine=True, response=None,
+                               corners=None, grad=None):
+        """Device version (rgb: int32/uint32 tensor of packed colours): snapped indices into `idx`
+        (int32 tensor); returns (count, corners)."""
+        k, nc = ctypes.c_int64(), ctypes.c_int64()
+        self._check(self._lib.pfx_harris6d_keypoints_dev(self.h, _ptr(x), _ptr(y), _ptr(z), _ptr(rgb), x.numel(),
+                                                         radius, threshold, 1, 1 if refine else 0, _ptr(idx),
+                                                         idx.numel(), ctypes.byref(k), _ptr(response), _ptr(corners),
+                                                         ctypes.byref(nc), _ptr(grad)))
+        return k.value, nc.value
+
     # ---- RANSAC correspondence rejection (SURVEY 8(f) F2) -----------------------------------
     def ransac_rejector(self, src, tgt, query, match, threshold=0.015, max_iterations=1000):
         """Features::filterCorrespondences (features.h:282-297): (kept correspondence positions in

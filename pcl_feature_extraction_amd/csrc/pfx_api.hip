@@ -700,6 +700,61 @@ extern "C" pfx_status pfx_harris3d_keypoints(pfx_ctx* ctx, const float* x, const
   PFX_API_END(ctx)
 }
 
+extern "C" pfx_status pfx_harris6d_keypoints_dev(pfx_ctx* ctx, const float* d_x, const float* d_y, const float* d_z,
+                                                 const uint32_t* d_rgb, int64_t n, double radius, float threshold,
+                                                 int32_t non_max, int32_t refine, int32_t* d_idx, int64_t cap,
+                                                 int64_t* n_out, float* d_response, float* d_corners,
+                                                 int64_t* n_corners, float* d_grad) {
+  PFX_API_BEGIN
+  check_ctx(ctx);
+  check_points(d_x, d_y, d_z, n, "harris6d");
+  if (n && !d_rgb) throw Error(PFX_ERR_INVALID, "harris6d: null rgb");
+  check_harris(radius, non_max);
+  if (!n_out || cap < 0 || (cap && !d_idx)) throw Error(PFX_ERR_INVALID, "harris6d: invalid output arguments");
+  int64_t nc = 0;
+  const int64_t k = pfx::harris6d_dev(ctx, d_x, d_y, d_z, d_rgb, n, radius, threshold, refine, d_idx, cap, d_response,
+                                      d_corners, &nc, d_grad);
+  *n_out = k;
+  if (n_corners) *n_corners = nc;
+  if (k > cap || (d_corners && nc > cap))
+    throw Error(PFX_ERR_CAPACITY, "harris6d: " + std::to_string(std::max(k, nc)) + " keypoints/corners > cap");
+  PFX_API_END(ctx)
+}
+
+extern "C" pfx_status pfx_harris6d_keypoints(pfx_ctx* ctx, const float* x, const float* y, const float* z,
+                                             const uint32_t* rgb, int64_t n, double radius, float threshold,
+                                             int32_t non_max, int32_t refine, int32_t* idx, int64_t cap,
+                                             int64_t* n_out, float* response, float* corners, int64_t* n_corners,
+                                             float* grad) {
+  PFX_API_BEGIN
+  check_ctx(ctx);
+  check_points(x, y, z, n, "harris6d");
+  if (n && !rgb) throw Error(PFX_ERR_INVALID, "harris6d: null rgb");
+  check_harris(radius, non_max);
+  if (!n_out || cap < 0 || (cap && !idx)) throw Error(PFX_ERR_INVALID, "harris6d: invalid output arguments");
+  float* dx = stage_in(ctx, "in_x", x, n);
+  float* dy = stage_in(ctx, "in_y", y, n);
+  float* dz = stage_in(ctx, "in_z", z, n);
+  uint32_t* dc_rgb = ctx->buf("in_rgb").as<uint32_t>(n + 1);
+  if (n) PFX_HIP(hipMemcpyAsync(dc_rgb, rgb, sizeof(uint32_t) * n, hipMemcpyHostToDevice, ctx->stream));
+  int32_t* di = ctx->buf("out_h3_idx").as<int32_t>(n + 1);
+  float* dr = response ? ctx->buf("out_h3_resp").as<float>(n + 1) : nullptr;
+  float* dc = corners ? ctx->buf("out_h3_corners").as<float>(3 * (n + 1)) : nullptr;
+  float* dg = grad ? ctx->buf("out_h6_grad").as<float>(3 * (n + 1)) : nullptr;
+  int64_t nc = 0;
+  const int64_t k = pfx::harris6d_dev(ctx, dx, dy, dz, dc_rgb, n, radius, threshold, refine, di, n, dr, dc, &nc, dg);
+  *n_out = k;
+  if (n_corners) *n_corners = nc;
+  if (k > cap || (corners && nc > cap))
+    throw Error(PFX_ERR_CAPACITY, "harris6d: " + std::to_string(std::max(k, nc)) + " keypoints/corners > cap");
+  if (k) PFX_HIP(hipMemcpyAsync(idx, di, sizeof(int32_t) * k, hipMemcpyDeviceToHost, ctx->stream));
+  if (response && n) PFX_HIP(hipMemcpyAsync(response, dr, sizeof(float) * n, hipMemcpyDeviceToHost, ctx->stream));
+  if (corners && nc) PFX_HIP(hipMemcpyAsync(corners, dc, sizeof(float) * 3 * nc, hipMemcpyDeviceToHost, ctx->stream));
+  if (grad && n) PFX_HIP(hipMemcpyAsync(grad, dg, sizeof(float) * 3 * n, hipMemcpyDeviceToHost, ctx->stream));
+  PFX_HIP(hipStreamSynchronize(ctx->stream));
+  PFX_API_END(ctx)
+}
+
 extern "C" pfx_status pfx_ransac_rejector(pfx_ctx* ctx, const float* sx, const float* sy, const float* sz, int64_t ns,
                                           const float* tx, const float* ty, const float* tz, int64_t nt,
                                           const int32_t* query, const int32_t* match, int64_t n, double threshold,

@@ -21,6 +21,7 @@
 #include "pfx_internal.h"
 #include "pfx_nblist.h"
 #include "pfx_neighbors.h"
+#include "pfx_eigen6.h"
 #include "pfx_wave_sort.h"
 
 namespace pfx {
@@ -123,6 +124,157 @@ __global__ void __launch_bounds__(256) k_harris_nms(GridView g, NbLists L, const
   if (is_max) flag[i] = 1;
 }
 
+// ---- Harris6D (keypoints.h:164-176): IntensityGradientEstimation + responseTomasi ----------
+// IntensityFieldAccessor<PointXYZRGB>: I = float(299 r + 587 g + 114 b) * 0.001f
+__device__ __forceinline__ float rgb_intensity(uint32_t c) {
+  const int r = (int)((c >> 16) & 255u), g = (int)((c >> 8) & 255u), b = (int)(c & 255u);
+  return (float)(299 * r + 587 * g + 114 * b) * 0.001f;
+}
+// static_cast<uint8_t>(float) as x86-64 gcc compiles it (cvttss2si, low byte): the demeaned
+// intensities are far inside int32, where v_cvt_i32_f32 truncates the same way
+__device__ __forceinline__ int u8_trunc(float v) { return ((int32_t)v) & 255; }
+// IntensityFieldAccessor::demean (write I - mean back into r, g, b) followed by operator()
+__device__ __forceinline__ float rgb_demeaned(uint32_t c, float mean) {
+  const float iv = rgb_intensity(c) - mean;
+  const int r = u8_trunc(iv * 3.34448160535f), g = u8_trunc(iv * 1.70357751278f), b = u8_trunc(iv * 8.77192982456f);
+  return (float)(299 * r + 587 * g + 114 * b) * 0.001f;
+}
+
+// IntensityGradientEstimation::computeFeature + computePointIntensityGradient, then
+// HarrisKeypoint6D's normalisation (|g|^2 > 200 -> unit length): lane per list, two passes over
+// the FLANN-ordered r-neighbours (centroid and mean intensity, then the demeaned 3x3 system)
+__global__ void __launch_bounds__(256) k_intensity_gradient(GridView g, NbLists L, const uint32_t* __restrict__ rgb,
+                                                            const float* __restrict__ nx, const float* __restrict__ ny,
+                                                            const float* __restrict__ nz, float* __restrict__ gx,
+                                                            float* __restrict__ gy, float* __restrict__ gz,
+                                                            float* __restrict__ grad_out) {
+  __shared__ int32_t s_rt[9 * 256];
+  const int tid = threadIdx.x;
+  const int64_t j = (int64_t)blockIdx.x * 256 + tid;
+  if (j >= L.nq) return;  // no barriers below
+  const int32_t p = L.qpos[j];
+  const int k = L.cnt[j];
+  const uint32_t key = L.skeys[p];
+#pragma unroll
+  for (int r = 0; r < 9; ++r) {
+    int32_t s, len;
+    block_run(g, key, r, s, len);
+    s_rt[r * 256 + tid] = s;
+  }
+  const uint32_t* lst = L.list + L.off[j];
+  const int lg = L.lg[j];
+  auto nbr = [&](int m) { const uint32_t e = lst[(int64_t)m << lg];
+                          return g.perm[s_rt[entry_run(e) * 256 + tid] + (int32_t)entry_off(e)]; };
+  float cx = 0.f, cy = 0.f, cz = 0.f, mi = 0.f;
+  for (int m = 0; m < k; ++m) {
+    const int32_t q = nbr(m);
+    cx += g.ux[q];
+    cy += g.uy[q];
+    cz += g.uz[q];
+    mi += rgb_intensity(rgb[q]);
+  }
+  const float rk = 1.0f / (float)k;  // centroid /= float(k): Eigen 3.2 reciprocal
+  cx *= rk;
+  cy *= rk;
+  cz *= rk;
+  mi /= (float)k;
+  const int32_t i = g.perm[p];
+  float o[3];
+  if (k < 3) {
+    o[0] = o[1] = o[2] = __int_as_float(0x7fc00000);
+  } else {
+    float A00 = 0.f, A01 = 0.f, A02 = 0.f, A11 = 0.f, A12 = 0.f, A22 = 0.f, b0 = 0.f, b1 = 0.f, b2 = 0.f;
+    for (int m = 0; m < k; ++m) {
+      const int32_t q = nbr(m);
+      const float px = g.ux[q] - cx, py = g.uy[q] - cy, pz = g.uz[q] - cz;
+      const float iv = rgb_demeaned(rgb[q], mi);
+      A00 += px * px;
+      A01 += px * py;
+      A02 += px * pz;
+      A11 += py * py;
+      A12 += py * pz;
+      A22 += pz * pz;
+      b0 += px * iv;
+      b1 += py * iv;
+      b2 += pz * iv;
+    }
+    const float A[9] = {A00, A01, A02, A01, A11, A12, A02, A12, A22};
+    const float bv[3] = {b0, b1, b2};
+    float xs[3];
+    colpiv_solve3f(A, bv, xs);
+    const float nv[3] = {nx[i], ny[i], nz[i]};
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+      // Identity - n n^T.  The empty asm pins each coefficient in a register: otherwise the
+      // compiler folds (0 - p) * x into x * (-p), which is -0 where the reference's x86 code
+      // (IEEE: 0 - (+0) = +0) gets +0 -- the sign of zero gradient components
+      float m0 = (r == 0 ? 1.0f : 0.0f) - nv[r] * nv[0];
+      float m1 = (r == 1 ? 1.0f : 0.0f) - nv[r] * nv[1];
+      float m2 = (r == 2 ? 1.0f : 0.0f) - nv[r] * nv[2];
+      asm volatile("" : "+v"(m0), "+v"(m1), "+v"(m2));
+      o[r] = (m0 * xs[0] + m1 * xs[1]) + m2 * xs[2];
+    }
+    float len = (o[0] * o[0] + o[1] * o[1]) + o[2] * o[2];
+    if (len > 200.0f) {
+      len = (float)(1.0 / sqrt((double)len));
+      o[0] = o[0] * len;
+      o[1] = o[1] * len;
+      o[2] = o[2] * len;
+    }
+  }
+  gx[i] = o[0];
+  gy[i] = o[1];
+  gz[i] = o[2];
+  if (grad_out) {
+    grad_out[3 * (int64_t)i] = o[0];
+    grad_out[3 * (int64_t)i + 1] = o[1];
+    grad_out[3 * (int64_t)i + 2] = o[2];
+  }
+}
+
+// HarrisKeypoint6D::responseTomasi: lane per list, the 21 float sums of v v^T over the
+// neighbours with a finite normal_x and gradient[0] (v = normal, gradient), then the fourth
+// eigenvalue of the 6x6 (pfx_eigen6.h)
+__global__ void __launch_bounds__(256) k_harris6d_response(GridView g, NbLists L, const float* __restrict__ nx,
+                                                           const float* __restrict__ ny, const float* __restrict__ nz,
+                                                           const float* __restrict__ gx, const float* __restrict__ gy,
+                                                           const float* __restrict__ gz, float* __restrict__ resp) {
+  __shared__ int32_t s_rt[9 * 256];
+  const int tid = threadIdx.x;
+  const int64_t j = (int64_t)blockIdx.x * 256 + tid;
+  if (j >= L.nq) return;
+  const int32_t p = L.qpos[j];
+  const int k = L.cnt[j];
+  const uint32_t key = L.skeys[p];
+#pragma unroll
+  for (int r = 0; r < 9; ++r) {
+    int32_t s, len;
+    block_run(g, key, r, s, len);
+    s_rt[r * 256 + tid] = s;
+  }
+  const uint32_t* lst = L.list + L.off[j];
+  const int lg = L.lg[j];
+  float cv[21];
+#pragma unroll
+  for (int e = 0; e < 21; ++e) cv[e] = 0.f;
+  for (int m = 0; m < k; ++m) {
+    const uint32_t en = lst[(int64_t)m << lg];
+    const int32_t q = g.perm[s_rt[entry_run(en) * 256 + tid] + (int32_t)entry_off(en)];
+    const float a = nx[q], ga = gx[q];
+    if (!isfinite(a) || !isfinite(ga)) continue;
+    const float v[6] = {a, ny[q], nz[q], ga, gy[q], gz[q]};
+    int e = 0;
+#pragma unroll
+    for (int u = 0; u < 6; ++u)
+#pragma unroll
+      for (int w = u; w < 6; ++w) {
+        cv[e] = cv[e] + v[u] * v[w];
+        ++e;
+      }
+  }
+  resp[g.perm[p]] = eigen6f_value3(cv);
+}
+
 // matrices column-major as Eigen's Matrix3f::coeff(k)
 __device__ __forceinline__ void mat_vec3(const float a[9], const float v[3], float o[3]) {
 #pragma unroll
@@ -142,8 +294,9 @@ __device__ __forceinline__ float invert3x3_sym(const float c[9], float inv[9]) {
     inv[4] = c[0] * c[8] - c[2] * c[2];
     inv[5] = inv[7] = c[1] * c[2] - c[0] * c[5];
     inv[8] = c[0] * c[4] - c[1] * c[1];
+    const float rdet = 1.0f / det;  // `inverse /= det`: Eigen 3.2 multiplies by the reciprocal
 #pragma unroll
-    for (int k = 0; k < 9; ++k) inv[k] /= det;
+    for (int k = 0; k < 9; ++k) inv[k] *= rdet;
   }
   return det;
 }
@@ -289,35 +442,33 @@ struct NonNeg {
 
 }  // namespace
 
-int64_t harris3d_dev(pfx_ctx* ctx, const float* x, const float* y, const float* z, int64_t n, double radius,
-                     float threshold, int refine, int32_t* out, int64_t cap, float* resp_out, float* corners_out,
-                     int64_t* n_corners) {
-  PFX_CHECK(n >= 0, "harris3d: negative point count");
-  PFX_CHECK(radius > 0.0, "harris3d: radius must be > 0");
-  if (n_corners) *n_corners = 0;
-  if (n == 0) return 0;
+namespace {
+
+__global__ void k_fill_f32(float* __restrict__ p, int64_t n, float v) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < n) p[i] = v;
+}
+void fill_f32(pfx_ctx* ctx, float* p, int64_t n, float v) {
+  if (n <= 0) return;
+  k_fill_f32<<<(unsigned)ceil_div(n, 256), 256, 0, ctx->stream>>>(p, n, v);
+  check_launch("k_fill_f32");
+}
+
+// HarrisKeypoint3D/6D::detectKeypoints after the response (resp, caller order): non-maximum
+// suppression over the normals' lists, refineCorners (the same loop in harris_3d.hpp and
+// harris_6d.hpp) and Keypoints::getKeypointsCloud
+int64_t harris_finish_dev(pfx_ctx* ctx, int64_t n, double radius, float threshold, int refine, const float* nx,
+                          const float* ny, const float* nz, float* resp, int32_t* out, int64_t cap,
+                          float* corners_out, int64_t* n_corners, const char* tag) {
   hipStream_t st = ctx->stream;
-  TimeScope total(ctx, "harris3d");
-  // HarrisKeypoint3D::initCompute: NormalEstimation at the keypoint radius, viewpoint 0
-  float* nx = ctx->buf("h3_nx").as<float>(n);
-  float* ny = ctx->buf("h3_ny").as<float>(n);
-  float* nz = ctx->buf("h3_nz").as<float>(n);
-  float* cv = ctx->buf("h3_cv").as<float>(n);
-  normals_lists_dev(ctx, x, y, z, n, radius, nx, ny, nz, cv);
-  const float vp[3] = {0.f, 0.f, 0.f};
-  normals_chains_dev(ctx, ctx, nullptr, 1, vp, nx, ny, nz, cv);
   const NbLists& L = ctx->normals->L;
   const Grid& G = ctx->grid_a;
-  float* resp = resp_out ? resp_out : ctx->buf("h3_resp").as<float>(n);
   uint8_t* flag = ctx->buf("h3_flag").as<uint8_t>(n);
-  PFX_HIP(hipMemsetAsync(resp, 0, sizeof(float) * n, st));
   PFX_HIP(hipMemsetAsync(flag, 0, n, st));
   if (L.nq > 0) {
-    TimeScope ts(ctx, "harris3d_response");
     const unsigned nb = (unsigned)ceil_div(L.nq, 256);
-    k_harris_response<<<nb, 256, 0, st>>>(view(G), L, nx, ny, nz, resp);
     k_harris_nms<<<nb, 256, 0, st>>>(view(G), L, resp, threshold, flag);
-    check_launch("k_harris_response");
+    check_launch("k_harris_nms");
   }
   // corners in index order
   int32_t* corner = ctx->buf("h3_corner").as<int32_t>(n);
@@ -330,14 +481,14 @@ int64_t harris3d_dev(pfx_ctx* ctx, const float* x, const float* y, const float* 
   PFX_HIP(hipMemcpyAsync(&nc, d_cnt, sizeof(int64_t), hipMemcpyDeviceToHost, st));
   PFX_HIP(hipStreamSynchronize(st));
   if (n_corners) *n_corners = nc;
-  ctx->stats["harris3d_corners"] = nc;
+  ctx->stats[std::string(tag) + "_corners"] = nc;
   if (nc == 0) return 0;
   int32_t* snap = ctx->buf("h3_snap").as<int32_t>(nc);
   float* cxyz = ctx->buf("h3_cxyz").as<float>(3 * nc);
   int* head = ctx->buf("h3_head").as<int>(1);
   PFX_HIP(hipMemsetAsync(head, 0, sizeof(int), st));
   {
-    TimeScope ts(ctx, "harris3d_refine");
+    TimeScope ts(ctx, std::string(tag) + "_refine");
     const float rr = (float)(radius * radius);
     // the snap's d2 < 0.0001 test needs every point up to that distance: a ball a little larger
     // than the radius (the grid's cells are >= radius, so the 3x3x3 block still holds it)
@@ -359,6 +510,86 @@ int64_t harris3d_dev(pfx_ctx* ctx, const float* x, const float* y, const float* 
   if (corners_out && nc <= cap)
     PFX_HIP(hipMemcpyAsync(corners_out, cxyz, sizeof(float) * 3 * nc, hipMemcpyDeviceToDevice, st));
   return k;
+}
+
+
+}  // namespace
+
+int64_t harris3d_dev(pfx_ctx* ctx, const float* x, const float* y, const float* z, int64_t n, double radius,
+                     float threshold, int refine, int32_t* out, int64_t cap, float* resp_out, float* corners_out,
+                     int64_t* n_corners) {
+  PFX_CHECK(n >= 0, "harris3d: negative point count");
+  PFX_CHECK(radius > 0.0, "harris3d: radius must be > 0");
+  if (n_corners) *n_corners = 0;
+  if (n == 0) return 0;
+  hipStream_t st = ctx->stream;
+  TimeScope total(ctx, "harris3d");
+  // HarrisKeypoint3D::initCompute: NormalEstimation at the keypoint radius, viewpoint 0
+  float* nx = ctx->buf("h3_nx").as<float>(n);
+  float* ny = ctx->buf("h3_ny").as<float>(n);
+  float* nz = ctx->buf("h3_nz").as<float>(n);
+  float* cv = ctx->buf("h3_cv").as<float>(n);
+  normals_lists_dev(ctx, x, y, z, n, radius, nx, ny, nz, cv);
+  const float vp[3] = {0.f, 0.f, 0.f};
+  normals_chains_dev(ctx, ctx, nullptr, 1, vp, nx, ny, nz, cv);
+  const NbLists& L = ctx->normals->L;
+  const Grid& G = ctx->grid_a;
+  float* resp = resp_out ? resp_out : ctx->buf("h3_resp").as<float>(n);
+  PFX_HIP(hipMemsetAsync(resp, 0, sizeof(float) * n, st));
+  if (L.nq > 0) {
+    TimeScope ts(ctx, "harris3d_response");
+    const unsigned nb = (unsigned)ceil_div(L.nq, 256);
+    k_harris_response<<<nb, 256, 0, st>>>(view(G), L, nx, ny, nz, resp);
+    check_launch("k_harris_response");
+  }
+  return harris_finish_dev(ctx, n, radius, threshold, refine, nx, ny, nz, resp, out, cap, corners_out, n_corners,
+                           "harris3d");
+}
+
+int64_t harris6d_dev(pfx_ctx* ctx, const float* x, const float* y, const float* z, const uint32_t* rgb, int64_t n,
+                     double radius, float threshold, int refine, int32_t* out, int64_t cap, float* resp_out,
+                     float* corners_out, int64_t* n_corners, float* grad_out) {
+  PFX_CHECK(n >= 0, "harris6d: negative point count");
+  PFX_CHECK(radius > 0.0, "harris6d: radius must be > 0");
+  if (n_corners) *n_corners = 0;
+  if (n == 0) return 0;
+  hipStream_t st = ctx->stream;
+  TimeScope total(ctx, "harris6d");
+  // HarrisKeypoint6D::detectKeypoints: NormalEstimation at the keypoint radius, viewpoint 0
+  float* nx = ctx->buf("h3_nx").as<float>(n);
+  float* ny = ctx->buf("h3_ny").as<float>(n);
+  float* nz = ctx->buf("h3_nz").as<float>(n);
+  float* cv = ctx->buf("h3_cv").as<float>(n);
+  normals_lists_dev(ctx, x, y, z, n, radius, nx, ny, nz, cv);
+  const float vp[3] = {0.f, 0.f, 0.f};
+  normals_chains_dev(ctx, ctx, nullptr, 1, vp, nx, ny, nz, cv);
+  const NbLists& L = ctx->normals->L;
+  const Grid& G = ctx->grid_a;
+  float* gx = ctx->buf("h6_gx").as<float>(n);
+  float* gy = ctx->buf("h6_gy").as<float>(n);
+  float* gz = ctx->buf("h6_gz").as<float>(n);
+  float* resp = resp_out ? resp_out : ctx->buf("h3_resp").as<float>(n);
+  // points off the lists (non-finite) keep a NaN gradient and a zero response
+  fill_f32(ctx, gx, n, __builtin_nanf(""));
+  fill_f32(ctx, gy, n, __builtin_nanf(""));
+  fill_f32(ctx, gz, n, __builtin_nanf(""));
+  if (grad_out) fill_f32(ctx, grad_out, 3 * n, __builtin_nanf(""));
+  PFX_HIP(hipMemsetAsync(resp, 0, sizeof(float) * n, st));
+  if (L.nq > 0) {
+    const unsigned nb = (unsigned)ceil_div(L.nq, 256);
+    {
+      TimeScope ts(ctx, "harris6d_gradient");
+      k_intensity_gradient<<<nb, 256, 0, st>>>(view(G), L, rgb, nx, ny, nz, gx, gy, gz, grad_out);
+      check_launch("k_intensity_gradient");
+    }
+    {
+      TimeScope ts(ctx, "harris6d_response");
+      k_harris6d_response<<<nb, 256, 0, st>>>(view(G), L, nx, ny, nz, gx, gy, gz, resp);
+      check_launch("k_harris6d_response");
+    }
+  }
+  return harris_finish_dev(ctx, n, radius, threshold, refine, nx, ny, nz, resp, out, cap, corners_out, n_corners,
+                           "harris6d");
 }
 
 }  // namespace pfx

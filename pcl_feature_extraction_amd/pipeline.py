@@ -155,3 +155,12 @@ def keypoints_harris3d(ctx: Context, x, y, z, idx) -> int:
     cloud indices into `idx`; returns their number."""
     k, _ = ctx.harris3d_keypoints_dev(x, y, z, idx, radius=0.01, threshold=1e-6, refine=True)
     return k
+
+
+def keypoints_harris6d(ctx: Context, x, y, z, rgb, idx) -> int:
+    """Keypoints("Harris6D").compute (keypoints.h:164-176): HarrisKeypoint6D<PointXYZRGB,
+    PointXYZI> with non-maximum suppression, threshold 1e-6, radius 0.01 (the constructor's
+    default) and corner refinement, then getKeypointsCloud (keypoints.h:365-395); rgb: the
+    cloud's packed colours (int32 tensor).  Snapped cloud indices into `idx`; returns their number."""
+    k, _ = ctx.harris6d_keypoints_dev(x, y, z, rgb, idx, radius=0.01, threshold=1e-6, refine=True)
+    return k

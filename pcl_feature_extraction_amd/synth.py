@@ -115,6 +115,23 @@ def synth_seabed(n: int, seed: int = 3, depth: float | None = None):
     return _finish(rng, d, t, n)
 
 
+def texture_rgb(x, y, z, seed: int = 0):
+    """Packed 0x00RRGGBB colours of a smooth procedural texture (stripes and blobs at 2-10 cm
+    scales) over the scene: colour gradients for HarrisKeypoint6D (the generators' own rgb is
+    uniform noise, which the xyz-only path never reads)."""
+    rng = np.random.default_rng(seed + 104729)
+    x, y, z = (np.asarray(a, np.float64) for a in (x, y, z))
+    ch = []
+    for _ in range(3):
+        k = rng.normal(size=(3, 3)) * np.array([[60.0], [90.0], [140.0]])
+        ph = rng.uniform(0, 2 * np.pi, 3)
+        v = 0.0
+        for j in range(3):
+            v = v + np.sin(k[j, 0] * x + k[j, 1] * y + k[j, 2] * z + ph[j]) / (j + 1)
+        ch.append(np.clip(128.0 + 70.0 * v, 0, 255).astype(np.uint32))
+    return (ch[0] << 16) | (ch[1] << 8) | ch[2]
+
+
 def config(name: str):
     """The BASELINE.json configs as (x, y, z) generators."""
     if name == "cfg2_room100k":

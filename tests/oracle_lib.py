@@ -261,6 +261,56 @@ def harris3d(x, y, z, radius=0.01, threshold=1e-6, refine=True, threads=0):
     return idx[: k.value].copy(), resp[:n].copy(), corners[: nc.value].copy()
 
 
+def harris6d(x, y, z, rgb, radius=0.01, threshold=1e-6, refine=True, threads=0):
+    """HarrisKeypoint6D (keypoints.h:164-176) + getKeypointsCloud (keypoints.h:365-395):
+    (snapped cloud indices, per-point response, refined corners (nc, 3), normalised intensity
+    gradients (n, 3)).  rgb: packed 0x00RRGGBB."""
+    x, y, z = map(_f32, (x, y, z))
+    rgb = np.ascontiguousarray(rgb, dtype=np.uint32)
+    n = len(x)
+    cap = max(n, 1)
+    idx = np.empty(cap, np.int32)
+    resp = np.empty(max(n, 1), np.float32)
+    corners = np.empty((cap, 3), np.float32)
+    grad = np.empty((max(n, 1), 3), np.float32)
+    k, nc = ctypes.c_int64(), ctypes.c_int64()
+    rc = lib().orc_harris6d(_p(x), _p(y), _p(z), _p(rgb, ctypes.POINTER(ctypes.c_uint32)), _i64(n),
+                            ctypes.c_double(radius), ctypes.c_float(threshold), ctypes.c_int(1 if refine else 0),
+                            _p(idx, _i32p), _i64(cap), ctypes.byref(k), ctypes.byref(nc), _p(resp), _p(corners),
+                            _p(grad), ctypes.c_int(threads))
+    assert rc == 0, rc
+    return idx[: k.value].copy(), resp[:n].copy(), corners[: nc.value].copy(), grad[:n].copy()
+
+
+def eigen_selfadjoint6f(a):
+    """Eigen 3.2 SelfAdjointEigenSolver<Matrix<float,6,6>> eigenvalues of (m, 6, 6) float32
+    matrices (lower triangle read); returns (ev (m, 6), count of non-converged)."""
+    a = np.ascontiguousarray(np.asarray(a, np.float32).transpose(0, 2, 1))  # column-major
+    m = a.shape[0]
+    ev = np.empty((m, 6), np.float32)
+    bad = lib().orc_eigen_selfadjoint6f(_p(a), _i64(m), _p(ev))
+    return ev, bad
+
+
+def colpiv_solve3f(a, b):
+    """Eigen 3.2 ColPivHouseholderQR<Matrix3f>(a).solve(b) for (m, 3, 3) / (m, 3) float32."""
+    a = np.ascontiguousarray(np.asarray(a, np.float32).transpose(0, 2, 1))
+    b = np.ascontiguousarray(b, np.float32)
+    x = np.empty_like(b)
+    lib().orc_colpiv_solve3f(_p(a), _p(b), _i64(a.shape[0]), _p(x))
+    return x
+
+
+def u8_cast(v, native=False):
+    """static_cast<uint8_t>(float) as the restatement models it (native=True: the host g++'s
+    own code for the cast, the pin of the model)."""
+    v = _f32(v)
+    out = np.empty(len(v), np.int32)
+    f = lib().orc_u8_cast_native if native else lib().orc_u8_cast_model
+    f(_p(v), _i64(len(v)), _p(out, _i32p))
+    return out
+
+
 def ransac_rejector(src, tgt, query, match, threshold=0.015, max_iterations=1000):
     """Features::filterCorrespondences (features.h:282-297): (kept correspondence positions,
     4x4 best transformation, models evaluated).  src / tgt: (n, 3) keypoint clouds."""
