@@ -285,15 +285,17 @@ pfx_status pfx_iss_keypoints(pfx_ctx* ctx, const float* x, const float* y, const
  * to its nearest cloud point when d2 < 0.0001.  idx[0..cap): those cloud indices in corner
  * (= index) order, *n_out their number (PFX_ERR_CAPACITY when it or the corner count exceeds
  * cap).  response (nullable, n floats): per-point intensity; corners (nullable, 3 * cap floats)
- * and n_corners (nullable): the refined corners.  non_max == 0 -> PFX_ERR_UNSUPPORTED (not used
- * by the reference: keypoints.h:155). */
+ * and n_corners (nullable): the refined corners; corner_idx (nullable, cap int32): the cloud index
+ * of each corner's own point (PCL's output intensity = response[corner_idx]).  non_max == 0 ->
+ * PFX_ERR_UNSUPPORTED (not used by the reference: keypoints.h:155). */
 pfx_status pfx_harris3d_keypoints_dev(pfx_ctx* ctx, const float* d_x, const float* d_y, const float* d_z, int64_t n,
                                       double radius, float threshold, int32_t non_max, int32_t refine,
                                       int32_t* d_idx, int64_t cap, int64_t* n_out, float* d_response,
-                                      float* d_corners, int64_t* n_corners);
+                                      float* d_corners, int64_t* n_corners, int32_t* d_corner_idx);
 pfx_status pfx_harris3d_keypoints(pfx_ctx* ctx, const float* x, const float* y, const float* z, int64_t n,
                                   double radius, float threshold, int32_t non_max, int32_t refine, int32_t* idx,
-                                  int64_t cap, int64_t* n_out, float* response, float* corners, int64_t* n_corners);
+                                  int64_t cap, int64_t* n_out, float* response, float* corners, int64_t* n_corners,
+                                  int32_t* corner_idx);
 
 /* HarrisKeypoint6D (keypoints.h:164-176) + Keypoints::getKeypointsCloud: normals at the radius
  * (viewpoint 0), IntensityGradientEstimation at the radius over the colour intensity
@@ -306,11 +308,12 @@ pfx_status pfx_harris3d_keypoints(pfx_ctx* ctx, const float* x, const float* y, 
 pfx_status pfx_harris6d_keypoints_dev(pfx_ctx* ctx, const float* d_x, const float* d_y, const float* d_z,
                                       const uint32_t* d_rgb, int64_t n, double radius, float threshold,
                                       int32_t non_max, int32_t refine, int32_t* d_idx, int64_t cap, int64_t* n_out,
-                                      float* d_response, float* d_corners, int64_t* n_corners, float* d_grad);
+                                      float* d_response, float* d_corners, int64_t* n_corners, float* d_grad,
+                                      int32_t* d_corner_idx);
 pfx_status pfx_harris6d_keypoints(pfx_ctx* ctx, const float* x, const float* y, const float* z, const uint32_t* rgb,
                                   int64_t n, double radius, float threshold, int32_t non_max, int32_t refine,
                                   int32_t* idx, int64_t cap, int64_t* n_out, float* response, float* corners,
-                                  int64_t* n_corners, float* grad);
+                                  int64_t* n_corners, float* grad, int32_t* corner_idx);
 
 /* ---- RANSAC correspondence rejection --------------------------------- */
 /* CorrespondenceRejectorSampleConsensus::getCorrespondences + getBestTransformation (host

@@ -24,6 +24,7 @@
 #ifndef PFX_PCL_HPP_
 #define PFX_PCL_HPP_
 
+#include <algorithm>
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
@@ -123,6 +124,18 @@ struct Affine3f {
   }
 };
 
+// 4x4 float matrix (registration's getBestTransformation), row-major storage
+struct Matrix4f {
+  float m[16];
+  Matrix4f() { setIdentity(); }
+  static Matrix4f Identity() { return Matrix4f(); }
+  void setIdentity() {
+    for (int i = 0; i < 16; ++i) m[i] = (i % 5 == 0) ? 1.f : 0.f;
+  }
+  float& operator()(int r, int c) { return m[4 * r + c]; }
+  float operator()(int r, int c) const { return m[4 * r + c]; }
+};
+
 }  // namespace Eigen
 
 namespace pcl {
@@ -164,6 +177,11 @@ struct alignas(16) Normal {
 struct alignas(16) PointWithRange {
   float x = 0, y = 0, z = 0, data_pad = 1.f;
   float range = 0;
+  float pad_[3] = {0, 0, 0};
+};
+struct alignas(16) PointXYZI {
+  float x = 0, y = 0, z = 0, data_pad = 1.f;
+  float intensity = 0;
   float pad_[3] = {0, 0, 0};
 };
 struct FPFHSignature33 { float histogram[33]; };
@@ -588,6 +606,118 @@ inline double cloudResolution(const typename PointCloud<PointT>::ConstPtr& cloud
   return res;
 }
 
+// ---- HarrisKeypoint3D / HarrisKeypoint6D (keypoints.h:150-176) --------------------------------
+// compute(): the corners as PCL outputs them -- refined position, intensity = the response of
+// the corner's own point -- in corner (index) order (PCL: omp critical order).
+// Only the reference's configuration is accelerated: method HARRIS (3D) with non-maximum
+// suppression; anything else -> PCL_ERROR + empty output.  The radius defaults to PCL's 0.01.
+namespace detail {
+template <typename PointOutT, typename PointInT>
+inline void harris_output(const PointCloud<PointInT>& in, const std::vector<float>& resp,
+                          const std::vector<float>& corners, const std::vector<int32_t>& cidx, int64_t nc,
+                          PointCloud<PointOutT>& out) {
+  for (int64_t c = 0; c < nc; ++c) {
+    PointOutT p;
+    p.x = corners[3 * c];
+    p.y = corners[3 * c + 1];
+    p.z = corners[3 * c + 2];
+    p.intensity = resp[(size_t)cidx[c]];
+    out.push_back(p);
+  }
+  (void)in;
+  out.is_dense = true;
+}
+}  // namespace detail
+
+template <typename PointInT, typename PointOutT, typename NormalT = Normal>
+class HarrisKeypoint3D {
+ public:
+  typedef typename PointCloud<PointInT>::ConstPtr PointCloudInConstPtr;
+  enum ResponseMethod { HARRIS = 1, NOBLE, LOWE, TOMASI, CURVATURE };
+  explicit HarrisKeypoint3D(ResponseMethod method = HARRIS, float radius = 0.01f, float threshold = 0.0f)
+      : method_(method), radius_(radius), threshold_(threshold) {}
+  void setInputCloud(const PointCloudInConstPtr& cloud) { input_ = cloud; }
+  void setMethod(ResponseMethod m) { method_ = m; }
+  void setRadius(float r) { radius_ = r; }
+  void setRadiusSearch(double r) { radius_ = (float)r; }
+  void setThreshold(float t) { threshold_ = t; }
+  void setNonMaxSupression(bool b) { nonmax_ = b; }
+  void setRefine(bool b) { refine_ = b; }
+  void compute(PointCloud<PointOutT>& output) {
+    output.clear();
+    if (!input_) {
+      PCL_ERROR("[pcl::HarrisKeypoint3D::compute] no input cloud\n");
+      return;
+    }
+    if (method_ != HARRIS || !nonmax_) {
+      PCL_ERROR("[pcl::HarrisKeypoint3D::compute] only method HARRIS with non-maximum suppression is accelerated\n");
+      return;
+    }
+    if (!detail::context()) return;
+    const detail::SoA c = detail::soa_xyz(*input_);
+    const size_t n = c.x.size();
+    std::vector<int32_t> idx(n + 1), cidx(n + 1);
+    std::vector<float> resp(n + 1), corners(3 * (n + 1));
+    int64_t k = 0, nc = 0;
+    if (!detail::ok(pfx_harris3d_keypoints(detail::context(), c.x.data(), c.y.data(), c.z.data(), (int64_t)n, radius_,
+                                           threshold_, 1, refine_ ? 1 : 0, idx.data(), (int64_t)n + 1, &k, resp.data(),
+                                           corners.data(), &nc, cidx.data()),
+                    "HarrisKeypoint3D"))
+      return;
+    detail::harris_output(*input_, resp, corners, cidx, nc, output);
+  }
+
+ private:
+  PointCloudInConstPtr input_;
+  ResponseMethod method_;
+  float radius_, threshold_;
+  bool nonmax_ = false, refine_ = true;
+};
+
+// HarrisKeypoint6D<PointXYZRGB, ...>: the colour intensity comes from the points' rgb field
+template <typename PointInT, typename PointOutT, typename NormalT = Normal>
+class HarrisKeypoint6D {
+ public:
+  typedef typename PointCloud<PointInT>::ConstPtr PointCloudInConstPtr;
+  explicit HarrisKeypoint6D(float radius = 0.01f, float threshold = 0.0f) : radius_(radius), threshold_(threshold) {}
+  void setInputCloud(const PointCloudInConstPtr& cloud) { input_ = cloud; }
+  void setRadius(float r) { radius_ = r; }
+  void setRadiusSearch(double r) { radius_ = (float)r; }
+  void setThreshold(float t) { threshold_ = t; }
+  void setNonMaxSupression(bool b) { nonmax_ = b; }
+  void setRefine(bool b) { refine_ = b; }
+  void compute(PointCloud<PointOutT>& output) {
+    output.clear();
+    if (!input_) {
+      PCL_ERROR("[pcl::HarrisKeypoint6D::compute] no input cloud\n");
+      return;
+    }
+    if (!nonmax_) {
+      PCL_ERROR("[pcl::HarrisKeypoint6D::compute] only non-maximum suppression is accelerated\n");
+      return;
+    }
+    if (!detail::context()) return;
+    const detail::SoA c = detail::soa_xyz(*input_);
+    const size_t n = c.x.size();
+    std::vector<uint32_t> rgb(n + 1);
+    for (size_t i = 0; i < n; ++i) rgb[i] = input_->points[i].rgba & 0x00ffffffu;
+    std::vector<int32_t> idx(n + 1), cidx(n + 1);
+    std::vector<float> resp(n + 1), corners(3 * (n + 1));
+    int64_t k = 0, nc = 0;
+    if (!detail::ok(pfx_harris6d_keypoints(detail::context(), c.x.data(), c.y.data(), c.z.data(), rgb.data(),
+                                           (int64_t)n, radius_, threshold_, 1, refine_ ? 1 : 0, idx.data(),
+                                           (int64_t)n + 1, &k, resp.data(), corners.data(), &nc, nullptr, cidx.data()),
+                    "HarrisKeypoint6D"))
+      return;
+    detail::harris_output(*input_, resp, corners, cidx, nc, output);
+  }
+
+ private:
+  PointCloudInConstPtr input_;
+  float radius_, threshold_;
+  bool nonmax_ = false, refine_ = true;
+};
+
 // ---- descriptor matching (features.h:224-273) ------------------------------------------------
 struct Correspondence {
   int index_query = 0;
@@ -665,6 +795,122 @@ class KdTreeFLANN {
   mutable std::vector<int32_t> idx_;
   mutable std::vector<float> dist_;
 };
+
+// KdTreeFLANN over a point cloud (Keypoints::getKeypointsCloud, keypoints.h:374-392): exact
+// nearestKSearch(k = 1) as radius searches on the GPU (pfx_radius_search) over a growing ball --
+// the first non-empty ball holds the nearest point, the first entry of FLANN's (d2, index) order
+template <>
+class KdTreeFLANN<PointXYZRGB> {
+ public:
+  typedef PointCloud<PointXYZRGB>::ConstPtr PointCloudConstPtr;
+  explicit KdTreeFLANN(bool sorted = true) : sorted_(sorted) {}
+  void setInputCloud(const PointCloudConstPtr& cloud) {
+    target_ = cloud;
+    soa_ = cloud ? detail::soa_xyz(*cloud) : detail::SoA();
+    float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (size_t i = 0; i < soa_.x.size(); ++i) {
+      const float p[3] = {soa_.x[i], soa_.y[i], soa_.z[i]};
+      if (!(std::isfinite(p[0]) && std::isfinite(p[1]) && std::isfinite(p[2]))) continue;
+      for (int d = 0; d < 3; ++d) { lo[d] = std::min(lo[d], p[d]); hi[d] = std::max(hi[d], p[d]); }
+    }
+    extent_ = 0.0;
+    for (int d = 0; d < 3; ++d) extent_ = std::max(extent_, (double)hi[d] - (double)lo[d]);
+  }
+  int nearestKSearch(const PointXYZRGB& point, int k, std::vector<int>& k_indices,
+                     std::vector<float>& k_sqr_distances) const {
+    k_indices.clear();
+    k_sqr_distances.clear();
+    if (k != 1 || !target_ || soa_.x.empty()) {
+      if (k != 1) PCL_ERROR("[pcl::KdTreeFLANN::nearestKSearch] only k = 1 is accelerated\n");
+      return 0;
+    }
+    if (!(std::isfinite(point.x) && std::isfinite(point.y) && std::isfinite(point.z)) || !detail::context())
+      return 0;
+    std::lock_guard<std::mutex> lock(detail::context_mutex());
+    const float qx = point.x, qy = point.y, qz = point.z;
+    // the ball must reach the farthest point of the cloud's box: its diagonal from any point in it
+    const double limit = 4.0 * (extent_ + std::fabs((double)qx) + std::fabs((double)qy) + std::fabs((double)qz)) + 1.0;
+    for (double r = 0.01; r <= limit; r *= 4.0) {
+      int64_t cnt = 0;
+      int32_t idx = -1;
+      float d2 = 0.f;
+      if (!detail::ok(pfx_radius_search(detail::context(), soa_.x.data(), soa_.y.data(), soa_.z.data(),
+                                        (int64_t)soa_.x.size(), &qx, &qy, &qz, 1, r, &cnt, &idx, &d2, 1),
+                      "KdTreeFLANN"))
+        return 0;
+      if (cnt > 0) {
+        k_indices.assign(1, idx);
+        k_sqr_distances.assign(1, d2);
+        return 1;
+      }
+    }
+    return 0;
+  }
+
+ private:
+  bool sorted_;
+  PointCloudConstPtr target_;
+  detail::SoA soa_;
+  double extent_ = 0.0;
+};
+
+// ---- RANSAC correspondence rejection (features.h:282-297) -------------------------------------
+namespace registration {
+// CorrespondenceRejectorSampleConsensus<PointT>: PCL's fixed-seed sample sequence and adaptive
+// stop, every hypothesis scored on the GPU (pfx_ransac_rejector)
+template <typename PointT>
+class CorrespondenceRejectorSampleConsensus {
+ public:
+  typedef typename PointCloud<PointT>::ConstPtr PointCloudConstPtr;
+  void setInputSource(const PointCloudConstPtr& c) { source_ = c; }
+  void setInputTarget(const PointCloudConstPtr& c) { target_ = c; }
+  void setInputCorrespondences(const CorrespondencesConstPtr& c) { input_ = c; }
+  void setInlierThreshold(double t) { threshold_ = t; }
+  void setMaximumIterations(int n) { max_iterations_ = n; }
+  double getInlierThreshold() const { return threshold_; }
+  int getMaximumIterations() const { return max_iterations_; }
+  Eigen::Matrix4f getBestTransformation() const { return best_; }
+  // CorrespondenceRejector::getCorrespondences -> applyRejection(correspondences)
+  void getCorrespondences(Correspondences& out) {
+    out.clear();
+    best_.setIdentity();
+    if (!input_ || !source_ || !target_) {
+      PCL_ERROR("[pcl::registration::CorrespondenceRejectorSampleConsensus::getCorrespondences] no input\n");
+      return;
+    }
+    getRemainingCorrespondences(*input_, out);
+  }
+  void getRemainingCorrespondences(const Correspondences& original, Correspondences& remaining) {
+    remaining.clear();
+    best_.setIdentity();
+    if (!source_ || !target_ || !detail::context()) return;
+    const detail::SoA s = detail::soa_xyz(*source_), t = detail::soa_xyz(*target_);
+    const size_t n = original.size();
+    std::vector<int32_t> q(n + 1), m(n + 1), keep(n + 1);
+    for (size_t i = 0; i < n; ++i) {
+      q[i] = original[i].index_query;
+      m[i] = original[i].index_match;
+    }
+    int64_t nk = 0;
+    float T[16];
+    std::lock_guard<std::mutex> lock(detail::context_mutex());
+    if (!detail::ok(pfx_ransac_rejector(detail::context(), s.x.data(), s.y.data(), s.z.data(), (int64_t)s.x.size(),
+                                        t.x.data(), t.y.data(), t.z.data(), (int64_t)t.x.size(), q.data(), m.data(),
+                                        (int64_t)n, threshold_, max_iterations_, keep.data(), &nk, T),
+                    "CorrespondenceRejectorSampleConsensus"))
+      return;
+    for (int64_t j = 0; j < nk; ++j) remaining.push_back(original[(size_t)keep[j]]);
+    for (int i = 0; i < 16; ++i) best_.m[i] = T[i];
+  }
+
+ private:
+  PointCloudConstPtr source_, target_;
+  CorrespondencesConstPtr input_;
+  double threshold_ = 0.05;
+  int max_iterations_ = 1000;
+  Eigen::Matrix4f best_;
+};
+}  // namespace registration
 
 }  // namespace pcl
 

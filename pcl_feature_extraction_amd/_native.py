@@ -122,14 +122,16 @@ _SIGS = {
     "pfx_iss_keypoints": (c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, ctypes.c_double, ctypes.c_double, ctypes.c_int32,
                                   ctypes.c_double, ctypes.c_double, c_vp, c_i64, c_i64p, c_vp]),
     "pfx_harris3d_keypoints_dev": (c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, ctypes.c_double, ctypes.c_float,
-                                           ctypes.c_int32, ctypes.c_int32, c_vp, c_i64, c_i64p, c_vp, c_vp, c_i64p]),
-    "pfx_harris3d_keypoints": (c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, ctypes.c_double, ctypes.c_float,
-                                       ctypes.c_int32, ctypes.c_int32, c_vp, c_i64, c_i64p, c_vp, c_vp, c_i64p]),
-    "pfx_harris6d_keypoints_dev": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, ctypes.c_double, ctypes.c_float,
                                            ctypes.c_int32, ctypes.c_int32, c_vp, c_i64, c_i64p, c_vp, c_vp, c_i64p,
                                            c_vp]),
-    "pfx_harris6d_keypoints": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, ctypes.c_double, ctypes.c_float,
+    "pfx_harris3d_keypoints": (c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, ctypes.c_double, ctypes.c_float,
                                        ctypes.c_int32, ctypes.c_int32, c_vp, c_i64, c_i64p, c_vp, c_vp, c_i64p, c_vp]),
+    "pfx_harris6d_keypoints_dev": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, ctypes.c_double, ctypes.c_float,
+                                           ctypes.c_int32, ctypes.c_int32, c_vp, c_i64, c_i64p, c_vp, c_vp, c_i64p,
+                                           c_vp, c_vp]),
+    "pfx_harris6d_keypoints": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, ctypes.c_double, ctypes.c_float,
+                                       ctypes.c_int32, ctypes.c_int32, c_vp, c_i64, c_i64p, c_vp, c_vp, c_i64p, c_vp,
+                                       c_vp]),
     "pfx_ransac_rejector": (c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_i64,
                                     ctypes.c_double, ctypes.c_int32, c_vp, c_i64p, c_vp]),
 }

@@ -343,7 +343,8 @@ class Context:
         k, nc = ctypes.c_int64(), ctypes.c_int64()
         self._check(self._lib.pfx_harris3d_keypoints(self.h, _ptr(x), _ptr(y), _ptr(z), n, radius, threshold,
                                                      1 if non_max else 0, 1 if refine else 0, _ptr(idx), cap,
-                                                     ctypes.byref(k), _ptr(resp), _ptr(corners), ctypes.byref(nc)))
+                                                     ctypes.byref(k), _ptr(resp), _ptr(corners), ctypes.byref(nc),
+                                                     None))
         out = idx[: k.value].copy()
         return (out, resp[:n].copy(), corners[: nc.value].copy()) if details else out
 
@@ -354,7 +355,7 @@ class Context:
         self._check(self._lib.pfx_harris3d_keypoints_dev(self.h, _ptr(x), _ptr(y), _ptr(z), x.numel(), radius,
                                                          threshold, 1, 1 if refine else 0, _ptr(idx), idx.numel(),
                                                          ctypes.byref(k), _ptr(response), _ptr(corners),
-                                                         ctypes.byref(nc)))
+                                                         ctypes.byref(nc), None))
         return k.value, nc.value
 
     def harris6d_keypoints(self, x, y, z, rgb, radius=0.01, threshold=1e-6, refine=True, non_max=True,
@@ -376,7 +377,7 @@ class Context:
         self._check(self._lib.pfx_harris6d_keypoints(self.h, _ptr(x), _ptr(y), _ptr(z), _ptr(rgb), n, radius,
                                                      threshold, 1 if non_max else 0, 1 if refine else 0, _ptr(idx),
                                                      cap, ctypes.byref(k), _ptr(resp), _ptr(corners), ctypes.byref(nc),
-                                                     _ptr(grad)))
+                                                     _ptr(grad), None))
         out = idx[: k.value].copy()
         return (out, resp[:n].copy(), corners[: nc.value].copy(), grad[:n].copy()) if details else out
 
@@ -388,7 +389,7 @@ class Context:
         self._check(self._lib.pfx_harris6d_keypoints_dev(self.h, _ptr(x), _ptr(y), _ptr(z), _ptr(rgb), x.numel(),
                                                          radius, threshold, 1, 1 if refine else 0, _ptr(idx),
                                                          idx.numel(), ctypes.byref(k), _ptr(response), _ptr(corners),
-                                                         ctypes.byref(nc), _ptr(grad)))
+                                                         ctypes.byref(nc), _ptr(grad), None))
         return k.value, nc.value
 
     # ---- RANSAC correspondence rejection -----------------------------------

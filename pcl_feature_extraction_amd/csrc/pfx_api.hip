@@ -656,7 +656,8 @@ void check_harris(double radius, int32_t non_max) {
 extern "C" pfx_status pfx_harris3d_keypoints_dev(pfx_ctx* ctx, const float* d_x, const float* d_y, const float* d_z,
                                                  int64_t n, double radius, float threshold, int32_t non_max,
                                                  int32_t refine, int32_t* d_idx, int64_t cap, int64_t* n_out,
-                                                 float* d_response, float* d_corners, int64_t* n_corners) {
+                                                 float* d_response, float* d_corners, int64_t* n_corners,
+                                                 int32_t* d_corner_idx) {
   PFX_API_BEGIN
   check_ctx(ctx);
   check_points(d_x, d_y, d_z, n, "harris3d");
@@ -664,7 +665,7 @@ extern "C" pfx_status pfx_harris3d_keypoints_dev(pfx_ctx* ctx, const float* d_x,
   if (!n_out || cap < 0 || (cap && !d_idx)) throw Error(PFX_ERR_INVALID, "harris3d: invalid output arguments");
   int64_t nc = 0;
   const int64_t k = pfx::harris3d_dev(ctx, d_x, d_y, d_z, n, radius, threshold, refine, d_idx, cap, d_response,
-                                      d_corners, &nc);
+                                      d_corners, &nc, d_corner_idx);
   *n_out = k;
   if (n_corners) *n_corners = nc;
   if (k > cap || (d_corners && nc > cap))
@@ -675,7 +676,7 @@ extern "C" pfx_status pfx_harris3d_keypoints_dev(pfx_ctx* ctx, const float* d_x,
 extern "C" pfx_status pfx_harris3d_keypoints(pfx_ctx* ctx, const float* x, const float* y, const float* z, int64_t n,
                                              double radius, float threshold, int32_t non_max, int32_t refine,
                                              int32_t* idx, int64_t cap, int64_t* n_out, float* response,
-                                             float* corners, int64_t* n_corners) {
+                                             float* corners, int64_t* n_corners, int32_t* corner_idx) {
   PFX_API_BEGIN
   check_ctx(ctx);
   check_points(x, y, z, n, "harris3d");
@@ -687,8 +688,9 @@ extern "C" pfx_status pfx_harris3d_keypoints(pfx_ctx* ctx, const float* x, const
   int32_t* di = ctx->buf("out_h3_idx").as<int32_t>(n + 1);
   float* dr = response ? ctx->buf("out_h3_resp").as<float>(n + 1) : nullptr;
   float* dc = corners ? ctx->buf("out_h3_corners").as<float>(3 * (n + 1)) : nullptr;
+  int32_t* dci = corner_idx ? ctx->buf("out_h3_cidx").as<int32_t>(n + 1) : nullptr;
   int64_t nc = 0;
-  const int64_t k = pfx::harris3d_dev(ctx, dx, dy, dz, n, radius, threshold, refine, di, n, dr, dc, &nc);
+  const int64_t k = pfx::harris3d_dev(ctx, dx, dy, dz, n, radius, threshold, refine, di, n, dr, dc, &nc, dci);
   *n_out = k;
   if (n_corners) *n_corners = nc;
   if (k > cap || (corners && nc > cap))
@@ -696,6 +698,8 @@ extern "C" pfx_status pfx_harris3d_keypoints(pfx_ctx* ctx, const float* x, const
   if (k) PFX_HIP(hipMemcpyAsync(idx, di, sizeof(int32_t) * k, hipMemcpyDeviceToHost, ctx->stream));
   if (response && n) PFX_HIP(hipMemcpyAsync(response, dr, sizeof(float) * n, hipMemcpyDeviceToHost, ctx->stream));
   if (corners && nc) PFX_HIP(hipMemcpyAsync(corners, dc, sizeof(float) * 3 * nc, hipMemcpyDeviceToHost, ctx->stream));
+  if (corner_idx && nc)
+    PFX_HIP(hipMemcpyAsync(corner_idx, dci, sizeof(int32_t) * nc, hipMemcpyDeviceToHost, ctx->stream));
   PFX_HIP(hipStreamSynchronize(ctx->stream));
   PFX_API_END(ctx)
 }
@@ -704,7 +708,7 @@ extern "C" pfx_status pfx_harris6d_keypoints_dev(pfx_ctx* ctx, const float* d_x,
                                                  const uint32_t* d_rgb, int64_t n, double radius, float threshold,
                                                  int32_t non_max, int32_t refine, int32_t* d_idx, int64_t cap,
                                                  int64_t* n_out, float* d_response, float* d_corners,
-                                                 int64_t* n_corners, float* d_grad) {
+                                                 int64_t* n_corners, float* d_grad, int32_t* d_corner_idx) {
   PFX_API_BEGIN
   check_ctx(ctx);
   check_points(d_x, d_y, d_z, n, "harris6d");
@@ -713,7 +717,7 @@ extern "C" pfx_status pfx_harris6d_keypoints_dev(pfx_ctx* ctx, const float* d_x,
   if (!n_out || cap < 0 || (cap && !d_idx)) throw Error(PFX_ERR_INVALID, "harris6d: invalid output arguments");
   int64_t nc = 0;
   const int64_t k = pfx::harris6d_dev(ctx, d_x, d_y, d_z, d_rgb, n, radius, threshold, refine, d_idx, cap, d_response,
-                                      d_corners, &nc, d_grad);
+                                      d_corners, &nc, d_grad, d_corner_idx);
   *n_out = k;
   if (n_corners) *n_corners = nc;
   if (k > cap || (d_corners && nc > cap))
@@ -725,7 +729,7 @@ extern "C" pfx_status pfx_harris6d_keypoints(pfx_ctx* ctx, const float* x, const
                                              const uint32_t* rgb, int64_t n, double radius, float threshold,
                                              int32_t non_max, int32_t refine, int32_t* idx, int64_t cap,
                                              int64_t* n_out, float* response, float* corners, int64_t* n_corners,
-                                             float* grad) {
+                                             float* grad, int32_t* corner_idx) {
   PFX_API_BEGIN
   check_ctx(ctx);
   check_points(x, y, z, n, "harris6d");
@@ -741,8 +745,9 @@ extern "C" pfx_status pfx_harris6d_keypoints(pfx_ctx* ctx, const float* x, const
   float* dr = response ? ctx->buf("out_h3_resp").as<float>(n + 1) : nullptr;
   float* dc = corners ? ctx->buf("out_h3_corners").as<float>(3 * (n + 1)) : nullptr;
   float* dg = grad ? ctx->buf("out_h6_grad").as<float>(3 * (n + 1)) : nullptr;
+  int32_t* dci = corner_idx ? ctx->buf("out_h3_cidx").as<int32_t>(n + 1) : nullptr;
   int64_t nc = 0;
-  const int64_t k = pfx::harris6d_dev(ctx, dx, dy, dz, dc_rgb, n, radius, threshold, refine, di, n, dr, dc, &nc, dg);
+  const int64_t k = pfx::harris6d_dev(ctx, dx, dy, dz, dc_rgb, n, radius, threshold, refine, di, n, dr, dc, &nc, dg, dci);
   *n_out = k;
   if (n_corners) *n_corners = nc;
   if (k > cap || (corners && nc > cap))
@@ -751,6 +756,8 @@ extern "C" pfx_status pfx_harris6d_keypoints(pfx_ctx* ctx, const float* x, const
   if (response && n) PFX_HIP(hipMemcpyAsync(response, dr, sizeof(float) * n, hipMemcpyDeviceToHost, ctx->stream));
   if (corners && nc) PFX_HIP(hipMemcpyAsync(corners, dc, sizeof(float) * 3 * nc, hipMemcpyDeviceToHost, ctx->stream));
   if (grad && n) PFX_HIP(hipMemcpyAsync(grad, dg, sizeof(float) * 3 * n, hipMemcpyDeviceToHost, ctx->stream));
+  if (corner_idx && nc)
+    PFX_HIP(hipMemcpyAsync(corner_idx, dci, sizeof(int32_t) * nc, hipMemcpyDeviceToHost, ctx->stream));
   PFX_HIP(hipStreamSynchronize(ctx->stream));
   PFX_API_END(ctx)
 }

@@ -459,7 +459,7 @@ void fill_f32(pfx_ctx* ctx, float* p, int64_t n, float v) {
 // harris_6d.hpp) and Keypoints::getKeypointsCloud
 int64_t harris_finish_dev(pfx_ctx* ctx, int64_t n, double radius, float threshold, int refine, const float* nx,
                           const float* ny, const float* nz, float* resp, int32_t* out, int64_t cap,
-                          float* corners_out, int64_t* n_corners, const char* tag) {
+                          float* corners_out, int64_t* n_corners, const char* tag, int32_t* corner_idx_out) {
   hipStream_t st = ctx->stream;
   const NbLists& L = ctx->normals->L;
   const Grid& G = ctx->grid_a;
@@ -509,6 +509,8 @@ int64_t harris_finish_dev(pfx_ctx* ctx, int64_t n, double radius, float threshol
   if (k <= cap && k > 0) PFX_HIP(hipMemcpyAsync(out, sel, sizeof(int32_t) * k, hipMemcpyDeviceToDevice, st));
   if (corners_out && nc <= cap)
     PFX_HIP(hipMemcpyAsync(corners_out, cxyz, sizeof(float) * 3 * nc, hipMemcpyDeviceToDevice, st));
+  if (corner_idx_out && nc <= cap)  // the corners' own cloud indices (PCL's output intensity is theirs)
+    PFX_HIP(hipMemcpyAsync(corner_idx_out, corner, sizeof(int32_t) * nc, hipMemcpyDeviceToDevice, st));
   return k;
 }
 
@@ -517,7 +519,7 @@ int64_t harris_finish_dev(pfx_ctx* ctx, int64_t n, double radius, float threshol
 
 int64_t harris3d_dev(pfx_ctx* ctx, const float* x, const float* y, const float* z, int64_t n, double radius,
                      float threshold, int refine, int32_t* out, int64_t cap, float* resp_out, float* corners_out,
-                     int64_t* n_corners) {
+                     int64_t* n_corners, int32_t* corner_idx_out) {
   PFX_CHECK(n >= 0, "harris3d: negative point count");
   PFX_CHECK(radius > 0.0, "harris3d: radius must be > 0");
   if (n_corners) *n_corners = 0;
@@ -543,12 +545,12 @@ int64_t harris3d_dev(pfx_ctx* ctx, const float* x, const float* y, const float* 
     check_launch("k_harris_response");
   }
   return harris_finish_dev(ctx, n, radius, threshold, refine, nx, ny, nz, resp, out, cap, corners_out, n_corners,
-                           "harris3d");
+                           "harris3d", corner_idx_out);
 }
 
 int64_t harris6d_dev(pfx_ctx* ctx, const float* x, const float* y, const float* z, const uint32_t* rgb, int64_t n,
                      double radius, float threshold, int refine, int32_t* out, int64_t cap, float* resp_out,
-                     float* corners_out, int64_t* n_corners, float* grad_out) {
+                     float* corners_out, int64_t* n_corners, float* grad_out, int32_t* corner_idx_out) {
   PFX_CHECK(n >= 0, "harris6d: negative point count");
   PFX_CHECK(radius > 0.0, "harris6d: radius must be > 0");
   if (n_corners) *n_corners = 0;
@@ -589,7 +591,7 @@ int64_t harris6d_dev(pfx_ctx* ctx, const float* x, const float* y, const float* 
     }
   }
   return harris_finish_dev(ctx, n, radius, threshold, refine, nx, ny, nz, resp, out, cap, corners_out, n_corners,
-                           "harris6d");
+                           "harris6d", corner_idx_out);
 }
 
 }  // namespace pfx

@@ -182,12 +182,12 @@ int64_t ransac_rejector(pfx_ctx* ctx, const float* sx, const float* sy, const fl
                         float* T_out, int64_t* iters_out);
 int64_t harris3d_dev(pfx_ctx* ctx, const float* x, const float* y, const float* z, int64_t n, double radius,
                      float threshold, int refine, int32_t* out, int64_t cap, float* resp_out, float* corners_out,
-                     int64_t* n_corners);
+                     int64_t* n_corners, int32_t* corner_idx_out = nullptr);
 // Harris6D (keypoints.h:164-176): rgb packed 0x00RRGGBB; grad_out (nullable, 3 n floats): the
 // normalised intensity gradients (x, y, z per point)
 int64_t harris6d_dev(pfx_ctx* ctx, const float* x, const float* y, const float* z, const uint32_t* rgb, int64_t n,
                      double radius, float threshold, int refine, int32_t* out, int64_t cap, float* resp_out,
-                     float* corners_out, int64_t* n_corners, float* grad_out);
+                     float* corners_out, int64_t* n_corners, float* grad_out, int32_t* corner_idx_out = nullptr);
 void fpfh_support_mask_dev(pfx_ctx* ctx, const float* sx, const float* sy, const float* sz, int64_t ns,
                            const float* qx, const float* qy, const float* qz, int64_t nq, double r, uint8_t* mask);
 void radius_search_dev(pfx_ctx* ctx, const float* x, const float* y, const float* z, int64_t n,

@@ -1,4 +1,5 @@
-// facade_driver.cpp -- the reference's NARF + Features flow written against include/pfx_pcl.hpp.
+// facade_driver.cpp -- the reference's NARF / ISS / Harris + Features flow written against
+// include/pfx_pcl.hpp.
 //
 // Mirrors, call for call, include/pcl_feature_extraction/keypoints.h:199-231 (NARF branch),
 // features.h:175-196 (Features<T>::compute with the FeatureFromNormals probe) and tools.h:22-32
@@ -7,7 +8,10 @@
 //   facade_driver <cloud.pcd> <out_dir> [<target.pcd>]
 //   -> keypoints.i32, normals.f32 (n x 4), fpfh.f32 (K x 33), shot.f32 (K x 352), shot_rf.f32 (K x 9)
 //   with a target cloud also: fpfh_target.f32 and corr.i32 (index_query, index_match pairs) of
-//   features.h:224-273 (findCorrespondences / getCorrespondences, verbatim below).
+//   features.h:224-273 (findCorrespondences / getCorrespondences, verbatim below), then
+//   features.h:282-297 (filterCorrespondences) -> filtered.i32, transformation.f32; and the
+//   Harris3D / Harris6D branches (keypoints.h:150-176 + getKeypointsCloud keypoints.h:365-395)
+//   -> harris{3,6}d_xyz.f32 (snapped cloud points), harris{3,6}d_corners.f32 (x, y, z, intensity).
 #include <cstdio>
 #include <cstring>
 #include <fstream>
@@ -190,6 +194,73 @@ static void iss_keypoints(const PointCloudRGB::Ptr& cloud, PointCloudRGB::Ptr& c
     detector.compute(*cloud_keypoints);
 }
 
+// keypoints.h:365-395, Keypoints::getKeypointsCloud (the reference's own helper), against the
+// facade's KdTreeFLANN<PointRGB>
+static void getKeypointsCloud(const PointCloudRGB::Ptr& cloud, const PointCloud<PointXYZI>::Ptr& keypoints,
+                              PointCloudRGB::Ptr& cloud_keypoints) {
+  cloud_keypoints.reset(new PointCloudRGB);
+  if (!cloud || !keypoints || cloud->points.empty() || keypoints->points.empty()) return;
+  KdTreeFLANN<PointRGB> kdtree;
+  kdtree.setInputCloud(cloud);
+  for (size_t i = 0; i < keypoints->size(); ++i) {
+    PointXYZI pt_tmp = keypoints->points[i];
+    PointRGB pt;
+    pt.x = pt_tmp.x;
+    pt.y = pt_tmp.y;
+    pt.z = pt_tmp.z;
+    if (!std::isfinite(pt.x) || !std::isfinite(pt.y) || !std::isfinite(pt.z)) continue;
+    std::vector<int> idx_vec;
+    std::vector<float> dist;
+    if (kdtree.nearestKSearch(pt, 1, idx_vec, dist) > 0) {
+      if (dist[0] < 0.0001) cloud_keypoints->points.push_back(cloud->points[idx_vec[0]]);
+    }
+  }
+}
+
+// keypoints.h:150-176, the HARRIS_3D and HARRIS_6D branches of Keypoints::compute
+static void harris_keypoints(const PointCloudRGB::Ptr& cloud, bool six, PointCloud<PointXYZI>::Ptr& keypoints,
+                             PointCloudRGB::Ptr& cloud_keypoints) {
+  keypoints.reset(new PointCloud<PointXYZI>);
+  if (!six) {
+    HarrisKeypoint3D<PointRGB, PointXYZI> harris3d;
+    harris3d.setNonMaxSupression(true);
+    harris3d.setInputCloud(cloud);
+    harris3d.setThreshold(1e-6);
+    harris3d.compute(*keypoints);
+  } else {
+    HarrisKeypoint6D<PointRGB, PointXYZI> harris6d;
+    harris6d.setNonMaxSupression(true);
+    harris6d.setInputCloud(cloud);
+    harris6d.setThreshold(1e-6);
+    harris6d.compute(*keypoints);
+  }
+  getKeypointsCloud(cloud, keypoints, cloud_keypoints);
+}
+
+// features.h:282-297, Features<T>::filterCorrespondences
+static void filterCorrespondences(const PointCloudRGB::Ptr source, const PointCloudRGB::Ptr target,
+                                  CorrespondencesPtr correspondences, CorrespondencesPtr& filtered_correspondences,
+                                  Eigen::Matrix4f& transformation) {
+  registration::CorrespondenceRejectorSampleConsensus<PointRGB> rejector;
+  rejector.setInputSource(source);
+  rejector.setInputTarget(target);
+  rejector.setInputCorrespondences(correspondences);
+  rejector.setInlierThreshold(0.015);
+  rejector.setMaximumIterations(1000);
+  rejector.getCorrespondences(*filtered_correspondences);
+  transformation = rejector.getBestTransformation();
+}
+
+static void dump_xyz(const std::string& path, const PointCloudRGB& c) {
+  std::vector<float> v;
+  for (const PointRGB& p : c.points) {
+    v.push_back(p.x);
+    v.push_back(p.y);
+    v.push_back(p.z);
+  }
+  dump(path, v.data(), v.size());
+}
+
 int main(int argc, char** argv) {
   if (argc < 3) {
     std::fprintf(stderr, "usage: %s cloud.pcd out_dir\n", argv[0]);
@@ -243,6 +314,23 @@ int main(int argc, char** argv) {
   dump(out + "/resolution.f64", &res, 1);
   std::printf("iss keypoints %zu\n", iss_kp->size());
 
+  // ---- keypoints.h:150-176 (Harris3D / Harris6D) + getKeypointsCloud ----
+  for (int six = 0; six < 2; ++six) {
+    PointCloud<PointXYZI>::Ptr hk;
+    PointCloudRGB::Ptr hkp;
+    harris_keypoints(cloud, six != 0, hk, hkp);
+    dump_xyz(out + (six ? "/harris6d_xyz.f32" : "/harris3d_xyz.f32"), *hkp);
+    std::vector<float> corners;
+    for (const PointXYZI& p : hk->points) {
+      corners.push_back(p.x);
+      corners.push_back(p.y);
+      corners.push_back(p.z);
+      corners.push_back(p.intensity);
+    }
+    dump(out + (six ? "/harris6d_corners.f32" : "/harris3d_corners.f32"), corners.data(), corners.size());
+    std::printf("harris%dd corners %zu keypoints %zu\n", six ? 6 : 3, hk->size(), hkp->size());
+  }
+
   // ---- evaluation.cpp:342 (feat.findCorrespondences) between this cloud and a target ----
   if (argc > 3) {
     PointCloudRGB::Ptr target(new PointCloudRGB);
@@ -266,6 +354,20 @@ int main(int argc, char** argv) {
     }
     dump(out + "/corr.i32", pairs.data(), pairs.size());
     std::printf("target keypoints %zu correspondences %zu\n", tdesc->size(), corr->size());
+    // ---- features.h:282-297 (filterCorrespondences) on the keypoint clouds ----
+    CorrespondencesPtr filtered(new Correspondences);
+    Eigen::Matrix4f T;
+    filterCorrespondences(cloud_keypoints, target_keypoints, corr, filtered, T);
+    std::vector<int32_t> kept;
+    for (const Correspondence& c : *filtered) {
+      kept.push_back(c.index_query);
+      kept.push_back(c.index_match);
+    }
+    dump(out + "/filtered.i32", kept.data(), kept.size());
+    dump(out + "/transformation.f32", T.m, 16);
+    dump_xyz(out + "/src_kp_xyz.f32", *cloud_keypoints);
+    dump_xyz(out + "/tgt_kp_xyz.f32", *target_keypoints);
+    std::printf("filtered correspondences %zu\n", filtered->size());
   }
   return 0;
 }

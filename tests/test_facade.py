@@ -71,3 +71,37 @@ def test_facade_matches_c_abi(ctx, tmp_path):
     okp, _ = O.iss_keypoints(x, y, z, 6 * ores, 4 * ores)
     ixyz = np.fromfile(tmp_path / "iss_xyz.f32", np.float32).reshape(-1, 3)
     assert len(okp) > 0 and np.array_equal(ixyz, np.stack([x[okp], y[okp], z[okp]], 1))
+
+    # keypoints.h:150-176 (Harris3D / Harris6D) + getKeypointsCloud through the facade
+    rgb = np.ascontiguousarray(c.fields["rgb"]).view(np.uint32)
+    for six in (False, True):
+        tag = "harris6d" if six else "harris3d"
+        if six:
+            hk, resp, cor, _ = ctx.harris6d_keypoints(x, y, z, rgb, details=True)
+        else:
+            hk, resp, cor = ctx.harris3d_keypoints(x, y, z, details=True)
+        hxyz = np.fromfile(tmp_path / f"{tag}_xyz.f32", np.float32).reshape(-1, 3)
+        assert len(hk) > 0 and np.array_equal(hxyz, np.stack([x[hk], y[hk], z[hk]], 1))
+        hc = np.fromfile(tmp_path / f"{tag}_corners.f32", np.float32).reshape(-1, 4)
+        assert np.array_equal(hc[:, :3].view(np.uint32), cor.view(np.uint32))
+        # PCL's output intensity: the response of each corner's own point (refine=False: the
+        # corners are those points)
+        if six:
+            _, _, c0, _ = ctx.harris6d_keypoints(x, y, z, rgb, refine=False, details=True)
+        else:
+            _, _, c0 = ctx.harris3d_keypoints(x, y, z, refine=False, details=True)
+        rb = resp.view(np.uint32)
+        by_xyz = {}
+        for i, p in enumerate(np.stack([x, y, z], 1).tolist()):
+            by_xyz.setdefault(tuple(p), set()).add(int(rb[i]))  # duplicates: any of their responses
+        assert len(c0) == len(hc)
+        assert all(int(b) in by_xyz[tuple(p)] for p, b in zip(c0.tolist(), hc[:, 3].view(np.uint32)))
+
+    # features.h:282-297 (filterCorrespondences) through the facade
+    sk = np.fromfile(tmp_path / "src_kp_xyz.f32", np.float32).reshape(-1, 3)
+    tk = np.fromfile(tmp_path / "tgt_kp_xyz.f32", np.float32).reshape(-1, 3)
+    keep, T = ctx.ransac_rejector(sk, tk, q, m)
+    filt = np.fromfile(tmp_path / "filtered.i32", np.int32).reshape(-1, 2)
+    assert np.array_equal(filt, np.stack([q[keep], m[keep]], 1))
+    Tf = np.fromfile(tmp_path / "transformation.f32", np.float32).reshape(4, 4)
+    assert np.array_equal(Tf.view(np.uint32), np.asarray(T, np.float32).view(np.uint32))
