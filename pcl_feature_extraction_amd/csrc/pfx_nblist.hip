@@ -22,18 +22,43 @@ namespace pfx {
 namespace {
 
 constexpr int kQ = 16;  // tile: consecutive queries of one cell
-constexpr int kArena = 4096;    // list entries per arena reservation of a tile workgroup
+constexpr int kArena = 16384;   // list entries per arena reservation of a tile workgroup (> a typical tile)
 constexpr int kArenaQuery = 16384;  // ... of a per-query workgroup (lists of 1k-4k entries)
 constexpr int kTcapSmall = 384, kTcapSparse = 1280, kTcapDense = 8000;
 constexpr int kCapQuery = 4096, kBucketsQuery = 1024;
 constexpr int kCapHuge = 1 << 18, kBucketsHuge = 4096, kHugeBlocks = 32;
 
-// tile descriptor: first query index (28 bits) | (tile size - 1) << 28
-__device__ __forceinline__ uint32_t tile_pack(int32_t start, int qn) {
-  return (uint32_t)start | ((uint32_t)(qn - 1) << 28);
+// Tile record (written by k_tile_class, one per tile, in class order): the 9 candidate runs of
+// the tile's 3x3x3 block, its first query (index into qpos) and query count.  A workgroup loads
+// the record of its next tile one lane per word while it works on the current one and unpacks it
+// with readlane into SGPRs, so a tile starts with no dependent global loads (the old chain
+// tiles -> qpos -> skeys -> cell_start was four serial latencies per tile).
+constexpr int kRecInts = 24;
+constexpr int kRecQ0 = 19, kRecQn = 20;
+
+__device__ __forceinline__ void rec_write(int32_t* __restrict__ rec, const Runs& R, int32_t q0, int qn) {
+#pragma unroll
+  for (int r = 0; r < 9; ++r) rec[r] = R.start[r];
+#pragma unroll
+  for (int r = 0; r < 10; ++r) rec[9 + r] = R.pref[r];
+  rec[kRecQ0] = q0;
+  rec[kRecQn] = qn;
 }
-__device__ __forceinline__ int32_t tile_start(uint32_t e) { return (int32_t)(e & 0x0fffffffu); }
-__device__ __forceinline__ int tile_qn(uint32_t e) { return (int)(e >> 28) + 1; }
+
+// lane l < kRecInts of the calling wave loads word l of record i (0 when !ok)
+__device__ __forceinline__ int rec_load(const int32_t* __restrict__ rec_base, int rec_step, int i, bool ok) {
+  const int lane = threadIdx.x & 63;
+  return (ok && lane < kRecInts) ? rec_base[(int64_t)i * rec_step + lane] : 0;
+}
+
+__device__ __forceinline__ void rec_unpack(int v, Runs& R, int32_t& q0, int& qn) {
+#pragma unroll
+  for (int r = 0; r < 9; ++r) R.start[r] = __builtin_amdgcn_readlane(v, r);
+#pragma unroll
+  for (int r = 0; r < 10; ++r) R.pref[r] = __builtin_amdgcn_readlane(v, 9 + r);
+  q0 = __builtin_amdgcn_readlane(v, kRecQ0);
+  qn = __builtin_amdgcn_readlane(v, kRecQn);
+}
 
 __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -66,26 +91,27 @@ __global__ void k_tile_flags(const int32_t* __restrict__ seg, const int64_t* __r
   flags[j] = (j < *nq_ptr) && ((j - seg[j]) % kQ == 0);
 }
 
-// candidate-block class of a tile: sparse, dense, or every query to the per-query path
-// (list slots reserved with one atomic per wave and class)
+// candidate-block class of a tile: small, sparse, dense, or every query to the per-query path.
+// The tile's record goes to its class's region of `recs` (slots reserved with one atomic per
+// wave and class): small at [0, n), sparse at [n, 2n) upward, dense at [n, 2n) downward from
+// 2n - 1 (sparse + dense <= tiles <= n, so the two never meet).
 __global__ void __launch_bounds__(256) k_tile_class(GridView g, const int32_t* __restrict__ qpos,
                                                     const uint32_t* __restrict__ skeys,
                                                     const int64_t* __restrict__ nq_ptr,
                                                     const int32_t* __restrict__ tiles,
                                                     const int64_t* __restrict__ ntiles_ptr,
-                                                    uint32_t* __restrict__ sparse, uint32_t* __restrict__ dense,
-                                                    uint32_t* __restrict__ small, int32_t* __restrict__ single,
-                                                    int* __restrict__ counts) {
+                                                    int32_t* __restrict__ recs, int64_t n,
+                                                    int32_t* __restrict__ single, int* __restrict__ counts) {
   const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   const int64_t ntiles = *ntiles_ptr;
   const int lane = threadIdx.x & 63;
   int cls = -1, qn = 0;
   int32_t start = 0;
+  Runs R;
   if (t < ntiles) {
     start = tiles[t];
     const int64_t next = (t + 1 < ntiles) ? tiles[t + 1] : *nq_ptr;  // tiles never span cells
     qn = (int)(next - start < kQ ? next - start : kQ);
-    Runs R;
     const int T = block_runs(g, skeys[qpos[start]], R);
     // 3: small tiles (<= kTcapSmall candidates, so no list can exceed them: a low-LDS kernel
     // with more workgroups per CU), 0: sparse, 1: dense, 2: per query
@@ -100,7 +126,11 @@ __global__ void __launch_bounds__(256) k_tile_class(GridView g, const int32_t* _
     const int ci = c == 3 ? 10 : c;
     if (lane == __builtin_ctzll(m)) base = atomicAdd(&counts[ci], __popcll(m));
     base = __shfl(base, __builtin_ctzll(m));
-    if (cls == c) (c == 3 ? small : (c ? dense : sparse))[base + __popcll(m & lanemask_lt())] = tile_pack(start, qn);
+    if (cls == c) {
+      const int64_t slot = base + __popcll(m & lanemask_lt());
+      const int64_t at = c == 3 ? slot : (c == 0 ? n + slot : 2 * n - 1 - slot);
+      rec_write(recs + at * kRecInts, R, start, qn);
+    }
   }
   int v = cls == 2 ? qn : 0, inc = v;
 #pragma unroll
@@ -336,8 +366,9 @@ __device__ __forceinline__ void wave_sort(uint16_t* L, int k, float qx, float qy
   TPROF_ADD(11, w3, w4);
 }
 
-// k <= 64: one entry per lane, rank = entries with a smaller (d2, caller index) key, counted
-// over register shuffles (no buckets, no LDS scan)
+// k <= 64: one entry per lane, rank = entries with a smaller d2, counted over v_readlane (no
+// LDS); only when two entries of the list share a d2 (rare) are the caller indices loaded and
+// the (d2, caller index) keys compared
 template <class Cand>
 __device__ __forceinline__ void wave_rank_sort(uint16_t* L, int k, float qx, float qy, float qz, const Cand& cand,
                                                const GridView& g, const Runs& R, int lane) {
@@ -346,12 +377,20 @@ __device__ __forceinline__ void wave_rank_sort(uint16_t* L, int k, float qx, flo
   float px, py, pz;
   cand.get(t, px, py, pz);
   const uint32_t d = in ? __float_as_uint(flann_d2(qx, qy, qz, px, py, pz)) : 0xffffffffu;
-  const int32_t id = in ? g.perm[run_pos(R, t)] : 0x7fffffff;
-  int rank = 0;
+  int rank = 0, eq = 0;
   for (int m = 0; m < k; ++m) {
-    const uint32_t dm = (uint32_t)__shfl((int)d, m);
-    const int32_t im = __shfl(id, m);
-    rank += (dm < d || (dm == d && im < id)) ? 1 : 0;
+    const uint32_t dm = (uint32_t)__builtin_amdgcn_readlane((int)d, m);
+    rank += dm < d ? 1 : 0;
+    eq += dm == d ? 1 : 0;
+  }
+  if (__builtin_amdgcn_ballot_w64(in && eq > 1)) {
+    const int32_t id = in ? g.perm[run_pos(R, t)] : 0x7fffffff;
+    rank = 0;
+    for (int m = 0; m < k; ++m) {
+      const uint32_t dm = (uint32_t)__builtin_amdgcn_readlane((int)d, m);
+      const int32_t im = __builtin_amdgcn_readlane(id, m);
+      rank += (dm < d || (dm == d && im < id)) ? 1 : 0;
+    }
   }
   wave_sync();
   if (in) L[rank] = (uint16_t)t;
@@ -371,62 +410,106 @@ __device__ __forceinline__ void sort_list(uint16_t* L, int k, float qx, float qy
   else wave_sort<NB>(L, k, qx, qy, qz, cand, bscale, Sd, St, bcount, bpos, g, R, lane);
 }
 
-// STAGE: candidates staged in LDS (sparse tiles); otherwise read from L2 (dense tiles, where
-// staging 8000 candidates would cap the kernel at one workgroup per CU)
+// STAGE: candidates staged in LDS (small and sparse tiles); otherwise read from L2 (dense tiles,
+// where staging 8000 candidates would cap the kernel at one workgroup per CU).
+// Software pipeline, per tile i (its record unpacked into SGPRs, its candidates and query
+// positions already in LDS):
+//   [A] load the record of tile i+1 (one lane per word)   [B] test -> barrier
+//   [C] sort, one list per wave at a time -> barrier
+//   [D] unpack record i+1; issue its candidate + query-position loads into registers; write the
+//       lists of tile i to HBM; store the registers to LDS -> barrier
+// so the one global-latency round of a tile (staging loads, list stores) is shared.  Tiles come
+// from a dynamic queue `chunk` at a time; thread 0 keeps the next chunk's base fetched one chunk
+// ahead and publishes it in [D].
+template <int TCAP, bool STAGE>
+struct Stager {
+  static constexpr int PT = STAGE ? (TCAP + 255) / 256 : 0;
+  float x[PT > 0 ? PT : 1], y[PT > 0 ? PT : 1], z[PT > 0 ? PT : 1];
+  int32_t qp;
+  __device__ __forceinline__ void load(const GridView& g, const int32_t* __restrict__ qpos, const Runs& R,
+                                       int32_t start, int qn, bool ok) {
+    // branch-free: every load is issued (clamped index, one address computation), so all of
+    // them are in flight at once
+    const int tid = threadIdx.x;
+    const int T = ok ? R.pref[9] : 0;
+#pragma unroll
+    for (int u = 0; u < PT; ++u) {
+      const int tc = max(0, min(tid + 256 * u, T - 1));
+      const float4 c = g.sp[run_pos(R, tc)];
+      x[u] = c.x; y[u] = c.y; z[u] = c.z;
+    }
+    qp = qpos[start + (tid < qn ? tid : 0)];
+  }
+  // unconditional (slots >= T get don't-care values; the arrays hold PT * 256): a conditional
+  // store lets the compiler sink each load into its own branch and wait for it there
+  __device__ __forceinline__ void store(float* cx, float* cy, float* cz, int32_t* s_qp, int qn) const {
+    const int tid = threadIdx.x;
+#pragma unroll
+    for (int u = 0; u < PT; ++u) {
+      const int t = tid + 256 * u;
+      cx[t] = x[u]; cy[t] = y[u]; cz[t] = z[u];
+    }
+    if (tid < qn) s_qp[tid] = qp;
+  }
+};
+
 template <int LCAP, int NB, int TCAP, bool STAGE>
 __global__ void __launch_bounds__(256, TCAP <= kTcapSmall ? 4 : (STAGE ? 3 : 2)) k_nb_tile(GridView g, const int32_t* __restrict__ qpos,
-                                                 const uint32_t* __restrict__ skeys,
-                                                 const uint32_t* __restrict__ tiles, const int* __restrict__ ntiles_ptr,
+                                                 const int32_t* __restrict__ rec_base, int rec_step,
+                                                 const int* __restrict__ ntiles_ptr,
                                                  float rr, float bscale, int sorted, ListOut out,
                                                  int32_t* __restrict__ single, int* __restrict__ n_single,
                                                  int* __restrict__ next_tile, int chunk) {
   constexpr int Q = kQ, QW = Q / 4;  // queries per tile / per wave
-  __shared__ float cx[STAGE ? TCAP : 1], cy[STAGE ? TCAP : 1], cz[STAGE ? TCAP : 1];
+  constexpr int U = 2;               // candidates per lane in flight in the test loop
+  constexpr int SCAP = STAGE ? Stager<TCAP, STAGE>::PT * 256 : 1;
+  __shared__ float cx[SCAP], cy[SCAP], cz[SCAP];
   __shared__ uint16_t lists[Q][LCAP + 2];  // +2: odd dword row stride (no bank conflicts)
   __shared__ uint32_t sd[4][LCAP];
   __shared__ uint16_t stt[4][LCAP];
   __shared__ int bcount[4][NB], bpos[4][NB];
   __shared__ int s_k[Q];
+  __shared__ int32_t s_qp[Q];
   __shared__ unsigned long long s_base;
+  __shared__ int s_chunk;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  __shared__ int s_tile;
   const int ntiles = *ntiles_ptr;
-  // dynamic tile queue: tile costs vary by orders of magnitude with the local density.  Tiles
-  // are fetched kTileChunk at a time and the neighbour total is added once per workgroup: one
-  // queue atomic per tile made the counter's address the bottleneck when tiles are cheap (small
-  // radii); `chunk` tiles per fetch
   unsigned long long wg_total = 0, arena_base = 0, arena_left = 0;  // thread 0's
-  int64_t tile = 0, tile_end = 0;
-  for (;; ++tile) {
-    if (tile == tile_end) {
-      if (tid == 0) s_tile = atomicAdd(next_tile, chunk);
-      __syncthreads();
-      tile = s_tile;
-      tile_end = tile + chunk;
-      __syncthreads();  // every thread holds `tile` before thread 0 may fetch the next chunk
+  int next_chunk = 0;                                                // thread 0's
+  if (tid == 0) {
+    s_chunk = atomicAdd(next_tile, chunk);
+    next_chunk = atomicAdd(next_tile, chunk);
+  }
+  __syncthreads();
+  int i = __builtin_amdgcn_readfirstlane(s_chunk), i_end = i + chunk;
+  Runs R;
+  int32_t start = 0;
+  int qn = 0;
+  {
+    const int v = rec_load(rec_base, rec_step, i, i < ntiles);
+    rec_unpack(v, R, start, qn);
+    Stager<TCAP, STAGE> sg;
+    sg.load(g, qpos, R, start, qn, R.pref[9] <= TCAP);
+    __syncthreads();  // s_chunk read by every thread before it is republished
+    if (i + 1 == i_end && tid == 0) {
+      s_chunk = next_chunk;
+      next_chunk = atomicAdd(next_tile, chunk);
     }
-    if (tile >= ntiles) break;
-    TPROF_T(p0);
-    const uint32_t te = tiles[tile];
-    const int32_t start = tile_start(te);
-    const int qn = tile_qn(te);
-    Runs R;
-    const int T = block_runs(g, skeys[qpos[start]], R);
-    if (T > TCAP) {  // cannot happen after k_tile_class; keep the kernel safe regardless
-      if (tid < qn) single[atomicAdd(n_single, 1)] = start + tid;
-      continue;
-    }
-    if (STAGE) {
-      for (int t = tid; t < T; t += 256) {
-        const int32_t pos = run_pos(R, t);
-        cx[t] = g.sx[pos];
-        cy[t] = g.sy[pos];
-        cz[t] = g.sz[pos];
-      }
-    }
+    sg.store(cx, cy, cz, s_qp, qn);
     __syncthreads();
-    TPROF_T(p1);
-    TPROF_ADD(STAGE ? 0 : 4, p0, p1);
+  }
+  while (i < ntiles) {
+    TPROF_T(p0);
+    const int T = R.pref[9];
+    const bool ok = T <= TCAP;  // always true after k_tile_class; keep the kernel safe regardless
+    // [A] the next tile and its record
+    int ni = i + 1;
+    if (ni == i_end) {
+      ni = __builtin_amdgcn_readfirstlane(s_chunk);
+      i_end = ni + chunk;
+    }
+    const int recv = rec_load(rec_base, rec_step, ni, ni < ntiles);
+    // [B] test
     float qx[QW], qy[QW], qz[QW];
     int cursor[QW];
 #pragma unroll
@@ -435,32 +518,46 @@ __global__ void __launch_bounds__(256, TCAP <= kTcapSmall ? 4 : (STAGE ? 3 : 2))
       cursor[u] = 0;
       qx[u] = qy[u] = qz[u] = 0.f;
       if (j < qn) {
-        const float4 c = g.sp[qpos[start + j]];
-        qx[u] = c.x; qy[u] = c.y; qz[u] = c.z;
+        const int32_t p = s_qp[j];
+        if (STAGE) {  // a query lies in its own cell, i.e. in run 4 of its block
+          const int t = R.pref[4] + (p - R.start[4]);
+          qx[u] = cx[t]; qy[u] = cy[t]; qz[u] = cz[t];
+        } else {
+          const float4 c = g.sp[p];
+          qx[u] = c.x; qy[u] = c.y; qz[u] = c.z;
+        }
       }
     }
-    for (int t0 = 0; t0 < T; t0 += 64) {
-      const int t = t0 + lane;
-      const bool in = t < T;
-      float px = 0.f, py = 0.f, pz = 0.f;
-      if (in) {
-        if (STAGE) {
-          px = cx[t]; py = cy[t]; pz = cz[t];
-        } else {
-          const float4 c = g.sp[run_pos(R, t)];
-          px = c.x; py = c.y; pz = c.z;
+    for (int t0 = 0; ok && t0 < T; t0 += 64 * U) {
+      float px[U], py[U], pz[U];
+#pragma unroll
+      for (int v = 0; v < U; ++v) {
+        const int t = t0 + 64 * v + lane;
+        px[v] = py[v] = pz[v] = 0.f;
+        if (t < T) {
+          if (STAGE) {
+            px[v] = cx[t]; py[v] = cy[t]; pz[v] = cz[t];
+          } else {
+            const float4 c = g.sp[run_pos(R, t)];
+            px[v] = c.x; py[v] = c.y; pz[v] = c.z;
+          }
         }
       }
 #pragma unroll
-      for (int u = 0; u < QW; ++u) {
-        const int j = wv + 4 * u;
-        const bool hit = in && j < qn && flann_d2(qx[u], qy[u], qz[u], px, py, pz) < rr;
-        const uint64_t m = __ballot(hit);
-        if (hit) {
-          const int slot = cursor[u] + __popcll(m & lanemask_lt());
-          if (slot < LCAP) lists[j][slot] = (uint16_t)t;
+      for (int v = 0; v < U; ++v) {
+        const int t = t0 + 64 * v + lane;
+        const bool in = t < T;
+#pragma unroll
+        for (int u = 0; u < QW; ++u) {
+          const int j = wv + 4 * u;
+          const bool hit = in && j < qn && flann_d2(qx[u], qy[u], qz[u], px[v], py[v], pz[v]) < rr;
+          const uint64_t m = __ballot(hit);
+          if (hit) {
+            const int slot = cursor[u] + __popcll(m & lanemask_lt());
+            if (slot < LCAP) lists[j][slot] = (uint16_t)t;
+          }
+          cursor[u] += __popcll(m);
         }
-        cursor[u] += __popcll(m);
       }
     }
     // tile layout in HBM: the lists of the tile's qn queries interleaved with stride 2^lg >= qn
@@ -468,11 +565,12 @@ __global__ void __launch_bounds__(256, TCAP <= kTcapSmall ? 4 : (STAGE ? 3 : 2))
     if (lane == 0) {
 #pragma unroll
       for (int u = 0; u < QW; ++u)
-        if (wv + 4 * u < qn) s_k[wv + 4 * u] = cursor[u];
+        if (wv + 4 * u < qn) s_k[wv + 4 * u] = ok ? cursor[u] : LCAP + 1;
     }
     __syncthreads();
-    TPROF_T(p2);
-    TPROF_ADD(STAGE ? 1 : 5, p1, p2);
+    TPROF_T(p1);
+    TPROF_ADD(STAGE ? 1 : 5, p0, p1);
+    // [C] list slots, sort
     int lg = 0;
     while ((1 << lg) < qn) ++lg;
     int maxk = 0;
@@ -480,20 +578,8 @@ __global__ void __launch_bounds__(256, TCAP <= kTcapSmall ? 4 : (STAGE ? 3 : 2))
       const int k = s_k[j];
       maxk = (k <= LCAP && k > maxk) ? k : maxk;
     }
-    if (tid == 0) {
-      // list slots come from a per-workgroup arena reserved kArena entries at a time (one
-      // cursor atomic per arena, not per tile); unused arena tails are never read
-      const unsigned long long need = (unsigned long long)maxk << lg;
-      if (need > arena_left) {
-        const unsigned long long res = need > (unsigned long long)kArena ? need : (unsigned long long)kArena;
-        arena_base = atomicAdd(out.cursor, res);
-        arena_left = res;
-      }
-      s_base = arena_base;
-      arena_base += need;
-      arena_left -= need;
+    if (tid == 0)
       for (int j = 0; j < qn; ++j) wg_total += s_k[j] <= LCAP ? (unsigned long long)s_k[j] : 0ull;
-    }
     if (tid < qn) {
       const int k = s_k[tid];
       if (k > LCAP) {
@@ -508,7 +594,7 @@ __global__ void __launch_bounds__(256, TCAP <= kTcapSmall ? 4 : (STAGE ? 3 : 2))
       for (int u = 0; u < QW; ++u) {
         const int j = wv + 4 * u;
         const int k = cursor[u];
-        if (j < qn && k <= LCAP && k > 1) {  // wave-uniform
+        if (ok && j < qn && k <= LCAP && k > 1) {  // wave-uniform
           if (STAGE) {
             const CandLds cand{cx, cy, cz};
             sort_list<NB, CandLds, (TCAP <= kTcapSmall)>(lists[j], k, qx[u], qy[u], qz[u], cand, bscale, sd[wv],
@@ -522,8 +608,37 @@ __global__ void __launch_bounds__(256, TCAP <= kTcapSmall ? 4 : (STAGE ? 3 : 2))
       }
     }
     __syncthreads();
-    TPROF_T(p3);
-    TPROF_ADD(STAGE ? 2 : 6, p2, p3);
+    TPROF_T(p2);
+    TPROF_ADD(STAGE ? 2 : 6, p1, p2);
+    // [D] one latency round: the next tile's staging loads, the list-slot reservation and the
+    // queue fetch; their results land in LDS, then this tile's lists are written (stores in
+    // flight until the next tile's round)
+    Runs Rn;
+    int32_t start_n;
+    int qn_n;
+    rec_unpack(recv, Rn, start_n, qn_n);
+    const bool ok_n = ni < ntiles && Rn.pref[9] <= TCAP;
+    Stager<TCAP, STAGE> sg;
+    if (ni < ntiles) sg.load(g, qpos, Rn, start_n, qn_n, ok_n);
+    if (tid == 0) {
+      if (ni + 1 == i_end) {  // publish the next chunk (fetched one chunk ago), fetch the one after
+        s_chunk = next_chunk;
+        next_chunk = atomicAdd(next_tile, chunk);
+      }
+      // list slots come from a per-workgroup arena reserved kArena entries at a time (one
+      // cursor atomic per arena, not per tile); unused arena tails are never read
+      const unsigned long long need = (unsigned long long)maxk << lg;
+      if (need > arena_left) {
+        const unsigned long long res = need > (unsigned long long)kArena ? need : (unsigned long long)kArena;
+        arena_base = atomicAdd(out.cursor, res);
+        arena_left = res;
+      }
+      s_base = arena_base;
+      arena_base += need;
+      arena_left -= need;
+    }
+    if (ni < ntiles) sg.store(cx, cy, cz, s_qp, qn_n);
+    __syncthreads();
     const int64_t base = (int64_t)s_base;
     if (tid < qn && s_k[tid] <= LCAP) out.off[start + tid] = base + tid;
     // coalesced write of the interleaved block (padding slots are left unwritten)
@@ -537,9 +652,13 @@ __global__ void __launch_bounds__(256, TCAP <= kTcapSmall ? 4 : (STAGE ? 3 : 2))
         }
       }
     }
-    __syncthreads();  // LDS is reused by the next tile
-    TPROF_T(p4);
-    TPROF_ADD(STAGE ? 3 : 7, p3, p4);
+    __syncthreads();  // lists and s_k read before the next tile's test overwrites them
+    TPROF_T(p3);
+    TPROF_ADD(STAGE ? 3 : 7, p2, p3);
+    i = ni;
+    R = Rn;
+    start = start_n;
+    qn = qn_n;
   }
   if (tid == 0 && wg_total) atomicAdd(out.cursor + 1, wg_total);
 }
@@ -769,9 +888,8 @@ void build_lists(pfx_ctx* ctx, const Grid& G, const uint8_t* mask, double radius
   int32_t* seg = B("seg").as<int32_t>(n);
   int32_t* tiles = B("tiles").as<int32_t>(n);
   int64_t* d_ntiles = B("ntiles").as<int64_t>(1);
-  uint32_t* sparse = B("sparse").as<uint32_t>(n);
-  uint32_t* dense = B("dense").as<uint32_t>(n);
-  uint32_t* small = B("small").as<uint32_t>(n);
+  // tile records: small at [0, n), sparse at [n, 2n) upward, dense at [n, 2n) downward
+  int32_t* recs = B("recs").as<int32_t>((size_t)2 * n * kRecInts);
   int32_t* single = B("single").as<int32_t>(n);
   int32_t* huge = B("huge").as<int32_t>(n);
   int64_t* off = B("off").as<int64_t>(n);
@@ -805,8 +923,7 @@ void build_lists(pfx_ctx* ctx, const Grid& G, const uint8_t* mask, double radius
     PFX_HIP(rocprim::inclusive_scan(tmp, t2, seg, seg, (size_t)n, rocprim::maximum<int32_t>(), st));
     k_tile_flags<<<nb, 256, 0, st>>>(seg, d_nq, flags, n);
     PFX_HIP(rocprim::select(tmp, t3, rocprim::counting_iterator<int32_t>(0), flags, tiles, d_ntiles, (size_t)n, st));
-    k_tile_class<<<nb, 256, 0, st>>>(g, qpos, G.skeys, d_nq, tiles, d_ntiles, sparse, dense, small, single,
-                                     counters);
+    k_tile_class<<<nb, 256, 0, st>>>(g, qpos, G.skeys, d_nq, tiles, d_ntiles, recs, n, single, counters);
     check_launch("nblist tiles");
     PFX_HIP(hipMemcpyAsync(counters + 6, counters + 2, sizeof(int), hipMemcpyDeviceToDevice, st));
   }
@@ -834,18 +951,18 @@ void build_lists(pfx_ctx* ctx, const Grid& G, const uint8_t* mask, double radius
       {
         TimeScope t0(ctx, std::string(tag) + "_lists_small");
         k_nb_tile<kTcapSmall, 64, kTcapSmall, true><<<256 * 4 * 2, 256, 0, st>>>(
-            g, qpos, G.skeys, small, counters + 10, rr, 64.0f / rr, isort, lo, single, counters + 2, counters + 11,
+            g, qpos, recs, kRecInts, counters + 10, rr, 64.0f / rr, isort, lo, single, counters + 2, counters + 11,
             chunk);
       }
       {
         TimeScope t1(ctx, std::string(tag) + "_lists_sparse");
         k_nb_tile<512, 256, kTcapSparse, true><<<256 * 3 * 4, 256, 0, st>>>(
-            g, qpos, G.skeys, sparse, counters + 0, rr, 256.0f / rr, isort, lo, single, counters + 2, counters + 5, chunk);
+            g, qpos, recs + (size_t)n * kRecInts, kRecInts, counters + 0, rr, 256.0f / rr, isort, lo, single, counters + 2, counters + 5, chunk);
       }
       {
         TimeScope t2(ctx, std::string(tag) + "_lists_dense");
         k_nb_tile<1024, 256, kTcapDense, false><<<256 * 2 * 4, 256, 0, st>>>(
-            g, qpos, G.skeys, dense, counters + 1, rr, 256.0f / rr, isort, lo, single, counters + 2, counters + 7, chunk);
+            g, qpos, recs + (size_t)(2 * n - 1) * kRecInts, -kRecInts, counters + 1, rr, 256.0f / rr, isort, lo, single, counters + 2, counters + 7, chunk);
       }
       {
         TimeScope t3(ctx, std::string(tag) + "_lists_query");
