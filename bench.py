@@ -23,6 +23,10 @@ branch, keypoints.h:177-189): one step = cloud resolution + ISSKeypoint3D over t
 room: normals (r 0.01) + response + suppression + corner refinement + snap.
 `--workload harris6d`: F3's Harris6D branch (keypoints.h:164-176) over the same room with a
 procedural colour texture: normals + intensity gradients + 6x6 response + the Harris3D tail.
+`--workload config1`: configs[1], the 100k-point room (seed 1), NormalEstimation (r 0.05) + FPFH
+(r 0.05) at EVERY point (input == surface: PCL's all-points SPFH branch).
+`--workload dense`: SURVEY 8(d)'s "dense" data point, the configs[2] pass on the same room scene
+at 10x the point density (10M points, k(0.05) ~ 2,400).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--workload fpfh|shot|...] [--scans S]
                     [--no-cpu-baseline] [--no-e2e]
@@ -41,6 +45,7 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 BF16_PEAK_TFLOPS = 2500.0  # dense bf16 MFMA (MI355X_MICROARCH.md: ~2.5 PF dense)
 N_POINTS = 1_000_000
+DENSE_POINTS = 10_000_000  # SURVEY 8(d) dense variant: configs[2]'s scene at 10x density
 SHOT_SAMPLE = 10_000
 
 VERBOSE_TIMERS = ["grid_bbox", "grid_build", "normals", "normals_lists_phase", "normals_tiles", "normals_lists",
@@ -150,7 +155,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", choices=["fpfh", "shot", "match", "iss", "harris", "harris6d"], default="fpfh")
+    ap.add_argument("--workload", choices=["fpfh", "shot", "match", "iss", "harris", "harris6d", "config1", "dense"],
+                    default="fpfh")
     ap.add_argument("--scans", type=int, default=0,
                     help="fpfh workload: scans per step (default 1 = configs[2] at --gpus 1, 8 = configs[4] at N > 1)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -185,6 +191,8 @@ def main():
             return bench_iss(args, torch, dev, world, rank, local)
         if args.workload in ("harris", "harris6d"):
             return bench_harris(args, torch, dev, world, rank, local, six=args.workload == "harris6d")
+        if args.workload == "config1":
+            return bench_config1(args, torch, dev, world, rank, local)
         return bench_scans(args, torch, dist, dev, world, rank, local)
     finally:
         if world > 1:
@@ -225,9 +233,11 @@ def bench_scans(args, torch, dist, dev, world, rank, local):
     from pcl_feature_extraction_amd.dist import gather_to_root, in_scan_order, owned_scans
     from pcl_feature_extraction_amd.pipeline import (OverlappedNarfFpfh, alloc, alloc_shot, keypoint_rows,
                                                      narf_shot)
-    from pcl_feature_extraction_amd.synth import synth_room, synth_seabed
+    from pcl_feature_extraction_amd.synth import ROOM_SCALE, synth_room, synth_seabed
 
     shot = args.workload == "shot"
+    dense = args.workload == "dense"
+    npts = DENSE_POINTS if dense else N_POINTS
     if shot:
         n_scans, seeds = world, [3] if world == 1 else [300 + r for r in range(world)]
     else:
@@ -241,8 +251,11 @@ def bench_scans(args, torch, dist, dev, world, rank, local):
     run_fpfh = OverlappedNarfFpfh(torch, ctx, ctx_n, dev)
     scans, host = [], []
     for s in mine:
-        x, y, z, _ = (synth_seabed if shot else synth_room)(N_POINTS, seeds[s])
-        b = alloc(torch, N_POINTS, dev)
+        if dense:  # the configs[2] scene (same scale s) at 10x the density
+            x, y, z, _ = synth_room(npts, seeds[s], scale=ROOM_SCALE * (N_POINTS / npts) ** 0.5)
+        else:
+            x, y, z, _ = (synth_seabed if shot else synth_room)(npts, seeds[s])
+        b = alloc(torch, npts, dev)
         for t, a in zip((b.x, b.y, b.z), (x, y, z)):
             t.copy_(torch.from_numpy(a))
         scans.append(b)
@@ -259,7 +272,7 @@ def bench_scans(args, torch, dist, dev, world, rank, local):
             return sb.desc[:rows], None
         kp, k = run_fpfh(b)
         state["kp"] = kp
-        idx = torch.from_numpy(keypoint_rows(kp, N_POINTS).astype(np.int32)).to(dev, non_blocking=True)
+        idx = torch.from_numpy(keypoint_rows(kp, npts).astype(np.int32)).to(dev, non_blocking=True)
         return b.desc[:k], idx
 
     def step():
@@ -340,7 +353,7 @@ def bench_scans(args, torch, dist, dev, world, rank, local):
                 gather_to_root(torch, dist, blocks, 33, dev, per_rank_max)
         step_e2e()
         e_el = timed(torch, dist, dev, world, args.steps, step_e2e)
-        e2e = {"value": round(n_scans * N_POINTS * args.steps / e_el / 1e6, 4), "unit": "Mpoints/s",
+        e2e = {"value": round(n_scans * npts * args.steps / e_el / 1e6, 4), "unit": "Mpoints/s",
                "ms_per_step": round(e_el / args.steps * 1e3, 4),
                "note": ("host-pointer semantics: per scan 12 MB xyz H2D from pinned memory + K x 33 descriptors and "
                         "K indices D2H inside the timed step (SURVEY 8(d) definition); `value` is the same step with "
@@ -360,7 +373,7 @@ def bench_scans(args, torch, dist, dev, world, rank, local):
         ctx_n.set_timing(False)
 
     if rank == 0:
-        line = scans_line(args, world, n_scans, mine, shot, elapsed, timers, iso, nb_scan, long_scan, stat)
+        line = scans_line(args, world, n_scans, mine, shot, elapsed, timers, iso, nb_scan, long_scan, stat, npts)
         line["config"]["descriptor_rows"] = state["rows"]
         if batch is not None:
             line["config"]["gathered_on_rank0"] = batch
@@ -368,14 +381,17 @@ def bench_scans(args, torch, dist, dev, world, rank, local):
             line["config"]["backend"] = dist.get_backend()
         line["end_to_end_h2d_d2h"] = e2e
         cpu = None
-        if world == 1 and not args.no_cpu_baseline:
+        if world == 1 and not args.no_cpu_baseline and not dense:
             x, y, z = host[0]
             cb = cpu_baseline(x, y, z, args.workload, sample_np)
-            cpu = {"value": round(N_POINTS / cb["seconds"] / 1e6, 6), "unit": "Mpoints/s",
+            cpu = {"value": round(npts / cb["seconds"] / 1e6, 6), "unit": "Mpoints/s",
                    "cores": cb["threads"], "kind": "port", "sample": cb["sample"], "runs_s": cb["runs"],
                    **host_info(),
                    "parity": full_size_parity(cb["outputs"], state["kp"], scans[0], sb.desc if shot else scans[0].desc,
                                               state["rows"], shot)}
+        if dense:
+            cpu = {"value": None, "note": "not run: the CPU restatement needs ~10 min per pass at this density "
+                                          "(normals ~24.6G neighbour terms); see the configs[2] line"}
         line["cpu_baseline"] = cpu
         print(json.dumps(line), flush=True)
     run_fpfh.close()
@@ -383,11 +399,11 @@ def bench_scans(args, torch, dist, dev, world, rank, local):
     ctx_n.close()
 
 
-def scans_line(args, world, n_scans, mine, shot, elapsed, timers, iso, nb_scan, long_scan, stat):
+def scans_line(args, world, n_scans, mine, shot, elapsed, timers, iso, nb_scan, long_scan, stat, npts=N_POINTS):
     """The contract line of bench_scans (rank 0), roofline over the neighbour-gather stage."""
     per_scan_calls = args.steps * len(mine)
     ms_per_step = elapsed / args.steps * 1e3
-    value = n_scans * N_POINTS * args.steps / elapsed / 1e6
+    value = n_scans * npts * args.steps / elapsed / 1e6
     nb = sum(nb_scan) / len(nb_scan)
     long_nb = sum(l[0] for l in long_scan) / len(long_scan)
     long_q = sum(l[1] for l in long_scan) / len(long_scan)
@@ -395,13 +411,13 @@ def scans_line(args, world, n_scans, mine, shot, elapsed, timers, iso, nb_scan, 
     # the WHOLE stage that produces them: grid build + FLANN-ordered list builders + ordered
     # covariance chains + long lists (timer "normals": HIP events around pfx_normals_dev on its
     # stream, inside the timed step, averaged per scan)
-    algo = nb * 12 + N_POINTS * 16
+    algo = nb * 12 + npts * 16
     stage_ms = timers["normals"][0] / max(per_scan_calls, 1)
     stage_gbs = algo / (stage_ms / 1e3) / 1e9 if stage_ms > 0 else 0.0
     parts = ("grid_bbox", "grid_build", "normals_lists_small", "normals_lists_sparse", "normals_lists_dense",
              "normals_lists_query", "normals_chain", "normals_chain_big", "normals_long")
     kernels = {nm: round(timers[nm][0] / max(per_scan_calls, 1), 4) for nm in parts}
-    chain_algo = (nb - long_nb) * 12 + (N_POINTS - long_q) * 16
+    chain_algo = (nb - long_nb) * 12 + (npts - long_q) * 16
     chain_ms = kernels["normals_chain"] + kernels["normals_chain_big"]
     chain = {"kernel": "k_normals_chain + k_normals_chain_big",
              "algorithmic_bytes_per_launch": int(chain_algo), "ms": chain_ms,
@@ -453,11 +469,16 @@ def scans_line(args, world, n_scans, mine, shot, elapsed, timers, iso, nb_scan, 
                         f"(RCCL grouped send/recv)")
         data = "synthetic (synth_room: seeded pinhole room scan, k(0.05)~230; see synth.py)"
         scaling = "strong" if n_scans > 1 else "weak"
+        if npts != N_POINTS:
+            metric = "Mpoints/s through NARF keypoint + FPFH descriptor, configs[2] scene at 10x density"
+            workload = (f"SURVEY 8(d) dense variant: configs[2]'s room scene (same scale) at {npts // 1_000_000}M "
+                        f"points, NARF(support 0.2) + normals(r 0.05) + FPFH(r 0.08) at the keypoints")
+            data = f"synthetic (synth_room at 10x density: {npts} points, k(0.05)~{int(nb / npts)}; see synth.py)"
     return {
         "metric": metric, "value": round(value, 4), "unit": "Mpoints/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
         "higher_is_better": True, "scaling": scaling, "vs_baseline": None, "dtype": "f32", "data": data,
-        "config": {"workload": workload, "points_per_scan": N_POINTS, "scans_per_step": n_scans,
+        "config": {"workload": workload, "points_per_scan": npts, "scans_per_step": n_scans,
                    "image": "640x480", "parallelism": f"scan-per-gpu x{world}"},
         "roofline": roofline,
     }
@@ -748,6 +769,102 @@ def bench_harris(args, torch, dev, world, rank, local, six=False):
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
+    ctx.close()
+
+
+def bench_config1(args, torch, dev, world, rank, local):
+    """configs[1]: the 100k-point synthetic room (seed 1; replicas seed 1 + rank at N > 1),
+    NormalEstimationOMP (r 0.05) + FPFHEstimation (r 0.05) at every point, input == surface
+    (PCL's all-points SPFH branch, features.h:188-195 with the cloud as both).  One step =
+    pfx_normals_dev + pfx_fpfh_dev(same_as_surface) on the device-resident cloud.  roofline: the
+    SPFH stage (k_fpfh_spfh + exact + finalize), the dominant cost here: sum_{p in S} |N(p)| x
+    24 B, S = every point."""
+    import numpy as np
+
+    from pcl_feature_extraction_amd import Context
+    from pcl_feature_extraction_amd.pipeline import alloc
+    from pcl_feature_extraction_amd.synth import synth_room
+
+    n = 100_000
+    x, y, z, _ = synth_room(n, 1 + rank)
+    b = alloc(torch, n, dev, max_keypoints=n)
+    for t, a in zip((b.x, b.y, b.z), (x, y, z)):
+        t.copy_(torch.from_numpy(a))
+    ctx = Context(local)
+    ctx.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+
+    def step():
+        ctx.normals_dev(b.x, b.y, b.z, 0.05, b.nx, b.ny, b.nz, b.curv)
+        ctx.fpfh_dev(b.x, b.y, b.z, b.nx, b.ny, b.nz, b.x, b.y, b.z, 0.05, b.desc, same_as_surface=True)
+
+    for _ in range(max(args.warmup, 1)):
+        step()
+    torch.cuda.synchronize(dev)
+    ctx.set_timing(True)
+    ctx.reset_timing()
+    elapsed = timed(torch, torch.distributed, dev, world, args.steps, step)
+    if rank != 0:
+        ctx.close()
+        return
+    names = ("normals", "fpfh_mark", "fpfh_spfh", "fpfh_weight", "grid_build", "normals_lists_small",
+             "normals_lists_sparse", "normals_lists_dense", "normals_lists_query", "normals_chain",
+             "normals_chain_big", "normals_long")
+    stages = {nm: round(ctx.kernel_time(nm)[0] / args.steps, 4) for nm in names}
+    ctx.set_timing(False)
+    pairs = ctx.stat("fpfh_spfh_pairs")
+    nb = ctx.stat("normals_neighbors")
+    spfh_ms = stages["fpfh_spfh"]
+    algo = pairs * 24
+    achieved = algo / (spfh_ms / 1e3) / 1e9 if spfh_ms > 0 else 0.0
+    cpu = None
+    if world == 1 and not args.no_cpu_baseline:
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import oracle_lib as O
+        threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
+
+        def once(cx, cy, cz):
+            t0 = time.perf_counter()
+            on = O.normals(cx, cy, cz, 0.05, threads=threads)
+            t1 = time.perf_counter()
+            od = O.fpfh(cx, cy, cz, on[0], on[1], on[2], cx, cy, cz, 0.05, same_as_surface=True, threads=1)
+            return (t1 - t0, time.perf_counter() - t1), (on, od)
+        once(x[::10], y[::10], z[::10])  # warm-up on a 1/10 subsample
+        runs, out = [], None
+        for _ in range(5):
+            t, out = once(x, y, z)
+            runs.append(t)
+        tot = sorted(sum(t) for t in runs)
+        med = tot[len(tot) // 2]
+        st = [sorted(t[i] for t in runs)[len(runs) // 2] for i in range(2)]
+
+        def same(a, c):
+            a, c = np.asarray(a, np.float32), np.asarray(c, np.float32)
+            return bool(a.shape == c.shape and np.array_equal(np.nan_to_num(a, nan=7).view(np.uint32),
+                                                              np.nan_to_num(c, nan=7).view(np.uint32)))
+        parity = {"normals": all(same(t.cpu().numpy(), o) for t, o in zip((b.nx, b.ny, b.nz, b.curv), out[0])),
+                  "descriptors": same(b.desc[:n].cpu().numpy(), out[1])}
+        cpu = {"value": round(n / med / 1e6, 6), "unit": "Mpoints/s", "cores": threads, "kind": "port",
+               "sample": (f"the same 100k-point scan through the CPU restatement (oracle/), 1 warm-up (1/10 "
+                          f"subsample) + median of 5 full runs: normals {threads} threads {st[0]:.2f}s, FPFH at every "
+                          f"point 1 thread (PCL 1.7's non-OMP FPFHEstimation) {st[1]:.2f}s"),
+               "runs_s": [round(v, 3) for v in tot], **host_info(), "parity": parity}
+    line = {
+        "metric": "Mpoints/s through NormalEstimation + FPFH (r 0.05) at every point of a 100k-pt cloud",
+        "value": round(world * n * args.steps / elapsed / 1e6, 4), "unit": "Mpoints/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+        "data": "synthetic (synth_room(100000, seed 1): seeded pinhole room scan, k(0.05)~230; see synth.py)",
+        "config": {"workload": "configs[1] 100k-pt synthetic room, NormalEstimation(r 0.05) + FPFH(r 0.05) at all "
+                               "points (input == surface)", "points_per_scan": n,
+                   "parallelism": f"scan-per-gpu x{world}"},
+        "roofline": {"bound": "hbm", "kernel": "k_fpfh_spfh + k_fpfh_exact + k_fpfh_finalize", "achieved": round(achieved, 2),
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+                     "algorithmic_bytes_per_launch": int(algo), "avg_ms": spfh_ms, "pairs_per_launch": int(pairs),
+                     "note": "sum_{p in S} |N(p)| x 24 B (xyz + normal per pair, SURVEY 8(d)); S = all 100k points",
+                     "normals_neighbors": int(nb), "stages_ms_per_step": stages},
+        "cpu_baseline": cpu,
+    }
+    print(json.dumps(line), flush=True)
     ctx.close()
 
 

@@ -23,6 +23,8 @@ namespace {
 constexpr int kBins = 11;
 constexpr int kDesc = 33;
 constexpr int kCapW = 16384;  // sorted-neighbour capacity of the weighting kernel (LDS)
+constexpr int64_t kCapWGlobal = 1 << 22;  // ... of its global-scratch pass (overflow queries)
+constexpr int kWOvfBlocks = 16;           // workgroups of that pass
 constexpr int kChunkW = 128;  // SPFH rows staged per chunk in the weighting kernel
 constexpr int kWT = 1024;     // weighting workgroup: few queries, each as wide as possible
 constexpr int kHistCopies = 16;  // SPFH per-wave counter copies
@@ -444,11 +446,19 @@ __device__ __forceinline__ int lsb_exp(float v) {
 // the total is below 2^(L+52) every partial sum -- of the sequential loop or of any other order
 // -- is exact and the parallel sum is bit-identical to PCL's loop; otherwise the block sum is
 // recomputed sequentially.
+// GLOBAL = false: the sorted keys in LDS (kCapW); a query with more neighbours is pushed to
+// `ovf`.  GLOBAL = true: the overflow queries (count read on the device), keys in a
+// per-workgroup global scratch slice of gcap (PCL has no neighbour limit; kCapWGlobal here).
+template <bool GLOBAL>
 __global__ void __launch_bounds__(kWT) k_fpfh_weight(GridView g, const float* __restrict__ qx,
                                                      const float* __restrict__ qy, const float* __restrict__ qz,
                                                      int64_t nq, float rr, const float* __restrict__ spfh,
-                                                     float* __restrict__ out, int* __restrict__ err) {
-  extern __shared__ __attribute__((aligned(16))) uint64_t keys[];  // kCapW
+                                                     float* __restrict__ out, int* __restrict__ err,
+                                                     int32_t* __restrict__ ovf, int* __restrict__ n_ovf,
+                                                     uint64_t* __restrict__ scratch, int gcap) {
+  extern __shared__ __attribute__((aligned(16))) uint64_t keys_lds[];  // kCapW
+  uint64_t* keys = GLOBAL ? scratch + (size_t)blockIdx.x * gcap : keys_lds;
+  const int kcap = GLOBAL ? gcap : kCapW;
   __shared__ float rows[kChunkW][kDesc + 1];
   __shared__ float wts[kChunkW];
   __shared__ double red_s[3][kWT / 64];
@@ -456,10 +466,15 @@ __global__ void __launch_bounds__(kWT) k_fpfh_weight(GridView g, const float* __
   __shared__ int s_count;
   __shared__ double s_sum[3];
   const int tid = threadIdx.x;
-  for (int64_t q = blockIdx.x; q < nq; q += gridDim.x) {
-    const int k = sorted_neighbors(g, qx[q], qy[q], qz[q], rr, keys, kCapW, &s_count);
-    if (k > kCapW) {
-      if (tid == 0) atomicMax(err, k);
+  const int64_t count = GLOBAL ? (int64_t)*n_ovf : nq;
+  for (int64_t w = blockIdx.x; w < count; w += gridDim.x) {
+    const int64_t q = GLOBAL ? (int64_t)ovf[w] : w;
+    const int k = sorted_neighbors(g, qx[q], qy[q], qz[q], rr, keys, kcap, &s_count);
+    if (k > kcap) {
+      if (tid == 0) {
+        if (GLOBAL || !ovf) atomicMax(err, k);
+        else ovf[atomicAdd(n_ovf, 1)] = (int32_t)q;  // weighted by the global-scratch pass
+      }
       continue;
     }
     if (k == 0) {
@@ -659,19 +674,26 @@ void fpfh_dev(pfx_ctx* ctx, const float* sx, const float* sy, const float* sz, c
     PFX_HIP(rocprim::select(tmp, tmp_bytes, rocprim::counting_iterator<int32_t>(0), flags, slist, d_sel,
                             (size_t)ns, st));
   }
-  int* err = ctx->buf("fpfh_err").as<int>(8);  // [0] k over capacity, [1] max k, [2] inexact sums, [3] deferred pairs, [4..7] pairs
+  // [0] k over capacity, [1] max k, [2] inexact sums, [3] deferred pairs, [4..7] pairs,
+  // [8] queries over the LDS capacity (weighted by the global-scratch pass)
+  int* err = ctx->buf("fpfh_err").as<int>(10);
+  // a neighbourhood can only outgrow the LDS keys when the surface has more than kCapW points
+  const bool overflow_pass = ns > kCapW;
+  int32_t* ovf = overflow_pass ? ctx->buf("fpfh_wovf").as<int32_t>(nq) : nullptr;
+  const int gcap = overflow_pass ? (int)std::min<int64_t>(kCapWGlobal, (int64_t)1 << (64 - __builtin_clzll((unsigned long long)ns - 1))) : 0;
+  uint64_t* wscratch = overflow_pass ? ctx->buf("fpfh_wscratch").as<uint64_t>((size_t)kWOvfBlocks * gcap) : nullptr;
   unsigned long long* d_pairs = reinterpret_cast<unsigned long long*>(err + 4);
   unsigned* n_slow = reinterpret_cast<unsigned*>(err + 3);
   int* hcount = ctx->buf("fpfh_hcount").as<int>(ns * kDesc);
   int* kcount = ctx->buf("fpfh_kcount").as<int>(ns);
-  int h[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  int h[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   int64_t count = 0;
   // deferred pairs are rare (cancellation near bin edges); a cloud that overflows the queue is
   // run once more with a queue of the size it reported
   int64_t reruns = 0;
   const char* cap_env = getenv("PFX_FPFH_SLOW_CAP");  // test hook: forces the rerun path
   for (unsigned slow_cap = cap_env ? (unsigned)std::max(1, atoi(cap_env)) : 1u << 20;;) {
-    PFX_HIP(hipMemsetAsync(err, 0, 8 * sizeof(int), st));
+    PFX_HIP(hipMemsetAsync(err, 0, 10 * sizeof(int), st));
     int2* slowq = ctx->buf("fpfh_slowq").as<int2>(slow_cap);
     {
       // the S count stays on the device: grid-stride launches sized for the worst case
@@ -687,9 +709,12 @@ void fpfh_dev(pfx_ctx* ctx, const float* sx, const float* sy, const float* sz, c
     {
       TimeScope ts(ctx, "fpfh_weight");
       const size_t lds = sizeof(uint64_t) * kCapW;
-      PFX_HIP(hipFuncSetAttribute((const void*)k_fpfh_weight, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+      PFX_HIP(hipFuncSetAttribute((const void*)k_fpfh_weight<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
       const unsigned blocks = (unsigned)std::min<int64_t>(nq, 256 * 2);
-      k_fpfh_weight<<<blocks, kWT, lds, st>>>(g, qx, qy, qz, nq, rr, spfh, out, err);
+      k_fpfh_weight<false><<<blocks, kWT, lds, st>>>(g, qx, qy, qz, nq, rr, spfh, out, err, ovf, err + 8, nullptr, 0);
+      if (overflow_pass)
+        k_fpfh_weight<true><<<kWOvfBlocks, kWT, 0, st>>>(g, qx, qy, qz, nq, rr, spfh, out, err, ovf, err + 8, wscratch,
+                                                          gcap);
       check_launch("k_fpfh_weight");
     }
     PFX_HIP(hipMemcpyAsync(h, err, sizeof(h), hipMemcpyDeviceToHost, st));
@@ -710,9 +735,10 @@ void fpfh_dev(pfx_ctx* ctx, const float* sx, const float* sy, const float* sz, c
   }
   ctx->stats["fpfh_weight_kmax"] = h[1];
   ctx->stats["fpfh_weight_sequential"] = h[2];
+  ctx->stats["fpfh_weight_global"] = h[8];
   if (h[0] > 0)
     throw Error(PFX_ERR_CAPACITY, "fpfh: a query has " + std::to_string(h[0]) + " neighbours (> " +
-                                      std::to_string(kCapW) + " supported)");
+                                      std::to_string(kCapWGlobal) + " supported)");
 }
 
 }  // namespace pfx

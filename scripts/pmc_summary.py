@@ -43,22 +43,31 @@ for us, k, a in rows[:20]:
     print("   " + "  ".join(f"{c}={v:.4g}" for c, v in sorted({**a, **extra}.items())))
 
 # machine-readable HBM traffic of one stage for bench.py's roofline.traffic: the sum over the
-# named kernels (comma-separated prefixes) of their per-dispatch averages
+# named kernels (comma-separated prefixes; every template instance of a prefix counts) of their
+# per-dispatch averages
 if len(sys.argv) > 3:
     import json
     kernels, dest = sys.argv[2].split(","), sys.argv[3]
     fetch = write = 0.0
-    found = []
-    for kernel in kernels:
-        for us, k, a in rows:
-            if k == kernel or k.startswith(kernel + "<") or k.startswith(kernel + "("):
-                fetch += a.get("FETCH_SIZE_x2_MB", 0.0) * 1024 * 1024
-                write += a.get("WRITE_SIZE_MB", 0.0) * 1024 * 1024
-                found.append(k)
-                break
+    found, per = [], {}
+    for us, k, a in rows:
+        if any(k == p or k.startswith(p + "<") or k.startswith(p + "(") for p in kernels):
+            f = a.get("FETCH_SIZE_x2_MB", 0.0) * 1024 * 1024
+            w = a.get("WRITE_SIZE_MB", 0.0) * 1024 * 1024
+            fetch += f
+            write += w
+            found.append(k)
+            per[k] = {"hbm_bytes": int(f + w), "us_profiled": round(us, 1),
+                      **{c: a[c] for c in ("SQ_WAIT_ANY_frac", "SQ_LDS_BANK_CONFLICT", "SQ_ACTIVE_INST_LDS")
+                         if c in a}}
+            if "SQ_WAVE_CYCLES" in a and a["SQ_WAVE_CYCLES"] and "SQ_WAIT_ANY" in a:
+                per[k]["SQ_WAIT_ANY_frac"] = a["SQ_WAIT_ANY"] / a["SQ_WAVE_CYCLES"]
+            if a.get("SQ_ACTIVE_INST_LDS"):
+                per[k]["lds_conflict_per_active"] = a.get("SQ_LDS_BANK_CONFLICT", 0.0) / a["SQ_ACTIVE_INST_LDS"]
     with open(dest, "w") as f:
         json.dump({"kernel": " + ".join(found), "hbm_bytes_per_launch": int(fetch + write),
-                   "fetch_bytes_x2": int(fetch), "write_bytes": int(write),
+                   "stage_hbm_bytes_per_launch": int(fetch + write),
+                   "fetch_bytes_x2": int(fetch), "write_bytes": int(write), "kernels": per,
                    "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes, FETCH x2 "
                              "(MI355X_MICROARCH.md gfx950 correction); sum of the kernels' per-dispatch "
                              "averages over bench.py warmup + timed steps"}, f, indent=1)

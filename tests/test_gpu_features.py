@@ -186,3 +186,46 @@ def test_fpfh_deferred_pair_queue_overflow(ctx, monkeypatch):
     assert ctx.stat("fpfh_spfh_reruns") == 1
     assert _nan_aware_equal(g, base)
     assert _nan_aware_equal(g, O.fpfh(x, y, z, nx, ny, nz, x[q], y[q], z[q], 0.08))
+
+
+def _shell(n, radius, seed, centre=(0.3, -0.2, 1.5)):
+    """n points on a sphere shell of the given radius (float32 SoA) plus outward normals."""
+    rng = np.random.default_rng(seed)
+    v = rng.normal(size=(n, 3))
+    v /= np.linalg.norm(v, axis=1, keepdims=True)
+    p = (np.asarray(centre) + radius * v).astype(np.float32)
+    return p[:, 0].copy(), p[:, 1].copy(), p[:, 2].copy(), v.astype(np.float32)
+
+
+def test_radius_search_beyond_lds_capacity(ctx):
+    """PCL's radiusSearch (max_nn = 0) returns every neighbour: lists longer than the LDS
+    capacity (16,384) are ordered by the global-scratch pass, bit-exact like the rest."""
+    rng = np.random.default_rng(11)
+    n = 20_000
+    c = np.array([0.1, 0.2, 1.0])
+    p = (c + rng.uniform(-0.015, 0.015, (n, 3))).astype(np.float32)
+    x, y, z = p[:, 0].copy(), p[:, 1].copy(), p[:, 2].copy()
+    q = np.array([0, 17, 19_999])
+    cap = n
+    c_gpu, i_gpu, d_gpu = ctx.radius_search(x, y, z, x[q], y[q], z[q], 0.05, cap=cap)
+    c_ref, i_ref, d_ref = O.radius_search(x, y, z, x[q], y[q], z[q], 0.05, cap=cap)
+    assert (c_ref > 16384).all()
+    assert np.array_equal(c_gpu, c_ref)
+    for j in range(len(q)):
+        k = c_ref[j]
+        assert np.array_equal(i_gpu[j, :k], i_ref[j, :k]), j
+        assert _bits_equal(d_gpu[j, :k], d_ref[j, :k]), j
+
+
+def test_fpfh_weighting_beyond_lds_capacity(ctx):
+    """A keypoint with more than 16,384 neighbours (the weighting kernel's LDS capacity) is
+    weighted by the global-scratch pass: same descriptor bits as the restatement."""
+    x, y, z, nv = _shell(17_000, 0.045, 5)
+    nx, ny, nz = nv[:, 0].copy(), nv[:, 1].copy(), nv[:, 2].copy()
+    qx = np.array([0.3, x[0]], np.float32)
+    qy = np.array([-0.2, y[0]], np.float32)
+    qz = np.array([1.5, z[0]], np.float32)
+    g = ctx.fpfh(x, y, z, nx, ny, nz, qx, qy, qz, 0.05)
+    assert ctx.stat("fpfh_weight_global") == 1
+    o = O.fpfh(x, y, z, nx, ny, nz, qx, qy, qz, 0.05, threads=8)
+    assert _nan_aware_equal(g, o)
