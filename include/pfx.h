@@ -153,6 +153,10 @@ pfx_status pfx_fpfh(pfx_ctx* ctx, const float* sx, const float* sy, const float*
                     const float* snx, const float* sny, const float* snz, int64_t n_surface,
                     const float* qx, const float* qy, const float* qz, int64_t nq,
                     int same_as_surface, double radius, float* out);
+/* _dev, same_as_surface: when the last pfx_normals_dev / pfx_normals_lists_dev on this ctx ran on
+ * the same (d_sx, d_sy, d_sz, n_surface) at the same radius -- Features::compute's sequence,
+ * features.h:187-195 -- its FLANN-ordered neighbour lists are reused for the weighting (the
+ * coordinates must not have changed in between). */
 pfx_status pfx_fpfh_dev(pfx_ctx* ctx, const float* d_sx, const float* d_sy, const float* d_sz,
                         const float* d_snx, const float* d_sny, const float* d_snz,
                         int64_t n_surface, const float* d_qx, const float* d_qy,

@@ -282,7 +282,7 @@ pfx_status pfx_fpfh_dev(pfx_ctx* ctx, const float* d_sx, const float* d_sy, cons
   if (same_as_surface && nq != n_surface)
     throw Error(PFX_ERR_INVALID, "fpfh: same_as_surface requires nq == n_surface");
   pfx::fpfh_dev(ctx, d_sx, d_sy, d_sz, d_snx, d_sny, d_snz, n_surface, d_qx, d_qy, d_qz, nq, same_as_surface,
-                radius, d_out);
+                radius, d_out, /*reuse_normal_lists=*/true);
   PFX_API_END(ctx)
 }
 

@@ -15,6 +15,7 @@
 #include <cstring>
 #include <rocprim/rocprim.hpp>
 
+#include "pfx_nblist.h"
 #include "pfx_neighbors.h"
 
 namespace pfx {
@@ -589,6 +590,127 @@ __global__ void __launch_bounds__(kWT) k_fpfh_weight(GridView g, const float* __
   }
 }
 
+// Weighting for input == surface (PCL's all-points branch): the queries are the surface's grid
+// points, so their FLANN-ordered neighbour lists come from build_lists (pfx_nblist.hip).  One
+// wave per query: 64 list entries at a time are resolved by the lanes (position, caller index,
+// w = 1/d2), then lane b < 33 runs bin b's float chain over them in list order, reading the
+// neighbours' SPFH rows 8 at a time (loads in flight together).  Block sums: each lane's double
+// partial sum + smallest binade, combined in any order when exact (as k_fpfh_weight), else PCL's
+// sequential loop by one lane per block.
+__device__ __forceinline__ int32_t entry_pos(uint32_t e, const int32_t (&rs)[9]) {
+  const int r = entry_run(e);
+  int32_t s = rs[0];
+#pragma unroll
+  for (int i = 1; i < 9; ++i) s = r == i ? rs[i] : s;
+  return s + (int32_t)entry_off(e);
+}
+
+__global__ void __launch_bounds__(256) k_fpfh_weight_lists(GridView g, const int32_t* __restrict__ qpos,
+                                                           const int64_t* __restrict__ loff,
+                                                           const int32_t* __restrict__ lcnt,
+                                                           const uint8_t* __restrict__ llg,
+                                                           const uint32_t* __restrict__ list,
+                                                           const uint32_t* __restrict__ skeys, int64_t nq,
+                                                           const float* __restrict__ spfh, float* __restrict__ out,
+                                                           int* __restrict__ err) {
+  __shared__ double s_ps[4][kDesc];
+  __shared__ int s_pl[4][kDesc];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  int kmax = 0;  // added to err[1] once per wave (same-address atomics serialise)
+  for (int64_t j = (int64_t)blockIdx.x * 4 + wv; j < nq; j += nw) {
+    const int32_t qp = qpos[j];
+    const int k = lcnt[j];
+    const int64_t off = loff[j];
+    const int lg = llg[j];
+    Runs R;
+    block_runs(g, skeys[qp], R);
+    int32_t rs[9];
+#pragma unroll
+    for (int r = 0; r < 9; ++r) rs[r] = R.start[r];
+    const float4 q = g.sp[qp];
+    const int32_t qi = g.perm[qp];
+    float fh = 0.0f;
+    double ps = 0.0;
+    int pl = 1 << 20;
+    for (int c0 = 0; c0 < k; c0 += 64) {
+      const int m = min(64, k - c0);
+      const int32_t pos = lane < m ? entry_pos(list[off + ((int64_t)(c0 + lane) << lg)], rs) : qp;
+      const int32_t idx = g.perm[pos];
+      const float4 p = g.sp[pos];
+      const float d2 = flann_d2(q.x, q.y, q.z, p.x, p.y, p.z);
+      const float w = d2 == 0.0f ? 0.0f : 1.0f / d2;  // 0 marks a skipped neighbour (the query itself)
+      for (int j0 = 0; j0 < m; j0 += 8) {
+        float v[8], wu[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int jj = j0 + u < m ? j0 + u : m - 1;
+          const int id = __builtin_amdgcn_readlane(idx, jj);
+          wu[u] = j0 + u < m ? __int_as_float(__builtin_amdgcn_readlane(__float_as_int(w), jj)) : 0.0f;
+          v[u] = lane < kDesc ? spfh[(int64_t)id * kDesc + lane] : 0.0f;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          // w = 0 adds +0 (rows finite, fh >= +0): PCL's `continue`, bit for bit
+          const float val = v[u] * wu[u];
+          fh = fh + val;
+          if (wu[u] != 0.0f && val != 0.0f) {
+            ps += (double)val;
+            pl = min(pl, lsb_exp(val));
+          }
+        }
+      }
+    }
+    if (lane < kDesc) {
+      s_ps[wv][lane] = ps;
+      s_pl[wv][lane] = pl;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    double scale = 0.0;
+    if (lane < 3) {
+      double sum = 0.0;
+      int L = 1 << 20;
+      for (int b = 0; b < kBins; ++b) {
+        sum += s_ps[wv][lane * kBins + b];
+        L = min(L, s_pl[wv][lane * kBins + b]);
+      }
+      if (!(sum == 0.0 || (L < 1000 && sum < ldexp(1.0, L + 52)))) {  // PCL's sequential loop
+        atomicAdd(err + 2, 1);
+        sum = 0.0;
+        for (int c = 0; c < k; ++c) {
+          const int32_t pos = entry_pos(list[off + ((int64_t)c << lg)], rs);
+          const float4 p = g.sp[pos];
+          const float d2 = flann_d2(q.x, q.y, q.z, p.x, p.y, p.z);
+          if (d2 == 0.0f) continue;
+          const float wc = 1.0f / d2;
+          const float* row = spfh + (int64_t)g.perm[pos] * kDesc + lane * kBins;
+          for (int b = 0; b < kBins; ++b) sum = sum + (double)(row[b] * wc);
+        }
+      }
+      scale = sum != 0.0 ? 100.0 / sum : 0.0;
+      s_ps[wv][lane] = scale;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    if (lane < kDesc) out[(int64_t)qi * kDesc + lane] = fh * (float)s_ps[wv][lane / kBins];
+    kmax = max(kmax, k);
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+  }
+  if (lane == 0 && kmax) atomicMax(err + 1, kmax);
+}
+
+// NaN rows for the non-finite surface points (PCL: no neighbours -> NaN); the finite ones are
+// written by k_fpfh_weight_lists
+__global__ void k_nan_rows_nonfinite(const float* __restrict__ x, const float* __restrict__ y,
+                                     const float* __restrict__ z, int64_t n, float* __restrict__ out) {
+  const int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (e >= n * kDesc) return;
+  const int64_t i = e / kDesc;
+  if (!(isfinite(x[i]) && isfinite(y[i]) && isfinite(z[i]))) out[e] = __builtin_nanf("");
+}
+
 }  // namespace
 
 void fpfh_prepare_dev(pfx_ctx* ctx, const float* sx, const float* sy, const float* sz, int64_t ns, double r) {
@@ -632,7 +754,7 @@ void fpfh_support_mask_dev(pfx_ctx* ctx, const float* sx, const float* sy, const
 
 void fpfh_dev(pfx_ctx* ctx, const float* sx, const float* sy, const float* sz, const float* snx,
               const float* sny, const float* snz, int64_t ns, const float* qx, const float* qy, const float* qz,
-              int64_t nq, int same, double r, float* out) {
+              int64_t nq, int same, double r, float* out, bool reuse_normal_lists) {
   PFX_CHECK(r > 0.0, "fpfh: radius must be > 0");
   if (nq == 0) return;
   hipStream_t st = ctx->stream;
@@ -706,7 +828,24 @@ void fpfh_dev(pfx_ctx* ctx, const float* sx, const float* sy, const float* sz, c
           g, slist, d_sel, hcount, kcount, spfh);
       check_launch("k_fpfh_spfh");
     }
-    {
+    if (same) {  // input == surface: FLANN-ordered lists of every grid point, a wave per query
+      TimeScope ts(ctx, "fpfh_weight");
+      // Features::compute estimates the normals of the same cloud first (features.h:187-195):
+      // when that search had this radius, its lists are this one's (grid_a indexes the same
+      // points); otherwise they are built on the FPFH grid
+      const NormalsState* nst = ctx->normals;
+      const bool reuse = reuse_normal_lists && nst && nst->ready && nst->x == sx && nst->y == sy && nst->z == sz && nst->n == ns &&
+                         nst->r == r;
+      NbLists L;
+      if (reuse) L = nst->L;
+      else build_lists(ctx, G, nullptr, r, true, L, "fpfh");
+      ctx->stats["fpfh_weight_lists_reused"] = reuse ? 1 : 0;
+      k_nan_rows_nonfinite<<<(unsigned)ceil_div(ns * kDesc, 256), 256, 0, st>>>(sx, sy, sz, ns, out);
+      if (L.nq > 0)
+        k_fpfh_weight_lists<<<(unsigned)std::min<int64_t>(ceil_div(L.nq, 4), 256 * 8), 256, 0, st>>>(
+            reuse ? view(ctx->grid_a) : g, L.qpos, L.off, L.cnt, L.lg, L.list, L.skeys, L.nq, spfh, out, err);
+      check_launch("k_fpfh_weight_lists");
+    } else {
       TimeScope ts(ctx, "fpfh_weight");
       const size_t lds = sizeof(uint64_t) * kCapW;
       PFX_HIP(hipFuncSetAttribute((const void*)k_fpfh_weight<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));

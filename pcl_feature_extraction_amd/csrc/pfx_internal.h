@@ -195,7 +195,8 @@ void radius_search_dev(pfx_ctx* ctx, const float* x, const float* y, const float
                        int64_t* d_counts, int32_t* d_idx, float* d_d2, int64_t cap);
 void fpfh_dev(pfx_ctx* ctx, const float* sx, const float* sy, const float* sz, const float* snx,
               const float* sny, const float* snz, int64_t ns, const float* qx, const float* qy,
-              const float* qz, int64_t nq, int same, double r, float* out);
+              const float* qz, int64_t nq, int same, double r, float* out,
+              bool reuse_normal_lists = false);
 void fpfh_prepare_dev(pfx_ctx* ctx, const float* sx, const float* sy, const float* sz, int64_t ns, double r);
 void shot_dev(pfx_ctx* ctx, const float* sx, const float* sy, const float* sz, const float* snx,
               const float* sny, const float* snz, int64_t ns, const float* qx, const float* qy,

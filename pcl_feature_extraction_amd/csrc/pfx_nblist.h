@@ -44,6 +44,8 @@ constexpr int kLongList = 1024;
 struct NormalsState {
   NbLists L;
   int64_t n = 0;
+  const float *x = nullptr, *y = nullptr, *z = nullptr;  // the cloud and radius the lists belong to
+  double r = 0.0;
   bool ready = false;
 };
 

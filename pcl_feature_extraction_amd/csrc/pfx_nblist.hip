@@ -26,7 +26,8 @@ constexpr int kArena = 16384;   // list entries per arena reservation of a tile 
 constexpr int kArenaQuery = 16384;  // ... of a per-query workgroup (lists of 1k-4k entries)
 constexpr int kTcapSmall = 384, kTcapSparse = 1280, kTcapDense = 8000;
 constexpr int kCapQuery = 4096, kBucketsQuery = 1024;
-constexpr int kCapHuge = 1 << 18, kBucketsHuge = 4096, kHugeBlocks = 32;
+constexpr int kCapMid = 16384, kBucketsMid = 2048;  // 144 KB of LDS: one workgroup per CU
+constexpr int kCapHuge = 1 << 18, kBucketsHuge = 4096, kHugeBlocks = 256;  // 1 GB scratch, allocated on demand
 
 // Tile record (written by k_tile_class, one per tile, in class order): the 9 candidate runs of
 // the tile's 3x3x3 block, its first query (index into qpos) and query count.  A workgroup loads
@@ -897,8 +898,10 @@ void build_lists(pfx_ctx* ctx, const Grid& G, const uint8_t* mask, double radius
   uint8_t* lgs = B("lg").as<uint8_t>(n);
   // counters: 0 sparse tiles, 1 dense tiles, 2 per-query work, 3 huge work, 4 max k over cap,
   // 5 / 7 sparse / dense tile queue heads, 6 per-query work queued by the classifier (restored
-  // for a rerun), 8 / 9 per-query / huge work queue heads, 10 small tiles, 11 their queue head
-  int* counters = B("counters").as<int>(12);
+  // for a rerun), 8 / 9 per-query / huge work queue heads, 10 small tiles, 11 their queue head,
+  // 12 mid work (lists of 4k-16k entries), 13 its queue head
+  int* counters = B("counters").as<int>(14);
+  int32_t* mid = B("mid").as<int32_t>(n);
   unsigned long long* cursor = B("cursor").as<unsigned long long>(4);
   size_t t1 = 0, t2 = 0, t3 = 0;
   PFX_HIP(rocprim::select(nullptr, t1, rocprim::counting_iterator<int32_t>(0), flags, qpos, d_nq, (size_t)n, st));
@@ -906,7 +909,7 @@ void build_lists(pfx_ctx* ctx, const Grid& G, const uint8_t* mask, double radius
   PFX_HIP(rocprim::select(nullptr, t3, rocprim::counting_iterator<int32_t>(0), flags, tiles, d_ntiles, (size_t)n,
                           st));
   void* tmp = B("tmp").get(std::max(t1, std::max(t2, t3)) + 16);
-  PFX_HIP(hipMemsetAsync(counters, 0, 12 * sizeof(int), st));
+  PFX_HIP(hipMemsetAsync(counters, 0, 14 * sizeof(int), st));
   const unsigned nb = (unsigned)ceil_div(n, 256);
   {
     TimeScope ts(ctx, std::string(tag) + "_tiles");
@@ -930,6 +933,9 @@ void build_lists(pfx_ctx* ctx, const Grid& G, const uint8_t* mask, double radius
   const size_t lds_q = sizeof(uint32_t) * 2 * kCapQuery;
   PFX_HIP(hipFuncSetAttribute((const void*)k_nb_query<kCapQuery, kBucketsQuery, false>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_q));
+  const size_t lds_m = sizeof(uint32_t) * 2 * kCapMid;
+  PFX_HIP(hipFuncSetAttribute((const void*)k_nb_query<kCapMid, kBucketsMid, false>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_m));
   DevBuf& lb = B("list");
   if (!lb.ptr) lb.get(sizeof(uint32_t) * 64 * (size_t)(n + 1));
   const int isort = sorted ? 1 : 0;
@@ -943,9 +949,9 @@ void build_lists(pfx_ctx* ctx, const Grid& G, const uint8_t* mask, double radius
       PFX_HIP(hipMemcpyAsync(counters + 2, counters + 6, sizeof(int), hipMemcpyDeviceToDevice, st));
       PFX_HIP(hipMemsetAsync(counters + 3, 0, 3 * sizeof(int), st));  // huge, max k, sparse queue
       PFX_HIP(hipMemsetAsync(counters + 7, 0, 3 * sizeof(int), st));  // dense, query, huge queues
-      PFX_HIP(hipMemsetAsync(counters + 11, 0, sizeof(int), st));      // small queue
+      PFX_HIP(hipMemsetAsync(counters + 11, 0, 3 * sizeof(int), st));  // small queue, mid work + queue
     }
-    int h_cnt[8];
+    int h_cnt[14];
     {
       TimeScope ts(ctx, std::string(tag) + "_lists");
       {
@@ -967,8 +973,12 @@ void build_lists(pfx_ctx* ctx, const Grid& G, const uint8_t* mask, double radius
       {
         TimeScope t3(ctx, std::string(tag) + "_lists_query");
         k_nb_query<kCapQuery, kBucketsQuery, false><<<256 * 4, 256, lds_q, st>>>(
-            g, qpos, G.skeys, single, counters + 2, rr, (float)kBucketsQuery / rr, isort, lo, huge, counters + 3,
+            g, qpos, G.skeys, single, counters + 2, rr, (float)kBucketsQuery / rr, isort, lo, mid, counters + 12,
             counters + 4, nullptr, counters + 8);
+        // lists of 4k-16k entries (dense clouds); the count stays on the device
+        k_nb_query<kCapMid, kBucketsMid, false><<<256, 256, lds_m, st>>>(
+            g, qpos, G.skeys, mid, counters + 12, rr, (float)kBucketsMid / rr, isort, lo, huge, counters + 3,
+            counters + 4, nullptr, counters + 13);
       }
       check_launch("nblist lists");
       PFX_HIP(hipMemcpyAsync(h_cnt, counters, sizeof(h_cnt), hipMemcpyDeviceToHost, st));
@@ -994,7 +1004,8 @@ void build_lists(pfx_ctx* ctx, const Grid& G, const uint8_t* mask, double radius
       // The slot demand of a run is the entries + interleave padding (fixed by the input) + the
       // unused arena tails (scheduling-dependent, at most one arena per launched workgroup), so
       // this run's demand plus the tail bound always fits the rebuild.
-      const size_t tails = (size_t)(256 * 4 * 2 + 256 * 3 * 4 + 256 * 2 * 4) * kArena + (size_t)(256 * 4 + kHugeBlocks) * kArenaQuery;
+      const size_t tails = (size_t)(256 * 4 * 2 + 256 * 3 * 4 + 256 * 2 * 4) * kArena +
+                           (size_t)(256 * 4 + 256 + kHugeBlocks) * kArenaQuery;
       lb.release();
       lb.get(sizeof(uint32_t) * ((size_t)h_cur[0] + tails + ((size_t)1 << 20)));
       continue;
@@ -1014,6 +1025,7 @@ void build_lists(pfx_ctx* ctx, const Grid& G, const uint8_t* mask, double radius
     ctx->stats[std::string(tag) + "_tiles_dense"] = h_cnt[1];
     ctx->stats[std::string(tag) + "_single"] = h_cnt[2];
     ctx->stats[std::string(tag) + "_huge"] = h_cnt[3];
+    ctx->stats[std::string(tag) + "_mid"] = h_cnt[12];
 #ifdef PFX_SHOT_PROFILE
     {
       unsigned long long pr[16];

@@ -494,6 +494,10 @@ void normals_lists_dev(pfx_ctx* ctx, const float* x, const float* y, const float
   NormalsState& ns = *ctx->normals;
   ns.ready = false;
   ns.n = n;
+  ns.x = x;
+  ns.y = y;
+  ns.z = z;
+  ns.r = r;
   ns.L = NbLists();
   if (n == 0) {
     ns.ready = true;

@@ -92,18 +92,20 @@ def test_normals_edge_cases(ctx):
 
 def test_normals_every_list_path(ctx):
     """Densities that route queries through every neighbour-list path (pfx_nblist.hip): sparse
-    and dense tiles, the per-query LDS kernel (k > 1024) and the global-scratch kernel (k > 4096),
+    and dense tiles, the per-query LDS kernels (k > 1024, k > 4096) and the global-scratch kernel
+    (k > 16384),
     plus lane-per-query and nine-lanes-per-query chains; duplicates exercise the index tie-break."""
     rng = np.random.default_rng(23)
     sparse = np.c_[rng.uniform(0, 1, (4000, 2)), np.full(4000, 1.0)]
     dense = np.c_[rng.uniform(2, 2.3, (9000, 2)), np.full(9000, 1.0)]          # k ~ 400..800
     denser = np.c_[rng.uniform(3, 3.1, (9000, 2)), np.full(9000, 1.0)]         # k ~ 1800..7000
     blob = rng.normal(0, 0.01, (1500, 3)) + [4, 4, 1]                          # k ~ 900..1500
-    huge = np.repeat(rng.normal(0, 0.004, (1700, 3)) + [6, 6, 1], 3, axis=0)  # k = 5100, ties
-    pts = np.concatenate([sparse, dense, denser, blob, huge]).astype(np.float32)
+    mid = np.repeat(rng.normal(0, 0.004, (1700, 3)) + [6, 6, 1], 3, axis=0)   # k = 5100, ties
+    huge = np.repeat(rng.normal(0, 0.004, (5500, 3)) + [8, 8, 1], 3, axis=0)  # k = 16500 > 16384
+    pts = np.concatenate([sparse, dense, denser, blob, mid, huge]).astype(np.float32)
     x, y, z = pts[:, 0].copy(), pts[:, 1].copy(), pts[:, 2].copy()
     g = ctx.normals(x, y, z, 0.05)
-    for nm in ["normals_tiles_sparse", "normals_tiles_dense", "normals_single", "normals_huge"]:
+    for nm in ["normals_tiles_sparse", "normals_tiles_dense", "normals_single", "normals_mid", "normals_huge"]:
         assert ctx.stat(nm) > 0, nm
     o = O.normals(x, y, z, 0.05)
     for a, b in zip(g, o):
@@ -229,3 +231,34 @@ def test_fpfh_weighting_beyond_lds_capacity(ctx):
     assert ctx.stat("fpfh_weight_global") == 1
     o = O.fpfh(x, y, z, nx, ny, nz, qx, qy, qz, 0.05, threads=8)
     assert _nan_aware_equal(g, o)
+
+
+def test_fpfh_same_as_surface_dev_reuses_normal_lists():
+    """Device API, Features::compute's sequence (features.h:187-195): normals then FPFH on the
+    same device cloud at the same radius reuse the normals' FLANN-ordered lists for the
+    weighting; another radius builds its own.  Both bit-exact against the restatement."""
+    import torch
+    from pcl_feature_extraction_amd import Context
+    x, y, z = _cloud("indoor_source")
+    x, y, z = x[::3].copy(), y[::3].copy(), z[::3].copy()
+    n = len(x)
+    dev = torch.device("cuda", 0)
+    dx, dy, dz = (torch.from_numpy(a).to(dev) for a in (x, y, z))
+    nx, ny, nz, cv = (torch.empty(n, device=dev) for _ in range(4))
+    out = torch.empty((n, 33), device=dev)
+    with Context(0) as c:
+        c.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+        c.normals_dev(dx, dy, dz, 0.05, nx, ny, nz, cv)
+        c.fpfh_dev(dx, dy, dz, nx, ny, nz, dx, dy, dz, 0.05, out, same_as_surface=True)
+        torch.cuda.synchronize(dev)
+        assert c.stat("fpfh_weight_lists_reused") == 1
+        g5 = out.cpu().numpy()
+        c.fpfh_dev(dx, dy, dz, nx, ny, nz, dx, dy, dz, 0.06, out, same_as_surface=True)
+        torch.cuda.synchronize(dev)
+        assert c.stat("fpfh_weight_lists_reused") == 0
+        g6 = out.cpu().numpy()
+    on = O.normals(x, y, z, 0.05)
+    for a, b in zip((nx, ny, nz, cv), on):
+        assert _nan_aware_equal(a.cpu().numpy(), b)
+    assert _nan_aware_equal(g5, O.fpfh(x, y, z, on[0], on[1], on[2], x, y, z, 0.05, same_as_surface=True))
+    assert _nan_aware_equal(g6, O.fpfh(x, y, z, on[0], on[1], on[2], x, y, z, 0.06, same_as_surface=True))
