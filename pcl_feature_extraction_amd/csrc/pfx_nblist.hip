@@ -465,6 +465,10 @@ __global__ void __launch_bounds__(256, TCAP <= kTcapSmall ? 4 : (STAGE ? 3 : 2))
   constexpr int U = 2;               // candidates per lane in flight in the test loop
   constexpr int SCAP = STAGE ? Stager<TCAP, STAGE>::PT * 256 : 1;
   __shared__ float cx[SCAP], cy[SCAP], cz[SCAP];
+  // dense tiles: the test loop reads candidates from LDS chunks of CH staged by the whole
+  // workgroup (one latency round and one run search per candidate, not per wave and candidate)
+  constexpr int CH = STAGE ? 1 : 1024;
+  __shared__ float hx[CH], hy[CH], hz[CH];
   __shared__ uint16_t lists[Q][LCAP + 2];  // +2: odd dword row stride (no bank conflicts)
   __shared__ uint32_t sd[4][LCAP];
   __shared__ uint16_t stt[4][LCAP];
@@ -529,35 +533,50 @@ __global__ void __launch_bounds__(256, TCAP <= kTcapSmall ? 4 : (STAGE ? 3 : 2))
         }
       }
     }
-    for (int t0 = 0; ok && t0 < T; t0 += 64 * U) {
-      float px[U], py[U], pz[U];
+    for (int c0 = 0; ok && c0 < T; c0 += (STAGE ? T : CH)) {  // one pass for staged tiles
+      const int cend = STAGE ? T : min(T, c0 + CH);
+      if (!STAGE) {
+        constexpr int CPT = CH >= 256 ? CH / 256 : 1;
+        float4 cc[CPT];
 #pragma unroll
-      for (int v = 0; v < U; ++v) {
-        const int t = t0 + 64 * v + lane;
-        px[v] = py[v] = pz[v] = 0.f;
-        if (t < T) {
-          if (STAGE) {
-            px[v] = cx[t]; py[v] = cy[t]; pz[v] = cz[t];
-          } else {
-            const float4 c = g.sp[run_pos(R, t)];
-            px[v] = c.x; py[v] = c.y; pz[v] = c.z;
+        for (int u = 0; u < CPT; ++u) cc[u] = g.sp[run_pos(R, min(c0 + tid + 256 * u, T - 1))];
+        __syncthreads();  // the previous chunk's readers are done
+#pragma unroll
+        for (int u = 0; u < CPT; ++u) {
+          hx[tid + 256 * u] = cc[u].x;
+          hy[tid + 256 * u] = cc[u].y;
+          hz[tid + 256 * u] = cc[u].z;
+        }
+        __syncthreads();
+      }
+      const float* Xs = STAGE ? cx : hx - c0;
+      const float* Ys = STAGE ? cy : hy - c0;
+      const float* Zs = STAGE ? cz : hz - c0;
+      for (int t0 = c0; t0 < cend; t0 += 64 * U) {
+        float px[U], py[U], pz[U];
+#pragma unroll
+        for (int v = 0; v < U; ++v) {
+          const int t = t0 + 64 * v + lane;
+          px[v] = py[v] = pz[v] = 0.f;
+          if (t < cend) {
+            px[v] = Xs[t]; py[v] = Ys[t]; pz[v] = Zs[t];
           }
         }
-      }
 #pragma unroll
-      for (int v = 0; v < U; ++v) {
-        const int t = t0 + 64 * v + lane;
-        const bool in = t < T;
+        for (int v = 0; v < U; ++v) {
+          const int t = t0 + 64 * v + lane;
+          const bool in = t < cend;
 #pragma unroll
-        for (int u = 0; u < QW; ++u) {
-          const int j = wv + 4 * u;
-          const bool hit = in && j < qn && flann_d2(qx[u], qy[u], qz[u], px[v], py[v], pz[v]) < rr;
-          const uint64_t m = __ballot(hit);
-          if (hit) {
-            const int slot = cursor[u] + __popcll(m & lanemask_lt());
-            if (slot < LCAP) lists[j][slot] = (uint16_t)t;
+          for (int u = 0; u < QW; ++u) {
+            const int j = wv + 4 * u;
+            const bool hit = in && j < qn && flann_d2(qx[u], qy[u], qz[u], px[v], py[v], pz[v]) < rr;
+            const uint64_t m = __ballot(hit);
+            if (hit) {
+              const int slot = cursor[u] + __popcll(m & lanemask_lt());
+              if (slot < LCAP) lists[j][slot] = (uint16_t)t;
+            }
+            cursor[u] += __popcll(m);
           }
-          cursor[u] += __popcll(m);
         }
       }
     }

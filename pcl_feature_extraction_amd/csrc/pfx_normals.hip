@@ -408,71 +408,131 @@ __global__ void __launch_bounds__(256, 1) k_normals_chain_big(GridView g, NbList
   }
 }
 
-// long lists: nine lanes per query (one chain each), seven queries per wave; every lane of a
-// query loads the same entries (one cache line per query per load), entries two batches ahead.
+// long lists: nine lanes per query (one chain each), seven queries per wave.  The chains of a
+// list are strictly sequential, so the kernel's time is the longest list's chain; a batch of
+// global gathers per few steps put one memory latency on that chain every batch.  Here the wave
+// gathers kLB (64) steps of its seven lists at a time into LDS (seven coordinate loads per lane,
+// issued one batch ahead, with the list entries two batches ahead), and the chains read LDS
+// (four steps per ds_read_b128): one latency per 64 steps instead of per 16.
 // Persistent waves (grid-stride over groups of seven queries): the queue length is only known
 // on the device, and a grid sized for the worst case spends its time dispatching empty waves.
+constexpr int kPerWave = 7, kLB = 64;
+struct LongLds {
+  float c[2][3][kPerWave][kLB];  // double-buffered x | y | z per query and step (10.5 KB)
+  int32_t rtab[kPerWave * 9];
+};
+
 __global__ void __launch_bounds__(256) k_normals_long(GridView g, NbLists L, const int32_t* __restrict__ longq,
                                                       const int* __restrict__ n_long, float vpx, float vpy,
                                                       float vpz, float* __restrict__ nx, float* __restrict__ ny,
                                                       float* __restrict__ nz, float* __restrict__ curv) {
-  constexpr int kPerWave = 7, kB = 16;
-  __shared__ int32_t rtab[4][kPerWave * 9];
+  __shared__ LongLds S4[4];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  LongLds& S = S4[wv];
   const int qi = lane / 9, a = lane - 9 * qi;
   const int count = *n_long;
   const int64_t nwaves = (int64_t)gridDim.x * 4;
+  auto wsync = [] {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+  };
   for (int64_t w = (int64_t)blockIdx.x * 4 + wv; w * kPerWave < count; w += nwaves) {
     const int64_t slot = w * kPerWave + qi;
     const bool active = qi < kPerWave && slot < count;
-    int k = 0, lg = 0;
+    int k = 0;
     int32_t j = 0;
-    const uint32_t* lst = L.list;
     if (active) {
       j = longq[slot];
       k = L.cnt[j];
-      lg = L.lg[j];
-      lst = L.list + L.off[j];
       int32_t s, len;
       block_run(g, L.skeys[L.qpos[j]], a, s, len);
-      rtab[wv][9 * qi + a] = s;
+      S.rtab[9 * qi + a] = s;
     }
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    const int32_t* tb = rtab[wv] + 9 * (qi < kPerWave ? qi : 0);
+    // gather slot i of this lane: query i, step `lane` of a batch (every lane serves all seven)
+    int kq[kPerWave], lgq[kPerWave];
+    int64_t offq[kPerWave];
+    int kmax = 0;
+#pragma unroll
+    for (int i = 0; i < kPerWave; ++i) {
+      const int64_t si = w * kPerWave + i;
+      const int32_t ji = si < count ? longq[si] : 0;
+      kq[i] = si < count ? L.cnt[ji] : 0;
+      lgq[i] = si < count ? L.lg[ji] : 0;
+      offq[i] = si < count ? L.off[ji] : 0;
+      kmax = max(kmax, kq[i]);
+    }
+    wsync();  // rtab
+    // entry of step m of query i (clamped: padded steps repeat the last entry, summed as zeros)
+    auto entry = [&](int i, int m) -> uint32_t {
+      const int mm = kq[i] > 0 ? min(m, kq[i] - 1) : 0;
+      return kq[i] > 0 ? L.list[offq[i] + ((int64_t)mm << lgq[i])] : 0u;
+    };
+    auto coord = [&](int i, uint32_t e) -> float4 {
+      return kq[i] > 0 ? g.sp[S.rtab[9 * i + entry_run(e)] + (int32_t)entry_off(e)] : make_float4(0.f, 0.f, 0.f, 0.f);
+    };
+    uint32_t e1[kPerWave], e2[kPerWave];
+    float4 cv[kPerWave];
+    // staged steps past a list's end are exact zeros (acc is never -0: + 0.0f is the identity),
+    // so every lane runs whole batches without bounds checks
+    auto put = [&](int buf, int m0) {
+#pragma unroll
+      for (int i = 0; i < kPerWave; ++i) {
+        const bool in = m0 + lane < kq[i];
+        S.c[buf][0][i][lane] = in ? cv[i].x : 0.f;
+        S.c[buf][1][i][lane] = in ? cv[i].y : 0.f;
+        S.c[buf][2][i][lane] = in ? cv[i].z : 0.f;
+      }
+    };
+#pragma unroll
+    for (int i = 0; i < kPerWave; ++i) e1[i] = entry(i, lane);
+#pragma unroll
+    for (int i = 0; i < kPerWave; ++i) cv[i] = coord(i, e1[i]);
+#pragma unroll
+    for (int i = 0; i < kPerWave; ++i) e1[i] = entry(i, kLB + lane);
+    put(0, 0);
+    wsync();
+    // chain term a = u * v over the coordinate planes: x*x x*y x*z y*y y*z z*z x y z
+    const int pu = (a == 0 || a == 1 || a == 2 || a == 6) ? 0 : ((a == 3 || a == 4 || a == 7) ? 1 : 2);
+    const int pv = (a == 0) ? 0 : ((a == 1 || a == 3) ? 1 : 2);
+    const bool linear = a >= 6;
+    const int q7 = qi < kPerWave ? qi : 0;
     float acc = 0.0f;
-    uint32_t e[kB], e1[kB];
-    const int last = k - 1;  // branch-free: clamped entry loads, exact-zero padded terms
-    auto at = [&](int m) { return lst[(int64_t)(m < last ? m : last) << lg]; };
-    if (k > 0) {
+    for (int m0 = 0, buf = 0; m0 < kmax; m0 += kLB, buf ^= 1) {
+      const bool more = m0 + kLB < kmax;
+      if (more) {
 #pragma unroll
-      for (int b = 0; b < kB; ++b) {
-        e[b] = at(b);
-        e1[b] = at(kB + b);
+        for (int i = 0; i < kPerWave; ++i) cv[i] = coord(i, e1[i]);  // batch m0 + kLB
+#pragma unroll
+        for (int i = 0; i < kPerWave; ++i) e2[i] = entry(i, m0 + 2 * kLB + lane);
       }
-    }
-    for (int m0 = 0; m0 < k; m0 += kB) {
-      float4 c[kB];
+      const float4* bu = reinterpret_cast<const float4*>(&S.c[buf][pu][q7][0]);
+      const float4* bv = reinterpret_cast<const float4*>(&S.c[buf][pv][q7][0]);
+#pragma unroll 2
+      for (int t4 = 0; t4 < kLB / 4; t4 += 4) {
+        float4 u4[4], v4[4];
 #pragma unroll
-      for (int b = 0; b < kB; ++b) c[b] = g.sp[tb[entry_run(e[b])] + (int32_t)entry_off(e[b])];
+        for (int i = 0; i < 4; ++i) {
+          u4[i] = bu[t4 + i];
+          v4[i] = bv[t4 + i];
+        }
+        const float* fu = reinterpret_cast<const float*>(u4);
+        const float* fv = reinterpret_cast<const float*>(v4);
 #pragma unroll
-      for (int b = 0; b < kB; ++b) {
-        e[b] = e1[b];
-        e1[b] = at(m0 + 2 * kB + b);
+        for (int i = 0; i < 16; ++i) acc = acc + (linear ? fu[i] : fu[i] * fv[i]);
       }
+      if (more) {
+        put(buf ^ 1, m0 + kLB);
 #pragma unroll
-      for (int b = 0; b < kB; ++b) {
-        const bool in = m0 + b < k;
-        acc = acc + chain_term(a, in ? c[b].x : 0.f, in ? c[b].y : 0.f, in ? c[b].z : 0.f);
+        for (int i = 0; i < kPerWave; ++i) e1[i] = e2[i];
       }
+      wsync();
     }
     float accu[9];
     const int base = 9 * (lane < 63 ? qi : 0);
 #pragma unroll
     for (int i = 0; i < 9; ++i) accu[i] = __shfl(acc, base + i);
     if (active && a == 0) store_normal(g, L.qpos[j], accu, k, vpx, vpy, vpz, nx, ny, nz, curv);
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    __builtin_amdgcn_wave_barrier();  // rtab is rewritten by the next group
+    wsync();  // LDS is rewritten by the next group
   }
 }
 

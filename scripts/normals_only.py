@@ -36,4 +36,5 @@ for name, gen, seed in (("room", synth_room, 2), ("seabed", synth_seabed, 3)):
         nb = ctx.stat("normals_neighbors")
         chain = t["normals_chain"] + t["normals_chain_big"]
         gbs = (nb * 12 + len(x) * 16) / (chain / 1e3) / 1e9
-        print(name, json.dumps(t), "chain GB/s %.0f frac %.3f" % (gbs, gbs / 8000.0), flush=True)
+        st = {k: ctx.stat("normals_" + k) for k in ("single", "mid", "huge")}
+        print(name, json.dumps(t), json.dumps(st), "chain GB/s %.0f frac %.3f" % (gbs, gbs / 8000.0), flush=True)
