@@ -423,7 +423,8 @@ def scans_line(args, world, n_scans, mine, shot, elapsed, timers, iso, nb_scan, 
              "algorithmic_bytes_per_launch": int(chain_algo), "ms": chain_ms,
              "achieved": round(chain_algo / (chain_ms / 1e3) / 1e9, 2) if chain_ms > 0 else None}
     chain["frac"] = round(chain["achieved"] / HBM_PEAK_GBS, 5) if chain["achieved"] else None
-    pmc = load_pmc("pmc_normals_stage.json") or {}
+    # the committed PMC summary was collected on configs[2]'s scan: only that line may cite it
+    pmc = (load_pmc("pmc_normals_stage.json") or {}) if npts == N_POINTS else {}
     roofline = {"bound": "hbm", "kernel": "normals stage: grid + k_nb_tile/k_nb_query list builders + "
                                           "k_normals_chain(_big) + k_normals_long",
                 "achieved": round(stage_gbs, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
