@@ -416,9 +416,9 @@ __global__ void __launch_bounds__(256, 1) k_normals_chain_big(GridView g, NbList
 // (four steps per ds_read_b128): one latency per 64 steps instead of per 16.
 // Persistent waves (grid-stride over groups of seven queries): the queue length is only known
 // on the device, and a grid sized for the worst case spends its time dispatching empty waves.
-constexpr int kPerWave = 7, kLB = 64;
+constexpr int kPerWave = 7, kLB = 32;
 struct LongLds {
-  float c[2][3][kPerWave][kLB];  // double-buffered x | y | z per query and step (10.5 KB)
+  float c[2][3][kPerWave][kLB];  // double-buffered x | y | z per query and step (5.3 KB)
   int32_t rtab[kPerWave * 9];
 };
 
@@ -448,7 +448,8 @@ __global__ void __launch_bounds__(256) k_normals_long(GridView g, NbLists L, con
       block_run(g, L.skeys[L.qpos[j]], a, s, len);
       S.rtab[9 * qi + a] = s;
     }
-    // gather slot i of this lane: query i, step `lane` of a batch (every lane serves all seven)
+    // the group's seven lists (wave-uniform: SGPRs); a batch gathers step (lane & 31) of query
+    // 2 * i + (lane >> 5) in slot i, i < 4 (every lane serves up to four queries)
     int kq[kPerWave], lgq[kPerWave];
     int64_t offq[kPerWave];
     int kmax = 0;
@@ -456,39 +457,59 @@ __global__ void __launch_bounds__(256) k_normals_long(GridView g, NbLists L, con
     for (int i = 0; i < kPerWave; ++i) {
       const int64_t si = w * kPerWave + i;
       const int32_t ji = si < count ? longq[si] : 0;
-      kq[i] = si < count ? L.cnt[ji] : 0;
-      lgq[i] = si < count ? L.lg[ji] : 0;
-      offq[i] = si < count ? L.off[ji] : 0;
+      kq[i] = __builtin_amdgcn_readfirstlane(si < count ? L.cnt[ji] : 0);
+      lgq[i] = __builtin_amdgcn_readfirstlane(si < count ? (int)L.lg[ji] : 0);
+      const int64_t o = si < count ? L.off[ji] : 0;
+      offq[i] = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(o >> 32)) << 32) |
+                          (uint32_t)__builtin_amdgcn_readfirstlane((int)o));
       kmax = max(kmax, kq[i]);
     }
     wsync();  // rtab
-    // entry of step m of query i (clamped: padded steps repeat the last entry, summed as zeros)
-    auto entry = [&](int i, int m) -> uint32_t {
-      const int mm = kq[i] > 0 ? min(m, kq[i] - 1) : 0;
-      return kq[i] > 0 ? L.list[offq[i] + ((int64_t)mm << lgq[i])] : 0u;
+    // entry of step m of query qq (clamped: padded steps repeat the last entry, summed as zeros)
+    const int half = lane >> 5, st = lane & 31;
+    auto pick = [&](const int (&v)[kPerWave], int qq) {
+      int r = v[0];
+#pragma unroll
+      for (int i = 1; i < kPerWave; ++i) r = qq == i ? v[i] : r;
+      return r;
     };
-    auto coord = [&](int i, uint32_t e) -> float4 {
-      return kq[i] > 0 ? g.sp[S.rtab[9 * i + entry_run(e)] + (int32_t)entry_off(e)] : make_float4(0.f, 0.f, 0.f, 0.f);
+    auto entry = [&](int slot, int m) -> uint32_t {
+      const int qq = 2 * slot + half;
+      const int kk = qq < kPerWave ? pick(kq, qq) : 0;
+      int64_t of = offq[0];
+#pragma unroll
+      for (int i = 1; i < kPerWave; ++i) of = qq == i ? offq[i] : of;
+      const int mm = kk > 0 ? min(m, kk - 1) : 0;
+      return kk > 0 ? L.list[of + ((int64_t)mm << pick(lgq, qq))] : 0u;
     };
-    uint32_t e1[kPerWave], e2[kPerWave];
-    float4 cv[kPerWave];
+    auto coord = [&](int slot, uint32_t e) -> float4 {
+      const int qq = 2 * slot + half;
+      const bool ok = qq < kPerWave && pick(kq, qq) > 0;
+      return ok ? g.sp[S.rtab[9 * qq + entry_run(e)] + (int32_t)entry_off(e)] : make_float4(0.f, 0.f, 0.f, 0.f);
+    };
+    constexpr int NS = (kPerWave + 1) / 2;  // slots per lane
+    uint32_t e1[NS], e2[NS];
+    float4 cv[NS];
     // staged steps past a list's end are exact zeros (acc is never -0: + 0.0f is the identity),
     // so every lane runs whole batches without bounds checks
     auto put = [&](int buf, int m0) {
 #pragma unroll
-      for (int i = 0; i < kPerWave; ++i) {
-        const bool in = m0 + lane < kq[i];
-        S.c[buf][0][i][lane] = in ? cv[i].x : 0.f;
-        S.c[buf][1][i][lane] = in ? cv[i].y : 0.f;
-        S.c[buf][2][i][lane] = in ? cv[i].z : 0.f;
+      for (int i = 0; i < NS; ++i) {
+        const int qq = 2 * i + half;
+        if (qq < kPerWave) {
+          const bool in = m0 + st < pick(kq, qq);
+          S.c[buf][0][qq][st] = in ? cv[i].x : 0.f;
+          S.c[buf][1][qq][st] = in ? cv[i].y : 0.f;
+          S.c[buf][2][qq][st] = in ? cv[i].z : 0.f;
+        }
       }
     };
 #pragma unroll
-    for (int i = 0; i < kPerWave; ++i) e1[i] = entry(i, lane);
+    for (int i = 0; i < NS; ++i) e1[i] = entry(i, st);
 #pragma unroll
-    for (int i = 0; i < kPerWave; ++i) cv[i] = coord(i, e1[i]);
+    for (int i = 0; i < NS; ++i) cv[i] = coord(i, e1[i]);
 #pragma unroll
-    for (int i = 0; i < kPerWave; ++i) e1[i] = entry(i, kLB + lane);
+    for (int i = 0; i < NS; ++i) e1[i] = entry(i, kLB + st);
     put(0, 0);
     wsync();
     // chain term a = u * v over the coordinate planes: x*x x*y x*z y*y y*z z*z x y z
@@ -501,13 +522,13 @@ __global__ void __launch_bounds__(256) k_normals_long(GridView g, NbLists L, con
       const bool more = m0 + kLB < kmax;
       if (more) {
 #pragma unroll
-        for (int i = 0; i < kPerWave; ++i) cv[i] = coord(i, e1[i]);  // batch m0 + kLB
+        for (int i = 0; i < NS; ++i) cv[i] = coord(i, e1[i]);  // batch m0 + kLB
 #pragma unroll
-        for (int i = 0; i < kPerWave; ++i) e2[i] = entry(i, m0 + 2 * kLB + lane);
+        for (int i = 0; i < NS; ++i) e2[i] = entry(i, m0 + 2 * kLB + st);
       }
       const float4* bu = reinterpret_cast<const float4*>(&S.c[buf][pu][q7][0]);
       const float4* bv = reinterpret_cast<const float4*>(&S.c[buf][pv][q7][0]);
-#pragma unroll 2
+#pragma unroll 1
       for (int t4 = 0; t4 < kLB / 4; t4 += 4) {
         float4 u4[4], v4[4];
 #pragma unroll
@@ -523,7 +544,7 @@ __global__ void __launch_bounds__(256) k_normals_long(GridView g, NbLists L, con
       if (more) {
         put(buf ^ 1, m0 + kLB);
 #pragma unroll
-        for (int i = 0; i < kPerWave; ++i) e1[i] = e2[i];
+        for (int i = 0; i < NS; ++i) e1[i] = e2[i];
       }
       wsync();
     }
@@ -620,7 +641,8 @@ void normals_chains_dev(pfx_ctx* ctx, pfx_ctx* owner, const uint8_t* mask, int w
   {
     TimeScope ts(ctx, "normals_long");
     // persistent: the queue length stays on the device (no host round trip)
-    const int64_t lb = std::min<int64_t>(ceil_div(L.nq, 7 * 4), 2048);
+    // (sized to what is resident at once: waves beyond it would wait for a second round)
+    const int64_t lb = std::min<int64_t>(ceil_div(L.nq, 7 * 4), 256 * 4);
     k_normals_long<<<(unsigned)lb, 256, 0, st>>>(view(G), L, longq, n_long, vp[0], vp[1], vp[2], nx, ny, nz, curv);
     check_launch("k_normals_long");
   }
