@@ -303,8 +303,7 @@ __global__ void __launch_bounds__(256, PFX_SPFH_WPE) k_fpfh_spfh(GridView g, con
                                                       int* __restrict__ hcount, int* __restrict__ kcount,
                                                       int2* __restrict__ slowq, unsigned* __restrict__ n_slow,
                                                       unsigned slow_cap, unsigned long long* __restrict__ pairs) {
-  constexpr int SU = 4;  // candidate loads per lane in flight in the scan
-  __shared__ uint32_t queue[4][64 + 64 * SU];
+  __shared__ uint32_t queue[4][128];
   // 16 copies of each wave's counters (lane & 15): pairs of a planar patch pile into a few bins,
   // and same-address LDS atomics serialise
   __shared__ int hist[4][kHistCopies][kDesc];
@@ -357,37 +356,29 @@ __global__ void __launch_bounds__(256, PFX_SPFH_WPE) k_fpfh_spfh(GridView g, con
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
       __builtin_amdgcn_wave_barrier();
     };
-    // candidates run by run (contiguous positions: no per-candidate run lookup), SU loads per
-    // lane in flight (clamped addresses, branch-free) so a run costs one L2 latency per 64 * SU
-    // candidates instead of one per 64
+    // candidates run by run (contiguous positions: no per-candidate run lookup)
 #pragma unroll
     for (int r = 0; r < 9; ++r) {
       const int32_t rs = R.start[r], rn = R.pref[r + 1] - R.pref[r];
-      for (int32_t t0 = 0; t0 < rn; t0 += 64 * SU) {
-        float4 c[SU];
-#pragma unroll
-        for (int u = 0; u < SU; ++u) c[u] = g.sp[rs + min(t0 + 64 * u + lane, rn - 1)];
-#pragma unroll
-        for (int u = 0; u < SU; ++u) {
-          const int32_t t = t0 + 64 * u + lane;
-          const int32_t pos = rs + t;
-          const bool hit = t < rn && flann_d2(pc.x, pc.y, pc.z, c[u].x, c[u].y, c[u].z) < rr;
-          k += __popcll(__ballot(hit));
-          const bool push = hit && pos != s;
-          const uint64_t m = __ballot(push);
-          if (push) queue[wv][qn + __popcll(m & lanemask_lt())] = (uint32_t)pos;
-          qn += __popcll(m);
+      for (int32_t t0 = 0; t0 < rn; t0 += 64) {
+        const int32_t t = t0 + lane;
+        bool hit = false;
+        const int32_t pos = rs + t;
+        if (t < rn) {
+          const float4 c = g.sp[pos];
+          hit = flann_d2(pc.x, pc.y, pc.z, c.x, c.y, c.z) < rr;
         }
-        while (qn >= 64) {
+        k += __popcll(__ballot(hit));
+        const bool push = hit && pos != s;
+        const uint64_t m = __ballot(push);
+        if (push) queue[wv][qn + __popcll(m & lanemask_lt())] = (uint32_t)pos;
+        qn += __popcll(m);
+        if (qn >= 64) {
           process(64);
-          uint32_t rest[SU];
-#pragma unroll
-          for (int u = 0; u < SU; ++u) rest[u] = (64 + 64 * u + lane < qn) ? queue[wv][64 + 64 * u + lane] : 0u;
+          const uint32_t rest = (lane + 64 < qn) ? queue[wv][lane + 64] : 0u;
           __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
           __builtin_amdgcn_wave_barrier();
-#pragma unroll
-          for (int u = 0; u < SU; ++u)
-            if (64 + 64 * u + lane < qn) queue[wv][64 * u + lane] = rest[u];
+          if (lane + 64 < qn) queue[wv][lane] = rest;
           qn -= 64;
         }
       }
