@@ -23,7 +23,7 @@ namespace {
 
 constexpr int kBins = 11;
 constexpr int kDesc = 33;
-constexpr int kCapW = 16384;  // sorted-neighbour capacity of the weighting kernel (LDS)
+constexpr int kCapW = 8192;   // sorted-neighbour capacity of the weighting kernel (LDS: keys + sort scratch)
 constexpr int64_t kCapWGlobal = 1 << 22;  // ... of its global-scratch pass (overflow queries)
 constexpr int kWOvfBlocks = 16;           // workgroups of that pass
 constexpr int kChunkW = 128;  // SPFH rows staged per chunk in the weighting kernel
@@ -457,7 +457,8 @@ __global__ void __launch_bounds__(kWT) k_fpfh_weight(GridView g, const float* __
                                                      float* __restrict__ out, int* __restrict__ err,
                                                      int32_t* __restrict__ ovf, int* __restrict__ n_ovf,
                                                      uint64_t* __restrict__ scratch, int gcap) {
-  extern __shared__ __attribute__((aligned(16))) uint64_t keys_lds[];  // kCapW
+  extern __shared__ __attribute__((aligned(16))) uint64_t keys_lds[];  // kCapW keys + kCapW sort scratch
+  __shared__ BucketLdsT<kWT> SB;
   uint64_t* keys = GLOBAL ? scratch + (size_t)blockIdx.x * gcap : keys_lds;
   const int kcap = GLOBAL ? gcap : kCapW;
   __shared__ float rows[kChunkW][kDesc + 1];
@@ -470,7 +471,10 @@ __global__ void __launch_bounds__(kWT) k_fpfh_weight(GridView g, const float* __
   const int64_t count = GLOBAL ? (int64_t)*n_ovf : nq;
   for (int64_t w = blockIdx.x; w < count; w += gridDim.x) {
     const int64_t q = GLOBAL ? (int64_t)ovf[w] : w;
-    const int k = sorted_neighbors(g, qx[q], qy[q], qz[q], rr, keys, kcap, &s_count);
+    // LDS: bucketed sort (a few barrier phases); global scratch: the bitonic network
+    const int k = GLOBAL ? sorted_neighbors(g, qx[q], qy[q], qz[q], rr, keys, kcap, &s_count)
+                         : sorted_neighbors_bucketed<kWT>(g, qx[q], qy[q], qz[q], rr, keys, keys + kCapW, kcap,
+                                                          &s_count, SB);
     if (k > kcap) {
       if (tid == 0) {
         if (GLOBAL || !ovf) atomicMax(err, k);
@@ -847,7 +851,7 @@ void fpfh_dev(pfx_ctx* ctx, const float* sx, const float* sy, const float* sz, c
       check_launch("k_fpfh_weight_lists");
     } else {
       TimeScope ts(ctx, "fpfh_weight");
-      const size_t lds = sizeof(uint64_t) * kCapW;
+      const size_t lds = sizeof(uint64_t) * 2 * kCapW;
       PFX_HIP(hipFuncSetAttribute((const void*)k_fpfh_weight<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
       const unsigned blocks = (unsigned)std::min<int64_t>(nq, 256 * 2);
       k_fpfh_weight<false><<<blocks, kWT, lds, st>>>(g, qx, qy, qz, nq, rr, spfh, out, err, ovf, err + 8, nullptr, 0);

@@ -192,39 +192,42 @@ __device__ __forceinline__ int sorted_neighbors(const GridView& g, float qx, flo
   return k;
 }
 
-// ---- bucketed sort (256-thread blocks): FLANN order without a bitonic network ----
+// ---- bucketed sort: FLANN order without a bitonic network ----
 // d2 -> bucket is monotone (one multiplication by a positive constant, then floor), so bucket
 // order is d2 order; inside a bucket every key's final slot is its exact rank among the bucket's
 // keys (keys are unique: the index breaks ties).  Neighbours of a surface point spread evenly
 // over d2 (area grows with d2), so buckets hold a handful of keys; a bucket above kMaxBucket
-// makes the caller fall back to the bitonic sort.
+// makes the caller fall back to the bitonic sort.  NT threads (a multiple of 64), NT buckets.
 constexpr int kSortBuckets = 256;
 constexpr int kMaxBucket = 96;
 
-struct BucketLds {
-  int off[kSortBuckets + 1];
-  int cur[kSortBuckets];
-  int wsum[4];
+template <int NT = kSortBuckets>
+struct BucketLdsT {
+  int off[NT + 1];
+  int cur[NT];
+  int wsum[NT / 64];
   int maxn;
 };
+using BucketLds = BucketLdsT<kSortBuckets>;
 
-__device__ __forceinline__ int d2_bucket(float d2, float inv) {
+__device__ __forceinline__ int d2_bucket(float d2, float inv, int nb) {
   const int b = (int)(d2 * inv);
-  return b < kSortBuckets - 1 ? b : kSortBuckets - 1;
+  return b < nb - 1 ? b : nb - 1;
 }
 
-// gather (as gather_keys) + sort into keys[0..k); tmp: cap more keys.  Requires blockDim.x == 256.
+// gather (as gather_keys) + sort into keys[0..k); tmp: cap more keys.  Requires blockDim.x == NT.
 // Returns k (> cap: nothing sorted, as sorted_neighbors).
+template <int NT = kSortBuckets>
 __device__ __forceinline__ int sorted_neighbors_bucketed(const GridView& g, float qx, float qy, float qz,
                                                          float rr, uint64_t* keys, uint64_t* tmp, int cap,
-                                                         int* s_count, BucketLds& B) {
+                                                         int* s_count, BucketLdsT<NT>& B) {
   const int tid = threadIdx.x, lane = tid & 63;
-  const float inv = (float)kSortBuckets / rr;
+  const float inv = (float)NT / rr;
   B.off[tid] = 0;  // counts first
   if (tid == 0) B.maxn = 0;
   const int k = gather_keys(g, qx, qy, qz, rr, keys, cap, s_count);  // (its barriers order the zeroing)
   if (k > cap) return k;
-  for (int i = tid; i < k; i += 256) atomicAdd(&B.off[d2_bucket(key_d2(keys[i]), inv)], 1);
+  for (int i = tid; i < k; i += NT) atomicAdd(&B.off[d2_bucket(key_d2(keys[i]), inv, NT)], 1);
   __syncthreads();
   const int c = B.off[tid];
   int incl = c;
@@ -242,24 +245,24 @@ __device__ __forceinline__ int sorted_neighbors_bucketed(const GridView& g, floa
   __syncthreads();  // every count read before the offsets overwrite them
   B.off[tid] = ex;
   B.cur[tid] = ex;
-  if (tid == 0) B.off[kSortBuckets] = k;
+  if (tid == 0) B.off[NT] = k;
   const bool fallback = B.maxn > kMaxBucket;
   __syncthreads();
   if (fallback) {
     const int P = next_pow2(k);
-    for (int i = k + tid; i < P; i += 256) keys[i] = ~0ull;
+    for (int i = k + tid; i < P; i += NT) keys[i] = ~0ull;
     __syncthreads();
     bitonic_sort(keys, P);
     return k;
   }
-  for (int i = tid; i < k; i += 256) {
+  for (int i = tid; i < k; i += NT) {
     const uint64_t key = keys[i];
-    tmp[atomicAdd(&B.cur[d2_bucket(key_d2(key), inv)], 1)] = key;
+    tmp[atomicAdd(&B.cur[d2_bucket(key_d2(key), inv, NT)], 1)] = key;
   }
   __syncthreads();
-  for (int i = tid; i < k; i += 256) {
+  for (int i = tid; i < k; i += NT) {
     const uint64_t key = tmp[i];
-    const int b = d2_bucket(key_d2(key), inv);
+    const int b = d2_bucket(key_d2(key), inv, NT);
     const int o = B.off[b], e = B.off[b + 1];
     int r = 0;
     for (int j = o; j < e; ++j) r += tmp[j] < key;

@@ -220,7 +220,7 @@ def test_radius_search_beyond_lds_capacity(ctx):
 
 
 def test_fpfh_weighting_beyond_lds_capacity(ctx):
-    """A keypoint with more than 16,384 neighbours (the weighting kernel's LDS capacity) is
+    """A keypoint with more neighbours than the weighting kernel's LDS capacity (8,192) is
     weighted by the global-scratch pass: same descriptor bits as the restatement."""
     x, y, z, nv = _shell(17_000, 0.045, 5)
     nx, ny, nz = nv[:, 0].copy(), nv[:, 1].copy(), nv[:, 2].copy()
