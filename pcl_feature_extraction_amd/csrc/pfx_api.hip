@@ -120,6 +120,7 @@ void pfx_ctx_destroy(pfx_ctx* ctx) {
   for (auto& p : ctx->timer.pending) { (void)hipEventDestroy(p.a); (void)hipEventDestroy(p.b); }
   for (auto e : ctx->timer.pool) (void)hipEventDestroy(e);
   if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);
+  if (ctx->host_rb) (void)hipHostFree(ctx->host_rb);
   delete ctx;
 }
 

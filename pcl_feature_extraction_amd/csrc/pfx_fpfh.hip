@@ -860,9 +860,14 @@ void fpfh_dev(pfx_ctx* ctx, const float* sx, const float* sy, const float* sz, c
                                                           gcap);
       check_launch("k_fpfh_weight");
     }
-    PFX_HIP(hipMemcpyAsync(h, err, sizeof(h), hipMemcpyDeviceToHost, st));
-    PFX_HIP(hipMemcpyAsync(&count, d_sel, sizeof(int64_t), hipMemcpyDeviceToHost, st));
-    PFX_HIP(hipStreamSynchronize(st));
+    {  // one pinned readback of the error/statistics words and the S count
+      int* rb = ctx->readback<int>();
+      PFX_HIP(hipMemcpyAsync(rb, err, sizeof(h), hipMemcpyDeviceToHost, st));
+      PFX_HIP(hipMemcpyAsync(rb + 16, d_sel, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+      PFX_HIP(hipStreamSynchronize(st));
+      std::memcpy(h, rb, sizeof(h));
+      std::memcpy(&count, rb + 16, sizeof(int64_t));
+    }
     if ((unsigned)h[3] <= slow_cap) break;
     slow_cap = (unsigned)h[3];
     ++reruns;

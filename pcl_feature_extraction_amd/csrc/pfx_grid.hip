@@ -151,8 +151,8 @@ void build_grid(pfx_ctx* ctx, Grid& g, const float* d_x, const float* d_y, const
     k_bbox<<<blocks, 256, 0, st>>>(d_x, d_y, d_z, n, mm);
     check_launch("k_bbox");
   }
-  uint32_t host_mm[6];
-  PFX_HIP(hipMemcpyAsync(host_mm, mm, sizeof(host_mm), hipMemcpyDeviceToHost, st));
+  uint32_t* host_mm = ctx->readback<uint32_t>();  // pinned
+  PFX_HIP(hipMemcpyAsync(host_mm, mm, 6 * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
   PFX_HIP(hipStreamSynchronize(st));
   double lo[3] = {0, 0, 0}, hi[3] = {0, 0, 0};
   bool any = host_mm[0] != 0xffffffffu && host_mm[3] != 0u;

@@ -117,6 +117,13 @@ struct pfx_ctx {
   pfx::NormalsState* normals = nullptr;  // neighbour lists between the two normal phases
   pfx::KeypointState* kp = nullptr;      // grids + lists of the keypoint detectors
   pfx::DevBuf& buf(const char* name) { return bufs[name]; }
+  // small pinned host block for the per-call readbacks (counters, cursors): one D2H copy of
+  // pinned memory per synchronisation instead of staged pageable copies
+  void* host_rb = nullptr;
+  template <class T> T* readback() {
+    if (!host_rb) PFX_HIP(hipHostMalloc(&host_rb, 4096, hipHostMallocDefault));
+    return static_cast<T*>(host_rb);
+  }
 };
 
 namespace pfx {

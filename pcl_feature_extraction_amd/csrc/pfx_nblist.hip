@@ -970,7 +970,22 @@ void build_lists(pfx_ctx* ctx, const Grid& G, const uint8_t* mask, double radius
       PFX_HIP(hipMemsetAsync(counters + 7, 0, 3 * sizeof(int), st));  // dense, query, huge queues
       PFX_HIP(hipMemsetAsync(counters + 11, 0, 3 * sizeof(int), st));  // small queue, mid work + queue
     }
-    int h_cnt[14];
+    // one synchronisation per call: counters, cursors and the query count in one pinned block
+    struct Rb { int cnt[14]; int pad[2]; unsigned long long cur[4]; int64_t nq; };
+    Rb* rb = ctx->readback<Rb>();
+    auto read_back = [&] {
+      PFX_HIP(hipMemcpyAsync(rb->cnt, counters, sizeof(rb->cnt), hipMemcpyDeviceToHost, st));
+      PFX_HIP(hipMemcpyAsync(rb->cur, cursor, sizeof(rb->cur), hipMemcpyDeviceToHost, st));
+      PFX_HIP(hipMemcpyAsync(&rb->nq, d_nq, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+      PFX_HIP(hipStreamSynchronize(st));
+    };
+    DevBuf& hs = B("scratch");
+    auto launch_huge = [&] {
+      k_nb_query<kCapHuge, kBucketsHuge, true><<<kHugeBlocks, 256, 0, st>>>(
+          g, qpos, G.skeys, huge, counters + 3, rr, (float)kBucketsHuge / rr, isort, lo, nullptr, nullptr, counters + 4,
+          static_cast<uint32_t*>(hs.ptr), counters + 9);
+      check_launch("nblist huge lists");
+    };
     {
       TimeScope ts(ctx, std::string(tag) + "_lists");
       {
@@ -998,24 +1013,21 @@ void build_lists(pfx_ctx* ctx, const Grid& G, const uint8_t* mask, double radius
         k_nb_query<kCapMid, kBucketsMid, false><<<256, 256, lds_m, st>>>(
             g, qpos, G.skeys, mid, counters + 12, rr, (float)kBucketsMid / rr, isort, lo, huge, counters + 3,
             counters + 4, nullptr, counters + 13);
+        // beyond 16k entries: once the 1 GB scratch exists the launch is unconditional (count on
+        // the device); the first time, the readback below decides
+        if (hs.ptr) launch_huge();
       }
       check_launch("nblist lists");
-      PFX_HIP(hipMemcpyAsync(h_cnt, counters, sizeof(h_cnt), hipMemcpyDeviceToHost, st));
-      PFX_HIP(hipStreamSynchronize(st));
-      if (h_cnt[3] > 0) {  // very long lists: sort arrays in global scratch
-        uint32_t* scratch = B("scratch").as<uint32_t>((size_t)kHugeBlocks * 4 * kCapHuge);
-        k_nb_query<kCapHuge, kBucketsHuge, true><<<kHugeBlocks, 256, 0, st>>>(
-            g, qpos, G.skeys, huge, counters + 3, rr, (float)kBucketsHuge / rr, isort, lo, nullptr, nullptr, counters + 4,
-            scratch, counters + 9);
-        check_launch("nblist huge lists");
-      }
     }
-    int64_t h_nq = 0;
-    unsigned long long h_cur[4] = {0, 0, 0, 0};
-    PFX_HIP(hipMemcpyAsync(&h_nq, d_nq, sizeof(int64_t), hipMemcpyDeviceToHost, st));
-    PFX_HIP(hipMemcpyAsync(h_cur, cursor, sizeof(h_cur), hipMemcpyDeviceToHost, st));
-    PFX_HIP(hipMemcpyAsync(h_cnt, counters, sizeof(h_cnt), hipMemcpyDeviceToHost, st));
-    PFX_HIP(hipStreamSynchronize(st));
+    read_back();
+    if (!hs.ptr && rb->cnt[3] > 0) {  // very long lists, first time: allocate the scratch and sort them
+      hs.get(sizeof(uint32_t) * (size_t)kHugeBlocks * 4 * kCapHuge);
+      launch_huge();
+      read_back();
+    }
+    int* h_cnt = rb->cnt;
+    unsigned long long* h_cur = rb->cur;
+    const int64_t h_nq = rb->nq;
     if (h_cnt[4] > 0)
       throw Error(PFX_ERR_CAPACITY, std::string(tag) + ": a query has " + std::to_string(h_cnt[4]) +
                                         " neighbours (> " + std::to_string(kCapHuge) + " supported)");
