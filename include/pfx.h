@@ -153,7 +153,10 @@ pfx_status pfx_fpfh(pfx_ctx* ctx, const float* sx, const float* sy, const float*
                     const float* snx, const float* sny, const float* snz, int64_t n_surface,
                     const float* qx, const float* qy, const float* qz, int64_t nq,
                     int same_as_surface, double radius, float* out);
-/* _dev, same_as_surface: when the last pfx_normals_dev / pfx_normals_lists_dev on this ctx ran on
+/* _dev: stream-ordered, no host synchronisation; its statistics (pfx_ctx_last_stats) and a
+ * neighbourhood beyond the 2^22 capacity (PFX_ERR_CAPACITY) are reported by the next
+ * pfx_ctx_synchronize / pfx_ctx_last_stats on this ctx.
+ * _dev, same_as_surface: when the last pfx_normals_dev / pfx_normals_lists_dev on this ctx ran on
  * the same (d_sx, d_sy, d_sz, n_surface) at the same radius -- Features::compute's sequence,
  * features.h:187-195 -- its FLANN-ordered neighbour lists are reused for the weighting (the
  * coordinates must not have changed in between). */

@@ -121,6 +121,7 @@ void pfx_ctx_destroy(pfx_ctx* ctx) {
   for (auto e : ctx->timer.pool) (void)hipEventDestroy(e);
   if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);
   if (ctx->host_rb) (void)hipHostFree(ctx->host_rb);
+  if (ctx->fpfh_rb_mem) (void)hipHostFree(ctx->fpfh_rb_mem);
   delete ctx;
 }
 
@@ -148,6 +149,7 @@ pfx_status pfx_ctx_synchronize(pfx_ctx* ctx) {
   PFX_API_BEGIN
   check_ctx(ctx);
   PFX_HIP(hipStreamSynchronize(ctx->stream));
+  pfx::fpfh_resolve(ctx);  // deferred statistics / capacity errors of the stream-ordered calls
   PFX_API_END(ctx)
 }
 
@@ -181,6 +183,10 @@ pfx_status pfx_ctx_kernel_time(pfx_ctx* ctx, const char* name, double* total_ms,
 pfx_status pfx_ctx_last_stats(pfx_ctx* ctx, const char* what, int64_t* value) {
   PFX_API_BEGIN
   if (!ctx || !what || !value) throw Error(PFX_ERR_INVALID, "null argument");
+  if (ctx->fpfh_pending) {
+    PFX_HIP(hipStreamSynchronize(ctx->stream));
+    pfx::fpfh_resolve(ctx);
+  }
   auto it = ctx->stats.find(what);
   if (it == ctx->stats.end()) throw Error(PFX_ERR_INVALID, std::string("unknown stat ") + what);
   *value = it->second;
@@ -321,6 +327,7 @@ pfx_status pfx_fpfh(pfx_ctx* ctx, const float* sx, const float* sy, const float*
   pfx::fpfh_dev(ctx, dsx, dsy, dsz, dnx, dny, dnz, n_surface, dqx, dqy, dqz, nq, same_as_surface, radius, dout);
   if (nq) PFX_HIP(hipMemcpyAsync(out, dout, sizeof(float) * nq * 33, hipMemcpyDeviceToHost, ctx->stream));
   PFX_HIP(hipStreamSynchronize(ctx->stream));
+  pfx::fpfh_resolve(ctx);  // the host API reports at once
   PFX_API_END(ctx)
 }
 

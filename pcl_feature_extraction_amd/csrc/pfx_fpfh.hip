@@ -351,7 +351,18 @@ __global__ void __launch_bounds__(256, PFX_SPFH_WPE) k_fpfh_spfh(GridView g, con
         if (lane == 0) base = atomicAdd(n_slow, (unsigned)__popcll(m));
         base = __shfl(base, 0);
         const unsigned slot = base + __popcll(m & lanemask_lt());
-        if (!fast && slot < slow_cap) slowq[slot] = make_int2((int)w, (int)q);
+        if (!fast) {
+          if (slot < slow_cap) {
+            slowq[slot] = make_int2((int)w, (int)q);
+          } else {  // queue full (rare): the exact path right here, so no pass ever reruns
+            const float4 qc = g.sp[q], qnv = snp[q];
+            const int hb = pair_bins_exact(pp.x, pp.y, pp.z, pn.x, pn.y, pn.z, qc.x, qc.y, qc.z, qnv.x, qnv.y, qnv.z);
+            int* hc = hist[wv][lane & (kHistCopies - 1)];
+            atomicAdd(&hc[hb & 0xff], 1);
+            atomicAdd(&hc[kBins + ((hb >> 8) & 0xff)], 1);
+            atomicAdd(&hc[2 * kBins + (hb >> 16)], 1);
+          }
+        }
       }
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
       __builtin_amdgcn_wave_barrier();
@@ -403,7 +414,7 @@ __global__ void __launch_bounds__(256) k_fpfh_exact(GridView g, const float4* __
                                                     const int2* __restrict__ slowq, const unsigned* __restrict__ n_slow,
                                                     unsigned slow_cap, int* __restrict__ hcount,
                                                     unsigned long long* __restrict__ pairs) {
-  const unsigned n = min(*n_slow, slow_cap);  // over capacity: the host reruns with a larger queue
+  const unsigned n = min(*n_slow, slow_cap);  // past capacity k_fpfh_spfh took the exact path itself
   const unsigned i = blockIdx.x * 256 + threadIdx.x;
   if (i == 0) atomicAdd(pairs + 1, (unsigned long long)n);
   for (unsigned j = i; j < n; j += gridDim.x * 256) {
@@ -802,7 +813,10 @@ void fpfh_dev(pfx_ctx* ctx, const float* sx, const float* sy, const float* sz, c
   }
   // [0] k over capacity, [1] max k, [2] inexact sums, [3] deferred pairs, [4..7] pairs,
   // [8] queries over the LDS capacity (weighted by the global-scratch pass)
-  int* err = ctx->buf("fpfh_err").as<int>(10);
+  DevBuf& eb = ctx->buf("fpfh_err");
+  const bool fresh = !eb.ptr;
+  int* err = eb.as<int>(10);
+  if (fresh) PFX_HIP(hipMemsetAsync(err, 0, 10 * sizeof(int), st));  // the sticky word starts clear
   // a neighbourhood can only outgrow the LDS keys when the surface has more than kCapW points
   const bool overflow_pass = ns > kCapW;
   int32_t* ovf = overflow_pass ? ctx->buf("fpfh_wovf").as<int32_t>(nq) : nullptr;
@@ -812,81 +826,87 @@ void fpfh_dev(pfx_ctx* ctx, const float* sx, const float* sy, const float* sz, c
   unsigned* n_slow = reinterpret_cast<unsigned*>(err + 3);
   int* hcount = ctx->buf("fpfh_hcount").as<int>(ns * kDesc);
   int* kcount = ctx->buf("fpfh_kcount").as<int>(ns);
-  int h[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-  int64_t count = 0;
-  // deferred pairs are rare (cancellation near bin edges); a cloud that overflows the queue is
-  // run once more with a queue of the size it reported
-  int64_t reruns = 0;
-  const char* cap_env = getenv("PFX_FPFH_SLOW_CAP");  // test hook: forces the rerun path
-  for (unsigned slow_cap = cap_env ? (unsigned)std::max(1, atoi(cap_env)) : 1u << 20;;) {
-    PFX_HIP(hipMemsetAsync(err, 0, 10 * sizeof(int), st));
-    int2* slowq = ctx->buf("fpfh_slowq").as<int2>(slow_cap);
-    {
-      // the S count stays on the device: grid-stride launches sized for the worst case
-      TimeScope ts(ctx, "fpfh_spfh");
-      const int64_t waves = std::min<int64_t>(ns, 256 * 4 * 32);  // up to 32 waves per CU in flight
-      k_fpfh_spfh<<<(unsigned)std::max<int64_t>(8, ceil_div(waves, 4) & ~7), 256, 0, st>>>(
-          g, snp, slist, d_sel, rr, hcount, kcount, slowq, n_slow, slow_cap, d_pairs);
-      k_fpfh_exact<<<256, 256, 0, st>>>(g, snp, slist, slowq, n_slow, slow_cap, hcount, d_pairs);
-      k_fpfh_finalize<<<(unsigned)std::min<int64_t>(ceil_div(ns * kDesc, 256), 4096), 256, 0, st>>>(
-          g, slist, d_sel, hcount, kcount, spfh);
-      check_launch("k_fpfh_spfh");
-    }
-    if (same) {  // input == surface: FLANN-ordered lists of every grid point, a wave per query
-      TimeScope ts(ctx, "fpfh_weight");
-      // Features::compute estimates the normals of the same cloud first (features.h:187-195):
-      // when that search had this radius, its lists are this one's (grid_a indexes the same
-      // points); otherwise they are built on the FPFH grid
-      const NormalsState* nst = ctx->normals;
-      const bool reuse = reuse_normal_lists && nst && nst->ready && nst->x == sx && nst->y == sy && nst->z == sz && nst->n == ns &&
-                         nst->r == r;
-      NbLists L;
-      if (reuse) L = nst->L;
-      else build_lists(ctx, G, nullptr, r, true, L, "fpfh");
-      ctx->stats["fpfh_weight_lists_reused"] = reuse ? 1 : 0;
-      k_nan_rows_nonfinite<<<(unsigned)ceil_div(ns * kDesc, 256), 256, 0, st>>>(sx, sy, sz, ns, out);
-      if (L.nq > 0)
-        k_fpfh_weight_lists<<<(unsigned)std::min<int64_t>(ceil_div(L.nq, 4), 256 * 8), 256, 0, st>>>(
-            reuse ? view(ctx->grid_a) : g, L.qpos, L.off, L.cnt, L.lg, L.list, L.skeys, L.nq, spfh, out, err);
-      check_launch("k_fpfh_weight_lists");
-    } else {
-      TimeScope ts(ctx, "fpfh_weight");
-      const size_t lds = sizeof(uint64_t) * 2 * kCapW;
-      PFX_HIP(hipFuncSetAttribute((const void*)k_fpfh_weight<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-      const unsigned blocks = (unsigned)std::min<int64_t>(nq, 256 * 2);
-      k_fpfh_weight<false><<<blocks, kWT, lds, st>>>(g, qx, qy, qz, nq, rr, spfh, out, err, ovf, err + 8, nullptr, 0);
-      if (overflow_pass)
-        k_fpfh_weight<true><<<kWOvfBlocks, kWT, 0, st>>>(g, qx, qy, qz, nq, rr, spfh, out, err, ovf, err + 8, wscratch,
-                                                          gcap);
-      check_launch("k_fpfh_weight");
-    }
-    {  // one pinned readback of the error/statistics words and the S count
-      int* rb = ctx->readback<int>();
-      PFX_HIP(hipMemcpyAsync(rb, err, sizeof(h), hipMemcpyDeviceToHost, st));
-      PFX_HIP(hipMemcpyAsync(rb + 16, d_sel, sizeof(int64_t), hipMemcpyDeviceToHost, st));
-      PFX_HIP(hipStreamSynchronize(st));
-      std::memcpy(h, rb, sizeof(h));
-      std::memcpy(&count, rb + 16, sizeof(int64_t));
-    }
-    if ((unsigned)h[3] <= slow_cap) break;
-    slow_cap = (unsigned)h[3];
-    ++reruns;
-  }
-  ctx->stats["fpfh_spfh_reruns"] = reruns;
-  ctx->stats["fpfh_spfh_points"] = count;
+  // pairs the fast path cannot bin go to a queue for the exact path; past its capacity
+  // k_fpfh_spfh runs the exact path in place (PFX_FPFH_SLOW_CAP: test hook for that branch)
+  const char* cap_env = getenv("PFX_FPFH_SLOW_CAP");
+  const unsigned slow_cap = cap_env ? (unsigned)std::max(1, atoi(cap_env)) : 1u << 20;
+  // err[0] (neighbourhood beyond capacity) is sticky until the check after the next
+  // synchronisation (fpfh_resolve); the statistics words are per call
+  PFX_HIP(hipMemsetAsync(err + 1, 0, 9 * sizeof(int), st));
+  int2* slowq = ctx->buf("fpfh_slowq").as<int2>(slow_cap);
   {
-    unsigned long long pr;
-    std::memcpy(&pr, h + 4, sizeof(pr));
-    ctx->stats["fpfh_spfh_pairs"] = (int64_t)pr;
-    std::memcpy(&pr, h + 6, sizeof(pr));
-    ctx->stats["fpfh_spfh_exact_pairs"] = (int64_t)pr;
+    // the S count stays on the device: grid-stride launches sized for the worst case
+    TimeScope ts(ctx, "fpfh_spfh");
+    const int64_t waves = std::min<int64_t>(ns, 256 * 4 * 32);  // up to 32 waves per CU in flight
+    k_fpfh_spfh<<<(unsigned)std::max<int64_t>(8, ceil_div(waves, 4) & ~7), 256, 0, st>>>(
+        g, snp, slist, d_sel, rr, hcount, kcount, slowq, n_slow, slow_cap, d_pairs);
+    k_fpfh_exact<<<256, 256, 0, st>>>(g, snp, slist, slowq, n_slow, slow_cap, hcount, d_pairs);
+    k_fpfh_finalize<<<(unsigned)std::min<int64_t>(ceil_div(ns * kDesc, 256), 4096), 256, 0, st>>>(
+        g, slist, d_sel, hcount, kcount, spfh);
+    check_launch("k_fpfh_spfh");
   }
+  if (same) {  // input == surface: FLANN-ordered lists of every grid point, a wave per query
+    TimeScope ts(ctx, "fpfh_weight");
+    // Features::compute estimates the normals of the same cloud first (features.h:187-195):
+    // when that search had this radius, its lists are this one's (grid_a indexes the same
+    // points); otherwise they are built on the FPFH grid
+    const NormalsState* nst = ctx->normals;
+    const bool reuse = reuse_normal_lists && nst && nst->ready && nst->x == sx && nst->y == sy && nst->z == sz &&
+                       nst->n == ns && nst->r == r;
+    NbLists L;
+    if (reuse) L = nst->L;
+    else build_lists(ctx, G, nullptr, r, true, L, "fpfh");
+    ctx->stats["fpfh_weight_lists_reused"] = reuse ? 1 : 0;
+    k_nan_rows_nonfinite<<<(unsigned)ceil_div(ns * kDesc, 256), 256, 0, st>>>(sx, sy, sz, ns, out);
+    if (L.nq > 0)
+      k_fpfh_weight_lists<<<(unsigned)std::min<int64_t>(ceil_div(L.nq, 4), 256 * 8), 256, 0, st>>>(
+          reuse ? view(ctx->grid_a) : g, L.qpos, L.off, L.cnt, L.lg, L.list, L.skeys, L.nq, spfh, out, err);
+    check_launch("k_fpfh_weight_lists");
+  } else {
+    TimeScope ts(ctx, "fpfh_weight");
+    const size_t lds = sizeof(uint64_t) * 2 * kCapW;
+    PFX_HIP(hipFuncSetAttribute((const void*)k_fpfh_weight<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    const unsigned blocks = (unsigned)std::min<int64_t>(nq, 256 * 2);
+    k_fpfh_weight<false><<<blocks, kWT, lds, st>>>(g, qx, qy, qz, nq, rr, spfh, out, err, ovf, err + 8, nullptr, 0);
+    if (overflow_pass)
+      k_fpfh_weight<true><<<kWOvfBlocks, kWT, 0, st>>>(g, qx, qy, qz, nq, rr, spfh, out, err, ovf, err + 8, wscratch,
+                                                        gcap);
+    check_launch("k_fpfh_weight");
+  }
+  // statistics and the sticky error word land in pinned memory in stream order; no host
+  // synchronisation here (the step's critical path ends with this call)
+  FpfhReadback* rb = ctx->fpfh_rb();
+  PFX_HIP(hipMemcpyAsync(rb->h, err, sizeof(rb->h), hipMemcpyDeviceToHost, st));
+  PFX_HIP(hipMemcpyAsync(&rb->count, d_sel, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+  rb->slow_cap = slow_cap;
+  ctx->fpfh_pending = true;
+}
+
+// After a synchronisation of ctx's stream: the last fpfh_dev's statistics, and its capacity check
+// (PFX_ERR_CAPACITY, reported here for the stream-ordered API; the host API calls this at once).
+void fpfh_resolve(pfx_ctx* ctx) {
+  if (!ctx->fpfh_pending) return;
+  ctx->fpfh_pending = false;
+  const FpfhReadback* rb = ctx->fpfh_rb();
+  const int* h = rb->h;
+  const unsigned n_slow = (unsigned)h[3];
+  ctx->stats["fpfh_spfh_points"] = rb->count;
+  unsigned long long pr;
+  std::memcpy(&pr, h + 4, sizeof(pr));
+  ctx->stats["fpfh_spfh_pairs"] = (int64_t)pr;
+  std::memcpy(&pr, h + 6, sizeof(pr));
+  ctx->stats["fpfh_spfh_exact_pairs"] = (int64_t)pr;
+  ctx->stats["fpfh_spfh_deferred"] = n_slow;
+  ctx->stats["fpfh_spfh_inline_exact"] = n_slow > rb->slow_cap ? n_slow - rb->slow_cap : 0;
   ctx->stats["fpfh_weight_kmax"] = h[1];
   ctx->stats["fpfh_weight_sequential"] = h[2];
   ctx->stats["fpfh_weight_global"] = h[8];
-  if (h[0] > 0)
+  if (h[0] > 0) {
+    int* err = ctx->buf("fpfh_err").as<int>(10);
+    PFX_HIP(hipMemsetAsync(err, 0, sizeof(int), ctx->stream));  // reported once
     throw Error(PFX_ERR_CAPACITY, "fpfh: a query has " + std::to_string(h[0]) + " neighbours (> " +
                                       std::to_string(kCapWGlobal) + " supported)");
+  }
 }
 
 }  // namespace pfx

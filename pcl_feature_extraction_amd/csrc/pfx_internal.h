@@ -93,6 +93,12 @@ struct GridView {
   int32_t nx, ny, nz;
 };
 
+struct FpfhReadback {  // pfx_fpfh.hip
+  int h[10];
+  int64_t count;
+  unsigned slow_cap;
+};
+
 struct NarfState;     // pfx_narf.hip
 struct NormalsState;  // pfx_normals.hip
 struct KeypointState;  // pfx_iss.hip
@@ -117,6 +123,14 @@ struct pfx_ctx {
   pfx::NormalsState* normals = nullptr;  // neighbour lists between the two normal phases
   pfx::KeypointState* kp = nullptr;      // grids + lists of the keypoint detectors
   pfx::DevBuf& buf(const char* name) { return bufs[name]; }
+  // fpfh_dev's statistics / sticky error word, copied to pinned memory in stream order and read
+  // after the next synchronisation (pfx::fpfh_resolve)
+  void* fpfh_rb_mem = nullptr;
+  bool fpfh_pending = false;
+  pfx::FpfhReadback* fpfh_rb() {
+    if (!fpfh_rb_mem) PFX_HIP(hipHostMalloc(&fpfh_rb_mem, sizeof(pfx::FpfhReadback), hipHostMallocDefault));
+    return static_cast<pfx::FpfhReadback*>(fpfh_rb_mem);
+  }
   // small pinned host block for the per-call readbacks (counters, cursors): one D2H copy of
   // pinned memory per synchronisation instead of staged pageable copies
   void* host_rb = nullptr;
@@ -200,6 +214,8 @@ void fpfh_support_mask_dev(pfx_ctx* ctx, const float* sx, const float* sy, const
 void radius_search_dev(pfx_ctx* ctx, const float* x, const float* y, const float* z, int64_t n,
                        const float* qx, const float* qy, const float* qz, int64_t nq, double r,
                        int64_t* d_counts, int32_t* d_idx, float* d_d2, int64_t cap);
+// after a synchronisation of ctx->stream: the last fpfh_dev's statistics and capacity check
+void fpfh_resolve(pfx_ctx* ctx);
 void fpfh_dev(pfx_ctx* ctx, const float* sx, const float* sy, const float* sz, const float* snx,
               const float* sny, const float* snz, int64_t ns, const float* qx, const float* qy,
               const float* qz, int64_t nq, int same, double r, float* out,

@@ -1,6 +1,6 @@
 #!/bin/bash
-# kernel-trace timeline of the bench step (for stream-overlap analysis with scripts/timeline.py)
-TAG=${1:-trace}; W=${2:-fpfh}
+# GPU-box: kernel trace of a short bench run (timeline / idle-gap analysis with scripts/gaps.py).
 R=$PWD; mkdir -p gpurun_out
-cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $R/gpurun_out/$TAG -o run -- python3 $R/bench.py --workload $W --steps 2 --warmup 1 --no-cpu-baseline > $R/gpurun_out/$TAG.log 2>&1 || { tail -20 $R/gpurun_out/$TAG.log; exit 1; }
-python3 $R/scripts/timeline.py $(find $R/gpurun_out/$TAG -name "*kernel_trace.csv" | head -1)
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $R/gpurun_out/trace -o run -- python3 $R/bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-e2e > $R/gpurun_out/trace.log 2>&1 || { tail -20 $R/gpurun_out/trace.log; exit 1; }
+cd $R && python3 scripts/gaps.py gpurun_out/trace/run_kernel_trace.csv

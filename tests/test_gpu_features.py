@@ -175,17 +175,17 @@ def test_config1_normals_fpfh_all_points():
 
 
 def test_fpfh_deferred_pair_queue_overflow(ctx, monkeypatch):
-    """Pairs the fast binning path cannot certify are queued for the exact path; a queue too
-    small for the cloud makes fpfh_dev rerun with the reported size -- same descriptors."""
+    """Pairs the fast binning path cannot certify are queued for the exact path; past the
+    queue's capacity the SPFH kernel runs the exact path in place -- same descriptors."""
     x, y, z = _cloud("indoor_source")
     nx, ny, nz, _ = O.normals(x, y, z, 0.05)
     rng = np.random.default_rng(6)
     q = np.sort(rng.choice(len(x), 400, replace=False))
     base = ctx.fpfh(x, y, z, nx, ny, nz, x[q], y[q], z[q], 0.08)
-    assert ctx.stat("fpfh_spfh_exact_pairs") > 4 and ctx.stat("fpfh_spfh_reruns") == 0
+    assert ctx.stat("fpfh_spfh_exact_pairs") > 4 and ctx.stat("fpfh_spfh_inline_exact") == 0
     monkeypatch.setenv("PFX_FPFH_SLOW_CAP", "4")
     g = ctx.fpfh(x, y, z, nx, ny, nz, x[q], y[q], z[q], 0.08)
-    assert ctx.stat("fpfh_spfh_reruns") == 1
+    assert ctx.stat("fpfh_spfh_exact_pairs") == 4 and ctx.stat("fpfh_spfh_inline_exact") > 0
     assert _nan_aware_equal(g, base)
     assert _nan_aware_equal(g, O.fpfh(x, y, z, nx, ny, nz, x[q], y[q], z[q], 0.08))
 
