@@ -536,6 +536,7 @@ __global__ void k_surface_change(Img I, const float4* __restrict__ P, const floa
 constexpr int kWinWords = 2048;     // 65,536-pixel window (e.g. 256 x 256)
 constexpr int kFullWords = 9600;    // 640 x 480 bits
 constexpr int kQueue = 2048;        // ring buffer of pending pixels
+constexpr int kContribCap = 2048;   // k_interest_ff: contributing pixels compacted per batch (4 KB LDS)
 
 __device__ __forceinline__ float norm_angle(float a) {
   const float pi = 3.14159265358979323846f;
@@ -632,7 +633,9 @@ __device__ __forceinline__ int angle_cell(float dvx, float d90, float d180) {
 
 struct InterestParams {
   float radius_squared, radius_reciprocal, min_scs, opt_dist, d90, d180;
+  float prune_below;  // sparse mode: min_interest_value (pixels that cannot reach it may stay 0); else -1
   double R;  // search radius for the window bound
+  double R_prune;  // sparse mode: radius within which a pixel can reach pos >= min_interest_value
 };
 
 // region-grow window of pixel (x, y): |du| <= fx R (tz + |tx|) / ((tz - R) tz) (+3 px margin
@@ -655,13 +658,17 @@ __device__ __forceinline__ void interest_window(const Img& I, float4 point, int 
 // NarfKeypoint's per-pixel contribution of an accepted pixel with scs >= min_scs: histogram
 // maximum of the positive score per direction cell, minimum of the negative score (both
 // order-free, LDS atomics on float bit patterns of non-negative values)
+__device__ __forceinline__ float negative_score(const InterestParams& ip, float sc, float df) {
+  const float neg = 1.0f - 0.5f * sc * fmaxf(1.0f - df / ip.opt_dist, 0.0f);
+  return neg * neg;
+}
+
 __device__ __forceinline__ void contribute(const InterestParams& ip, float sc, float4 dv, float d2, float pd, f3 tmp0,
                                            f3 tmp1, f3 tmp2, unsigned* hist, unsigned* neg_bits) {
   const f3 dir = mk3(dv.x, dv.y, dv.z);
   const float distance = sqrtf(d2);
   const float df = ip.radius_reciprocal * distance;
-  float neg = 1.0f - 0.5f * sc * fmaxf(1.0f - df / ip.opt_dist, 0.0f);
-  neg = neg * neg;
+  const float neg = negative_score(ip, sc, df);
   const float pos = (pd < 2.0f) ? sc : sc * (1.0f - df);
   const f3 rot = mk3(0.0f + dot3(tmp0, dir), 0.0f + dot3(tmp1, dir), 0.0f + dot3(tmp2, dir));
   const float nrm = sqrtf(rot.x * rot.x + rot.y * rot.y);
@@ -811,6 +818,68 @@ __global__ void __launch_bounds__(64) k_interest(Img I, const float4* __restrict
   }
 }
 
+// Which pixels need the region grow: valid, not shadow / veil, and a contributing pixel in the
+// window (summed-area table).  Sparse mode (prune_below = min_interest_value) adds two bounds
+// under which the pixel cannot reach min_interest_value (its interest then stays 0):
+//  * p and its accepted contributing 8-neighbours are always in the region (pd <= 1 needs no
+//    distance test), so interest = neg * sqrt(acv) <= their smallest negative score (acv <= 1);
+//  * interest <= max pos (acv <= pos_max^2, neg <= 1) and pos = sc (1 - d / R) for pd >= 2 with
+//    sc <= 1, so only a contributing pixel with scs >= min_interest_value within
+//    R_prune = R (1 - 0.99 min_interest_value) of p (or within 2 px) can lift p to it.
+// Pixels that pass are listed for k_interest_ff; every other pixel's interest is written as 0.
+__global__ void __launch_bounds__(256) k_interest_classify(Img I, const float4* __restrict__ P,
+                                                           const float4* __restrict__ PK,
+                                                           const uint32_t* __restrict__ traits,
+                                                           const float* __restrict__ scs,
+                                                           const int* __restrict__ rowp, InterestParams ip,
+                                                           float* __restrict__ interest, int* __restrict__ list,
+                                                           int* __restrict__ n_list,
+                                                           unsigned long long* __restrict__ work) {
+  const int index = blockIdx.x * blockDim.x + threadIdx.x;
+  const int lane = threadIdx.x & 63;
+  const uint32_t skip = TB(T_SHADOW_BORDER) | TB(T_VEIL_POINT);
+  bool grow = false, pruned = false;
+  if (index < I.w * I.h) {
+    const float4 point = P[index];
+    if (isfinite(point.w) && !(traits[index] & skip)) {
+      const int y = index / I.w, x = index - y * I.w;
+      grow = true;
+      if (ip.prune_below > 0.0f) {
+        float nb = 1.0f;
+        for (int k = 0; k < 9; ++k) {
+          const int xq = x + k % 3 - 1, yq = y + k / 3 - 1;
+          if (xq < 0 || xq >= I.w || yq < 0 || yq >= I.h) continue;
+          const int iq = yq * I.w + xq;
+          const float4 q = PK[iq];
+          if ((__float_as_uint(q.w) & 3u) != 3u) continue;
+          const float df = ip.radius_reciprocal * sqrtf(sq_dist(point, q));
+          nb = fminf(nb, negative_score(ip, scs[iq], df));
+        }
+        int a0, b0, aw, bh;
+        interest_window(I, point, x, y, ip.R_prune, a0, b0, aw, bh);
+        pruned = nb < ip.prune_below || !window_contributes(I, rowp, a0, b0, aw, bh, lane);
+        grow = !pruned;
+      }
+      if (grow) {
+        int x0, y0, ww, wh;
+        interest_window(I, point, x, y, ip.R, x0, y0, ww, wh);
+        grow = window_contributes(I, rowp, x0, y0, ww, wh, lane);
+      }
+    }
+    if (!grow) interest[index] = 0.0f;
+  }
+  const uint64_t m = __ballot(grow);
+  if (m) {
+    const int leader = __builtin_ctzll(m);
+    int base = 0;
+    if (lane == leader) base = atomicAdd(n_list, __popcll(m));
+    base = __shfl(base, leader);
+    if (grow) list[base + __popcll(m & ((1ull << lane) - 1ull))] = index;
+  }
+  const uint64_t mp = __ballot(pruned);
+  if (mp && lane == 0 && work) atomicAdd(&work[3], (unsigned long long)__popcll(mp));
+}
+
 // ---- flood-fill region grow (windows of <= 128 rows x <= 128 columns) ---------------------
 // Lane l holds rows l and l + 64 of the window, each as two 64-bit masks: A = pixels the region
 // grow accepts (valid, not shadow/veil, within 2 px or R of p) and C = accepted pixels that
@@ -820,6 +889,11 @@ __global__ void __launch_bounds__(64) k_interest(Img I, const float4* __restrict
 struct Rows2 {  // [half h: rows l + 64 h][word w: columns 64 w .. 64 w + 63]
   uint64_t m00 = 0, m01 = 0, m10 = 0, m11 = 0;
 };
+
+// m of lane l <- v (v and l wave-uniform): one compare and two v_cndmask
+__device__ __forceinline__ void put_row(uint64_t& m, uint64_t v, int l) {
+  m = ((int)threadIdx.x == l) ? v : m;
+}
 
 // horizontal 3-dilation of one row held as (lo, hi) words
 __device__ __forceinline__ void hdil(uint64_t lo, uint64_t hi, uint64_t& dlo, uint64_t& dhi) {
@@ -841,69 +915,62 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8)))
                                                     const uint32_t* __restrict__ traits,
                                                     const float* __restrict__ scs, const float4* __restrict__ scd,
                                                     const int* __restrict__ rowp, InterestParams ip,
+                                                    const int* __restrict__ list, const int* __restrict__ n_list,
                                                     float* __restrict__ interest, int* __restrict__ fallback,
                                                     int* __restrict__ n_fallback, int* __restrict__ err,
                                                     unsigned long long* __restrict__ work) {
   __shared__ unsigned hist[18];
   __shared__ unsigned neg_bits;
+  __shared__ uint16_t s_px[kContribCap];
   const int lane = threadIdx.x;
-  const int npx = I.w * I.h;
-  const uint32_t skip = TB(T_SHADOW_BORDER) | TB(T_VEIL_POINT);
   unsigned long long n_grown = 0, n_window = 0, n_visits = 0;
-  for (int index = blockIdx.x; index < npx; index += gridDim.x) {
+  const int n = *n_list;
+  for (int it = blockIdx.x; it < n; it += gridDim.x) {
+    const int index = list[it];
     const float4 point = P[index];
-    if (!isfinite(point.w) || (traits[index] & skip)) {
-      if (lane == 0) interest[index] = 0.0f;
-      continue;
-    }
     const int y = index / I.w, x = index - y * I.w;
     int x0, y0, ww, wh;
-    FF_T(q0);
     interest_window(I, point, x, y, ip.R, x0, y0, ww, wh);
-    const bool contributes = window_contributes(I, rowp, x0, y0, ww, wh, lane);
-    FF_T(q1);
-    FF_ADD(0, q0, q1);
-    if (!contributes) {  // nothing can contribute: interest 0
-      if (lane == 0) interest[index] = 0.0f;
-      continue;
-    }
     if (wh > 128 || ww > 128) {
       if (lane == 0) fallback[atomicAdd(n_fallback, 1)] = index;
       continue;
     }
     // acceptance / contribution masks (lanes = columns); four rows per iteration so that their
     // loads are in flight together (the window rows are independent)
+    // branch-free per row: the two ballots are the row's masks, written into lane (r & 63) with
+    // v_writelane (the row, half and word are wave-uniform)
     Rows2 A, C;
+    const int nwd = ww > 64 ? 2 : 1;
     for (int r0 = 0; r0 < wh; r0 += 4) {
-      for (int wd = 0; wd * 64 < ww; ++wd) {
+      for (int wd = 0; wd < nwd; ++wd) {
         const int c = wd * 64 + lane;
         const bool col = c < ww;
+        const int cc = col ? c : 0;
         float4 p2[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
           const int rr = r0 + u < wh ? r0 + u : wh - 1;  // clamped: rows past the window are ignored
-          p2[u] = PK[(y0 + rr) * I.w + x0 + (col ? c : 0)];
+          p2[u] = PK[(y0 + rr) * I.w + x0 + cc];
         }
+        const int adx = abs(x0 + cc - x);
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
           const int r = r0 + u;
           if (r >= wh) break;  // wave-uniform
-          bool acc = false, con = false;
-          if (col) {
-            const uint32_t f = __float_as_uint(p2[u].w);
-            acc = f & 1u;
-            const float pd = (float)max(abs(x0 + c - x), abs(y0 + r - y));
-            const float d2 = sq_dist(point, p2[u]);
-            if (acc && pd > 2.0f && d2 > ip.radius_squared) acc = false;
-            con = acc && (f & 2u);
-          }
+          const uint32_t f = __float_as_uint(p2[u].w);
+          const int pd = max(adx, abs(y0 + r - y));
+          const float d2 = sq_dist(point, p2[u]);
+          // PCL: accepted unless (pd > 2 && d2 > R^2)
+          const bool acc = col & ((f & 1u) != 0u) & ((pd <= 2) | !(d2 > ip.radius_squared));
+          const bool con = acc & ((f & 2u) != 0u);
           const uint64_t ma = __ballot(acc), mc = __ballot(con);
-          const bool mine = lane == (r & 63), hi = r >= 64;
-          if (mine) {
-            if (!hi && wd == 0) { A.m00 = ma; C.m00 = mc; }
-            if (!hi && wd == 1) { A.m01 = ma; C.m01 = mc; }
-            if (hi && wd == 0) { A.m10 = ma; C.m10 = mc; }
-            if (hi && wd == 1) { A.m11 = ma; C.m11 = mc; }
+          const int l = r & 63;
+          if (r < 64) {
+            if (wd == 0) { put_row(A.m00, ma, l); put_row(C.m00, mc, l); }
+            else { put_row(A.m01, ma, l); put_row(C.m01, mc, l); }
+          } else {
+            if (wd == 0) { put_row(A.m10, ma, l); put_row(C.m10, mc, l); }
+            else { put_row(A.m11, ma, l); put_row(C.m11, mc, l); }
           }
         }
       }
@@ -961,42 +1028,49 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8)))
     if (lane == 0) neg_bits = __float_as_uint(1.0f);
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
+    {
+      // the accepted contributing pixels compacted into LDS as window-relative (row << 8 | col)
+      // (lane l lists rows l and 64 + l), then contributed 64 at a time by full waves
+      const uint64_t M00 = R.m00 & C.m00, M01 = R.m01 & C.m01, M10 = R.m10 & C.m10, M11 = R.m11 & C.m11;
+      const int c0 = __popcll(M00) + __popcll(M01), c1 = __popcll(M10) + __popcll(M11);
+      int i0 = c0, i1 = c1;
 #pragma unroll
-    for (int half = 0; half < 2; ++half) {
-      const uint64_t M0 = half ? (R.m10 & C.m10) : (R.m00 & C.m00);
-      const uint64_t M1 = half ? (R.m11 & C.m11) : (R.m01 & C.m01);
-      uint64_t rows = __ballot((M0 | M1) != 0);
-      while (rows) {  // up to four rows per iteration: their loads in flight together
-        int rr[4];
-        uint64_t mm[4][2];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          rr[u] = rows ? __builtin_ctzll(rows) : -1;
-          if (rows) rows &= rows - 1;
-          mm[u][0] = rr[u] >= 0 ? __shfl(M0, rr[u]) : 0ull;
-          mm[u][1] = rr[u] >= 0 ? __shfl(M1, rr[u]) : 0ull;
+      for (int o = 1; o < 64; o <<= 1) {
+        const int a = __shfl_up(i0, o), b = __shfl_up(i1, o);
+        if (lane >= o) { i0 += a; i1 += b; }
+      }
+      const int tot0 = __shfl(i0, 63);
+      const int T = tot0 + __shfl(i1, 63);
+      for (int base = 0; base < T; base += kContribCap) {
+        int p = i0 - c0 - base;
+        auto emit = [&](uint64_t m, int row, int col0) {
+          while (m) {
+            const int b = __builtin_ctzll(m);
+            m &= m - 1;
+            if (p >= 0 && p < kContribCap) s_px[p] = (uint16_t)((row << 8) | (col0 + b));
+            ++p;
+          }
+        };
+        emit(M00, lane, 0);
+        emit(M01, lane, 64);
+        p = tot0 + i1 - c1 - base;
+        emit(M10, 64 + lane, 0);
+        emit(M11, 64 + lane, 64);
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        const int nb = min(T - base, kContribCap);
+        for (int e = lane; e < nb; e += 64) {
+          const int v = s_px[e];
+          const int xx = x0 + (v & 255), yy = y0 + (v >> 8);
+          const int idx2 = yy * I.w + xx;
+          const float4 p2 = PK[idx2];
+          const float sv = scs[idx2];
+          const float4 dv = scd[idx2];
+          const float pd = (float)max(abs(xx - x), abs(yy - y));
+          contribute(ip, sv, dv, sq_dist(point, p2), pd, tmp0, tmp1, tmp2, hist, &neg_bits);
         }
-        float4 p2[4][2], dv[4][2];
-        float sv[4][2];
-#pragma unroll
-        for (int u = 0; u < 4; ++u)
-#pragma unroll
-          for (int wd = 0; wd < 2; ++wd) {
-            const bool on = (mm[u][wd] >> lane) & 1ull;
-            const int idx2 = on ? (y0 + 64 * half + rr[u]) * I.w + x0 + wd * 64 + lane : 0;
-            p2[u][wd] = on ? PK[idx2] : make_float4(0.f, 0.f, 0.f, 0.f);
-            sv[u][wd] = on ? scs[idx2] : 0.f;
-            dv[u][wd] = on ? scd[idx2] : make_float4(0.f, 0.f, 0.f, 0.f);
-          }
-#pragma unroll
-        for (int u = 0; u < 4; ++u)
-#pragma unroll
-          for (int wd = 0; wd < 2; ++wd) {
-            if (!((mm[u][wd] >> lane) & 1ull)) continue;
-            const int xx = x0 + wd * 64 + lane, yy = y0 + 64 * half + rr[u];
-            const float pd = (float)max(abs(xx - x), abs(yy - y));
-            contribute(ip, sv[u][wd], dv[u][wd], sq_dist(point, p2[u][wd]), pd, tmp0, tmp1, tmp2, hist, &neg_bits);
-          }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+        __builtin_amdgcn_wave_barrier();
       }
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -1157,7 +1231,7 @@ int64_t narf_dev(pfx_ctx* ctx, const float* x, const float* y, const float* z, i
   float4* scd = S.scd.as<float4>(npx);
   float* interest = S.interest.as<float>(npx);
   int* cand = S.cand.as<int>(npx);
-  int* counters = S.counters.as<int>(4);
+  int* counters = S.counters.as<int>(5);
   {
     TimeScope ts(ctx, "narf_border");
     const int step = (p.pixel_radius_plane_extraction / 2) + 1;
@@ -1192,7 +1266,9 @@ int64_t narf_dev(pfx_ctx* ctx, const float* x, const float* y, const float* z, i
   ip.d90 = 90.0f * deg;
   ip.d180 = 180.0f * deg;
   ip.R = search_radius;
-  PFX_HIP(hipMemsetAsync(counters, 0, 4 * sizeof(int), st));
+  ip.prune_below = p.calculate_sparse_interest_image ? p.min_interest_value : -1.0f;
+  ip.R_prune = ip.R * std::max(0.0, 1.0 - 0.99 * (double)p.min_interest_value);
+  PFX_HIP(hipMemsetAsync(counters, 0, 5 * sizeof(int), st));
   int* rowp = S.rowp.as<int>((I.w + 1) * I.h);
   int* sat = S.sat.as<int>((I.w + 1) * (I.h + 1));
   unsigned long long* work = S.work.as<unsigned long long>(4);
@@ -1210,8 +1286,12 @@ int64_t narf_dev(pfx_ctx* ctx, const float* x, const float* y, const float* z, i
     int* fb1 = S.fb1.as<int>(npx);
     float4* pk = S.pk.as<float4>(npx);
     k_pack_px<<<nblk(npx), 256, 0, st>>>(I, P, traits, scs, ip.min_scs, pk);
-    k_interest_ff<<<256 * 16, 64, 0, st>>>(I, P, pk, traits, scs, scd, sat, ip, interest, fb1, counters + 3,
-                                            counters + 1, work);
+    int* grow_list = reinterpret_cast<int*>(uL);  // uL is dead after k_classify
+    k_interest_classify<<<nblk(npx), 256, 0, st>>>(I, P, pk, traits, scs, sat, ip, interest, grow_list, counters + 4,
+                                                   work);
+    check_launch("k_interest_classify");
+    k_interest_ff<<<256 * 16, 64, 0, st>>>(I, P, pk, traits, scs, scd, sat, ip, grow_list, counters + 4, interest,
+                                            fb1, counters + 3, counters + 1, work);
     check_launch("k_interest_ff");
     // windows beyond the flood-fill masks: queue-based grow in a windowed LDS bitmap
     k_interest<kWinWords, false><<<256 * 4, 64, 0, st>>>(I, P, traits, scs, scd, sat, ip, fb1, counters + 3,
@@ -1253,6 +1333,7 @@ int64_t narf_dev(pfx_ctx* ctx, const float* x, const float* y, const float* z, i
   ctx->stats["narf_interest_queue_grown"] = h_cnt[3];
   ctx->stats["narf_interest_window_px"] = (int64_t)h_work[1];
   ctx->stats["narf_interest_visits"] = (int64_t)h_work[2];
+  ctx->stats["narf_interest_pruned"] = (int64_t)h_work[3];
   if (h_cnt[1] & 1) throw Error(PFX_ERR_CAPACITY, "narf: interest region-grow queue overflow");
   if (h_cnt[1] & 2) throw Error(PFX_ERR_DEVICE, "narf: interest region left its window bound (internal error)");
   const int nc = h_cnt[0];
