@@ -1290,7 +1290,7 @@ int64_t narf_dev(pfx_ctx* ctx, const float* x, const float* y, const float* z, i
     k_interest_classify<<<nblk(npx), 256, 0, st>>>(I, P, pk, traits, scs, sat, ip, interest, grow_list, counters + 4,
                                                    work);
     check_launch("k_interest_classify");
-    k_interest_ff<<<256 * 16, 64, 0, st>>>(I, P, pk, traits, scs, scd, sat, ip, grow_list, counters + 4, interest,
+    k_interest_ff<<<256 * 20, 64, 0, st>>>(I, P, pk, traits, scs, scd, sat, ip, grow_list, counters + 4, interest,
                                             fb1, counters + 3, counters + 1, work);
     check_launch("k_interest_ff");
     // windows beyond the flood-fill masks: queue-based grow in a windowed LDS bitmap
