@@ -120,6 +120,9 @@ void pfx_ctx_destroy(pfx_ctx* ctx) {
   for (auto& p : ctx->timer.pending) { (void)hipEventDestroy(p.a); (void)hipEventDestroy(p.b); }
   for (auto e : ctx->timer.pool) (void)hipEventDestroy(e);
   if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);
+  if (ctx->side) (void)hipStreamDestroy(ctx->side);
+  for (auto& e : ctx->fork_ev)
+    if (e) (void)hipEventDestroy(e);
   if (ctx->host_rb) (void)hipHostFree(ctx->host_rb);
   if (ctx->fpfh_rb_mem) (void)hipHostFree(ctx->fpfh_rb_mem);
   delete ctx;

@@ -131,6 +131,14 @@ struct pfx_ctx {
     if (!fpfh_rb_mem) PFX_HIP(hipHostMalloc(&fpfh_rb_mem, sizeof(pfx::FpfhReadback), hipHostMallocDefault));
     return static_cast<pfx::FpfhReadback*>(fpfh_rb_mem);
   }
+  // one side stream + fork/join events (normal estimation's long-list chains), created on first use
+  hipStream_t side = nullptr;
+  hipEvent_t fork_ev[2] = {nullptr, nullptr};
+  void ensure_side() {
+    if (side) return;
+    PFX_HIP(hipStreamCreateWithFlags(&side, hipStreamNonBlocking));
+    for (auto& e : fork_ev) PFX_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  }
   // small pinned host block for the per-call readbacks (counters, cursors): one D2H copy of
   // pinned memory per synchronisation instead of staged pageable copies
   void* host_rb = nullptr;

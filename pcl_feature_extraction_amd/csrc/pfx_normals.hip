@@ -336,10 +336,7 @@ __device__ __forceinline__ void chain_wg(ChainLds<CAP>& S, const GridView& g, co
   const bool rec = wm && lane == __builtin_ctzll(wm);
 #endif
   if (!active) return;
-  if (k > kLaneMax) {
-    longq[wave_push_slot(n_long)] = (int32_t)j;
-    return;
-  }
+  if (k > kLaneMax) return;  // listed by k_long_lists, chained by k_normals_long
   const uint32_t* lst = L.list + L.off[j];
   const int lg = L.lg[j];
   float a[9];
@@ -421,6 +418,15 @@ struct LongLds {
   float c[2][3][kPerWave][kLB];  // double-buffered x | y | z per query and step (5.3 KB)
   int32_t rtab[kPerWave * 9];
 };
+
+// the lists longer than kLaneMax of this pass (mask[caller] == want), for k_normals_long
+__global__ void __launch_bounds__(256) k_long_lists(GridView g, NbLists L, const uint8_t* __restrict__ mask, int want,
+                                                    int32_t* __restrict__ longq, int* __restrict__ n_long) {
+  const int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  bool push = false;
+  if (j < L.nq && L.cnt[j] > kLaneMax) push = !mask || ((mask[g.perm[L.qpos[j]]] != 0) == (want != 0));
+  if (push) longq[wave_push_slot(n_long)] = (int32_t)j;
+}
 
 __global__ void __launch_bounds__(256) k_normals_long(GridView g, NbLists L, const int32_t* __restrict__ longq,
                                                       const int* __restrict__ n_long, float vpx, float vpy,
@@ -615,6 +621,21 @@ void normals_chains_dev(pfx_ctx* ctx, pfx_ctx* owner, const uint8_t* mask, int w
   int* n_long = ctx->buf("normals_nlong").as<int>(5);
   PFX_HIP(hipMemsetAsync(n_long, 0, 5 * sizeof(int), st));
   const int64_t nb = ceil_div(L.nq, 256);
+  // the long lists first: their chains (k_normals_long, bound by the longest list) run on a side
+  // stream concurrently with the short-list chains, which leave them out
+  k_long_lists<<<(unsigned)nb, 256, 0, st>>>(view(G), L, mask, want, longq, n_long);
+  check_launch("k_long_lists");
+  ctx->ensure_side();
+  PFX_HIP(hipEventRecord(ctx->fork_ev[0], st));
+  PFX_HIP(hipStreamWaitEvent(ctx->side, ctx->fork_ev[0], 0));
+  {
+    // persistent: the queue length stays on the device (no host round trip)
+    // (sized to what is resident at once: waves beyond it would wait for a second round)
+    const int64_t lb = std::min<int64_t>(ceil_div(L.nq, 7 * 4), 256 * 4);
+    k_normals_long<<<(unsigned)lb, 256, 0, ctx->side>>>(view(G), L, longq, n_long, vp[0], vp[1], vp[2], nx, ny, nz,
+                                                        curv);
+    check_launch("k_normals_long");
+  }
   {
     // natural block order = round-robin over the 8 XCDs: the dense (heavy) workgroups cluster in
     // space, so contiguous per-XCD slices would leave one XCD with ~1.4x the mean work
@@ -639,12 +660,9 @@ void normals_chains_dev(pfx_ctx* ctx, pfx_ctx* owner, const uint8_t* mask, int w
     check_launch("k_normals_chain_big");
   }
   {
-    TimeScope ts(ctx, "normals_long");
-    // persistent: the queue length stays on the device (no host round trip)
-    // (sized to what is resident at once: waves beyond it would wait for a second round)
-    const int64_t lb = std::min<int64_t>(ceil_div(L.nq, 7 * 4), 256 * 4);
-    k_normals_long<<<(unsigned)lb, 256, 0, st>>>(view(G), L, longq, n_long, vp[0], vp[1], vp[2], nx, ny, nz, curv);
-    check_launch("k_normals_long");
+    TimeScope ts(ctx, "normals_long");  // the join: what the long chains add after the short ones
+    PFX_HIP(hipEventRecord(ctx->fork_ev[1], ctx->side));
+    PFX_HIP(hipStreamWaitEvent(st, ctx->fork_ev[1], 0));
   }
   static const bool verbose = getenv("PFX_VERBOSE_STATS") != nullptr;
   if (verbose) {  // diagnostics only (host sync): how the chain workgroups fetched
