@@ -895,6 +895,23 @@ __device__ __forceinline__ void put_row(uint64_t& m, uint64_t v, int l) {
   m = ((int)threadIdx.x == l) ? v : m;
 }
 
+// whole-wave lane shifts by one (DPP wave_shr:1 / wave_shl:1, no LDS round trip): lane i gets
+// lane i - 1 (up) or lane i + 1 (down); the lane shifted in from outside the wave gets 0
+__device__ __forceinline__ uint64_t lane_up1(uint64_t v) {
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)v, 0x138, 0xf, 0xf, true);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)(v >> 32), 0x138, 0xf, 0xf, true);
+  return ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo;
+}
+__device__ __forceinline__ uint64_t lane_dn1(uint64_t v) {
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)v, 0x130, 0xf, 0xf, true);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)(v >> 32), 0x130, 0xf, 0xf, true);
+  return ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo;
+}
+__device__ __forceinline__ uint64_t lane_get(uint64_t v, int l) {  // l wave-uniform
+  return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l) << 32) |
+         (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
+}
+
 // horizontal 3-dilation of one row held as (lo, hi) words
 __device__ __forceinline__ void hdil(uint64_t lo, uint64_t hi, uint64_t& dlo, uint64_t& dhi) {
   dlo = lo | (lo << 1) | (lo >> 1) | (hi << 63);
@@ -910,7 +927,7 @@ __device__ unsigned long long g_ff_prof[8];  // cycles: window test, masks, floo
 #define FF_ADD(i, a, b)
 #endif
 
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8))) k_interest_ff(Img I, const float4* __restrict__ P,
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5, 8))) k_interest_ff(Img I, const float4* __restrict__ P,
                                                     const float4* __restrict__ PK,
                                                     const uint32_t* __restrict__ traits,
                                                     const float* __restrict__ scs, const float4* __restrict__ scd,
@@ -937,11 +954,15 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8)))
     }
     // acceptance / contribution masks (lanes = columns); four rows per iteration so that their
     // loads are in flight together (the window rows are independent)
-    // branch-free per row: the two ballots are the row's masks, written into lane (r & 63) with
-    // v_writelane (the row, half and word are wave-uniform)
+    FF_T(q1);
+    // Acceptance / contribution masks, computed lazily in groups of four rows (lanes = columns;
+    // branch-free per row: the two ballots are the row's masks, written into lane (r & 63)): the
+    // band of computed rows starts around p and grows while the component reaches its first or
+    // last row -- rows the component cannot reach are never loaded (outside the band A = 0, so
+    // the fill cannot enter them before they exist).
     Rows2 A, C;
     const int nwd = ww > 64 ? 2 : 1;
-    for (int r0 = 0; r0 < wh; r0 += 4) {
+    auto rows4 = [&](int r0) {
       for (int wd = 0; wd < nwd; ++wd) {
         const int c = wd * 64 + lane;
         const bool col = c < ww;
@@ -974,30 +995,39 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8)))
           }
         }
       }
-    }
-    FF_T(q2);
-    FF_ADD(1, q1, q2);
-    // 8-connected component of p in A
+    };
+    // does the component hold a pixel in window row r?  (wave-uniform)
     Rows2 R;
-    {
-      const int ry = y - y0, rx = x - x0;
-      if (lane == (ry & 63)) {
-        const uint64_t bit = 1ull << (rx & 63);
-        if (ry < 64) { if (rx < 64) R.m00 = bit; else R.m01 = bit; }
-        else { if (rx < 64) R.m10 = bit; else R.m11 = bit; }
-      }
+    auto row_hit = [&](int r) {
+      const uint64_t v = r < 64 ? (R.m00 | R.m01) : (R.m10 | R.m11);
+      const int l = r & 63;
+      return (__builtin_amdgcn_readlane((int)(uint32_t)v, l) | __builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), l)) != 0;
+    };
+    const int ry = y - y0, rx = x - x0;
+    // computed rows [blo, bhi), four-row groups, at first the groups of rows ry - 1 .. ry + 1
+    int blo = max(ry - 1, 0) & ~3, bhi = min(((ry + 1) | 3) + 1, wh);
+    for (int r0 = blo; r0 < bhi; r0 += 4) rows4(r0);
+    int rows_done = bhi - blo;
+    FF_T(q2);
+    // 8-connected component of p in A
+    if (lane == (ry & 63)) {
+      const uint64_t bit = 1ull << (rx & 63);
+      if (ry < 64) { if (rx < 64) R.m00 = bit; else R.m01 = bit; }
+      else { if (rx < 64) R.m10 = bit; else R.m11 = bit; }
     }
     while (true) {
       uint64_t h00, h01, h10, h11;
       hdil(R.m00, R.m01, h00, h01);
       hdil(R.m10, R.m11, h10, h11);
       // row above: lane-1 of the same half; lane 0 of the upper half takes lane 63 of the lower
-      uint64_t u00 = __shfl_up(h00, 1), u01 = __shfl_up(h01, 1), u10 = __shfl_up(h10, 1), u11 = __shfl_up(h11, 1);
-      const uint64_t l63_0 = __shfl(h00, 63), l63_1 = __shfl(h01, 63);
-      const uint64_t f0_0 = __shfl(h10, 0), f0_1 = __shfl(h11, 0);
-      uint64_t d00 = __shfl_down(h00, 1), d01 = __shfl_down(h01, 1), d10 = __shfl_down(h10, 1), d11 = __shfl_down(h11, 1);
-      if (lane == 0) { u00 = 0; u01 = 0; u10 = l63_0; u11 = l63_1; }
-      if (lane == 63) { d00 = f0_0; d01 = f0_1; d10 = 0; d11 = 0; }
+      uint64_t u00 = lane_up1(h00), u01 = lane_up1(h01), u10 = lane_up1(h10), u11 = lane_up1(h11);
+      uint64_t d00 = lane_dn1(h00), d01 = lane_dn1(h01), d10 = lane_dn1(h10), d11 = lane_dn1(h11);
+      if (wh > 64) {  // the two halves meet: row 63 (lane 63, lower) and row 64 (lane 0, upper)
+        const uint64_t l63_0 = lane_get(h00, 63), l63_1 = lane_get(h01, 63);
+        const uint64_t f0_0 = lane_get(h10, 0), f0_1 = lane_get(h11, 0);
+        if (lane == 0) { u10 = l63_0; u11 = l63_1; }
+        if (lane == 63) { d00 = f0_0; d01 = f0_1; }
+      }
       Rows2 N;
       N.m00 = (h00 | u00 | d00) & A.m00;
       N.m01 = (h01 | u01 | d01) & A.m01;
@@ -1005,7 +1035,21 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8)))
       N.m11 = (h11 | u11 | d11) & A.m11;
       const bool changed = N.m00 != R.m00 || N.m01 != R.m01 || N.m10 != R.m10 || N.m11 != R.m11;
       R = N;
-      if (!__ballot(changed)) break;
+      // the band grows as soon as the component reaches its edge row
+      bool grew = false;
+      if (blo > 0 && row_hit(blo)) {
+        blo -= 4;
+        rows4(blo);
+        rows_done += 4;
+        grew = true;
+      }
+      if (bhi < wh && row_hit(bhi - 1)) {
+        rows4(bhi);
+        rows_done += min(4, wh - bhi);
+        bhi = min(bhi + 4, wh);
+        grew = true;
+      }
+      if (!grew && !__ballot(changed)) break;
     }
     // checked invariant: the component stays strictly inside the window (unless at the image edge)
     {
@@ -1020,6 +1064,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8)))
       if (__ballot(edge) && lane == 0) atomicOr(err, 2);
     }
     FF_T(q3);
+    FF_ADD(1, q1, q2);
     FF_ADD(2, q2, q3);
     // contributions of the accepted contributing pixels
     f3 tmp0, tmp1, tmp2;
@@ -1084,7 +1129,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4, 8)))
     if (lane == 0) {
       interest[index] = interest_value(hist, neg_bits);
       n_grown += 1;
-      n_window += (unsigned long long)ww * wh;
+      n_window += (unsigned long long)ww * rows_done;
       n_visits += (unsigned long long)tot;
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -1318,7 +1363,7 @@ int64_t narf_dev(pfx_ctx* ctx, const float* x, const float* y, const float* z, i
     unsigned long long pr[8];
     PFX_HIP(hipStreamSynchronize(st));
     PFX_HIP(hipMemcpyFromSymbol(pr, HIP_SYMBOL(g_ff_prof), sizeof(pr)));
-    fprintf(stderr, "narf ff cycles (summed over pixels): window test %llu masks %llu flood %llu contrib %llu\n", pr[0],
+    fprintf(stderr, "narf ff cycles (summed over pixels): - %llu first rows %llu flood + lazy rows %llu contrib %llu\n", pr[0],
             pr[1], pr[2], pr[3]);
     const unsigned long long z[8] = {};
     PFX_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_ff_prof), z, sizeof(z)));
