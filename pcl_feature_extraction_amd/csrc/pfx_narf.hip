@@ -732,10 +732,6 @@ __global__ void __launch_bounds__(64) k_interest(Img I, const float4* __restrict
     const int y = index / I.w, x = index - y * I.w;
     int x0 = 0, y0 = 0, ww = I.w, wh = I.h;
     if (!FULL) interest_window(I, point, x, y, ip.R, x0, y0, ww, wh);
-    if (!window_contributes(I, sat, x0, y0, ww, wh, lane)) {  // nothing can contribute: interest 0
-      if (lane == 0) interest[index] = 0.0f;
-      continue;
-    }
     if (!FULL && (int64_t)ww * wh > (int64_t)WORDS * 32) {
       if (lane == 0) fallback[atomicAdd(n_fallback, 1)] = index;
       continue;
@@ -818,6 +814,36 @@ __global__ void __launch_bounds__(64) k_interest(Img I, const float4* __restrict
   }
 }
 
+// Sparse mode, reverse bound: interest(p) <= max pos over p's region (see k_interest_classify),
+// so p can reach min_interest_value only through a contributing pixel q (accepted, scs >= min_scs)
+// with pos(q) = sc_q (pd <= 1) or sc_q (1 - d / R) >= min_interest_value, i.e. sc_q >= it and
+// d = |p - q| <= R (1 - min_interest_value / sc_q).  One wave per such q (few: the high surface-
+// change pixels) marks every pixel within that distance (or within 1 px) -- the only candidates.
+__global__ void __launch_bounds__(256) k_interest_reach(Img I, const float4* __restrict__ PK,
+                                                        const float* __restrict__ scs, InterestParams ip,
+                                                        uint8_t* __restrict__ reach) {
+  const int lane = threadIdx.x & 63;
+  const int npx = I.w * I.h;
+  for (int q = blockIdx.x * 4 + (threadIdx.x >> 6); q < npx; q += gridDim.x * 4) {
+    const float4 pq = PK[q];
+    const float sc = scs[q];
+    if ((__float_as_uint(pq.w) & 3u) != 3u || !(sc >= ip.prune_below)) continue;  // wave-uniform
+    const int yq = q / I.w, xq = q - yq * I.w;
+    const double Rq = ip.R * std::max(0.0, 1.0 - 0.999 * (double)ip.prune_below / (double)sc);
+    const float rq2 = (float)(Rq * Rq * 1.0001);
+    int x0, y0, ww, wh;
+    interest_window(I, pq, xq, yq, Rq, x0, y0, ww, wh);
+    for (int r = 0; r < wh; ++r) {
+      const int py = y0 + r;
+      for (int c = lane; c < ww; c += 64) {
+        const int px = x0 + c, p = py * I.w + px;
+        const int pd = max(abs(px - xq), abs(py - yq));
+        if (pd <= 1 || sq_dist(pq, PK[p]) <= rq2) reach[p] = 1;
+      }
+    }
+  }
+}
+
 // Which pixels need the region grow: valid, not shadow / veil, and a contributing pixel in the
 // window (summed-area table).  Sparse mode (prune_below = min_interest_value) adds two bounds
 // under which the pixel cannot reach min_interest_value (its interest then stays 0):
@@ -832,6 +858,7 @@ __global__ void __launch_bounds__(256) k_interest_classify(Img I, const float4* 
                                                            const uint32_t* __restrict__ traits,
                                                            const float* __restrict__ scs,
                                                            const int* __restrict__ rowp, InterestParams ip,
+                                                           const uint8_t* __restrict__ reach,
                                                            float* __restrict__ interest, int* __restrict__ list,
                                                            int* __restrict__ n_list,
                                                            unsigned long long* __restrict__ work) {
@@ -843,24 +870,25 @@ __global__ void __launch_bounds__(256) k_interest_classify(Img I, const float4* 
     const float4 point = P[index];
     if (isfinite(point.w) && !(traits[index] & skip)) {
       const int y = index / I.w, x = index - y * I.w;
-      grow = true;
       if (ip.prune_below > 0.0f) {
-        float nb = 1.0f;
-        for (int k = 0; k < 9; ++k) {
-          const int xq = x + k % 3 - 1, yq = y + k / 3 - 1;
-          if (xq < 0 || xq >= I.w || yq < 0 || yq >= I.h) continue;
-          const int iq = yq * I.w + xq;
-          const float4 q = PK[iq];
-          if ((__float_as_uint(q.w) & 3u) != 3u) continue;
-          const float df = ip.radius_reciprocal * sqrtf(sq_dist(point, q));
-          nb = fminf(nb, negative_score(ip, scs[iq], df));
+        // sparse mode: k_interest_reach's mark (it implies a contributing pixel in the window,
+        // so no summed-area test), then the neighbours' negative-score bound
+        grow = reach[index] != 0;
+        if (grow) {
+          float nb = 1.0f;
+          for (int k = 0; k < 9; ++k) {
+            const int xq = x + k % 3 - 1, yq = y + k / 3 - 1;
+            if (xq < 0 || xq >= I.w || yq < 0 || yq >= I.h) continue;
+            const int iq = yq * I.w + xq;
+            const float4 q = PK[iq];
+            if ((__float_as_uint(q.w) & 3u) != 3u) continue;
+            const float df = ip.radius_reciprocal * sqrtf(sq_dist(point, q));
+            nb = fminf(nb, negative_score(ip, scs[iq], df));
+          }
+          grow = !(nb < ip.prune_below);
         }
-        int a0, b0, aw, bh;
-        interest_window(I, point, x, y, ip.R_prune, a0, b0, aw, bh);
-        pruned = nb < ip.prune_below || !window_contributes(I, rowp, a0, b0, aw, bh, lane);
-        grow = !pruned;
-      }
-      if (grow) {
+        pruned = !grow;
+      } else {
         int x0, y0, ww, wh;
         interest_window(I, point, x, y, ip.R, x0, y0, ww, wh);
         grow = window_contributes(I, rowp, x0, y0, ww, wh, lane);
@@ -1324,16 +1352,23 @@ int64_t narf_dev(pfx_ctx* ctx, const float* x, const float* y, const float* z, i
     // if a contributing pixel with scs >= min_interest_value lies in its region (interest =
     // neg * sqrt(max h1 h2 nd) <= max scs, neg <= 1); pixels without one keep interest 0, which
     // changes no keypoint (NMS and selection only look at pixels >= min_interest_value).
-    const float thr = p.calculate_sparse_interest_image
-                          ? std::max(ip.min_scs, p.min_interest_value * 0.9999f) : ip.min_scs;
-    k_contrib_rows<<<I.h, 1024, 0, st>>>(I, P, traits, scs, thr, rowp);
-    k_contrib_sat<<<(unsigned)((I.w + 1 + 255) / 256), 256, 0, st>>>(I, rowp, sat);
+    // (sparse mode: k_interest_reach's marks replace the summed-area window test)
+    if (!p.calculate_sparse_interest_image) {
+      k_contrib_rows<<<I.h, 1024, 0, st>>>(I, P, traits, scs, ip.min_scs, rowp);
+      k_contrib_sat<<<(unsigned)((I.w + 1 + 255) / 256), 256, 0, st>>>(I, rowp, sat);
+    }
     int* fb1 = S.fb1.as<int>(npx);
     float4* pk = S.pk.as<float4>(npx);
     k_pack_px<<<nblk(npx), 256, 0, st>>>(I, P, traits, scs, ip.min_scs, pk);
     int* grow_list = reinterpret_cast<int*>(uL);  // uL is dead after k_classify
-    k_interest_classify<<<nblk(npx), 256, 0, st>>>(I, P, pk, traits, scs, sat, ip, interest, grow_list, counters + 4,
-                                                   work);
+    uint8_t* reach = S.svalid.as<uint8_t>(npx);    // svalid is dead after k_surface_change
+    if (ip.prune_below > 0.0f) {
+      PFX_HIP(hipMemsetAsync(reach, 0, npx, st));
+      k_interest_reach<<<512, 256, 0, st>>>(I, pk, scs, ip, reach);
+      check_launch("k_interest_reach");
+    }
+    k_interest_classify<<<nblk(npx), 256, 0, st>>>(I, P, pk, traits, scs, sat, ip, reach, interest, grow_list,
+                                                   counters + 4, work);
     check_launch("k_interest_classify");
     k_interest_ff<<<256 * 20, 64, 0, st>>>(I, P, pk, traits, scs, scd, sat, ip, grow_list, counters + 4, interest,
                                             fb1, counters + 3, counters + 1, work);
@@ -1342,16 +1377,11 @@ int64_t narf_dev(pfx_ctx* ctx, const float* x, const float* y, const float* z, i
     k_interest<kWinWords, false><<<256 * 4, 64, 0, st>>>(I, P, traits, scs, scd, sat, ip, fb1, counters + 3,
                                                           interest, cand, counters + 2, counters + 1, work);
     check_launch("k_interest");
-    int nfb = 0;
-    PFX_HIP(hipMemcpyAsync(&nfb, counters + 2, sizeof(int), hipMemcpyDeviceToHost, st));
-    PFX_HIP(hipStreamSynchronize(st));
-    ctx->stats["narf_interest_fullimage"] = nfb;
-    if (nfb > 0) {
-      k_interest<kFullWords, true><<<std::min(nfb, 256 * 3), 64, 0, st>>>(I, P, traits, scs, scd, sat, ip, cand,
-                                                                          counters + 2, interest, nullptr, nullptr,
-                                                                          counters + 1, work);
-      check_launch("k_interest_full");
-    }
+    // beyond the windowed bitmap: the whole image (the count stays on the device; no host round
+    // trip -- the workgroups exit at once when there is nothing to grow)
+    k_interest<kFullWords, true><<<256 * 3, 64, 0, st>>>(I, P, traits, scs, scd, sat, ip, cand, counters + 2,
+                                                          interest, nullptr, nullptr, counters + 1, work);
+    check_launch("k_interest_full");
   }
   {
     TimeScope ts(ctx, "narf_nms");
@@ -1375,6 +1405,7 @@ int64_t narf_dev(pfx_ctx* ctx, const float* x, const float* y, const float* z, i
   PFX_HIP(hipMemcpyAsync(h_work, work, sizeof(h_work), hipMemcpyDeviceToHost, st));
   PFX_HIP(hipStreamSynchronize(st));
   ctx->stats["narf_interest_grown"] = (int64_t)h_work[0];
+  ctx->stats["narf_interest_fullimage"] = h_cnt[2];
   ctx->stats["narf_interest_queue_grown"] = h_cnt[3];
   ctx->stats["narf_interest_window_px"] = (int64_t)h_work[1];
   ctx->stats["narf_interest_visits"] = (int64_t)h_work[2];
