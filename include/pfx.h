@@ -180,6 +180,14 @@ pfx_status pfx_fpfh_support_mask_dev(pfx_ctx* ctx, const float* d_sx, const floa
                                      int64_t n_surface, const float* d_qx, const float* d_qy,
                                      const float* d_qz, int64_t nq, double radius, uint8_t* d_mask);
 
+/* Conservative form of pfx_fpfh_support_mask_dev: d_mask[i] = 1 for every surface point within
+ * 2 * radius of a query (a superset of the normals FPFHEstimation reads, marked in one pass over
+ * the queries' 5x5x5 cell blocks instead of one per SPFH point).  Same contract for the next
+ * pfx_fpfh_dev on ctx. */
+pfx_status pfx_fpfh_support_ball_dev(pfx_ctx* ctx, const float* d_sx, const float* d_sy, const float* d_sz,
+                                     int64_t n_surface, const float* d_qx, const float* d_qy,
+                                     const float* d_qz, int64_t nq, double radius, uint8_t* d_mask);
+
 /* ---- SHOT-352: SHOTEstimationOMP + SHOTLocalReferenceFrameEstimation ---------------- */
 /* desc: nq x 352, rf: nq x 9 (x_axis, y_axis, z_axis) -- SHOT352::{descriptor, rf}. */
 pfx_status pfx_shot(pfx_ctx* ctx, const float* sx, const float* sy, const float* sz,

@@ -346,6 +346,18 @@ pfx_status pfx_fpfh_support_mask_dev(pfx_ctx* ctx, const float* d_sx, const floa
   PFX_API_END(ctx)
 }
 
+pfx_status pfx_fpfh_support_ball_dev(pfx_ctx* ctx, const float* d_sx, const float* d_sy, const float* d_sz,
+                                     int64_t n_surface, const float* d_qx, const float* d_qy, const float* d_qz,
+                                     int64_t nq, double radius, uint8_t* d_mask) {
+  PFX_API_BEGIN
+  check_ctx(ctx);
+  if (n_surface < 0 || nq < 0 || (n_surface && (!d_sx || !d_sy || !d_sz || !d_mask)) ||
+      (nq && (!d_qx || !d_qy || !d_qz)))
+    throw Error(PFX_ERR_INVALID, "fpfh support ball: invalid arguments");
+  pfx::fpfh_support_ball_dev(ctx, d_sx, d_sy, d_sz, n_surface, d_qx, d_qy, d_qz, nq, radius, d_mask);
+  PFX_API_END(ctx)
+}
+
 pfx_status pfx_shot_dev(pfx_ctx* ctx, const float* d_sx, const float* d_sy, const float* d_sz,
                         const float* d_snx, const float* d_sny, const float* d_snz, int64_t n_surface,
                         const float* d_qx, const float* d_qy, const float* d_qz, int64_t nq, double radius,

@@ -283,6 +283,34 @@ __global__ void __launch_bounds__(256) k_fpfh_mark_support(GridView g, const int
   }
 }
 
+// Conservative support: every surface point within 2r of a query (the r-neighbours of the
+// r-neighbours lie there).  One workgroup per query over the 5 x 5 x 5 cells around it (cells are
+// >= r, so the 2r ball is inside); a superset of k_fpfh_mark_support's set at a fraction of its
+// cost (no pass over the SPFH points).
+__global__ void __launch_bounds__(256) k_fpfh_mark_ball(GridView g, const float* __restrict__ qx,
+                                                        const float* __restrict__ qy, const float* __restrict__ qz,
+                                                        int64_t nq, float rr4, uint8_t* __restrict__ mask) {
+  for (int64_t q = blockIdx.x; q < nq; q += gridDim.x) {
+    const float x = qx[q], y = qy[q], z = qz[q];
+    if (!(isfinite(x) && isfinite(y) && isfinite(z))) continue;
+    const int64_t cx = (int64_t)floor(((double)x - g.ox) * g.inv);
+    const int64_t cy = (int64_t)floor(((double)y - g.oy) * g.inv);
+    const int64_t cz = (int64_t)floor(((double)z - g.oz) * g.inv);
+    const int64_t z0 = max<int64_t>(cz - 2, 0), z1 = min<int64_t>(cz + 2, g.nz - 1);
+    if (z0 > z1) continue;
+    for (int c = 0; c < 25; ++c) {
+      const int64_t ix = cx + c / 5 - 2, iy = cy + c % 5 - 2;
+      if (ix < 0 || ix >= g.nx || iy < 0 || iy >= g.ny) continue;
+      const int64_t base = (ix * g.ny + iy) * g.nz;
+      const int32_t p0 = g.cell_start[base + z0], p1 = g.cell_start[base + z1 + 1];
+      for (int32_t p = p0 + threadIdx.x; p < p1; p += blockDim.x) {
+        const float4 c4 = g.sp[p];
+        if (flann_d2(x, y, z, c4.x, c4.y, c4.z) <= rr4) mask[g.perm[p]] = 1;
+      }
+    }
+  }
+}
+
 __global__ void k_all_finite(const uint32_t* __restrict__ skeys, int64_t n, uint64_t ncells,
                              uint8_t* __restrict__ flags) {
   const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
@@ -764,6 +792,24 @@ void fpfh_support_mask_dev(pfx_ctx* ctx, const float* sx, const float* sy, const
                           st));
   k_fpfh_mark_support<<<8192, 256, 0, st>>>(g, slist, d_sel, rr, mask);
   check_launch("k_fpfh_mark_support");
+  ctx->fpfh_support = mask;  // consumed by the next fpfh_dev on this context
+}
+
+void fpfh_support_ball_dev(pfx_ctx* ctx, const float* sx, const float* sy, const float* sz, int64_t ns,
+                           const float* qx, const float* qy, const float* qz, int64_t nq, double r, uint8_t* mask) {
+  PFX_CHECK(r > 0.0, "fpfh support: radius must be > 0");
+  ctx->fpfh_support = nullptr;
+  if (ns == 0) return;
+  hipStream_t st = ctx->stream;
+  PFX_HIP(hipMemsetAsync(mask, 0, ns, st));
+  if (nq == 0) return;
+  if (!(ctx->prep_x == sx && ctx->prep_n == ns && ctx->prep_r == r)) fpfh_prepare_dev(ctx, sx, sy, sz, ns, r);
+  TimeScope ts(ctx, "fpfh_support");
+  // (2r)^2 with a relative margin far above the float rounding of the squared distance
+  const float rr4 = (float)(4.0 * r * r * (1.0 + 1e-5));
+  k_fpfh_mark_ball<<<(unsigned)std::min<int64_t>(nq, 8192), 256, 0, st>>>(view(ctx->grid_b), qx, qy, qz, nq, rr4,
+                                                                          mask);
+  check_launch("k_fpfh_mark_ball");
   ctx->fpfh_support = mask;  // consumed by the next fpfh_dev on this context
 }
 

@@ -9,6 +9,7 @@
 // with row-major keys (x, y, z) the block is 9 contiguous runs of 3 z-cells.
 // Non-finite points get key C and sort behind every cell (never a neighbour, as PCL's
 // kd-tree skips them).
+#include <algorithm>
 #include <cstring>
 #include <rocprim/rocprim.hpp>
 
@@ -28,6 +29,9 @@ __host__ __device__ __forceinline__ float ord2f(uint32_t u) {
   return f;
 }
 
+// per-block bounds (ordered-uint encoding: min slots start at 0xffffffff, max at 0), reduced on
+// the host -- no device-side initialisation (a pageable H2D copy) before the launch
+constexpr int kBboxBlocks = 128;
 __global__ void __launch_bounds__(256) k_bbox(const float* __restrict__ x, const float* __restrict__ y,
                                               const float* __restrict__ z, int64_t n,
                                               uint32_t* __restrict__ mm) {
@@ -54,15 +58,14 @@ __global__ void __launch_bounds__(256) k_bbox(const float* __restrict__ x, const
     for (int d = 0; d < 3; ++d) { s_lo[d][wv] = lo[d]; s_hi[d][wv] = hi[d]; }
   }
   __syncthreads();
-  if (threadIdx.x == 0) {  // one atomic per block and bound
+  if (threadIdx.x == 0) {
 #pragma unroll
     for (int d = 0; d < 3; ++d) {
-      float l = fminf(fminf(s_lo[d][0], s_lo[d][1]), fminf(s_lo[d][2], s_lo[d][3]));
-      float h = fmaxf(fmaxf(s_hi[d][0], s_hi[d][1]), fmaxf(s_hi[d][2], s_hi[d][3]));
-      if (l <= h) {
-        atomicMin(&mm[d], f2ord(l));
-        atomicMax(&mm[3 + d], f2ord(h));
-      }
+      const float l = fminf(fminf(s_lo[d][0], s_lo[d][1]), fminf(s_lo[d][2], s_lo[d][3]));
+      const float h = fmaxf(fmaxf(s_hi[d][0], s_hi[d][1]), fmaxf(s_hi[d][2], s_hi[d][3]));
+      const bool any = l <= h;
+      mm[blockIdx.x * 6 + d] = any ? f2ord(l) : 0xffffffffu;
+      mm[blockIdx.x * 6 + 3 + d] = any ? f2ord(h) : 0u;
     }
   }
 }
@@ -115,24 +118,37 @@ __global__ void __launch_bounds__(256) k_gather_sorted(const float* __restrict__
 
 }  // namespace
 
-void points_bbox(pfx_ctx* ctx, Grid& g, const float* d_x, const float* d_y, const float* d_z, int64_t n,
-                 double lo[3], double hi[3]) {
+// bounds of the finite points: per-block partials read back once (pinned) and reduced here
+static bool bbox_dev(pfx_ctx* ctx, Grid& g, const float* d_x, const float* d_y, const float* d_z, int64_t n,
+                     double lo[3], double hi[3]) {
   hipStream_t st = ctx->stream;
-  uint32_t* mm = g.b_minmax.as<uint32_t>(6);
-  uint32_t init[6] = {0xffffffffu, 0xffffffffu, 0xffffffffu, 0u, 0u, 0u};
-  PFX_HIP(hipMemcpyAsync(mm, init, sizeof(init), hipMemcpyHostToDevice, st));
-  if (n > 0) {
-    k_bbox<<<(int)std::min<int64_t>(ceil_div(n, 256), 256), 256, 0, st>>>(d_x, d_y, d_z, n, mm);
+  uint32_t* mm = g.b_minmax.as<uint32_t>(6 * kBboxBlocks);
+  const int blocks = (int)std::min<int64_t>(std::max<int64_t>(ceil_div(n, 256), 1), kBboxBlocks);
+  {
+    TimeScope ts(ctx, "grid_bbox");
+    k_bbox<<<blocks, 256, 0, st>>>(d_x, d_y, d_z, n, mm);
     check_launch("k_bbox");
   }
-  uint32_t h[6];
-  PFX_HIP(hipMemcpyAsync(h, mm, sizeof(h), hipMemcpyDeviceToHost, st));
+  uint32_t* h = ctx->readback<uint32_t>();  // pinned, 4 KB >= 6 * kBboxBlocks words
+  PFX_HIP(hipMemcpyAsync(h, mm, sizeof(uint32_t) * 6 * blocks, hipMemcpyDeviceToHost, st));
   PFX_HIP(hipStreamSynchronize(st));
-  const bool any = h[0] != 0xffffffffu && h[3] != 0u;
+  uint32_t r[6] = {0xffffffffu, 0xffffffffu, 0xffffffffu, 0u, 0u, 0u};
+  for (int b = 0; b < blocks; ++b)
+    for (int d = 0; d < 3; ++d) {
+      r[d] = std::min(r[d], h[b * 6 + d]);
+      r[3 + d] = std::max(r[3 + d], h[b * 6 + 3 + d]);
+    }
+  const bool any = r[0] != 0xffffffffu && r[3] != 0u;
   for (int d = 0; d < 3; ++d) {
-    lo[d] = any ? ord2f(h[d]) : 0.0;
-    hi[d] = any ? ord2f(h[3 + d]) : 0.0;
+    lo[d] = any ? ord2f(r[d]) : 0.0;
+    hi[d] = any ? ord2f(r[3 + d]) : 0.0;
   }
+  return any;
+}
+
+void points_bbox(pfx_ctx* ctx, Grid& g, const float* d_x, const float* d_y, const float* d_z, int64_t n,
+                 double lo[3], double hi[3]) {
+  bbox_dev(ctx, g, d_x, d_y, d_z, n, lo, hi);
 }
 
 void build_grid(pfx_ctx* ctx, Grid& g, const float* d_x, const float* d_y, const float* d_z,
@@ -142,21 +158,8 @@ void build_grid(pfx_ctx* ctx, Grid& g, const float* d_x, const float* d_y, const
   hipStream_t st = ctx->stream;
   g.n = n;
   g.ux = d_x; g.uy = d_y; g.uz = d_z;
-  uint32_t* mm = g.b_minmax.as<uint32_t>(6);
-  uint32_t init[6] = {0xffffffffu, 0xffffffffu, 0xffffffffu, 0u, 0u, 0u};
-  PFX_HIP(hipMemcpyAsync(mm, init, sizeof(init), hipMemcpyHostToDevice, st));
-  if (n > 0) {
-    TimeScope ts(ctx, "grid_bbox");
-    int blocks = (int)std::min<int64_t>(ceil_div(n, 256), 256);  // few blocks: few atomics
-    k_bbox<<<blocks, 256, 0, st>>>(d_x, d_y, d_z, n, mm);
-    check_launch("k_bbox");
-  }
-  uint32_t* host_mm = ctx->readback<uint32_t>();  // pinned
-  PFX_HIP(hipMemcpyAsync(host_mm, mm, 6 * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-  PFX_HIP(hipStreamSynchronize(st));
   double lo[3] = {0, 0, 0}, hi[3] = {0, 0, 0};
-  bool any = host_mm[0] != 0xffffffffu && host_mm[3] != 0u;
-  for (int d = 0; d < 3 && any; ++d) { lo[d] = ord2f(host_mm[d]); hi[d] = ord2f(host_mm[3 + d]); }
+  if (n > 0) bbox_dev(ctx, g, d_x, d_y, d_z, n, lo, hi);
   double cell = radius * (1.0 + 1e-6);
   const double max_cells = double(1 << 26);
   int64_t dims[3];

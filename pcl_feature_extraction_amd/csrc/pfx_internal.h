@@ -219,6 +219,8 @@ int64_t harris6d_dev(pfx_ctx* ctx, const float* x, const float* y, const float* 
                      float* corners_out, int64_t* n_corners, float* grad_out, int32_t* corner_idx_out = nullptr);
 void fpfh_support_mask_dev(pfx_ctx* ctx, const float* sx, const float* sy, const float* sz, int64_t ns,
                            const float* qx, const float* qy, const float* qz, int64_t nq, double r, uint8_t* mask);
+void fpfh_support_ball_dev(pfx_ctx* ctx, const float* sx, const float* sy, const float* sz, int64_t ns,
+                           const float* qx, const float* qy, const float* qz, int64_t nq, double r, uint8_t* mask);
 void radius_search_dev(pfx_ctx* ctx, const float* x, const float* y, const float* z, int64_t n,
                        const float* qx, const float* qy, const float* qz, int64_t nq, double r,
                        int64_t* d_counts, int32_t* d_idx, float* d_d2, int64_t cap);

@@ -1379,8 +1379,10 @@ int64_t narf_dev(pfx_ctx* ctx, const float* x, const float* y, const float* z, i
     check_launch("k_interest");
     // beyond the windowed bitmap: the whole image (the count stays on the device; no host round
     // trip -- the workgroups exit at once when there is nothing to grow)
-    k_interest<kFullWords, true><<<256 * 3, 64, 0, st>>>(I, P, traits, scs, scd, sat, ip, cand, counters + 2,
-                                                          interest, nullptr, nullptr, counters + 1, work);
+    // (a few workgroups: such pixels lie within ~R of the sensor plane and are rare; an empty
+    // launch must not hold LDS the concurrent normal estimation needs)
+    k_interest<kFullWords, true><<<32, 64, 0, st>>>(I, P, traits, scs, scd, sat, ip, cand, counters + 2, interest,
+                                                     nullptr, nullptr, counters + 1, work);
     check_launch("k_interest_full");
   }
   {

@@ -66,9 +66,16 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_wave_barrier();
 }
 
-__global__ void k_iota(int32_t* __restrict__ out, int64_t n) {
-  int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  if (i < n) out[i] = (int32_t)i;
+// one launch for the list build's set-up: counters and cursors zeroed, and (unmasked builds)
+// qpos = 0..n-1 with the query count = the finite points (cell_start[ncells])
+__global__ void k_list_init(int32_t* __restrict__ qpos, int64_t n, const int32_t* __restrict__ nq_src,
+                            int64_t* __restrict__ d_nq, int* __restrict__ counters, int ncounters,
+                            unsigned long long* __restrict__ cursor) {
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (qpos && i < n) qpos[i] = (int32_t)i;
+  if (i < ncounters) counters[i] = 0;
+  if (i < 4) cursor[i] = 0ull;
+  if (i == 0 && nq_src) *d_nq = (int64_t)*nq_src;
 }
 
 __global__ void k_mask_flags(const int32_t* __restrict__ perm, const uint32_t* __restrict__ skeys, int64_t n,
@@ -928,18 +935,17 @@ void build_lists(pfx_ctx* ctx, const Grid& G, const uint8_t* mask, double radius
   PFX_HIP(rocprim::select(nullptr, t3, rocprim::counting_iterator<int32_t>(0), flags, tiles, d_ntiles, (size_t)n,
                           st));
   void* tmp = B("tmp").get(std::max(t1, std::max(t2, t3)) + 16);
-  PFX_HIP(hipMemsetAsync(counters, 0, 14 * sizeof(int), st));
   const unsigned nb = (unsigned)ceil_div(n, 256);
+  unsigned long long* cursor0 = B("cursor").as<unsigned long long>(4);
   {
     TimeScope ts(ctx, std::string(tag) + "_tiles");
     if (mask) {
+      k_list_init<<<1, 256, 0, st>>>(nullptr, 0, nullptr, d_nq, counters, 14, cursor0);
       k_mask_flags<<<nb, 256, 0, st>>>(G.perm, G.skeys, n, (uint64_t)G.ncells, mask, flags);
       PFX_HIP(rocprim::select(tmp, t1, rocprim::counting_iterator<int32_t>(0), flags, qpos, d_nq, (size_t)n, st));
     } else {
       // every finite point, in cell order: sorted positions [0, cell_start[ncells])
-      k_iota<<<nb, 256, 0, st>>>(qpos, n);
-      PFX_HIP(hipMemcpyAsync(d_nq, G.cell_start + G.ncells, sizeof(int32_t), hipMemcpyDeviceToDevice, st));
-      PFX_HIP(hipMemsetAsync(reinterpret_cast<char*>(d_nq) + 4, 0, 4, st));
+      k_list_init<<<nb, 256, 0, st>>>(qpos, n, G.cell_start + G.ncells, d_nq, counters, 14, cursor0);
     }
     k_seg_marks<<<nb, 256, 0, st>>>(qpos, G.skeys, d_nq, seg);
     PFX_HIP(rocprim::inclusive_scan(tmp, t2, seg, seg, (size_t)n, rocprim::maximum<int32_t>(), st));
@@ -963,8 +969,8 @@ void build_lists(pfx_ctx* ctx, const Grid& G, const uint8_t* mask, double radius
   const int chunk = chunk_env ? std::max(1, atoi(chunk_env)) : 4;
   for (int attempt = 0; attempt < 2; ++attempt) {
     ListOut lo{off, cnt, lgs, static_cast<uint32_t*>(lb.ptr), cursor, lb.bytes / sizeof(uint32_t)};
-    PFX_HIP(hipMemsetAsync(cursor, 0, 4 * sizeof(unsigned long long), st));
-    if (attempt) {
+    if (attempt) {  // (the first attempt's cursors were zeroed by k_list_init)
+      PFX_HIP(hipMemsetAsync(cursor, 0, 4 * sizeof(unsigned long long), st));
       PFX_HIP(hipMemcpyAsync(counters + 2, counters + 6, sizeof(int), hipMemcpyDeviceToDevice, st));
       PFX_HIP(hipMemsetAsync(counters + 3, 0, 3 * sizeof(int), st));  // huge, max k, sparse queue
       PFX_HIP(hipMemsetAsync(counters + 7, 0, 3 * sizeof(int), st));  // dense, query, huge queues

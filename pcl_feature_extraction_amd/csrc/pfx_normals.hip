@@ -419,6 +419,15 @@ struct LongLds {
   int32_t rtab[kPerWave * 9];
 };
 
+// NaN (PCL's value for points without a normal) in the four output arrays, one launch
+__global__ void k_nan_fill4(float* __restrict__ a, float* __restrict__ b, float* __restrict__ c,
+                            float* __restrict__ d, int64_t n) {
+  const float v = __uint_as_float(0xffffffffu);
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    a[i] = v; b[i] = v; c[i] = v; d[i] = v;
+  }
+}
+
 // the lists longer than kLaneMax of this pass (mask[caller] == want), for k_normals_long
 __global__ void __launch_bounds__(256) k_long_lists(GridView g, NbLists L, const uint8_t* __restrict__ mask, int want,
                                                     int32_t* __restrict__ longq, int* __restrict__ n_long) {
@@ -593,10 +602,8 @@ void normals_lists_dev(pfx_ctx* ctx, const float* x, const float* y, const float
   hipStream_t st = ctx->stream;
   TimeScope total(ctx, "normals_lists_phase");
   build_grid(ctx, ctx->grid_a, x, y, z, n, r);
-  PFX_HIP(hipMemsetAsync(nx, 0xff, sizeof(float) * n, st));
-  PFX_HIP(hipMemsetAsync(ny, 0xff, sizeof(float) * n, st));
-  PFX_HIP(hipMemsetAsync(nz, 0xff, sizeof(float) * n, st));
-  PFX_HIP(hipMemsetAsync(curv, 0xff, sizeof(float) * n, st));
+  k_nan_fill4<<<(unsigned)std::min<int64_t>(ceil_div(n, 256), 4096), 256, 0, st>>>(nx, ny, nz, curv, n);
+  check_launch("k_nan_fill4");
   build_lists(ctx, ctx->grid_a, nullptr, r, true, ns.L, "normals");
   ctx->stats["normals_neighbors"] = ns.L.total;
   ctx->stats["normals_long_neighbors"] = ns.L.long_total;

@@ -82,3 +82,33 @@ def test_two_phase_normals_and_support_mask():
     expect = np.zeros(n, np.uint8)
     expect[np.unique(idx2[idx2 >= 0])] = 1
     assert np.array_equal(mask.cpu().numpy(), expect)
+
+
+def test_support_ball_mask():
+    """pfx_fpfh_support_ball_dev: exactly the points within 2r of a query (float squared distance
+    in FLANN's order against (2r)^2 (1 + 1e-5)), a superset of the exact support mask."""
+    import torch
+    from pcl_feature_extraction_amd import Context
+    from pcl_feature_extraction_amd.synth import synth_room
+    n = 120_000
+    x, y, z, _ = synth_room(n, 34)
+    dev = torch.device("cuda", 0)
+    X, Y, Z = (torch.from_numpy(a).to(dev) for a in (x, y, z))
+    qi = np.arange(0, n, 1499)
+    Q = [t[torch.from_numpy(qi).to(dev)].contiguous() for t in (X, Y, Z)]
+    ball = torch.empty(n, dtype=torch.uint8, device=dev)
+    exact = torch.empty(n, dtype=torch.uint8, device=dev)
+    r = 0.08
+    with Context(0) as a:
+        a.fpfh_support_ball_dev(X, Y, Z, *Q, r, ball)
+        a.fpfh_support_mask_dev(X, Y, Z, *Q, r, exact)
+        a.synchronize()
+    ball, exact = ball.cpu().numpy(), exact.cpu().numpy()
+    lim = np.float32(4.0 * r * r * (1.0 + 1e-5))
+    expect = np.zeros(n, np.uint8)
+    for q in qi:
+        dx, dy, dz = x[q] - x, y[q] - y, z[q] - z
+        d2 = ((np.float32(0) + dx * dx) + dy * dy) + dz * dz
+        expect[d2 <= lim] = 1
+    assert np.array_equal(ball, expect)
+    assert np.all(ball[exact == 1] == 1) and exact.sum() > 0
