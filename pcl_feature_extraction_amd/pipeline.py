@@ -58,10 +58,11 @@ class OverlappedNarfFpfh:
     on a second context/stream driven from a worker thread (the C-ABI calls release the GIL), then
     FPFH on the main stream after an event wait for the normals.  Same results as narf_fpfh.
 
-    (Measured alternative, not used: normals of the FPFH support set first -- pfx_fpfh_support_
-    mask_dev + two masked pfx_normals_chains_dev passes -- so FPFH overlaps the other normals.
-    The exact support set (r-neighbours of the r-neighbourhoods of the keypoints) costs ~1 ms to
-    mark and holds most of the long neighbour lists, so the step got slower: 11.0 vs 9.5 ms.)"""
+    (Measured alternatives, not used: normals of the FPFH support set first -- a support mask +
+    two masked pfx_normals_chains_dev passes -- so FPFH overlaps the other normals.  The exact
+    support (pfx_fpfh_support_mask_dev) costs ~1 ms to mark: 11.0 vs 9.5 ms (round 1); the 2r
+    ball (pfx_fpfh_support_ball_dev, 60 us) still holds most of the chain work, and the second
+    pass's long-list kernel shares a hardware queue with FPFH: 7.44 vs 7.02 ms (round 2).)"""
 
     def __init__(self, torch, ctx_main: Context, ctx_side: Context, device, main_stream=None):
         from concurrent.futures import ThreadPoolExecutor
@@ -78,10 +79,12 @@ class OverlappedNarfFpfh:
         self.s_side.wait_stream(self.s_main)  # the scan was written on the main stream
         fut = self.pool.submit(self.ctx_side.normals_dev, b.x, b.y, b.z, normal_radius, b.nx, b.ny, b.nz, b.curv)
         try:
-            self.ctx.fpfh_prepare_dev(b.x, b.y, b.z, feat_radius)  # the FPFH surface grid, also normals-free
             kp = self.ctx.narf_keypoints_dev(b.x, b.y, b.z, params or narf_params(support_size=0.2),
                                              cam or camera())
             k = self.ctx.gather_points_dev(b.x, b.y, b.z, kp, b.kx, b.ky, b.kz)
+            # the FPFH surface grid (normals-free) after NARF: the step's first milliseconds
+            # belong to the normal-estimation grid and NARF, the critical and the longer path
+            self.ctx.fpfh_prepare_dev(b.x, b.y, b.z, feat_radius)
         finally:
             fut.result()
         ev = self.torch.cuda.Event()
