@@ -529,36 +529,57 @@ __global__ void __launch_bounds__(kWT) k_fpfh_weight(GridView g, const float* __
     float fh = 0.0f;
     double ps0 = 0.0, ps1 = 0.0, ps2 = 0.0;
     int pl0 = 1 << 20, pl1 = 1 << 20, pl2 = 1 << 20;
-    for (int c0 = 0; c0 < k; c0 += kChunkW) {
-      const int m = min(kChunkW, k - c0);
-      for (int e = tid; e < m * kDesc; e += kWT) {
+    // rows of a chunk (+ its weights in column kDesc); LDS path: two buffers in the freed sort
+    // scratch, so waves 1.. stage chunk c + 1 (and form chunk c's block partial sums) while wave 0
+    // runs the 33 float chains over chunk c -- one barrier per chunk, the chains never wait for
+    // a gather.  Global-scratch path: one buffer, stage then chain.
+    constexpr int RS = kDesc + 1;
+    float* rb0 = GLOBAL ? &rows[0][0] : reinterpret_cast<float*>(keys_lds + kCapW);
+    float* rb1 = GLOBAL ? rb0 : rb0 + kChunkW * RS;
+    const int nch = (k + kChunkW - 1) / kChunkW;
+    auto stage = [&](int c, float* rbuf, int t0, int nt) {
+      const int c0 = c * kChunkW, m = min(kChunkW, k - c0);
+      for (int e = t0; e < m * kDesc; e += nt) {
         const int j = e / kDesc, b = e - j * kDesc;
-        rows[j][b] = spfh[(int64_t)key_idx(keys[c0 + j]) * kDesc + b];
+        rbuf[j * RS + b] = spfh[(int64_t)key_idx(keys[c0 + j]) * kDesc + b];
       }
-      if (tid < m) {
-        const float d2 = key_d2(keys[c0 + tid]);
-        wts[tid] = d2 == 0.0f ? 0.0f : 1.0f / d2;  // 0 marks a skipped neighbour (d2 == 0)
+      for (int j = t0; j < m; j += nt) {
+        const float d2 = key_d2(keys[c0 + j]);
+        rbuf[j * RS + kDesc] = d2 == 0.0f ? 0.0f : 1.0f / d2;  // 0 marks a skipped neighbour (d2 == 0)
       }
-      __syncthreads();
+    };
+    stage(0, rb0, tid, kWT);
+    __syncthreads();
+    for (int c = 0; c < nch; ++c) {
+      const int c0 = c * kChunkW, m = min(kChunkW, k - c0);
+      const float* cur = (c & 1) ? rb1 : rb0;
+      if (!GLOBAL && tid >= 64 && c + 1 < nch) stage(c + 1, (c & 1) ? rb0 : rb1, tid - 64, kWT - 64);
       if (tid < kDesc) {
         // skipped neighbours have w = 0: SPFH rows are finite and fh >= +0, so adding the +0
         // product leaves fh unchanged bit for bit (== PCL's `continue`)
 #pragma unroll 8
-        for (int j = 0; j < m; ++j) fh = fh + rows[j][tid] * wts[j];
+        for (int j = 0; j < m; ++j) fh = fh + cur[j * RS + tid] * cur[j * RS + kDesc];
       }
-      for (int e = tid; e < m * kDesc; e += kWT) {
-        const int j = e / kDesc, b = e - j * kDesc;
-        const float w = wts[j];
-        if (w == 0.0f) continue;
-        const float v = rows[j][b] * w;
-        if (v != 0.0f) {
-          const int l = lsb_exp(v);
-          if (b < kBins) { ps0 += (double)v; pl0 = min(pl0, l); }
-          else if (b < 2 * kBins) { ps1 += (double)v; pl1 = min(pl1, l); }
-          else { ps2 += (double)v; pl2 = min(pl2, l); }
+      const int pt0 = GLOBAL ? tid : tid - 64, pnt = GLOBAL ? kWT : kWT - 64;
+      if (pt0 >= 0) {
+        for (int e = pt0; e < m * kDesc; e += pnt) {
+          const int j = e / kDesc, b = e - j * kDesc;
+          const float w = cur[j * RS + kDesc];
+          if (w == 0.0f) continue;
+          const float v = cur[j * RS + b] * w;
+          if (v != 0.0f) {
+            const int l = lsb_exp(v);
+            if (b < kBins) { ps0 += (double)v; pl0 = min(pl0, l); }
+            else if (b < 2 * kBins) { ps1 += (double)v; pl1 = min(pl1, l); }
+            else { ps2 += (double)v; pl2 = min(pl2, l); }
+          }
         }
       }
       __syncthreads();
+      if (GLOBAL && c + 1 < nch) {
+        stage(c + 1, rb0, tid, kWT);
+        __syncthreads();
+      }
     }
     // block reduction (any order: only used when every partial sum is exact)
 #pragma unroll
