@@ -410,7 +410,7 @@ __device__ __forceinline__ void sort_list(uint16_t* L, int k, float qx, float qy
                                           float bscale, uint32_t* Sd, uint16_t* St, int* bcount, int* bpos,
                                           const GridView& g, const Runs& R, int lane) {
   if (k <= 64) wave_rank_sort(L, k, qx, qy, qz, cand, g, R, lane);
-  else if (SMALL && k > 128) wave_sort<NB>(L, k, qx, qy, qz, cand, bscale, Sd, St, bcount, bpos, g, R, lane);
+  else if (SMALL && k > 256) wave_sort_regs<NB, 6>(L, k, qx, qy, qz, cand, bscale, Sd, St, bcount, bpos, g, R, lane);
   else if (k <= 128) wave_sort_regs<NB, 2>(L, k, qx, qy, qz, cand, bscale, Sd, St, bcount, bpos, g, R, lane);
   else if (k <= 256) wave_sort_regs<NB, 4>(L, k, qx, qy, qz, cand, bscale, Sd, St, bcount, bpos, g, R, lane);
   else if (k <= 512) wave_sort_regs<NB, 8>(L, k, qx, qy, qz, cand, bscale, Sd, St, bcount, bpos, g, R, lane);
@@ -996,8 +996,8 @@ void build_lists(pfx_ctx* ctx, const Grid& G, const uint8_t* mask, double radius
       TimeScope ts(ctx, std::string(tag) + "_lists");
       {
         TimeScope t0(ctx, std::string(tag) + "_lists_small");
-        k_nb_tile<kTcapSmall, 64, kTcapSmall, true><<<256 * 4 * 2, 256, 0, st>>>(
-            g, qpos, recs, kRecInts, counters + 10, rr, 64.0f / rr, isort, lo, single, counters + 2, counters + 11,
+        k_nb_tile<kTcapSmall, 256, kTcapSmall, true><<<256 * 4 * 2, 256, 0, st>>>(
+            g, qpos, recs, kRecInts, counters + 10, rr, 256.0f / rr, isort, lo, single, counters + 2, counters + 11,
             chunk);
       }
       {
