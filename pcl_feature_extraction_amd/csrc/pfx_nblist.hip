@@ -409,11 +409,15 @@ template <int NB, class Cand, bool SMALL = false>
 __device__ __forceinline__ void sort_list(uint16_t* L, int k, float qx, float qy, float qz, const Cand& cand,
                                           float bscale, uint32_t* Sd, uint16_t* St, int* bcount, int* bpos,
                                           const GridView& g, const Runs& R, int lane) {
+  // register tiers in steps of 64-128 elements: the unrolled per-element work of a tier runs for
+  // every slot, so a list is sorted by the smallest tier that holds it
   if (k <= 64) wave_rank_sort(L, k, qx, qy, qz, cand, g, R, lane);
-  else if (SMALL && k > 256) wave_sort_regs<NB, 6>(L, k, qx, qy, qz, cand, bscale, Sd, St, bcount, bpos, g, R, lane);
   else if (k <= 128) wave_sort_regs<NB, 2>(L, k, qx, qy, qz, cand, bscale, Sd, St, bcount, bpos, g, R, lane);
+  else if (k <= 192) wave_sort_regs<NB, 3>(L, k, qx, qy, qz, cand, bscale, Sd, St, bcount, bpos, g, R, lane);
   else if (k <= 256) wave_sort_regs<NB, 4>(L, k, qx, qy, qz, cand, bscale, Sd, St, bcount, bpos, g, R, lane);
+  else if (SMALL || k <= 384) wave_sort_regs<NB, 6>(L, k, qx, qy, qz, cand, bscale, Sd, St, bcount, bpos, g, R, lane);
   else if (k <= 512) wave_sort_regs<NB, 8>(L, k, qx, qy, qz, cand, bscale, Sd, St, bcount, bpos, g, R, lane);
+  else if (k <= 768) wave_sort_regs<NB, 12>(L, k, qx, qy, qz, cand, bscale, Sd, St, bcount, bpos, g, R, lane);
   else if (k <= 1024) wave_sort_regs<NB, 16>(L, k, qx, qy, qz, cand, bscale, Sd, St, bcount, bpos, g, R, lane);
   else wave_sort<NB>(L, k, qx, qy, qz, cand, bscale, Sd, St, bcount, bpos, g, R, lane);
 }
