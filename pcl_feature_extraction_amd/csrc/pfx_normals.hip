@@ -628,17 +628,20 @@ void normals_chains_dev(pfx_ctx* ctx, pfx_ctx* owner, const uint8_t* mask, int w
   int* n_long = ctx->buf("normals_nlong").as<int>(5);
   PFX_HIP(hipMemsetAsync(n_long, 0, 5 * sizeof(int), st));
   const int64_t nb = ceil_div(L.nq, 256);
-  // the long lists first: their chains (k_normals_long, bound by the longest list) run on a side
-  // stream concurrently with the short-list chains, which leave them out
+  // the long lists first: when they are few (their chains, bound by the longest list, leave the
+  // device mostly idle) k_normals_long runs on a side stream concurrently with the short-list
+  // chains, which leave them out; when most lists are long (dense clouds) the two kernels would
+  // only crowd each other, so it runs after them on the same stream
   k_long_lists<<<(unsigned)nb, 256, 0, st>>>(view(G), L, mask, want, longq, n_long);
   check_launch("k_long_lists");
-  ctx->ensure_side();
-  PFX_HIP(hipEventRecord(ctx->fork_ev[0], st));
-  PFX_HIP(hipStreamWaitEvent(ctx->side, ctx->fork_ev[0], 0));
-  {
+  // (sized to what is resident at once: waves beyond it would wait for a second round)
+  const int64_t lb = std::min<int64_t>(ceil_div(L.nq, 7 * 4), 256 * 4);
+  const bool fork = L.long_nq * 8 <= L.nq;
+  if (fork) {
+    ctx->ensure_side();
+    PFX_HIP(hipEventRecord(ctx->fork_ev[0], st));
+    PFX_HIP(hipStreamWaitEvent(ctx->side, ctx->fork_ev[0], 0));
     // persistent: the queue length stays on the device (no host round trip)
-    // (sized to what is resident at once: waves beyond it would wait for a second round)
-    const int64_t lb = std::min<int64_t>(ceil_div(L.nq, 7 * 4), 256 * 4);
     k_normals_long<<<(unsigned)lb, 256, 0, ctx->side>>>(view(G), L, longq, n_long, vp[0], vp[1], vp[2], nx, ny, nz,
                                                         curv);
     check_launch("k_normals_long");
@@ -667,9 +670,14 @@ void normals_chains_dev(pfx_ctx* ctx, pfx_ctx* owner, const uint8_t* mask, int w
     check_launch("k_normals_chain_big");
   }
   {
-    TimeScope ts(ctx, "normals_long");  // the join: what the long chains add after the short ones
-    PFX_HIP(hipEventRecord(ctx->fork_ev[1], ctx->side));
-    PFX_HIP(hipStreamWaitEvent(st, ctx->fork_ev[1], 0));
+    TimeScope ts(ctx, "normals_long");  // (forked: the join, what the long chains add after the short ones)
+    if (fork) {
+      PFX_HIP(hipEventRecord(ctx->fork_ev[1], ctx->side));
+      PFX_HIP(hipStreamWaitEvent(st, ctx->fork_ev[1], 0));
+    } else {
+      k_normals_long<<<(unsigned)lb, 256, 0, st>>>(view(G), L, longq, n_long, vp[0], vp[1], vp[2], nx, ny, nz, curv);
+      check_launch("k_normals_long");
+    }
   }
   static const bool verbose = getenv("PFX_VERBOSE_STATS") != nullptr;
   if (verbose) {  // diagnostics only (host sync): how the chain workgroups fetched
