@@ -1373,8 +1373,10 @@ int64_t narf_dev(pfx_ctx* ctx, const float* x, const float* y, const float* z, i
     k_interest_ff<<<256 * 20, 64, 0, st>>>(I, P, pk, traits, scs, scd, sat, ip, grow_list, counters + 4, interest,
                                             fb1, counters + 3, counters + 1, work);
     check_launch("k_interest_ff");
-    // windows beyond the flood-fill masks: queue-based grow in a windowed LDS bitmap
-    k_interest<kWinWords, false><<<256 * 4, 64, 0, st>>>(I, P, traits, scs, scd, sat, ip, fb1, counters + 3,
+    // windows beyond the flood-fill masks: queue-based grow in a windowed LDS bitmap (one
+    // workgroup per CU: such windows are few, and an empty launch must not queue a thousand
+    // workgroups behind the concurrent list kernels)
+    k_interest<kWinWords, false><<<256, 64, 0, st>>>(I, P, traits, scs, scd, sat, ip, fb1, counters + 3,
                                                           interest, cand, counters + 2, counters + 1, work);
     check_launch("k_interest");
     // beyond the windowed bitmap: the whole image (the count stays on the device; no host round
