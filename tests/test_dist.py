@@ -39,8 +39,10 @@ def _worker(rank, world, port, ks, out_q):
                   for s in mine]
         root = gather_to_root(torch, dist, blocks, 33, torch.device("cpu"), -(-n_scans // world))
         if root is not None:
-            root = [(d.clone(), i.clone()) for d, i in in_scan_order(root, n_scans, world)]
-        out_q.put((rank, [g.clone() for g in got], root))
+            root = [(d.numpy().copy(), i.numpy().copy()) for d, i in in_scan_order(root, n_scans, world)]
+        # numpy, not tensors: torch shares tensor storage through file descriptors served by this
+        # process, which may already have exited when the parent unpickles them
+        out_q.put((rank, [g.numpy().copy() for g in got], root))
     finally:
         dist.destroy_process_group()
 
@@ -63,15 +65,15 @@ def test_gather_gloo(ks):
         assert [g.shape[0] for g in got] == ks
         for src, k in enumerate(ks):
             want = torch.arange(k * 33, dtype=torch.float32).reshape(k, 33) + 1000.0 * src
-            assert torch.equal(got[src], want)
+            assert torch.equal(torch.from_numpy(got[src]), want)
         assert (root is None) == (rank != 0)
     n_scans = 2 * world + 1
     root = results[0][1]
     assert len(root) == n_scans
     for s, (d, i) in enumerate(root):
         k = ks[s % world] + s % 3
-        assert torch.equal(d, torch.full((k, 33), float(s)))
-        assert torch.equal(i, torch.arange(k, dtype=torch.int32) + 100 * s)
+        assert torch.equal(torch.from_numpy(d), torch.full((k, 33), float(s)))
+        assert torch.equal(torch.from_numpy(i), torch.arange(k, dtype=torch.int32) + 100 * s)
 
 
 def test_owned_scans_round_robin():
