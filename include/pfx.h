@@ -172,6 +172,12 @@ pfx_status pfx_fpfh_dev(pfx_ctx* ctx, const float* d_sx, const float* d_sy, cons
  * same (d_sx, n_surface, radius) consumes it; the surface must not change in between. */
 pfx_status pfx_fpfh_prepare_dev(pfx_ctx* ctx, const float* d_sx, const float* d_sy, const float* d_sz,
                                 int64_t n_surface, double radius);
+/* Also marks the SPFH point set S of the next pfx_fpfh_dev (input != surface) for these queries
+ * (d_qx must be the same pointer, nq the same count): S needs only the coordinates, so it can be
+ * found while the normals are still being computed.  Builds the surface grid first if needed. */
+pfx_status pfx_fpfh_prepare_queries_dev(pfx_ctx* ctx, const float* d_sx, const float* d_sy, const float* d_sz,
+                                        int64_t n_surface, const float* d_qx, const float* d_qy,
+                                        const float* d_qz, int64_t nq, double radius);
 /* d_mask[i] = 1 for every surface point whose normal FPFHEstimation reads for these queries
  * (the r-neighbours of the SPFH set S = the r-neighbourhoods of the queries, fpfh.hpp), else 0.
  * n_surface bytes.  The next pfx_fpfh_dev on ctx reads only these normals, so the others may

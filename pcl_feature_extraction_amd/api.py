@@ -214,6 +214,11 @@ class Context:
         self._check(self._lib.pfx_fpfh_support_ball_dev(self.h, _ptr(sx), _ptr(sy), _ptr(sz), sx.numel(), _ptr(qx),
                                                          _ptr(qy), _ptr(qz), qx.numel(), float(r), _ptr(mask)))
 
+    def fpfh_prepare_queries_dev(self, sx, sy, sz, qx, qy, qz, r):
+        """The next fpfh_dev's SPFH point set for these queries (same tensors), found ahead."""
+        self._check(self._lib.pfx_fpfh_prepare_queries_dev(self.h, _ptr(sx), _ptr(sy), _ptr(sz), sx.numel(),
+                                                            _ptr(qx), _ptr(qy), _ptr(qz), qx.numel(), float(r)))
+
     def fpfh_prepare_dev(self, sx, sy, sz, r):
         """Build the FPFH search-surface index ahead of fpfh_dev (see pfx_fpfh_prepare_dev)."""
         self._check(self._lib.pfx_fpfh_prepare_dev(self.h, _ptr(sx), _ptr(sy), _ptr(sz), sx.numel(), float(r)))

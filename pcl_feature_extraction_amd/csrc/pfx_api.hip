@@ -306,6 +306,18 @@ pfx_status pfx_fpfh_prepare_dev(pfx_ctx* ctx, const float* d_sx, const float* d_
   PFX_API_END(ctx)
 }
 
+pfx_status pfx_fpfh_prepare_queries_dev(pfx_ctx* ctx, const float* d_sx, const float* d_sy, const float* d_sz,
+                                        int64_t n_surface, const float* d_qx, const float* d_qy,
+                                        const float* d_qz, int64_t nq, double radius) {
+  PFX_API_BEGIN
+  check_ctx(ctx);
+  if (n_surface < 0 || nq < 0 || !(radius > 0.0) || (n_surface && (!d_sx || !d_sy || !d_sz)) ||
+      (nq && (!d_qx || !d_qy || !d_qz)))
+    throw Error(PFX_ERR_INVALID, "fpfh_prepare_queries: invalid arguments");
+  pfx::fpfh_prepare_queries_dev(ctx, d_sx, d_sy, d_sz, n_surface, d_qx, d_qy, d_qz, nq, radius);
+  PFX_API_END(ctx)
+}
+
 pfx_status pfx_fpfh(pfx_ctx* ctx, const float* sx, const float* sy, const float* sz, const float* snx,
                     const float* sny, const float* snz, int64_t n_surface, const float* qx, const float* qy,
                     const float* qz, int64_t nq, int same_as_surface, double radius, float* out) {

@@ -780,11 +780,41 @@ __global__ void k_nan_rows_nonfinite(const float* __restrict__ x, const float* _
 void fpfh_prepare_dev(pfx_ctx* ctx, const float* sx, const float* sy, const float* sz, int64_t ns, double r) {
   ctx->prep_x = nullptr;
   ctx->prep_n = -1;
+  ctx->prep_qx = nullptr;
+  ctx->prep_nq = -1;
   if (ns == 0) return;
   build_grid(ctx, ctx->grid_b, sx, sy, sz, ns, r);
   ctx->prep_x = sx;
   ctx->prep_n = ns;
   ctx->prep_r = r;
+}
+
+// S of the next fpfh_dev (input != surface) marked and compacted ahead of time: it needs only the
+// coordinates and the queries, so it can run while the normals are still being computed.
+void fpfh_prepare_queries_dev(pfx_ctx* ctx, const float* sx, const float* sy, const float* sz, int64_t ns,
+                              const float* qx, const float* qy, const float* qz, int64_t nq, double r) {
+  PFX_CHECK(r > 0.0, "fpfh_prepare_queries: radius must be > 0");
+  ctx->prep_qx = nullptr;
+  ctx->prep_nq = -1;
+  if (ns == 0 || nq == 0) return;
+  if (!(ctx->prep_x == sx && ctx->prep_n == ns && ctx->prep_r == r)) fpfh_prepare_dev(ctx, sx, sy, sz, ns, r);
+  hipStream_t st = ctx->stream;
+  const Grid& G = ctx->grid_b;
+  uint8_t* flags = ctx->buf("fpfh_flags").as<uint8_t>(ns);
+  int32_t* slist = ctx->buf("fpfh_list").as<int32_t>(ns);
+  int64_t* d_sel = ctx->buf("fpfh_nsel").as<int64_t>(1);
+  size_t tmp_bytes = 0;
+  PFX_HIP(rocprim::select(nullptr, tmp_bytes, rocprim::counting_iterator<int32_t>(0), flags, slist, d_sel,
+                          (size_t)ns, st));
+  void* tmp = ctx->buf("fpfh_tmp").get(tmp_bytes + 16);
+  TimeScope ts(ctx, "fpfh_prepare_queries");
+  PFX_HIP(hipMemsetAsync(flags, 0, ns, st));
+  k_fpfh_mark<<<(unsigned)std::min<int64_t>(nq, 8192), 256, 0, st>>>(view(G), qx, qy, qz, nq, (float)(r * r), flags);
+  check_launch("k_fpfh_mark");
+  PFX_HIP(rocprim::select(tmp, tmp_bytes, rocprim::counting_iterator<int32_t>(0), flags, slist, d_sel, (size_t)ns,
+                          st));
+  ctx->prep_qx = qx;
+  ctx->prep_nq = nq;
 }
 
 void fpfh_support_mask_dev(pfx_ctx* ctx, const float* sx, const float* sy, const float* sz, int64_t ns,
@@ -847,10 +877,14 @@ void fpfh_dev(pfx_ctx* ctx, const float* sx, const float* sy, const float* sz, c
     PFX_HIP(hipStreamSynchronize(st));
     return;
   }
-  if (!(ctx->prep_x == sx && ctx->prep_n == ns && ctx->prep_r == r))
-    build_grid(ctx, ctx->grid_b, sx, sy, sz, ns, r);
+  const bool grid_ready = ctx->prep_x == sx && ctx->prep_n == ns && ctx->prep_r == r;
+  if (!grid_ready) build_grid(ctx, ctx->grid_b, sx, sy, sz, ns, r);
+  // S marked ahead (fpfh_prepare_queries_dev on this grid and these queries)?
+  const bool s_ready = grid_ready && !same && ctx->prep_qx == qx && ctx->prep_nq == nq;
   ctx->prep_x = nullptr;  // one-shot
   ctx->prep_n = -1;
+  ctx->prep_qx = nullptr;
+  ctx->prep_nq = -1;
   const Grid& G = ctx->grid_b;
   GridView g = view(G);
   const float rr = (float)(r * r);
@@ -868,15 +902,17 @@ void fpfh_dev(pfx_ctx* ctx, const float* sx, const float* sy, const float* sz, c
     TimeScope ts(ctx, "fpfh_mark");
     k_sorted_normals<<<nb, 256, 0, st>>>(G.perm, ns, snx, sny, snz, same ? nullptr : ctx->fpfh_support, snp);
     ctx->fpfh_support = nullptr;  // one-shot
-    if (same) {
-      k_all_finite<<<nb, 256, 0, st>>>(G.skeys, ns, (uint64_t)G.ncells, flags);
-    } else {
-      PFX_HIP(hipMemsetAsync(flags, 0, ns, st));
-      k_fpfh_mark<<<(unsigned)std::min<int64_t>(nq, 8192), 256, 0, st>>>(g, qx, qy, qz, nq, rr, flags);
+    if (!s_ready) {
+      if (same) {
+        k_all_finite<<<nb, 256, 0, st>>>(G.skeys, ns, (uint64_t)G.ncells, flags);
+      } else {
+        PFX_HIP(hipMemsetAsync(flags, 0, ns, st));
+        k_fpfh_mark<<<(unsigned)std::min<int64_t>(nq, 8192), 256, 0, st>>>(g, qx, qy, qz, nq, rr, flags);
+      }
+      check_launch("k_fpfh_mark");
+      PFX_HIP(rocprim::select(tmp, tmp_bytes, rocprim::counting_iterator<int32_t>(0), flags, slist, d_sel,
+                              (size_t)ns, st));
     }
-    check_launch("k_fpfh_mark");
-    PFX_HIP(rocprim::select(tmp, tmp_bytes, rocprim::counting_iterator<int32_t>(0), flags, slist, d_sel,
-                            (size_t)ns, st));
   }
   // [0] k over capacity, [1] max k, [2] inexact sums, [3] deferred pairs, [4..7] pairs,
   // [8] queries over the LDS capacity (weighted by the global-scratch pass)

@@ -117,6 +117,9 @@ struct pfx_ctx {
   const float* prep_x = nullptr;
   int64_t prep_n = -1;
   double prep_r = 0.0;
+  // ... and its SPFH point set for these queries (pfx_fpfh_prepare_queries_dev)
+  const float* prep_qx = nullptr;
+  int64_t prep_nq = -1;
   const uint8_t* fpfh_support = nullptr;  // pfx_fpfh_support_mask_dev -> next pfx_fpfh_dev
   std::map<std::string, pfx::DevBuf> bufs;  // named scratch
   pfx::NarfState* narf = nullptr;
@@ -231,6 +234,8 @@ void fpfh_dev(pfx_ctx* ctx, const float* sx, const float* sy, const float* sz, c
               const float* qz, int64_t nq, int same, double r, float* out,
               bool reuse_normal_lists = false);
 void fpfh_prepare_dev(pfx_ctx* ctx, const float* sx, const float* sy, const float* sz, int64_t ns, double r);
+void fpfh_prepare_queries_dev(pfx_ctx* ctx, const float* sx, const float* sy, const float* sz, int64_t ns,
+                              const float* qx, const float* qy, const float* qz, int64_t nq, double r);
 void shot_dev(pfx_ctx* ctx, const float* sx, const float* sy, const float* sz, const float* snx,
               const float* sny, const float* snz, int64_t ns, const float* qx, const float* qy,
               const float* qz, int64_t nq, double r, float* desc, float* rf);

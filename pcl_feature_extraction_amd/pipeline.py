@@ -85,6 +85,8 @@ class OverlappedNarfFpfh:
             # the FPFH surface grid (normals-free) after NARF: the step's first milliseconds
             # belong to the normal-estimation grid and NARF, the critical and the longer path
             self.ctx.fpfh_prepare_dev(b.x, b.y, b.z, feat_radius)
+            if k > 0:  # FPFH's SPFH point set, also normals-free
+                self.ctx.fpfh_prepare_queries_dev(b.x, b.y, b.z, b.kx[:k], b.ky[:k], b.kz[:k], feat_radius)
         finally:
             fut.result()
         ev = self.torch.cuda.Event()
