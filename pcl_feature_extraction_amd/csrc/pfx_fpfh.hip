@@ -238,8 +238,10 @@ __device__ __attribute__((noinline)) int pair_bins_exact(float p1x, float p1y, f
 // written by a concurrent normal-estimation pass (pfx_normals_chains_dev on another stream)
 __global__ void k_sorted_normals(const int32_t* __restrict__ perm, int64_t n, const float* __restrict__ nx,
                                  const float* __restrict__ ny, const float* __restrict__ nz,
-                                 const uint8_t* __restrict__ support, float4* __restrict__ out) {
+                                 const uint8_t* __restrict__ support, float4* __restrict__ out,
+                                 int* __restrict__ zero9) {
   const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (zero9 && i < 9) zero9[i] = 0;
   if (i >= n) return;
   const int32_t p = perm[i];
   if (support && !support[p]) {
@@ -898,9 +900,18 @@ void fpfh_dev(pfx_ctx* ctx, const float* sx, const float* sy, const float* sz, c
                           (size_t)ns, st));
   void* tmp = ctx->buf("fpfh_tmp").get(tmp_bytes + 16);
   const unsigned nb = (unsigned)ceil_div(ns, 256);
+  // [0] k over capacity, [1] max k, [2] inexact sums, [3] deferred pairs, [4..7] pairs,
+  // [8] queries over the LDS capacity (weighted by the global-scratch pass)
+  DevBuf& eb = ctx->buf("fpfh_err");
+  const bool fresh = !eb.ptr;
+  int* err = eb.as<int>(10);
+  if (fresh) PFX_HIP(hipMemsetAsync(err, 0, 10 * sizeof(int), st));  // the sticky word starts clear
   {
     TimeScope ts(ctx, "fpfh_mark");
-    k_sorted_normals<<<nb, 256, 0, st>>>(G.perm, ns, snx, sny, snz, same ? nullptr : ctx->fpfh_support, snp);
+    // (also zeroes the per-call statistics words err[1..9]: err[0] (neighbourhood beyond
+    // capacity) is sticky until the check after the next synchronisation, fpfh_resolve)
+    k_sorted_normals<<<nb, 256, 0, st>>>(G.perm, ns, snx, sny, snz, same ? nullptr : ctx->fpfh_support, snp,
+                                         err + 1);
     ctx->fpfh_support = nullptr;  // one-shot
     if (!s_ready) {
       if (same) {
@@ -914,12 +925,6 @@ void fpfh_dev(pfx_ctx* ctx, const float* sx, const float* sy, const float* sz, c
                               (size_t)ns, st));
     }
   }
-  // [0] k over capacity, [1] max k, [2] inexact sums, [3] deferred pairs, [4..7] pairs,
-  // [8] queries over the LDS capacity (weighted by the global-scratch pass)
-  DevBuf& eb = ctx->buf("fpfh_err");
-  const bool fresh = !eb.ptr;
-  int* err = eb.as<int>(10);
-  if (fresh) PFX_HIP(hipMemsetAsync(err, 0, 10 * sizeof(int), st));  // the sticky word starts clear
   // a neighbourhood can only outgrow the LDS keys when the surface has more than kCapW points
   const bool overflow_pass = ns > kCapW;
   int32_t* ovf = overflow_pass ? ctx->buf("fpfh_wovf").as<int32_t>(nq) : nullptr;
@@ -933,9 +938,6 @@ void fpfh_dev(pfx_ctx* ctx, const float* sx, const float* sy, const float* sz, c
   // k_fpfh_spfh runs the exact path in place (PFX_FPFH_SLOW_CAP: test hook for that branch)
   const char* cap_env = getenv("PFX_FPFH_SLOW_CAP");
   const unsigned slow_cap = cap_env ? (unsigned)std::max(1, atoi(cap_env)) : 1u << 20;
-  // err[0] (neighbourhood beyond capacity) is sticky until the check after the next
-  // synchronisation (fpfh_resolve); the statistics words are per call
-  PFX_HIP(hipMemsetAsync(err + 1, 0, 9 * sizeof(int), st));
   int2* slowq = ctx->buf("fpfh_slowq").as<int2>(slow_cap);
   {
     // the S count stays on the device: grid-stride launches sized for the worst case
