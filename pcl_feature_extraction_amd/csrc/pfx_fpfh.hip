@@ -942,7 +942,9 @@ void fpfh_dev(pfx_ctx* ctx, const float* sx, const float* sy, const float* sz, c
   {
     // the S count stays on the device: grid-stride launches sized for the worst case
     TimeScope ts(ctx, "fpfh_spfh");
-    const int64_t waves = std::min<int64_t>(ns, 256 * 4 * 32);  // up to 32 waves per CU in flight
+    // 16 waves per CU (measured, 1M-point room: 8 -> 1.06 ms, 12 -> 1.13, 16 -> 0.94, 20 -> 0.99,
+    // 32 -> 1.24, 128 -> 2.45)
+    const int64_t waves = std::min<int64_t>(ns, 256 * 4 * 16);
     k_fpfh_spfh<<<(unsigned)std::max<int64_t>(8, ceil_div(waves, 4) & ~7), 256, 0, st>>>(
         g, snp, slist, d_sel, rr, hcount, kcount, slowq, n_slow, slow_cap, d_pairs);
     k_fpfh_exact<<<256, 256, 0, st>>>(g, snp, slist, slowq, n_slow, slow_cap, hcount, d_pairs);
