@@ -78,6 +78,7 @@ _SIGS = {
     "pfx_ctx_get_stream": (c_vp, [c_vp]),
     "pfx_ctx_synchronize": (c_int, [c_vp]),
     "pfx_ctx_set_timing": (c_int, [c_vp, c_int]),
+    "pfx_ctx_set_shared": (c_int, [c_vp, c_int]),
     "pfx_ctx_reset_timing": (c_int, [c_vp]),
     "pfx_ctx_kernel_time": (c_int, [c_vp, ctypes.c_char_p, ctypes.POINTER(c_dbl), c_i64p]),
     "pfx_ctx_last_stats": (c_int, [c_vp, ctypes.c_char_p, c_i64p]),

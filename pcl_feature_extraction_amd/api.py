@@ -96,6 +96,11 @@ class Context:
     def synchronize(self):
         self._check(self._lib.pfx_ctx_synchronize(self.h))
 
+    def set_shared(self, shared=True):
+        """Launch-shape hint: another stream runs latency-critical work on this device
+        concurrently (pfx_ctx_set_shared); results are unchanged."""
+        self._check(self._lib.pfx_ctx_set_shared(self.h, 1 if shared else 0))
+
     def set_timing(self, enable=True):
         self._check(self._lib.pfx_ctx_set_timing(self.h, 1 if enable else 0))
 

@@ -164,6 +164,13 @@ pfx_status pfx_ctx_set_timing(pfx_ctx* ctx, int enable) {
   PFX_API_END(ctx)
 }
 
+pfx_status pfx_ctx_set_shared(pfx_ctx* ctx, int shared) {
+  PFX_API_BEGIN
+  check_ctx(ctx);
+  ctx->shared_device = shared != 0;
+  PFX_API_END(ctx)
+}
+
 pfx_status pfx_ctx_reset_timing(pfx_ctx* ctx) {
   PFX_API_BEGIN
   check_ctx(ctx);

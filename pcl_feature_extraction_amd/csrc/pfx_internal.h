@@ -110,6 +110,9 @@ struct pfx_ctx {
   hipStream_t own_stream = nullptr;
   hipStream_t stream = nullptr;
   std::string last_error;
+  // another stream runs latency-critical work on this device concurrently (pfx_ctx_set_shared):
+  // throughput kernels whose grid is free (work queues) launch narrower
+  bool shared_device = false;
   pfx::KernelTimer timer;
   std::map<std::string, int64_t> stats;
   pfx::Grid grid_a, grid_b;          // normal-radius grid, feature-radius grid

@@ -72,6 +72,7 @@ class OverlappedNarfFpfh:
         self.s_side = torch.cuda.Stream(device)
         ctx_main.set_stream(self.s_main.cuda_stream)
         ctx_side.set_stream(self.s_side.cuda_stream)
+        ctx_main.set_shared(True)  # NARF shares the device with the critical normal estimation
         self.pool = ThreadPoolExecutor(max_workers=1)
 
     def __call__(self, b: ScanBuffers, normal_radius: float = 0.05, feat_radius: float = 0.08, params=None,
