@@ -972,9 +972,19 @@ void build_lists(pfx_ctx* ctx, const Grid& G, const uint8_t* mask, double radius
   DevBuf& lb = B("list");
   if (!lb.ptr) lb.get(sizeof(uint32_t) * 64 * (size_t)(n + 1));
   const int isort = sorted ? 1 : 0;
-  // tiles per queue fetch (measured: 4 beats 1 at r = 0.05 too; PFX_TILE_CHUNK overrides)
-  static const char* chunk_env = getenv("PFX_TILE_CHUNK");
-  const int chunk = chunk_env ? std::max(1, atoi(chunk_env)) : 4;
+  // tiles per queue fetch, per class: many cheap small tiles amortise the queue atomic over 4,
+  // the heavy sparse / dense tiles balance better with 2 / 1 (sweep S/P/D on the 1M-pt room,
+  // configs[1] and Harris3D: 4/4/4 162.7, 31.7, 230.4; 4/2/2 166.0, 33.2, 230.3; 4/2/1 166.6,
+  // 34.9, 229.6; 2/2/2 166.5, 33.5, 208.4 Mpoints/s).  PFX_TILE_CHUNK sets all three,
+  // PFX_TILE_CHUNK_S / _P / _D one class (sweeps)
+  auto env_or = [](const char* name, int dflt) {
+    const char* e = getenv(name);
+    return e ? std::max(1, atoi(e)) : dflt;
+  };
+  static const int chunk_all = env_or("PFX_TILE_CHUNK", 0);
+  static const int ch_small = env_or("PFX_TILE_CHUNK_S", chunk_all ? chunk_all : 4),
+                   ch_sparse = env_or("PFX_TILE_CHUNK_P", chunk_all ? chunk_all : 2),
+                   ch_dense = env_or("PFX_TILE_CHUNK_D", chunk_all ? chunk_all : 1);
   for (int attempt = 0; attempt < 2; ++attempt) {
     ListOut lo{off, cnt, lgs, static_cast<uint32_t*>(lb.ptr), cursor, lb.bytes / sizeof(uint32_t)};
     if (attempt) {  // (the first attempt's cursors were zeroed by k_list_init)
@@ -1006,17 +1016,17 @@ void build_lists(pfx_ctx* ctx, const Grid& G, const uint8_t* mask, double radius
         TimeScope t0(ctx, std::string(tag) + "_lists_small");
         k_nb_tile<kTcapSmall, 256, kTcapSmall, true><<<256 * 4 * 2, 256, 0, st>>>(
             g, qpos, recs, kRecInts, counters + 10, rr, 256.0f / rr, isort, lo, single, counters + 2, counters + 11,
-            chunk);
+            ch_small);
       }
       {
         TimeScope t1(ctx, std::string(tag) + "_lists_sparse");
         k_nb_tile<512, 256, kTcapSparse, true><<<256 * 3 * 4, 256, 0, st>>>(
-            g, qpos, recs + (size_t)n * kRecInts, kRecInts, counters + 0, rr, 256.0f / rr, isort, lo, single, counters + 2, counters + 5, chunk);
+            g, qpos, recs + (size_t)n * kRecInts, kRecInts, counters + 0, rr, 256.0f / rr, isort, lo, single, counters + 2, counters + 5, ch_sparse);
       }
       {
         TimeScope t2(ctx, std::string(tag) + "_lists_dense");
         k_nb_tile<1024, 256, kTcapDense, false><<<256 * 2 * 4, 256, 0, st>>>(
-            g, qpos, recs + (size_t)(2 * n - 1) * kRecInts, -kRecInts, counters + 1, rr, 256.0f / rr, isort, lo, single, counters + 2, counters + 7, chunk);
+            g, qpos, recs + (size_t)(2 * n - 1) * kRecInts, -kRecInts, counters + 1, rr, 256.0f / rr, isort, lo, single, counters + 2, counters + 7, ch_dense);
       }
       {
         TimeScope t3(ctx, std::string(tag) + "_lists_query");
