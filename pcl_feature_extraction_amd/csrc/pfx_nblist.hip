@@ -973,18 +973,21 @@ void build_lists(pfx_ctx* ctx, const Grid& G, const uint8_t* mask, double radius
   if (!lb.ptr) lb.get(sizeof(uint32_t) * 64 * (size_t)(n + 1));
   const int isort = sorted ? 1 : 0;
   // tiles per queue fetch, per class: many cheap small tiles amortise the queue atomic over 4,
-  // the heavy sparse / dense tiles balance better with 2 / 1 (sweep S/P/D on the 1M-pt room,
-  // configs[1] and Harris3D: 4/4/4 162.7, 31.7, 230.4; 4/2/2 166.0, 33.2, 230.3; 4/2/1 166.6,
-  // 34.9, 229.6; 2/2/2 166.5, 33.5, 208.4 Mpoints/s).  PFX_TILE_CHUNK sets all three,
-  // PFX_TILE_CHUNK_S / _P / _D one class (sweeps)
+  // the heavy sparse / dense tiles balance better with 2 / 1 at ~1M queries (sweep S/P/D on the
+  // 1M-pt room, configs[1] and Harris3D: 4/4/4 162.7, 31.7, 230.4; 4/2/2 166.0, 33.2, 230.3;
+  // 4/2/1 166.6, 34.9, 229.6; 2/2/2 166.5, 33.5, 208.4 Mpoints/s), while the 10M-pt dense
+  // variant, with ~10x the heavy tiles per workgroup, wants 4 again (P/D 2/1 8.83, 2/2 9.11,
+  // 2/4 9.22, 4/4 9.25 Mpoints/s): the heavy classes take n / 2M tiles per fetch, clamped to
+  // [2, 4] / [1, 4].  PFX_TILE_CHUNK sets all three, PFX_TILE_CHUNK_S / _P / _D one class
   auto env_or = [](const char* name, int dflt) {
     const char* e = getenv(name);
     return e ? std::max(1, atoi(e)) : dflt;
   };
   static const int chunk_all = env_or("PFX_TILE_CHUNK", 0);
-  static const int ch_small = env_or("PFX_TILE_CHUNK_S", chunk_all ? chunk_all : 4),
-                   ch_sparse = env_or("PFX_TILE_CHUNK_P", chunk_all ? chunk_all : 2),
-                   ch_dense = env_or("PFX_TILE_CHUNK_D", chunk_all ? chunk_all : 1);
+  const int heavy = (int)std::min<int64_t>(4, n >> 21);
+  const int ch_small = env_or("PFX_TILE_CHUNK_S", chunk_all ? chunk_all : 4),
+            ch_sparse = env_or("PFX_TILE_CHUNK_P", chunk_all ? chunk_all : std::max(2, heavy)),
+            ch_dense = env_or("PFX_TILE_CHUNK_D", chunk_all ? chunk_all : std::max(1, heavy));
   for (int attempt = 0; attempt < 2; ++attempt) {
     ListOut lo{off, cnt, lgs, static_cast<uint32_t*>(lb.ptr), cursor, lb.bytes / sizeof(uint32_t)};
     if (attempt) {  // (the first attempt's cursors were zeroed by k_list_init)
