@@ -142,7 +142,12 @@ struct pfx_ctx {
   hipEvent_t fork_ev[2] = {nullptr, nullptr};
   void ensure_side() {
     if (side) return;
-    PFX_HIP(hipStreamCreateWithFlags(&side, hipStreamNonBlocking));
+    // the forked work runs at the priority of the stream the ctx was driven on when it forked
+    // first (the overlapped step's normal estimation runs on a high-priority stream; measured
+    // neutral on the headline, 167.7 vs 167.8 Mpoints/s, kept so a caller's priority holds)
+    int prio = 0;
+    if (stream) PFX_HIP(hipStreamGetPriority(stream, &prio));
+    PFX_HIP(hipStreamCreateWithPriority(&side, hipStreamNonBlocking, prio));
     for (auto& e : fork_ev) PFX_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   }
   // small pinned host block for the per-call readbacks (counters, cursors): one D2H copy of
