@@ -123,6 +123,7 @@ void pfx_ctx_destroy(pfx_ctx* ctx) {
   if (ctx->side) (void)hipStreamDestroy(ctx->side);
   for (auto& e : ctx->fork_ev)
     if (e) (void)hipEventDestroy(e);
+  if (ctx->spin_ev) (void)hipEventDestroy(ctx->spin_ev);
   if (ctx->host_rb) (void)hipHostFree(ctx->host_rb);
   if (ctx->fpfh_rb_mem) (void)hipHostFree(ctx->fpfh_rb_mem);
   delete ctx;

@@ -131,7 +131,7 @@ static bool bbox_dev(pfx_ctx* ctx, Grid& g, const float* d_x, const float* d_y, 
   }
   uint32_t* h = ctx->readback<uint32_t>();  // pinned, 4 KB >= 6 * kBboxBlocks words
   PFX_HIP(hipMemcpyAsync(h, mm, sizeof(uint32_t) * 6 * blocks, hipMemcpyDeviceToHost, st));
-  PFX_HIP(hipStreamSynchronize(st));
+  ctx->sync_spin(st);
   uint32_t r[6] = {0xffffffffu, 0xffffffffu, 0xffffffffu, 0u, 0u, 0u};
   for (int b = 0; b < blocks; ++b)
     for (int d = 0; d < 3; ++d) {

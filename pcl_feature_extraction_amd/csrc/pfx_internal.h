@@ -2,6 +2,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <cstdlib>
 
 #include <map>
 #include <stdexcept>
@@ -140,6 +141,23 @@ struct pfx_ctx {
   // one side stream + fork/join events (normal estimation's long-list chains), created on first use
   hipStream_t side = nullptr;
   hipEvent_t fork_ev[2] = {nullptr, nullptr};
+  // host wait for a stream on the critical path of a call (a readback that sizes the next
+  // launches): an event polled with hipEventQuery instead of hipStreamSynchronize's blocking
+  // wait, whose wake-up left ~150 us idle on the stream per readback (PFX_SYNC_BLOCK=1: blocking)
+  hipEvent_t spin_ev = nullptr;
+  void sync_spin(hipStream_t st) {
+    static const bool block = getenv("PFX_SYNC_BLOCK") != nullptr;
+    if (block) {
+      PFX_HIP(hipStreamSynchronize(st));
+      return;
+    }
+    if (!spin_ev) PFX_HIP(hipEventCreateWithFlags(&spin_ev, hipEventDisableTiming));
+    PFX_HIP(hipEventRecord(spin_ev, st));
+    hipError_t e;
+    while ((e = hipEventQuery(spin_ev)) == hipErrorNotReady) {
+    }
+    PFX_HIP(e);
+  }
   void ensure_side() {
     if (side) return;
     // the forked work runs at the priority of the stream the ctx was driven on when it forked

@@ -1004,7 +1004,7 @@ void build_lists(pfx_ctx* ctx, const Grid& G, const uint8_t* mask, double radius
       PFX_HIP(hipMemcpyAsync(rb->cnt, counters, sizeof(rb->cnt), hipMemcpyDeviceToHost, st));
       PFX_HIP(hipMemcpyAsync(rb->cur, cursor, sizeof(rb->cur), hipMemcpyDeviceToHost, st));
       PFX_HIP(hipMemcpyAsync(&rb->nq, d_nq, sizeof(int64_t), hipMemcpyDeviceToHost, st));
-      PFX_HIP(hipStreamSynchronize(st));
+      ctx->sync_spin(st);
     };
     DevBuf& hs = B("scratch");
     auto launch_huge = [&] {
