@@ -92,6 +92,13 @@ __global__ void __launch_bounds__(256) k_cell_keys(const float* __restrict__ x, 
   vals[i] = (uint32_t)i;
 }
 
+// cell_start[0, m) = v: a plain kernel launch (hipMemsetD32Async spent ~70 us of host time per
+// call in the HIP API trace, on the critical path of the grid build)
+__global__ void __launch_bounds__(256) k_fill_i32(int32_t* __restrict__ p, int64_t m, int32_t v) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < m; i += (int64_t)gridDim.x * blockDim.x)
+    p[i] = v;
+}
+
 // first sorted position of every occupied cell (cells are then completed by a suffix minimum)
 __global__ void __launch_bounds__(256) k_mark_starts(const uint32_t* __restrict__ skeys, int64_t n,
                                                      int32_t* __restrict__ cell_start) {
@@ -209,7 +216,8 @@ void build_grid(pfx_ctx* ctx, Grid& g, const float* d_x, const float* d_y, const
     TimeScope ts(ctx, "grid_build");
     // cell_start[c] = first sorted position with key >= c: mark the first position of every
     // occupied cell, then a suffix minimum fills the empty cells (no per-point atomics)
-    PFX_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(g.cell_start), (int)n, (size_t)(C + 2), st));
+    k_fill_i32<<<(unsigned)std::min<int64_t>(ceil_div(C + 2, 256), 2048), 256, 0, st>>>(g.cell_start, C + 2,
+                                                                                       (int32_t)n);
     if (n > 0) {
       k_cell_keys<<<(unsigned)ceil_div(n, 256), 256, 0, st>>>(d_x, d_y, d_z, n, inv, lo[0], lo[1], lo[2],
                                                               g.nx, g.ny, g.nz, keys, vals);
