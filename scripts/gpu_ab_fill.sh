@@ -1,7 +1,7 @@
 #!/bin/bash
 # A/B: base vs current library on the headline step (three pairs), after the grid/list tests
 mkdir -p gpurun_out
-timeout -k 10 400 python -u -m pytest tests -x -q -m gpu --timeout 120 --timeout-method thread -k "normals or pipeline or determinism or radius or iss or harris" > gpurun_out/ab_t.log 2>&1 || { tail -30 gpurun_out/ab_t.log; exit 1; }
+timeout -k 10 400 python -u -m pytest tests -x -q -m gpu --timeout 120 --timeout-method thread -k "normals or pipeline or determinism or radius or iss or harris or grid or fpfh" > gpurun_out/ab_t.log 2>&1 || { tail -30 gpurun_out/ab_t.log; exit 1; }
 tail -1 gpurun_out/ab_t.log
 for i in 1 2 3; do
 for L in libpfx_base.so libpfx.so; do
