@@ -327,11 +327,12 @@ pfx_status pfx_harris3d_keypoints(pfx_ctx* ctx, const float* x, const float* y, 
 /* HarrisKeypoint6D (keypoints.h:164-176) + Keypoints::getKeypointsCloud: normals at the radius
  * (viewpoint 0), IntensityGradientEstimation at the radius over the colour intensity
  * float(299 r + 587 g + 114 b) * 0.001f (IntensityFieldAccessor<PointXYZRGB>), gradients of
- * squared length > 200 scaled to unit length, the 6x6 covariance of (normal, gradient) over the
+ * squared length > 200 scaled to unit length and every other gradient (NaN ones included) set
+ * to 0 (harris_6d.hpp's else branch), the 6x6 covariance of (normal, gradient) over the
  * radius ball and its fourth eigenvalue as the response (responseTomasi), non-maximum
  * suppression above `threshold`, corner refinement, snap -- outputs as the Harris3D entry.
  * rgb: one packed 0x00RRGGBB word per point (the bits of PointXYZRGB::rgb).  grad (nullable,
- * 3 n floats): the normalised gradient of every point (NaN where PCL writes NaN). */
+ * 3 n floats): the normalised gradient of every point (0 where PCL's normalisation zeroes it). */
 pfx_status pfx_harris6d_keypoints_dev(pfx_ctx* ctx, const float* d_x, const float* d_y, const float* d_z,
                                       const uint32_t* d_rgb, int64_t n, double radius, float threshold,
                                       int32_t non_max, int32_t refine, int32_t* d_idx, int64_t cap, int64_t* n_out,

@@ -840,6 +840,8 @@ void h6_normalise(float g[3]) {  // HarrisKeypoint6D::detectKeypoints, "remove t
     g[0] = g[0] * len;
     g[1] = g[1] * len;
     g[2] = g[2] * len;
+  } else {  // harris_6d.hpp: gradient_x = gradient_y = gradient_z = 0 (a NaN len lands here too)
+    g[0] = g[1] = g[2] = 0.0f;
   }
 }
 

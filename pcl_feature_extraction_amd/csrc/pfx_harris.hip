@@ -141,7 +141,7 @@ __device__ __forceinline__ float rgb_demeaned(uint32_t c, float mean) {
 }
 
 // IntensityGradientEstimation::computeFeature + computePointIntensityGradient, then
-// HarrisKeypoint6D's normalisation (|g|^2 > 200 -> unit length): lane per list, two passes over
+// HarrisKeypoint6D's normalisation (|g|^2 > 200 -> unit length, else 0): lane per list, two passes over
 // the FLANN-ordered r-neighbours (centroid and mean intensity, then the demeaned 3x3 system)
 __global__ void __launch_bounds__(256) k_intensity_gradient(GridView g, NbLists L, const uint32_t* __restrict__ rgb,
                                                             const float* __restrict__ nx, const float* __restrict__ ny,
@@ -181,7 +181,9 @@ __global__ void __launch_bounds__(256) k_intensity_gradient(GridView g, NbLists 
   const int32_t i = g.perm[p];
   float o[3];
   if (k < 3) {
-    o[0] = o[1] = o[2] = __int_as_float(0x7fc00000);
+    // IntensityGradientEstimation writes NaN; the normalisation's len > 200 test fails on NaN
+    // and its else branch zeroes the gradient
+    o[0] = o[1] = o[2] = 0.0f;
   } else {
     float A00 = 0.f, A01 = 0.f, A02 = 0.f, A11 = 0.f, A12 = 0.f, A22 = 0.f, b0 = 0.f, b1 = 0.f, b2 = 0.f;
     for (int m = 0; m < k; ++m) {
@@ -220,6 +222,8 @@ __global__ void __launch_bounds__(256) k_intensity_gradient(GridView g, NbLists 
       o[0] = o[0] * len;
       o[1] = o[1] * len;
       o[2] = o[2] * len;
+    } else {  // harris_6d.hpp: gradient_x = gradient_y = gradient_z = 0 (NaN gradients included)
+      o[0] = o[1] = o[2] = 0.0f;
     }
   }
   gx[i] = o[0];

@@ -2,7 +2,7 @@
 keypoints.h:164-176, with getKeypointsCloud keypoints.h:365-395) through the C-ABI against the CPU
 restatement (oracle/or_keypoints.cpp orc_harris6d; parity vs real PCL unpinned).
 
-Bar: bit-exact -- the normalised intensity gradients (float bits, NaN where PCL writes NaN), the
+Bar: bit-exact -- the normalised intensity gradients (float bits; 0 where the > 200 normalisation zeroes them, NaN for non-finite points), the
 per-point response (the fourth eigenvalue of the 6x6 covariance, float bits), the refined corners
 (float bits) and the snapped keypoint indices.  Covers the reference's four clouds with their own
 colours, a textured synthetic scene with NaN points and duplicates, refinement on and off,

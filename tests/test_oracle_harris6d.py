@@ -82,15 +82,43 @@ def test_response_is_the_fourth_eigenvalue_of_the_6d_covariance(scene):
 
 def test_gradient_lies_in_the_tangent_plane(scene):
     x, y, z, rgb, (kp, resp, cor, grad), (nx, ny, nz, _) = scene
-    ok = np.isfinite(grad[:, 0])
+    assert np.isfinite(grad).all()  # NaN gradients (< 3 neighbours) fail len > 200 and are zeroed
+    ok = np.isfinite(nx)
     assert ok.mean() > 0.9
     n = np.stack([nx, ny, nz], 1)[ok]
     g = grad[ok].astype(np.float64)
     dot = np.abs((n * g).sum(1))
     assert (dot <= 1e-4 * np.maximum(1.0, np.linalg.norm(g, axis=1))).all()
-    # normalised when |g|^2 > 200, else untouched (so always |g|^2 <= 200 or ~1)
+    # normalised when |g|^2 > 200, else zeroed (harris_6d.hpp's else branch): 0 or ~1
     l2 = (g * g).sum(1)
-    assert ((l2 <= 200.0) | (np.abs(l2 - 1.0) < 1e-5)).all()
+    assert ((l2 == 0.0) | (np.abs(l2 - 1.0) < 1e-5)).all()
+
+
+def _ramp_plane(levels_per_metre, grey=True):
+    # a 1 m x 1 m plane at z = 2 sampled every 5 mm, grey (or blue) level rising along x
+    u = np.arange(0.0, 1.0, 0.005)
+    gx, gy = np.meshgrid(u, u, indexing="ij")
+    x = gx.ravel().astype(np.float32)
+    y = gy.ravel().astype(np.float32)
+    z = np.full_like(x, 2.0)
+    lv = np.clip(np.floor(x * levels_per_metre), 0, 255).astype(np.uint32)
+    return x, y, z, ((lv << 16) | (lv << 8) | lv) if grey else lv
+
+
+def test_weak_gradients_are_zeroed_strong_ones_unit_length():
+    # harris_6d.hpp: len = |g|^2; len > 200 -> g /= sqrt(len), else g = 0.  Blue steps of one
+    # level (intensity 0.114) every 20 cm give |g| of a few units at the steps (< sqrt(200)) and 0
+    # between them; a grey ramp of 200 levels per metre has |g| ~ 200
+    x, y, z, rgb = _ramp_plane(5.0, grey=False)
+    _, _, _, grad = O.harris6d(x, y, z, rgb, refine=False)
+    assert np.isfinite(grad).all()
+    assert np.array_equal(grad, np.zeros_like(grad))
+    x, y, z, rgb = _ramp_plane(200.0)
+    _, _, _, grad = O.harris6d(x, y, z, rgb, refine=False)
+    inner = (x > 0.05) & (x < 0.95) & (y > 0.05) & (y < 0.95)
+    g = grad[inner].astype(np.float64)
+    assert np.allclose((g * g).sum(1), 1.0, atol=1e-5)
+    assert (np.abs(g[:, 0]) > 0.95).all()  # along the ramp (up to the level quantisation)
 
 
 def test_uniform_colour_gives_the_normal_covariance_answer():
