@@ -231,8 +231,8 @@ def bench_scans(args, torch, dist, dev, world, rank, local):
 
     from pcl_feature_extraction_amd import Context
     from pcl_feature_extraction_amd.dist import gather_to_root, in_scan_order, owned_scans
-    from pcl_feature_extraction_amd.pipeline import (OverlappedNarfFpfh, alloc, alloc_shot, keypoint_rows,
-                                                     narf_shot)
+    from pcl_feature_extraction_amd.pipeline import (BatchNarfFpfh, OverlappedNarfFpfh, alloc, alloc_shot,
+                                                     keypoint_rows, narf_shot)
     from pcl_feature_extraction_amd.synth import ROOM_SCALE, synth_room, synth_seabed
 
     shot = args.workload == "shot"
@@ -249,6 +249,10 @@ def bench_scans(args, torch, dist, dev, world, rank, local):
     ctx.set_stream(torch.cuda.current_stream(dev).cuda_stream)
     ctx_n = Context(local)  # normal estimation overlapped with NARF on a second stream
     run_fpfh = OverlappedNarfFpfh(torch, ctx, ctx_n, dev)
+    # several scans on this rank (configs[4] at N < 8): the software-pipelined batch pass (scan
+    # i's FPFH and scan i+1's NARF under scan i+1's normal estimation); one scan: the overlapped pass
+    run_batch = (BatchNarfFpfh(torch, ctx, ctx_n, dev, side_stream=run_fpfh.s_side)
+                 if (len(mine) > 1 and not shot) else None)
     scans, host = [], []
     for s in mine:
         if dense:  # the configs[2] scene (same scale s) at 10x the density
@@ -275,8 +279,16 @@ def bench_scans(args, torch, dist, dev, world, rank, local):
         idx = torch.from_numpy(keypoint_rows(kp, npts).astype(np.int32)).to(dev, non_blocking=True)
         return b.desc[:k], idx
 
+    def batch_scans():
+        blocks = []
+        for b, (kp, k) in zip(scans, run_batch(scans)):
+            state["kp"] = kp
+            idx = torch.from_numpy(keypoint_rows(kp, npts).astype(np.int32)).to(dev, non_blocking=True)
+            blocks.append((b.desc[:k], idx))
+        return blocks
+
     def step():
-        blocks = [one_scan(b) for b in scans]
+        blocks = batch_scans() if run_batch is not None else [one_scan(b) for b in scans]
         state["rows"] = int(blocks[-1][0].shape[0]) if blocks else 0
         if world > 1 and not shot:
             state["gathered"] = gather_to_root(torch, dist, blocks, 33, dev, per_rank_max)
@@ -286,19 +298,30 @@ def bench_scans(args, torch, dist, dev, world, rank, local):
     nb_scan, long_scan = [], []
     for w in range(max(args.warmup, 1)):
         blocks = []
-        for b in scans:
-            blocks.append(one_scan(b))
-            if w == 0:
-                c = ctx if shot else ctx_n
-                nb_scan.append(c.stat("normals_neighbors"))
-                long_scan.append((c.stat("normals_long_neighbors"), c.stat("normals_long_queries")))
+        if w == 0 or run_batch is None:
+            for b in scans:
+                blocks.append(one_scan(b))
+                if w == 0:
+                    c = ctx if shot else ctx_n
+                    nb_scan.append(c.stat("normals_neighbors"))
+                    long_scan.append((c.stat("normals_long_neighbors"), c.stat("normals_long_queries")))
+        else:
+            blocks = batch_scans()
         if world > 1 and not shot:
             gather_to_root(torch, dist, blocks, 33, dev, per_rank_max)
     torch.cuda.synchronize(dev)
+    # the same scans back to back through the single-scan overlapped pass (no cross-scan
+    # pipelining), for the batch pipeline's gain; not part of `value`
+    seq_ms = None
+    if run_batch is not None and rank == 0:
+        seq_el = timed(torch, dist, dev, 1, max(1, args.steps // 4), lambda: [one_scan(b) for b in scans])
+        seq_ms = seq_el / max(1, args.steps // 4) * 1e3
     for c in (ctx, ctx_n):
         c.set_timing(True)
         c.reset_timing()
     elapsed = timed(torch, dist, dev, world, args.steps, step)
+    # deferred errors of the stream-ordered calls (FPFH capacity), outside the timed region
+    (run_batch or run_fpfh).check()
     timers = {nm: (ctx.kernel_time(nm)[0] + ctx_n.kernel_time(nm)[0], ctx.kernel_time(nm)[1] + ctx_n.kernel_time(nm)[1])
               for nm in VERBOSE_TIMERS}
     for c in (ctx, ctx_n):
@@ -375,6 +398,13 @@ def bench_scans(args, torch, dist, dev, world, rank, local):
     if rank == 0:
         line = scans_line(args, world, n_scans, mine, shot, elapsed, timers, iso, nb_scan, long_scan, stat, npts)
         line["config"]["descriptor_rows"] = state["rows"]
+        if seq_ms is not None:
+            line["batch_pipeline"] = {
+                "scans_on_rank0": len(mine), "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+                "back_to_back_ms_per_step": round(seq_ms, 4),
+                "speedup": round(seq_ms / (elapsed / args.steps * 1e3), 4),
+                "note": "BatchNarfFpfh (scan i's FPFH and scan i+1's NARF under scan i+1's normals) vs the same "
+                        "scans through the single-scan overlapped pass back to back (rank 0 alone)"}
         if batch is not None:
             line["config"]["gathered_on_rank0"] = batch
             line["config"]["ranks_seen_by_rccl"] = dist.get_world_size()
@@ -395,6 +425,8 @@ def bench_scans(args, torch, dist, dev, world, rank, local):
         line["cpu_baseline"] = cpu
         print(json.dumps(line), flush=True)
     run_fpfh.close()
+    if run_batch is not None:
+        run_batch.close()
     ctx.close()
     ctx_n.close()
 
@@ -796,7 +828,8 @@ def bench_config1(args, torch, dev, world, rank, local):
 
     def step():
         ctx.normals_dev(b.x, b.y, b.z, 0.05, b.nx, b.ny, b.nz, b.curv)
-        ctx.fpfh_dev(b.x, b.y, b.z, b.nx, b.ny, b.nz, b.x, b.y, b.z, 0.05, b.desc, same_as_surface=True)
+        ctx.fpfh_dev(b.x, b.y, b.z, b.nx, b.ny, b.nz, b.x, b.y, b.z, 0.05, b.desc, same_as_surface=True,
+                     after_normals=True)
 
     for _ in range(max(args.warmup, 1)):
         step()

@@ -101,11 +101,17 @@ pfx_status pfx_ctx_create(int device, pfx_ctx** out);
 void pfx_ctx_destroy(pfx_ctx* ctx);
 const char* pfx_last_error(const pfx_ctx* ctx);
 /* Use an external hipStream_t (e.g. torch.cuda.current_stream().cuda_stream); NULL is HIP's
- * null stream (torch's default stream).  A new ctx runs on its own non-blocking stream. */
+ * null stream (torch's default stream).  A new ctx runs on its own non-blocking stream, created
+ * by the first call that runs on it (a ctx set to an external stream first never creates one). */
 pfx_status pfx_ctx_set_stream(pfx_ctx* ctx, void* hip_stream);
 /* Back to the ctx-owned non-blocking stream. */
 pfx_status pfx_ctx_use_own_stream(pfx_ctx* ctx);
 void* pfx_ctx_get_stream(pfx_ctx* ctx);
+/* Frees every device scratch buffer of ctx (grids, neighbour lists, the rarely used overflow
+ * scratch of the list builder and the FPFH weighting, NARF images) after synchronising its
+ * stream; the next call reallocates what it needs.  Held state (lists kept for
+ * pfx_normals_chains_dev / pfx_fpfh_after_normals_dev, prepared FPFH grids) is dropped. */
+pfx_status pfx_ctx_trim(pfx_ctx* ctx);
 pfx_status pfx_ctx_synchronize(pfx_ctx* ctx);
 /* Launch-shape hint, no effect on results: another stream of this process runs latency-critical
  * work on the device at the same time (the overlapped NARF + normal estimation step).
@@ -162,15 +168,23 @@ pfx_status pfx_fpfh(pfx_ctx* ctx, const float* sx, const float* sy, const float*
 /* _dev: stream-ordered, no host synchronisation; its statistics (pfx_ctx_last_stats) and a
  * neighbourhood beyond the 2^22 capacity (PFX_ERR_CAPACITY) are reported by the next
  * pfx_ctx_synchronize / pfx_ctx_last_stats on this ctx.
- * _dev, same_as_surface: when the last pfx_normals_dev / pfx_normals_lists_dev on this ctx ran on
- * the same (d_sx, d_sy, d_sz, n_surface) at the same radius -- Features::compute's sequence,
- * features.h:187-195 -- its FLANN-ordered neighbour lists are reused for the weighting (the
- * coordinates must not have changed in between). */
+ * pfx_fpfh_dev never reuses state of an earlier normal estimation: it builds its own lists. */
 pfx_status pfx_fpfh_dev(pfx_ctx* ctx, const float* d_sx, const float* d_sy, const float* d_sz,
                         const float* d_snx, const float* d_sny, const float* d_snz,
                         int64_t n_surface, const float* d_qx, const float* d_qy,
                         const float* d_qz, int64_t nq, int same_as_surface, double radius,
                         float* d_out);
+/* Features::compute's sequence (features.h:187-195): pfx_fpfh_dev right after a
+ * pfx_normals_dev / pfx_normals_lists_dev on this ctx over the same device cloud.  The caller
+ * vouches that (d_sx, d_sy, d_sz) still hold the cloud that normal estimation ran on; with
+ * same_as_surface, equal pointers, n_surface and radius, its FLANN-ordered neighbour lists are
+ * then reused for the weighting (else they are built as in pfx_fpfh_dev).  Either way the
+ * held lists are released, so a second call cannot reuse them. */
+pfx_status pfx_fpfh_after_normals_dev(pfx_ctx* ctx, const float* d_sx, const float* d_sy, const float* d_sz,
+                                      const float* d_snx, const float* d_sny, const float* d_snz,
+                                      int64_t n_surface, const float* d_qx, const float* d_qy,
+                                      const float* d_qz, int64_t nq, int same_as_surface, double radius,
+                                      float* d_out);
 
 /* Builds the search-surface index of the next pfx_fpfh_dev call on this ctx ahead of time (the
  * surface grid needs only the coordinates, so it can overlap normal estimation -- PCL builds the

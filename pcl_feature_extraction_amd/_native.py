@@ -77,6 +77,7 @@ _SIGS = {
     "pfx_ctx_use_own_stream": (c_int, [c_vp]),
     "pfx_ctx_get_stream": (c_vp, [c_vp]),
     "pfx_ctx_synchronize": (c_int, [c_vp]),
+    "pfx_ctx_trim": (c_int, [c_vp]),
     "pfx_ctx_set_timing": (c_int, [c_vp, c_int]),
     "pfx_ctx_set_shared": (c_int, [c_vp, c_int]),
     "pfx_ctx_reset_timing": (c_int, [c_vp]),
@@ -90,6 +91,8 @@ _SIGS = {
                          c_int, c_dbl, c_vp]),
     "pfx_fpfh_dev": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp,
                              c_i64, c_int, c_dbl, c_vp]),
+    "pfx_fpfh_after_normals_dev": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp,
+                                           c_i64, c_int, c_dbl, c_vp]),
     "pfx_fpfh_prepare_dev": (c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_dbl]),
     "pfx_fpfh_support_mask_dev": (c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_i64, c_dbl, c_vp]),
     "pfx_fpfh_support_ball_dev": (c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_i64, c_dbl, c_vp]),

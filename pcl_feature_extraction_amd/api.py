@@ -94,7 +94,13 @@ class Context:
         self._check(self._lib.pfx_ctx_use_own_stream(self.h))
 
     def synchronize(self):
+        """Waits for this context's stream; raises deferred errors of the stream-ordered calls
+        (an FPFH neighbourhood beyond capacity -> PfxError, its rows NaN)."""
         self._check(self._lib.pfx_ctx_synchronize(self.h))
+
+    def trim(self):
+        """Frees every device scratch buffer of this context (pfx_ctx_trim)."""
+        self._check(self._lib.pfx_ctx_trim(self.h))
 
     def set_shared(self, shared=True):
         """Launch-shape hint: another stream runs latency-critical work on this device
@@ -192,10 +198,13 @@ class Context:
         self._check(self._lib.pfx_normals_dev(self.h, _ptr(x), _ptr(y), _ptr(z), x.numel(), float(r), _ptr(vp),
                                               _ptr(nx), _ptr(ny), _ptr(nz), _ptr(curv)))
 
-    def fpfh_dev(self, sx, sy, sz, nx, ny, nz, qx, qy, qz, r, out, same_as_surface=False):
-        self._check(self._lib.pfx_fpfh_dev(self.h, _ptr(sx), _ptr(sy), _ptr(sz), _ptr(nx), _ptr(ny), _ptr(nz),
-                                           sx.numel(), _ptr(qx), _ptr(qy), _ptr(qz), qx.numel(),
-                                           1 if same_as_surface else 0, float(r), _ptr(out)))
+    def fpfh_dev(self, sx, sy, sz, nx, ny, nz, qx, qy, qz, r, out, same_as_surface=False, after_normals=False):
+        """after_normals: the caller vouches that (sx, sy, sz) still hold the cloud of this context's
+        last normals_dev (Features::compute's sequence) -> pfx_fpfh_after_normals_dev, which may
+        reuse that estimation's neighbour lists."""
+        fn = self._lib.pfx_fpfh_after_normals_dev if after_normals else self._lib.pfx_fpfh_dev
+        self._check(fn(self.h, _ptr(sx), _ptr(sy), _ptr(sz), _ptr(nx), _ptr(ny), _ptr(nz), sx.numel(), _ptr(qx),
+                       _ptr(qy), _ptr(qz), qx.numel(), 1 if same_as_surface else 0, float(r), _ptr(out)))
 
     def normals_lists_dev(self, x, y, z, r, nx, ny, nz, curv):
         """Phase 1 of normals_dev: neighbour lists of every point (kept in this context)."""

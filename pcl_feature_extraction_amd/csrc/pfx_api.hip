@@ -45,6 +45,13 @@ float* stage_in(pfx_ctx* ctx, const char* name, const float* host, int64_t count
 void check_ctx(pfx_ctx* ctx) {
   if (!ctx) throw Error(PFX_ERR_INVALID, "null pfx_ctx");
   PFX_HIP(hipSetDevice(ctx->device));
+  // the ctx-owned stream exists only once a call runs on it: a ctx re-pointed at the caller's
+  // stream right after creation (the torch pipeline, the batch driver) never holds one, so it
+  // takes no hardware queue (GPU_MAX_HW_QUEUES = 4 per process)
+  if (ctx->on_own_stream && !ctx->own_stream) {
+    PFX_HIP(hipStreamCreateWithFlags(&ctx->own_stream, hipStreamNonBlocking));
+    ctx->stream = ctx->own_stream;
+  }
 }
 
 }  // namespace
@@ -97,8 +104,7 @@ pfx_status pfx_ctx_create(int device, pfx_ctx** out) {
     ctx = new pfx_ctx();
     ctx->device = device;
     PFX_HIP(hipSetDevice(device));
-    PFX_HIP(hipStreamCreateWithFlags(&ctx->own_stream, hipStreamNonBlocking));
-    ctx->stream = ctx->own_stream;
+    ctx->on_own_stream = true;  // created on first use (check_ctx)
     *out = ctx;
     return PFX_OK;
   } catch (const Error& e) {
@@ -135,6 +141,7 @@ pfx_status pfx_ctx_set_stream(pfx_ctx* ctx, void* hip_stream) {
   PFX_API_BEGIN
   check_ctx(ctx);
   harvest_timing(ctx);
+  ctx->on_own_stream = false;
   ctx->stream = static_cast<hipStream_t>(hip_stream);  // NULL = HIP's null (legacy default) stream
   PFX_API_END(ctx)
 }
@@ -143,11 +150,41 @@ pfx_status pfx_ctx_use_own_stream(pfx_ctx* ctx) {
   PFX_API_BEGIN
   check_ctx(ctx);
   harvest_timing(ctx);
+  ctx->on_own_stream = true;
+  check_ctx(ctx);
   ctx->stream = ctx->own_stream;
   PFX_API_END(ctx)
 }
 
-void* pfx_ctx_get_stream(pfx_ctx* ctx) { return ctx ? (void*)ctx->stream : nullptr; }
+void* pfx_ctx_get_stream(pfx_ctx* ctx) {
+  if (!ctx) return nullptr;
+  try {
+    check_ctx(ctx);
+  } catch (const pfx::Error& e) {
+    ctx->last_error = e.what();
+    return nullptr;
+  }
+  return (void*)ctx->stream;
+}
+
+pfx_status pfx_ctx_trim(pfx_ctx* ctx) {
+  PFX_API_BEGIN
+  check_ctx(ctx);
+  PFX_HIP(hipStreamSynchronize(ctx->stream));
+  pfx::fpfh_resolve(ctx);
+  pfx::narf_release(ctx);
+  pfx::normals_release(ctx);
+  pfx::keypoints_release(ctx);
+  ctx->grid_a.release();
+  ctx->grid_b.release();
+  for (auto& kv : ctx->bufs) kv.second.release();
+  ctx->prep_x = nullptr;
+  ctx->prep_n = -1;
+  ctx->prep_qx = nullptr;
+  ctx->prep_nq = -1;
+  ctx->fpfh_support = nullptr;
+  PFX_API_END(ctx)
+}
 
 pfx_status pfx_ctx_synchronize(pfx_ctx* ctx) {
   PFX_API_BEGIN
@@ -287,11 +324,10 @@ pfx_status pfx_normals(pfx_ctx* ctx, const float* x, const float* y, const float
   PFX_API_END(ctx)
 }
 
-pfx_status pfx_fpfh_dev(pfx_ctx* ctx, const float* d_sx, const float* d_sy, const float* d_sz,
-                        const float* d_snx, const float* d_sny, const float* d_snz, int64_t n_surface,
-                        const float* d_qx, const float* d_qy, const float* d_qz, int64_t nq,
-                        int same_as_surface, double radius, float* d_out) {
-  PFX_API_BEGIN
+static void fpfh_dev_checked(pfx_ctx* ctx, const float* d_sx, const float* d_sy, const float* d_sz,
+                             const float* d_snx, const float* d_sny, const float* d_snz, int64_t n_surface,
+                             const float* d_qx, const float* d_qy, const float* d_qz, int64_t nq,
+                             int same_as_surface, double radius, float* d_out, bool after_normals) {
   check_ctx(ctx);
   if (n_surface < 0 || nq < 0 || (nq && !d_out) ||
       (n_surface && (!d_sx || !d_sy || !d_sz || !d_snx || !d_sny || !d_snz)) ||
@@ -300,7 +336,27 @@ pfx_status pfx_fpfh_dev(pfx_ctx* ctx, const float* d_sx, const float* d_sy, cons
   if (same_as_surface && nq != n_surface)
     throw Error(PFX_ERR_INVALID, "fpfh: same_as_surface requires nq == n_surface");
   pfx::fpfh_dev(ctx, d_sx, d_sy, d_sz, d_snx, d_sny, d_snz, n_surface, d_qx, d_qy, d_qz, nq, same_as_surface,
-                radius, d_out, /*reuse_normal_lists=*/true);
+                radius, d_out, after_normals);
+}
+
+pfx_status pfx_fpfh_dev(pfx_ctx* ctx, const float* d_sx, const float* d_sy, const float* d_sz,
+                        const float* d_snx, const float* d_sny, const float* d_snz, int64_t n_surface,
+                        const float* d_qx, const float* d_qy, const float* d_qz, int64_t nq,
+                        int same_as_surface, double radius, float* d_out) {
+  PFX_API_BEGIN
+  fpfh_dev_checked(ctx, d_sx, d_sy, d_sz, d_snx, d_sny, d_snz, n_surface, d_qx, d_qy, d_qz, nq, same_as_surface,
+                   radius, d_out, false);
+  PFX_API_END(ctx)
+}
+
+pfx_status pfx_fpfh_after_normals_dev(pfx_ctx* ctx, const float* d_sx, const float* d_sy, const float* d_sz,
+                                      const float* d_snx, const float* d_sny, const float* d_snz,
+                                      int64_t n_surface, const float* d_qx, const float* d_qy,
+                                      const float* d_qz, int64_t nq, int same_as_surface, double radius,
+                                      float* d_out) {
+  PFX_API_BEGIN
+  fpfh_dev_checked(ctx, d_sx, d_sy, d_sz, d_snx, d_sny, d_snz, n_surface, d_qx, d_qy, d_qz, nq, same_as_surface,
+                   radius, d_out, true);
   PFX_API_END(ctx)
 }
 

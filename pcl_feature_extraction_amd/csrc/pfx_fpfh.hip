@@ -517,10 +517,14 @@ __global__ void __launch_bounds__(kWT) k_fpfh_weight(GridView g, const float* __
                          : sorted_neighbors_bucketed<kWT>(g, qx[q], qy[q], qz[q], rr, keys, keys + kCapW, kcap,
                                                           &s_count, SB);
     if (k > kcap) {
+      const bool give_up = GLOBAL || !ovf;
       if (tid == 0) {
-        if (GLOBAL || !ovf) atomicMax(err, k);
+        if (give_up) atomicMax(err, k);
         else ovf[atomicAdd(n_ovf, 1)] = (int32_t)q;  // weighted by the global-scratch pass
       }
+      // beyond every capacity: a NaN row (never the previous call's contents); the sticky word
+      // reports PFX_ERR_CAPACITY after the next synchronisation
+      if (give_up && tid < kDesc) out[q * kDesc + tid] = __builtin_nanf("");
       continue;
     }
     if (k == 0) {
@@ -957,9 +961,12 @@ void fpfh_dev(pfx_ctx* ctx, const float* sx, const float* sy, const float* sz, c
     // Features::compute estimates the normals of the same cloud first (features.h:187-195):
     // when that search had this radius, its lists are this one's (grid_a indexes the same
     // points); otherwise they are built on the FPFH grid
-    const NormalsState* nst = ctx->normals;
+    // (only on the caller's word, pfx_fpfh_after_normals_dev: equal pointers do not prove that
+    // the buffers still hold the cloud those lists were built on)
+    NormalsState* nst = ctx->normals;
     const bool reuse = reuse_normal_lists && nst && nst->ready && nst->x == sx && nst->y == sy && nst->z == sz &&
                        nst->n == ns && nst->r == r;
+    if (nst && reuse_normal_lists) nst->ready = false;  // consumed: a later call cannot vouch for them
     NbLists L;
     if (reuse) L = nst->L;
     else build_lists(ctx, G, nullptr, r, true, L, "fpfh");

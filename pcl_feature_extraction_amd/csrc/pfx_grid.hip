@@ -188,6 +188,12 @@ void build_grid(pfx_ctx* ctx, Grid& g, const float* d_x, const float* d_y, const
                 int64_t n, double radius) {
   PFX_CHECK(n >= 0 && n < (int64_t(1) << 31), "point count must be in [0, 2^31)");
   PFX_CHECK(radius > 0.0, "radius must be > 0");
+  if (&g == &ctx->grid_b) {  // a grid prepared ahead for the next fpfh_dev no longer holds
+    ctx->prep_x = nullptr;
+    ctx->prep_n = -1;
+    ctx->prep_qx = nullptr;
+    ctx->prep_nq = -1;
+  }
   hipStream_t st = ctx->stream;
   g.n = n;
   g.ux = d_x; g.uy = d_y; g.uz = d_z;

@@ -110,6 +110,7 @@ struct pfx_ctx {
   int device = 0;
   hipStream_t own_stream = nullptr;
   hipStream_t stream = nullptr;
+  bool on_own_stream = true;  // stream == own_stream, created lazily (pfx_api.hip check_ctx)
   std::string last_error;
   // another stream runs latency-critical work on this device concurrently (pfx_ctx_set_shared):
   // throughput kernels whose grid is free (work queues) launch narrower

@@ -102,6 +102,89 @@ class OverlappedNarfFpfh:
                               b.desc[:k])
         return kp, k
 
+    def check(self):
+        """Once per batch, outside any timed region: synchronises both contexts so errors the
+        stream-ordered calls defer (an FPFH neighbourhood beyond capacity) are raised."""
+        self.ctx_side.synchronize()
+        self.ctx.synchronize()
+
+    def close(self):
+        self.pool.shutdown()
+
+
+class BatchNarfFpfh:
+    """The (Narf, FPFH) pass over a batch of device-resident scans on one GPU -- the per-scan loop
+    of evaluation.cpp:272-852 for the scans a rank owns (configs[4]) -- software-pipelined over two
+    streams: a worker thread issues every scan's normal estimation back to back on the side stream
+    (the step's critical path), while the calling thread issues scan i's NARF + keypoint gather +
+    FPFH surface/S preparation on the main stream and then scan i's FPFH behind an event on scan
+    i's normals.  So scan i's FPFH and scan i+1's NARF overlap scan i+1's normal estimation.
+    Results are those of narf_fpfh per scan (same kernels, same contexts per role)."""
+
+    def __init__(self, torch, ctx_main: Context, ctx_side: Context, device, main_stream=None, side_stream=None):
+        import os
+        self.torch = torch
+        self.ctx, self.ctx_side = ctx_main, ctx_side
+        self.s_main = main_stream if main_stream is not None else torch.cuda.current_stream(device)
+        # side_stream: share an OverlappedNarfFpfh's stream when both drive the same contexts
+        self.s_side = side_stream if side_stream is not None else torch.cuda.Stream(
+            device, priority=int(os.environ.get("PFX_SIDE_PRIO", "-1")))
+        ctx_main.set_stream(self.s_main.cuda_stream)
+        ctx_side.set_stream(self.s_side.cuda_stream)
+        ctx_main.set_shared(True)
+        from concurrent.futures import ThreadPoolExecutor
+        self.pool = ThreadPoolExecutor(max_workers=1)
+
+    def __call__(self, scans, normal_radius: float = 0.05, feat_radius: float = 0.08, params=None, cam=None):
+        """scans: list of ScanBuffers (coordinates written on the main stream before this call).
+        Returns [(kp pixel indices, K)] in scan order; descriptors in each scan's b.desc[:K]."""
+        import threading
+        torch = self.torch
+        self.s_side.wait_stream(self.s_main)
+        done = [threading.Event() for _ in scans]
+        evs = [torch.cuda.Event() for _ in scans]
+
+        failed = []
+
+        def normals_all():
+            try:
+                for i, b in enumerate(scans):
+                    self.ctx_side.normals_dev(b.x, b.y, b.z, normal_radius, b.nx, b.ny, b.nz, b.curv)
+                    evs[i].record(self.s_side)
+                    done[i].set()
+            except BaseException as e:
+                failed.append(e)
+                for d in done:  # release the issuing thread wherever it waits
+                    d.set()
+                raise
+
+        fut = self.pool.submit(normals_all)
+        out = []
+        try:
+            for i, b in enumerate(scans):
+                kp = self.ctx.narf_keypoints_dev(b.x, b.y, b.z, params or narf_params(support_size=0.2),
+                                                 cam or camera())
+                k = self.ctx.gather_points_dev(b.x, b.y, b.z, kp, b.kx, b.ky, b.kz)
+                self.ctx.fpfh_prepare_dev(b.x, b.y, b.z, feat_radius)
+                if k > 0:
+                    self.ctx.fpfh_prepare_queries_dev(b.x, b.y, b.z, b.kx[:k], b.ky[:k], b.kz[:k], feat_radius)
+                done[i].wait()
+                if failed:
+                    raise failed[0]
+                self.s_main.wait_event(evs[i])
+                if k > 0:
+                    self.ctx.fpfh_dev(b.x, b.y, b.z, b.nx, b.ny, b.nz, b.kx[:k], b.ky[:k], b.kz[:k], feat_radius,
+                                      b.desc[:k])
+                out.append((kp, k))
+        finally:
+            fut.result()
+        return out
+
+    def check(self):
+        """Raises deferred errors of the stream-ordered calls (see OverlappedNarfFpfh.check)."""
+        self.ctx_side.synchronize()
+        self.ctx.synchronize()
+
     def close(self):
         self.pool.shutdown()
 

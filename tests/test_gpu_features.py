@@ -234,9 +234,10 @@ def test_fpfh_weighting_beyond_lds_capacity(ctx):
 
 
 def test_fpfh_same_as_surface_dev_reuses_normal_lists():
-    """Device API, Features::compute's sequence (features.h:187-195): normals then FPFH on the
-    same device cloud at the same radius reuse the normals' FLANN-ordered lists for the
-    weighting; another radius builds its own.  Both bit-exact against the restatement."""
+    """Device API, Features::compute's sequence (features.h:187-195): normals then FPFH
+    (pfx_fpfh_after_normals_dev) on the same device cloud at the same radius reuse the normals'
+    FLANN-ordered lists for the weighting; another radius builds its own.  Both bit-exact against
+    the restatement."""
     import torch
     from pcl_feature_extraction_amd import Context
     x, y, z = _cloud("indoor_source")
@@ -249,11 +250,11 @@ def test_fpfh_same_as_surface_dev_reuses_normal_lists():
     with Context(0) as c:
         c.set_stream(torch.cuda.current_stream(dev).cuda_stream)
         c.normals_dev(dx, dy, dz, 0.05, nx, ny, nz, cv)
-        c.fpfh_dev(dx, dy, dz, nx, ny, nz, dx, dy, dz, 0.05, out, same_as_surface=True)
+        c.fpfh_dev(dx, dy, dz, nx, ny, nz, dx, dy, dz, 0.05, out, same_as_surface=True, after_normals=True)
         torch.cuda.synchronize(dev)
         assert c.stat("fpfh_weight_lists_reused") == 1
         g5 = out.cpu().numpy()
-        c.fpfh_dev(dx, dy, dz, nx, ny, nz, dx, dy, dz, 0.06, out, same_as_surface=True)
+        c.fpfh_dev(dx, dy, dz, nx, ny, nz, dx, dy, dz, 0.06, out, same_as_surface=True, after_normals=True)
         torch.cuda.synchronize(dev)
         assert c.stat("fpfh_weight_lists_reused") == 0
         g6 = out.cpu().numpy()
@@ -262,3 +263,41 @@ def test_fpfh_same_as_surface_dev_reuses_normal_lists():
         assert _nan_aware_equal(a.cpu().numpy(), b)
     assert _nan_aware_equal(g5, O.fpfh(x, y, z, on[0], on[1], on[2], x, y, z, 0.05, same_as_surface=True))
     assert _nan_aware_equal(g6, O.fpfh(x, y, z, on[0], on[1], on[2], x, y, z, 0.06, same_as_surface=True))
+
+
+def test_fpfh_dev_does_not_reuse_lists_of_rewritten_buffers():
+    """equal pointers do not prove equal contents.  Normals on scan A, then scan B
+    written into the same device buffers, then pfx_fpfh_dev (same_as_surface) with B's normals:
+    the result is B's descriptors (no stale lists), and a second after_normals call cannot
+    reuse lists that were consumed."""
+    import torch
+    from pcl_feature_extraction_amd import Context
+    xa, ya, za = (a[::3].copy() for a in _cloud("indoor_source"))
+    xb, yb, zb = (a[::3].copy() for a in _cloud("indoor_target"))
+    n = min(len(xa), len(xb))
+    xa, ya, za, xb, yb, zb = (a[:n].copy() for a in (xa, ya, za, xb, yb, zb))
+    dev = torch.device("cuda", 0)
+    dx, dy, dz = (torch.from_numpy(a).to(dev) for a in (xa, ya, za))
+    nx, ny, nz, cv = (torch.empty(n, device=dev) for _ in range(4))
+    out = torch.empty((n, 33), device=dev)
+    onb = O.normals(xb, yb, zb, 0.05)
+    with Context(0) as c:
+        c.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+        c.normals_dev(dx, dy, dz, 0.05, nx, ny, nz, cv)  # scan A's lists held by c
+        for d, h in zip((dx, dy, dz), (xb, yb, zb)):
+            d.copy_(torch.from_numpy(h).to(dev))           # scan B into the same buffers
+        for d, h in zip((nx, ny, nz), onb[:3]):
+            d.copy_(torch.from_numpy(h).to(dev))
+        c.fpfh_dev(dx, dy, dz, nx, ny, nz, dx, dy, dz, 0.05, out, same_as_surface=True)
+        torch.cuda.synchronize(dev)
+        assert c.stat("fpfh_weight_lists_reused") == 0
+        gb = out.cpu().numpy()
+        c.normals_dev(dx, dy, dz, 0.05, nx, ny, nz, cv)
+        c.fpfh_dev(dx, dy, dz, nx, ny, nz, dx, dy, dz, 0.05, out, same_as_surface=True, after_normals=True)
+        c.fpfh_dev(dx, dy, dz, nx, ny, nz, dx, dy, dz, 0.05, out, same_as_surface=True, after_normals=True)
+        torch.cuda.synchronize(dev)
+        assert c.stat("fpfh_weight_lists_reused") == 0  # the first call consumed them
+        gb2 = out.cpu().numpy()
+    ref = O.fpfh(xb, yb, zb, onb[0], onb[1], onb[2], xb, yb, zb, 0.05, same_as_surface=True)
+    assert _nan_aware_equal(gb, ref)
+    assert _nan_aware_equal(gb2, ref)
