@@ -10,10 +10,10 @@
 //  range_image_planar.hpp, features/src/range_image_border_extractor.cpp + impl/*.hpp,
 //  common/impl/vector_average.hpp, keypoints/src/narf_keypoint.cpp.
 //  Documented restatement choices (see DESIGN.md "NARF"):
-//    * interest image: the dense ("complete") formula at full resolution.  PCL's default
-//      sparse mode only skips pixels that cannot reach min_interest_value, so the keypoints
-//      are the same; the scale-space variant is not restated (planar images have no
-//      angular resolution).
+//    * interest image: the dense ("complete") formula at full resolution
+//      (calculateCompleteInterestImage); PCL's default sparse traversal only as a reconstruction
+//      (interestImageSparse, confidence L, params[7] = 2); the scale-space variant is not restated
+//      (planar images have no angular resolution).
 //    * VectorAverage covariance is used as a full symmetric matrix.
 //    * histogram cell of a NaN / negative angle -> 0 (UB in PCL).
 //  Single-threaded except the per-pixel interest loop (OpenMP, order-free).
@@ -672,6 +672,212 @@ void interestImage(const RangeImage& ri, const Border& B, const Params& P, std::
   }
 }
 
+// Reconstruction (confidence L) of PCL 1.7's NarfKeypoint::calculateSparseInterestImage, the
+// mode PCL's default Parameters (calculate_sparse_interest_image = true) select.  Its source
+// (keypoints/src/narf_keypoint.cpp) is not in this container and the NARF paper does not describe
+// it; the header documents it as "some heuristics to decide which areas of the interest image can
+// be left out".  What is restated here is the increased-radius scheme its locals name
+// (increased_radius = 1.5 R, radius_overhead = increased_radius - R, neighbours within the
+// overhead): pixels are visited in raster order; a visited pixel p grows its region with the
+// acceptance widened to the increased radius, computes its own interest exactly as the complete
+// formula does (contributions only from pixels within pixel distance 2 or within R of p, but
+// reached through the widened region), and bounds the interest of every pixel within the overhead
+// of p -- whose R-balls lie inside p's increased ball -- by the angle-change value of a histogram of
+// the raw surface-change scores over the increased region (pos <= scs, neg <= 1).  When that bound
+// is below min_interest_value those pixels are left out (interest 0, never visited).  The bound is
+// heuristic (the overhead pixels' own viewer rotations and region paths differ from p's), which is
+// exactly where this mode can depart from the complete one; tests/test_oracle_narf_sparse.py
+// measures whether it does on the reference's clouds and the bench scans.
+void interestImageSparse(const RangeImage& ri, const Border& B, const Params& P, std::vector<float>& interest) {
+  const int w = ri.w, h = ri.h;
+  const size_t n = (size_t)w * h;
+  interest.assign(n, 0.0f);
+  const float search_radius = 0.5f * P.support_size, radius_squared = search_radius * search_radius,
+              radius_reciprocal = 1.0f / search_radius, increased_radius = 1.5f * search_radius,
+              increased_radius_squared = increased_radius * increased_radius,
+              radius_overhead = increased_radius - search_radius,
+              radius_overhead_squared = radius_overhead * radius_overhead;
+  const int hist_size = 18;
+  const float deg = 0.017453292519943295769236907684886127134428718885417f;
+  const float d90 = 90.0f * deg, d180 = 180.0f * deg;
+  const V3 sensor = ri.sensorPos();
+  std::vector<char> touched(n, 0), done(n, 0);
+  std::vector<int> queue, overhead;
+  auto acv_of = [&](const float* hist) {
+    float acv = 0.0f;
+    for (int c1 = 0; c1 < hist_size - 1; ++c1) {
+      if (hist[c1] == 0.0f) continue;
+      for (int c2 = c1 + 1; c2 < hist_size; ++c2) {
+        if (hist[c2] == 0.0f) continue;
+        float nd = 2.0f * (float)(c2 - c1) / (float)hist_size;
+        nd = (nd <= 1.0f ? nd : 2.0f - nd);
+        acv = std::max(hist[c1] * hist[c2] * nd, acv);
+      }
+    }
+    return std::sqrt(acv);
+  };
+  for (int y = 0; y < h; ++y)
+    for (int x = 0; x < w; ++x) {
+      const int index = y * w + x;
+      if (done[(size_t)index]) continue;
+      if (!ri.isValidIdx(index)) continue;
+      if (B.traits[(size_t)index] & (bit(SHADOW_BORDER) | bit(VEIL_POINT))) continue;
+      done[(size_t)index] = 1;
+      const P4 point = ri.pts[(size_t)index];
+      V3 view = normalized3(sub(v3(point.x, point.y, point.z), sensor));
+      V3 tmp0 = normalized3(cross(v3(0.0f, -1.0f, 0.0f), view));
+      V3 tmp1 = normalized3(cross(view, tmp0));
+      V3 tmp2 = normalized3(view);
+      float hist[18], bound_hist[18];
+      for (int k = 0; k < hist_size; ++k) hist[k] = bound_hist[k] = 0.0f;
+      float negative_score = 1.0f;
+      queue.clear();
+      overhead.clear();
+      queue.push_back(index);
+      touched[(size_t)index] = 1;
+      for (size_t qi = 0; qi < queue.size(); ++qi) {
+        const int index2 = queue[qi];
+        if (!ri.isValidIdx(index2)) continue;
+        if (B.traits[(size_t)index2] & (bit(SHADOW_BORDER) | bit(VEIL_POINT))) continue;
+        const int y2 = index2 / w, x2 = index2 - y2 * w;
+        const P4 point2 = ri.pts[(size_t)index2];
+        const float pixelDistance = (float)std::max(std::abs(x2 - x), std::abs(y2 - y));
+        const float distance_squared = sqDist(point, point2);
+        if (pixelDistance > 2.0f && distance_squared > increased_radius_squared) continue;
+        for (int y3 = std::max(0, y2 - 1); y3 <= std::min(h - 1, y2 + 1); ++y3)
+          for (int x3 = std::max(0, x2 - 1); x3 <= std::min(w - 1, x2 + 1); ++x3) {
+            int index3 = y3 * w + x3;
+            if (!touched[(size_t)index3]) { queue.push_back(index3); touched[(size_t)index3] = 1; }
+          }
+        if (distance_squared <= radius_overhead_squared) overhead.push_back(index2);
+        const float scs = B.scs[(size_t)index2];
+        if (scs < P.min_surface_change_score) continue;
+        const V3 dir = B.scd[(size_t)index2];
+        V3 rot = v3(0.0f + dot3(tmp0, dir), 0.0f + dot3(tmp1, dir), 0.0f + dot3(tmp2, dir));
+        float inv = std::sqrt(rot.x * rot.x + rot.y * rot.y);
+        float dvx = rot.x * (1.0f / inv);
+        float angle = 0.5f * normAngle(2.0f * acosf_glibc(dvx));
+        float cellf = std::floor((angle + d90) / d180 * hist_size);
+        int cell;
+        if (!(cellf == cellf)) cell = 0;
+        else cell = std::min(hist_size - 1, (int)std::lrint(cellf));
+        if (cell < 0) cell = 0;
+        bound_hist[cell] = std::max(bound_hist[cell], scs);
+        if (pixelDistance > 2.0f && distance_squared > radius_squared) continue;  // not in p's own region
+        const float distance_factor = radius_reciprocal * std::sqrt(distance_squared);
+        float neg = 1.0f - 0.5f * scs * std::max(1.0f - distance_factor / P.optimal_distance_to_high_surface_change, 0.0f);
+        neg = neg * neg;
+        const float pos = (pixelDistance < 2.0) ? scs : scs * (1.0f - distance_factor);
+        hist[cell] = std::max(hist[cell], pos);
+        negative_score = std::min(negative_score, neg);
+      }
+      for (size_t qi = 0; qi < queue.size(); ++qi) touched[(size_t)queue[qi]] = 0;
+      interest[(size_t)index] = negative_score * acv_of(hist);
+      if (acv_of(bound_hist) < P.min_interest_value)
+        for (size_t k = 0; k < overhead.size(); ++k) done[(size_t)overhead[k]] = 1;
+    }
+}
+
+// Second reading of the same locals (confidence L): one region grow to the increased radius
+// around a seed p serves every not yet computed pixel q within the overhead of p (q's R-ball lies
+// inside the grown ball), whose interest is then formed from the seed's contributor list (the
+// complete formula's acceptance -- pixel distance <= 2 or distance <= R -- measured from q, but
+// the connectivity of the seed's region); seeds in raster order.  params[7] = 3.
+void interestImageSeeded(const RangeImage& ri, const Border& B, const Params& P, std::vector<float>& interest) {
+  const int w = ri.w, h = ri.h;
+  const size_t n = (size_t)w * h;
+  interest.assign(n, 0.0f);
+  const float search_radius = 0.5f * P.support_size, radius_squared = search_radius * search_radius,
+              radius_reciprocal = 1.0f / search_radius, increased_radius = 1.5f * search_radius,
+              increased_radius_squared = increased_radius * increased_radius,
+              radius_overhead = increased_radius - search_radius,
+              radius_overhead_squared = radius_overhead * radius_overhead;
+  const int hist_size = 18;
+  const float deg = 0.017453292519943295769236907684886127134428718885417f;
+  const float d90 = 90.0f * deg, d180 = 180.0f * deg;
+  const V3 sensor = ri.sensorPos();
+  std::vector<char> touched(n, 0), done(n, 0);
+  std::vector<int> queue, overhead, contrib;
+  auto usable = [&](int i) {
+    return ri.isValidIdx(i) && !(B.traits[(size_t)i] & (bit(SHADOW_BORDER) | bit(VEIL_POINT)));
+  };
+  for (int y = 0; y < h; ++y)
+    for (int x = 0; x < w; ++x) {
+      const int index = y * w + x;
+      if (done[(size_t)index] || !usable(index)) continue;
+      const P4 point = ri.pts[(size_t)index];
+      queue.clear();
+      overhead.clear();
+      contrib.clear();
+      queue.push_back(index);
+      touched[(size_t)index] = 1;
+      for (size_t qi = 0; qi < queue.size(); ++qi) {
+        const int index2 = queue[qi];
+        if (!usable(index2)) continue;
+        const int y2 = index2 / w, x2 = index2 - y2 * w;
+        const float pixelDistance = (float)std::max(std::abs(x2 - x), std::abs(y2 - y));
+        const float distance_squared = sqDist(point, ri.pts[(size_t)index2]);
+        if (pixelDistance > 2.0f && distance_squared > increased_radius_squared) continue;
+        for (int y3 = std::max(0, y2 - 1); y3 <= std::min(h - 1, y2 + 1); ++y3)
+          for (int x3 = std::max(0, x2 - 1); x3 <= std::min(w - 1, x2 + 1); ++x3) {
+            int index3 = y3 * w + x3;
+            if (!touched[(size_t)index3]) { queue.push_back(index3); touched[(size_t)index3] = 1; }
+          }
+        if (distance_squared <= radius_overhead_squared && !done[(size_t)index2]) overhead.push_back(index2);
+        if (B.scs[(size_t)index2] >= P.min_surface_change_score) contrib.push_back(index2);
+      }
+      for (size_t qi = 0; qi < queue.size(); ++qi) touched[(size_t)queue[qi]] = 0;
+      for (size_t oi = 0; oi < overhead.size(); ++oi) {
+        const int iq = overhead[oi];
+        const int yq = iq / w, xq = iq - yq * w;
+        const P4 pq = ri.pts[(size_t)iq];
+        V3 view = normalized3(sub(v3(pq.x, pq.y, pq.z), sensor));
+        V3 tmp0 = normalized3(cross(v3(0.0f, -1.0f, 0.0f), view));
+        V3 tmp1 = normalized3(cross(view, tmp0));
+        V3 tmp2 = normalized3(view);
+        float hist[18];
+        for (int k = 0; k < hist_size; ++k) hist[k] = 0.0f;
+        float negative_score = 1.0f;
+        for (size_t ci = 0; ci < contrib.size(); ++ci) {
+          const int is = contrib[ci];
+          const int ys = is / w, xs = is - ys * w;
+          const float pixelDistance = (float)std::max(std::abs(xs - xq), std::abs(ys - yq));
+          const float distance_squared = sqDist(pq, ri.pts[(size_t)is]);
+          if (pixelDistance > 2.0f && distance_squared > radius_squared) continue;
+          const float scs = B.scs[(size_t)is];
+          const V3 dir = B.scd[(size_t)is];
+          const float distance_factor = radius_reciprocal * std::sqrt(distance_squared);
+          float neg = 1.0f - 0.5f * scs * std::max(1.0f - distance_factor / P.optimal_distance_to_high_surface_change, 0.0f);
+          neg = neg * neg;
+          const float pos = (pixelDistance < 2.0) ? scs : scs * (1.0f - distance_factor);
+          V3 rot = v3(0.0f + dot3(tmp0, dir), 0.0f + dot3(tmp1, dir), 0.0f + dot3(tmp2, dir));
+          float inv = std::sqrt(rot.x * rot.x + rot.y * rot.y);
+          float dvx = rot.x * (1.0f / inv);
+          float angle = 0.5f * normAngle(2.0f * acosf_glibc(dvx));
+          float cellf = std::floor((angle + d90) / d180 * hist_size);
+          int cell;
+          if (!(cellf == cellf)) cell = 0;
+          else cell = std::min(hist_size - 1, (int)std::lrint(cellf));
+          if (cell < 0) cell = 0;
+          hist[cell] = std::max(hist[cell], pos);
+          negative_score = std::min(negative_score, neg);
+        }
+        float acv = 0.0f;
+        for (int c1 = 0; c1 < hist_size - 1; ++c1) {
+          if (hist[c1] == 0.0f) continue;
+          for (int c2 = c1 + 1; c2 < hist_size; ++c2) {
+            if (hist[c2] == 0.0f) continue;
+            float nd = 2.0f * (float)(c2 - c1) / (float)hist_size;
+            nd = (nd <= 1.0f ? nd : 2.0f - nd);
+            acv = std::max(hist[c1] * hist[c2] * nd, acv);
+          }
+        }
+        interest[(size_t)iq] = negative_score * std::sqrt(acv);
+        done[(size_t)iq] = 1;
+      }
+    }
+}
+
 void keypoints(const RangeImage& ri, const std::vector<float>& interest, const Params& P, std::vector<int>& out) {
   const int w = ri.w, h = ri.h;
   std::vector<InterestPoint> tmp;
@@ -742,7 +948,7 @@ int orc_range_image_planar(const float* x, const float* y, const float* z, i64 n
 }
 
 // params: float[16] packed as in pfx_narf_params order:
-//  support, max_no, min_dist, opt_dist, min_interest, min_scs, nms, sparse(ignored), poly(0), straight(0),
+//  support, max_no, min_dist, opt_dist, min_interest, min_scs, nms, sparse (2: reconstruction), poly(0), straight(0),
 //  prb, prpe, prbd, min_border_prob, prpc
 // debug_* optional (w*h): interest, surface change score, traits
 int orc_narf_keypoints(const float* x, const float* y, const float* z, i64 n, int w, int h, float cx, float cy,
@@ -770,7 +976,11 @@ int orc_narf_keypoints(const float* x, const float* y, const float* z, i64 n, in
   Border B(ri, P);
   B.run();
   std::vector<float> interest;
-  interestImage(ri, B, P, interest);
+  // params[7]: 2 = the reconstruction of PCL's sparse traversal (interestImageSparse); 0 / 1 =
+  // the complete formula (the GPU's output in either of its modes)
+  if ((int)params[7] == 2) interestImageSparse(ri, B, P, interest);
+  else if ((int)params[7] == 3) interestImageSeeded(ri, B, P, interest);
+  else interestImage(ri, B, P, interest);
   std::vector<int> kp;
   keypoints(ri, interest, P, kp);
   *n_out = (i64)kp.size();
