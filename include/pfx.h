@@ -369,6 +369,29 @@ pfx_status pfx_ransac_rejector(pfx_ctx* ctx, const float* sx, const float* sy, c
                                const int32_t* match, int64_t n, double threshold, int32_t max_iterations,
                                int32_t* keep, int64_t* n_keep, float* transformation);
 
+/* ---- multi-GPU scan batch (SURVEY 8(e), configs[4]) ------------------------------------- */
+/* Replaces the reference's per-scan loop for the (Narf, FPFH) pair (evaluation.cpp:272-852 over
+ * Keypoints::compute, keypoints.h:199-231, and Features<FPFHSignature33>::compute,
+ * features.h:175-196) for a C++ host with several GPUs in one process.  pfx_batch_create: the
+ * devices (ordinals), two contexts and two streams per device, and an RCCL communicator over them
+ * (ncclCommInitAll). */
+typedef struct pfx_batch pfx_batch;
+pfx_status pfx_batch_create(const int* devices, int n_devices, pfx_batch** out);
+void pfx_batch_destroy(pfx_batch* batch);
+const char* pfx_batch_last_error(const pfx_batch* batch);
+/* n_scans host clouds (x[s], y[s], z[s], n[s] points; SoA float); scan s runs on device
+ * s % n_devices: NARF keypoints (cam, params as pfx_narf_keypoints), the in-range pixel indices
+ * mapped to cloud points (keypoints.h:229), normals of the whole cloud at normal_radius, FPFH at the
+ * keypoints at feature_radius -- each device pipelines its scans over two streams.  The K_s x 33
+ * descriptors and K_s cloud indices of every scan are gathered on the first device over RCCL and
+ * copied out in scan order: rows[s] = K_s, scan s's rows start at sum_{t<s} K_t of desc
+ * (cap_rows x 33) and idx (cap_rows).  Results equal the per-scan entry points bit for bit.
+ * PFX_ERR_CAPACITY (rows filled in) when sum K_s > cap_rows. */
+pfx_status pfx_batch_narf_fpfh(pfx_batch* batch, int n_scans, const float* const* x, const float* const* y,
+                               const float* const* z, const int64_t* n, const pfx_camera* cam,
+                               const pfx_narf_params* params, double normal_radius, double feature_radius,
+                               float* desc, int32_t* idx, int64_t cap_rows, int64_t* rows);
+
 #ifdef __cplusplus
 } /* extern "C" */
 #endif

@@ -5,6 +5,6 @@ neighbourhoods, as hand-written HIP kernels behind the C-ABI in include/pfx.h (l
 See DESIGN.md.
 """
 from ._native import PfxError, lib  # noqa: F401
-from .api import Context, camera, narf_params  # noqa: F401
+from .api import Batch, Context, camera, narf_params  # noqa: F401
 
-__all__ = ["Context", "PfxError", "camera", "narf_params", "lib"]
+__all__ = ["Batch", "Context", "PfxError", "camera", "narf_params", "lib"]

@@ -138,6 +138,11 @@ _SIGS = {
     "pfx_harris6d_keypoints": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, ctypes.c_double, ctypes.c_float,
                                        ctypes.c_int32, ctypes.c_int32, c_vp, c_i64, c_i64p, c_vp, c_vp, c_i64p, c_vp,
                                        c_vp]),
+    "pfx_batch_create": (c_int, [c_vp, c_int, ctypes.POINTER(c_vp)]),
+    "pfx_batch_destroy": (None, [c_vp]),
+    "pfx_batch_last_error": (ctypes.c_char_p, [c_vp]),
+    "pfx_batch_narf_fpfh": (c_int, [c_vp, c_int, c_vp, c_vp, c_vp, c_vp, ctypes.POINTER(Camera),
+                                    ctypes.POINTER(NarfParams), c_dbl, c_dbl, c_vp, c_vp, c_i64, c_vp]),
     "pfx_ransac_rejector": (c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_i64,
                                     ctypes.c_double, ctypes.c_int32, c_vp, c_i64p, c_vp]),
 }

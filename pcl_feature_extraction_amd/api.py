@@ -434,3 +434,50 @@ class Context:
                                                   _ptr(tz), len(tx), _ptr(query), _ptr(match), n, threshold,
                                                   max_iterations, _ptr(keep), ctypes.byref(nk), _ptr(T)))
         return keep[: nk.value].copy(), T.reshape(4, 4)
+
+
+class Batch:
+    """pfx_batch: the multi-GPU scan batch of one process; scan s on devices[s % G],
+    results gathered on devices[0] over RCCL and returned in scan order."""
+
+    def __init__(self, devices=(0,)):
+        self._lib = N.lib()
+        devs = np.ascontiguousarray(devices, dtype=np.int32)
+        h = ctypes.c_void_p()
+        st = self._lib.pfx_batch_create(devs.ctypes.data_as(ctypes.c_void_p), len(devs), ctypes.byref(h))
+        if st != 0:
+            raise N.PfxError(st, "pfx_batch_create")
+        self.h = h
+
+    def close(self):
+        if getattr(self, "h", None):
+            self._lib.pfx_batch_destroy(self.h)
+            self.h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def narf_fpfh(self, clouds, normal_radius=0.05, feature_radius=0.08, params=None, cam=None, cap_rows=1 << 20):
+        """clouds: list of (x, y, z) host arrays.  Returns [(K_s x 33 descriptors, K_s cloud indices)]."""
+        cl = [tuple(_f32(a) for a in c) for c in clouds]
+        ns = len(cl)
+        arr = lambda i: (ctypes.c_void_p * max(ns, 1))(*[c[i].ctypes.data for c in cl])  # noqa: E731
+        xs, ys, zs = arr(0), arr(1), arr(2)
+        n = np.array([len(c[0]) for c in cl], np.int64)
+        desc = np.empty((cap_rows, 33), np.float32)
+        idx = np.empty(cap_rows, np.int32)
+        rows = np.zeros(max(ns, 1), np.int64)
+        st = self._lib.pfx_batch_narf_fpfh(self.h, ns, xs, ys, zs, _ptr(n), ctypes.byref(cam or camera()),
+                                           ctypes.byref(params or narf_params(support_size=0.2)),
+                                           float(normal_radius), float(feature_radius), _ptr(desc), _ptr(idx),
+                                           cap_rows, _ptr(rows))
+        if st != 0:
+            raise N.PfxError(st, self._lib.pfx_batch_last_error(self.h).decode())
+        out, o = [], 0
+        for k in rows[:ns]:
+            out.append((desc[o:o + k].copy(), idx[o:o + k].copy()))
+            o += int(k)
+        return out
