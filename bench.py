@@ -48,7 +48,7 @@ N_POINTS = 1_000_000
 DENSE_POINTS = 10_000_000  # SURVEY 8(d) dense variant: configs[2]'s scene at 10x density
 SHOT_SAMPLE = 10_000
 
-VERBOSE_TIMERS = ["grid_bbox", "grid_build", "normals", "normals_lists_phase", "normals_tiles", "normals_lists",
+VERBOSE_TIMERS = ["grid_bbox", "grid_build", "normals", "normals_fast", "normals_mfma", "normals_lists_phase", "normals_tiles", "normals_lists",
                   "normals_lists_small", "normals_lists_sparse",
                   "normals_lists_dense", "normals_lists_query", "normals_chain", "normals_chain_big", "normals_long", "range_image",
                   "narf_border", "narf_interest", "narf_nms", "narf_gather", "fpfh_mark", "fpfh_spfh",
@@ -157,7 +157,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", choices=["fpfh", "shot", "match", "iss", "harris", "harris6d", "config1", "dense"],
+    ap.add_argument("--workload", choices=["fpfh", "shot", "match", "iss", "harris", "harris6d", "config1", "dense",
+                                           "fastnormals"],
                     default="fpfh")
     ap.add_argument("--scans", type=int, default=0,
                     help="fpfh workload: scans per step (default 1 = configs[2] at --gpus 1, 8 = configs[4] at N > 1)")
@@ -239,6 +240,7 @@ def bench_scans(args, torch, dist, dev, world, rank, local):
 
     shot = args.workload == "shot"
     dense = args.workload == "dense"
+    fast = args.workload == "fastnormals"
     npts = DENSE_POINTS if dense else N_POINTS
     if shot:
         n_scans, seeds = world, [3] if world == 1 else [300 + r for r in range(world)]
@@ -251,6 +253,7 @@ def bench_scans(args, torch, dist, dev, world, rank, local):
     ctx.set_stream(torch.cuda.current_stream(dev).cuda_stream)
     ctx_n = Context(local)  # normal estimation overlapped with NARF on a second stream
     run_fpfh = OverlappedNarfFpfh(torch, ctx, ctx_n, dev)
+    run_fpfh.fast_normals = fast
     # several scans on this rank (configs[4] at N < 8): the software-pipelined batch pass (scan
     # i's FPFH and scan i+1's NARF under scan i+1's normal estimation); one scan: the overlapped pass
     run_batch = (BatchNarfFpfh(torch, ctx, ctx_n, dev, side_stream=run_fpfh.s_side)
@@ -302,8 +305,12 @@ def bench_scans(args, torch, dist, dev, world, rank, local):
         blocks = []
         if w == 0 or run_batch is None:
             for b in scans:
+                if w == 0 and fast:  # the neighbour count of the scan, from one exact estimation
+                    ctx_n.normals_dev(b.x, b.y, b.z, 0.05, b.nx, b.ny, b.nz, b.curv)
+                    nb_scan.append(ctx_n.stat("normals_neighbors"))
+                    long_scan.append((ctx_n.stat("normals_long_neighbors"), ctx_n.stat("normals_long_queries")))
                 blocks.append(one_scan(b))
-                if w == 0:
+                if w == 0 and not fast:
                     c = ctx if shot else ctx_n
                     nb_scan.append(c.stat("normals_neighbors"))
                     long_scan.append((c.stat("normals_long_neighbors"), c.stat("normals_long_queries")))
@@ -387,18 +394,32 @@ def bench_scans(args, torch, dist, dev, world, rank, local):
     # the same normal-estimation stage alone on the device (after the timed region, not part of
     # `value`): inside the step it shares the CUs with NARF on the other stream
     iso = None
+    deviation = None
+    if rank == 0 and fast:  # the fast mode against the product (parity-exact) path on the same scan
+        b = scans[0]
+        fast_n = [t.clone() for t in (b.nx, b.ny, b.nz, b.curv)]
+        fast_d = b.desc[:state["rows"]].clone()
+        run_fpfh.fast_normals = False
+        kp_exact, k_exact = run_fpfh(b)
+        torch.cuda.synchronize(dev)
+        deviation = fast_deviation(torch, fast_n, fast_d, b, k_exact, np.array_equal(np.asarray(kp_exact),
+                                                                                     np.asarray(state["kp"])))
+        run_fpfh.fast_normals = True
     if rank == 0 and not shot:
         b = scans[0]
         ctx_n.set_timing(True)
         ctx_n.reset_timing()
         for _ in range(3):
-            ctx_n.normals_dev(b.x, b.y, b.z, 0.05, b.nx, b.ny, b.nz, b.curv)
+            (ctx_n.normals_fast_dev if fast else ctx_n.normals_dev)(b.x, b.y, b.z, 0.05, b.nx, b.ny, b.nz, b.curv)
         torch.cuda.synchronize(dev)
         iso = {nm: ctx_n.kernel_time(nm)[0] / 3 for nm in VERBOSE_TIMERS}
         ctx_n.set_timing(False)
 
     if rank == 0:
-        line = scans_line(args, world, n_scans, mine, shot, elapsed, timers, iso, nb_scan, long_scan, stat, npts)
+        line = scans_line(args, world, n_scans, mine, shot, elapsed, timers, iso, nb_scan, long_scan, stat, npts,
+                          fast=fast)
+        if deviation is not None:
+            line["deviation_from_parity_path"] = deviation
         line["config"]["descriptor_rows"] = state["rows"]
         if seq_ms is not None:
             line["batch_pipeline"] = {
@@ -413,7 +434,10 @@ def bench_scans(args, torch, dist, dev, world, rank, local):
             line["config"]["backend"] = dist.get_backend()
         line["end_to_end_h2d_d2h"] = e2e
         cpu = None
-        if world == 1 and not args.no_cpu_baseline and not dense:
+        if fast:
+            cpu = {"value": None, "note": "see the configs[2] line: the CPU restatement is PCL's path, which this "
+                                          "opt-in mode departs from by design"}
+        elif world == 1 and not args.no_cpu_baseline and not dense:
             x, y, z = host[0]
             cb = cpu_baseline(x, y, z, args.workload, sample_np)
             cpu = {"value": round(npts / cb["seconds"] / 1e6, 6), "unit": "Mpoints/s",
@@ -433,7 +457,33 @@ def bench_scans(args, torch, dist, dev, world, rank, local):
     ctx_n.close()
 
 
-def scans_line(args, world, n_scans, mine, shot, elapsed, timers, iso, nb_scan, long_scan, stat, npts=N_POINTS):
+def fast_deviation(torch, fast_n, fast_d, b, k, same_kp):
+    """Opt-in MFMA normals vs the parity-exact path on one scan: normal angles (deg), curvature,
+    and the FPFH rows at the same keypoints (absolute L2 and L2 relative to the row norm)."""
+    import numpy as np
+    F = torch.stack(fast_n[:3], 1).double().cpu().numpy()
+    P = torch.stack((b.nx, b.ny, b.nz), 1).double().cpu().numpy()
+    ok = np.isfinite(P[:, 0]) & np.isfinite(F[:, 0])
+    ang = np.degrees(np.arccos(np.clip(np.abs(np.sum(F[ok] * P[ok], 1)), 0.0, 1.0)))
+    out = {"normals_compared": int(ok.sum()),
+           "nan_pattern_equal": bool(np.array_equal(np.isnan(F[:, 0]), np.isnan(P[:, 0]))),
+           "angle_deg": {"p50": round(float(np.median(ang)), 5), "p99": round(float(np.percentile(ang, 99)), 4),
+                         "max": round(float(ang.max()), 3)},
+           "same_keypoints": bool(same_kp)}
+    if same_kp and k == fast_d.shape[0] and k > 0:
+        D = fast_d.double().cpu().numpy()
+        E = b.desc[:k].double().cpu().numpy()
+        fin = np.isfinite(D).all(1) & np.isfinite(E).all(1)
+        l2 = np.linalg.norm(D[fin] - E[fin], axis=1)
+        rel = l2 / np.maximum(np.linalg.norm(E[fin], axis=1), 1e-30)
+        out["fpfh_rows"] = int(fin.sum())
+        out["fpfh_l2"] = {"p50": round(float(np.median(l2)), 4), "max": round(float(l2.max()), 4)}
+        out["fpfh_l2_rel"] = {"p50": round(float(np.median(rel)), 5), "max": round(float(rel.max()), 5)}
+    return out
+
+
+def scans_line(args, world, n_scans, mine, shot, elapsed, timers, iso, nb_scan, long_scan, stat, npts=N_POINTS,
+               fast=False):
     """The contract line of bench_scans (rank 0), roofline over the neighbour-gather stage."""
     per_scan_calls = args.steps * len(mine)
     ms_per_step = elapsed / args.steps * 1e3
@@ -446,7 +496,7 @@ def scans_line(args, world, n_scans, mine, shot, elapsed, timers, iso, nb_scan, 
     # covariance chains + long lists (timer "normals": HIP events around pfx_normals_dev on its
     # stream, inside the timed step, averaged per scan)
     algo = nb * 12 + npts * 16
-    stage_ms = timers["normals"][0] / max(per_scan_calls, 1)
+    stage_ms = timers["normals_fast" if fast else "normals"][0] / max(per_scan_calls, 1)
     stage_gbs = algo / (stage_ms / 1e3) / 1e9 if stage_ms > 0 else 0.0
     parts = ("grid_bbox", "grid_build", "normals_lists_small", "normals_lists_sparse", "normals_lists_dense",
              "normals_lists_query", "normals_chain", "normals_chain_big", "normals_long")
@@ -458,7 +508,7 @@ def scans_line(args, world, n_scans, mine, shot, elapsed, timers, iso, nb_scan, 
              "achieved": round(chain_algo / (chain_ms / 1e3) / 1e9, 2) if chain_ms > 0 else None}
     chain["frac"] = round(chain["achieved"] / HBM_PEAK_GBS, 5) if chain["achieved"] else None
     # the committed PMC summary was collected on configs[2]'s scan: only that line may cite it
-    pmc = (load_pmc("pmc_normals_stage.json") or {}) if npts == N_POINTS else {}
+    pmc = (load_pmc("pmc_normals_stage.json") or {}) if (npts == N_POINTS and not fast) else {}
     roofline = {"bound": "hbm", "kernel": "normals stage: grid + k_nb_tile/k_nb_query list builders + "
                                           "k_normals_chain(_big) + k_normals_long",
                 "achieved": round(stage_gbs, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -469,12 +519,23 @@ def scans_line(args, world, n_scans, mine, shot, elapsed, timers, iso, nb_scan, 
                          "with NARF on the other stream)",
                 "kernels_ms_per_scan": kernels, "chain": chain,
                 "pmc": pmc.get("kernels")}
+    if fast:  # the opt-in MFMA-covariance stage: grid build + k_normals_mfma (no lists)
+        mf = timers["normals_mfma"][0] / max(per_scan_calls, 1)
+        roofline.update({"kernel": "normals_fast stage: grid + k_normals_mfma (16x16x4 f32 MFMA: hit mask x "
+                                   "centred candidate features; no neighbour list, not parity-exact)",
+                         "kernels_ms_per_scan": {"grid_bbox": kernels["grid_bbox"], "grid_build": kernels["grid_build"],
+                                                 "normals_mfma": round(mf, 4)},
+                         "chain": None, "pmc": None, "traffic": None})
+        roofline["mfma_kernel"] = {"kernel": "k_normals_mfma", "ms": round(mf, 4),
+                                   "achieved": round(algo / (mf / 1e3) / 1e9, 2) if mf > 0 else None,
+                                   "frac": round(algo / (mf / 1e3) / 1e9 / HBM_PEAK_GBS, 5) if mf > 0 else None}
     if iso is not None:
-        iso_stage = iso["normals"]
+        iso_stage = iso["normals_fast" if fast else "normals"]
         roofline["isolated"] = {"avg_ms": round(iso_stage, 4),
                                 "achieved": round(algo / (iso_stage / 1e3) / 1e9, 2) if iso_stage > 0 else None,
                                 "frac": round(algo / (iso_stage / 1e3) / 1e9 / HBM_PEAK_GBS, 5) if iso_stage > 0 else None,
-                                "kernels_ms": {nm: round(iso[nm], 4) for nm in parts},
+                                "kernels_ms": {nm: round(iso[nm], 4) for nm in (("grid_bbox", "grid_build",
+                                                                                 "normals_mfma") if fast else parts)},
                                 "note": "pfx_normals_dev alone on the device after the timed region (not `value`)"}
     if shot:  # configs[3]: k_shot heads the line (the dominant kernel of that step)
         shot_ms, shot_n = timers["shot"]
@@ -504,6 +565,11 @@ def scans_line(args, world, n_scans, mine, shot, elapsed, timers, iso, nb_scan, 
                         f"(RCCL grouped send/recv)")
         data = "synthetic (synth_room: seeded pinhole room scan, k(0.05)~230; see synth.py)"
         scaling = "strong" if n_scans > 1 else "weak"
+        if fast:
+            metric = ("Mpoints/s through NARF keypoint + FPFH descriptor on 1M-pt cloud, opt-in MFMA-covariance "
+                      "normals (not parity-exact)")
+            workload = ("configs[2] scan with pfx_normals_fast_dev in place of the parity-exact normal estimation "
+                        "(deviation from the parity path in `deviation_from_parity_path`)")
         if npts != N_POINTS:
             metric = "Mpoints/s through NARF keypoint + FPFH descriptor, configs[2] scene at 10x density"
             workload = (f"SURVEY 8(d) dense variant: configs[2]'s room scene (same scale) at {npts // 1_000_000}M "

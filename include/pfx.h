@@ -158,6 +158,20 @@ pfx_status pfx_normals_chains_dev(pfx_ctx* ctx, pfx_ctx* lists_ctx, const uint8_
                                   const float viewpoint[3], float* d_nx, float* d_ny, float* d_nz,
                                   float* d_curvature);
 
+/* Opt-in fast mode, NOT parity-exact (BASELINE north_star "MFMA for the 3x3
+ * covariance accumulation"): the same neighbour set (FLANN's d2 < (float)(r*r)), but the
+ * covariance sums are one MFMA contraction per 16 points -- hit mask x candidate features,
+ * centred on the group's first point -- instead of PCL's sequential float chains in FLANN order,
+ * so no neighbour list is sorted or stored.  Results differ from pfx_normals by rounding (the
+ * sums carry less rounding than PCL's raw-coordinate ones); bench.py --workload fastnormals
+ * reports the deviation.  Same NaN rules (< 3 neighbours, non-finite points). */
+pfx_status pfx_normals_fast(pfx_ctx* ctx, const float* x, const float* y, const float* z, int64_t n,
+                            double radius, const float viewpoint[3], float* nx, float* ny, float* nz,
+                            float* curvature);
+pfx_status pfx_normals_fast_dev(pfx_ctx* ctx, const float* d_x, const float* d_y, const float* d_z,
+                                int64_t n, double radius, const float viewpoint[3], float* d_nx,
+                                float* d_ny, float* d_nz, float* d_curvature);
+
 /* ---- FPFH-33: FPFHEstimation (surface + normals, queries = input cloud) ------------- */
 /* same_as_surface != 0 selects PCL's "input_ == surface_ && indices == all" branch (queries
  * must then be the surface itself).  out: nq x 33 row-major (FPFHSignature33::histogram). */

@@ -87,6 +87,8 @@ _SIGS = {
                                   c_vp, c_vp, c_vp, c_i64]),
     "pfx_normals": (c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_dbl, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "pfx_normals_dev": (c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_dbl, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "pfx_normals_fast": (c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_dbl, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "pfx_normals_fast_dev": (c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_dbl, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "pfx_fpfh": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_i64,
                          c_int, c_dbl, c_vp]),
     "pfx_fpfh_dev": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp,

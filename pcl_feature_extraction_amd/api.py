@@ -147,6 +147,16 @@ class Context:
                                           _ptr(out[1]), _ptr(out[2]), _ptr(out[3])))
         return out[0], out[1], out[2], out[3]
 
+    def normals_fast(self, x, y, z, r, viewpoint=(0.0, 0.0, 0.0)):
+        """Opt-in MFMA-covariance normals (pfx_normals_fast): not parity-exact, see include/pfx.h."""
+        x, y, z = map(_f32, (x, y, z))
+        n = len(x)
+        out = np.empty((4, n), dtype=np.float32)
+        vp = _f32(viewpoint)
+        self._check(self._lib.pfx_normals_fast(self.h, _ptr(x), _ptr(y), _ptr(z), n, float(r), _ptr(vp),
+                                               _ptr(out[0]), _ptr(out[1]), _ptr(out[2]), _ptr(out[3])))
+        return out[0], out[1], out[2], out[3]
+
     def fpfh(self, sx, sy, sz, nx, ny, nz, qx, qy, qz, r, same_as_surface=False):
         sx, sy, sz, nx, ny, nz = map(_f32, (sx, sy, sz, nx, ny, nz))
         if same_as_surface:
@@ -197,6 +207,11 @@ class Context:
         vp = _f32(viewpoint)
         self._check(self._lib.pfx_normals_dev(self.h, _ptr(x), _ptr(y), _ptr(z), x.numel(), float(r), _ptr(vp),
                                               _ptr(nx), _ptr(ny), _ptr(nz), _ptr(curv)))
+
+    def normals_fast_dev(self, x, y, z, r, nx, ny, nz, curv, viewpoint=(0.0, 0.0, 0.0)):
+        vp = _f32(viewpoint)
+        self._check(self._lib.pfx_normals_fast_dev(self.h, _ptr(x), _ptr(y), _ptr(z), x.numel(), float(r), _ptr(vp),
+                                                   _ptr(nx), _ptr(ny), _ptr(nz), _ptr(curv)))
 
     def fpfh_dev(self, sx, sy, sz, nx, ny, nz, qx, qy, qz, r, out, same_as_surface=False, after_normals=False):
         """after_normals: the caller vouches that (sx, sy, sz) still hold the cloud of this context's

@@ -280,6 +280,40 @@ pfx_status pfx_normals_dev(pfx_ctx* ctx, const float* d_x, const float* d_y, con
   PFX_API_END(ctx)
 }
 
+pfx_status pfx_normals_fast_dev(pfx_ctx* ctx, const float* d_x, const float* d_y, const float* d_z, int64_t n,
+                                double radius, const float viewpoint[3], float* d_nx, float* d_ny, float* d_nz,
+                                float* d_curvature) {
+  PFX_API_BEGIN
+  check_ctx(ctx);
+  if (n < 0 || (n && (!d_x || !d_y || !d_z || !d_nx || !d_ny || !d_nz || !d_curvature)))
+    throw Error(PFX_ERR_INVALID, "normals_fast: invalid arguments");
+  const float vp0[3] = {0.f, 0.f, 0.f};
+  pfx::normals_fast_dev(ctx, d_x, d_y, d_z, n, radius, viewpoint ? viewpoint : vp0, d_nx, d_ny, d_nz, d_curvature);
+  PFX_API_END(ctx)
+}
+
+pfx_status pfx_normals_fast(pfx_ctx* ctx, const float* x, const float* y, const float* z, int64_t n, double radius,
+                            const float viewpoint[3], float* nx, float* ny, float* nz, float* curvature) {
+  PFX_API_BEGIN
+  check_ctx(ctx);
+  if (n < 0 || (n && (!x || !y || !z || !nx || !ny || !nz || !curvature)))
+    throw Error(PFX_ERR_INVALID, "normals_fast: invalid arguments");
+  float* dx = stage_in(ctx, "in_x", x, n);
+  float* dy = stage_in(ctx, "in_y", y, n);
+  float* dz = stage_in(ctx, "in_z", z, n);
+  float* o = ctx->buf("out_normals").as<float>(4 * n + 4);
+  const float vp0[3] = {0.f, 0.f, 0.f};
+  pfx::normals_fast_dev(ctx, dx, dy, dz, n, radius, viewpoint ? viewpoint : vp0, o, o + n, o + 2 * n, o + 3 * n);
+  if (n) {
+    PFX_HIP(hipMemcpyAsync(nx, o, sizeof(float) * n, hipMemcpyDeviceToHost, ctx->stream));
+    PFX_HIP(hipMemcpyAsync(ny, o + n, sizeof(float) * n, hipMemcpyDeviceToHost, ctx->stream));
+    PFX_HIP(hipMemcpyAsync(nz, o + 2 * n, sizeof(float) * n, hipMemcpyDeviceToHost, ctx->stream));
+    PFX_HIP(hipMemcpyAsync(curvature, o + 3 * n, sizeof(float) * n, hipMemcpyDeviceToHost, ctx->stream));
+  }
+  PFX_HIP(hipStreamSynchronize(ctx->stream));
+  PFX_API_END(ctx)
+}
+
 pfx_status pfx_normals_lists_dev(pfx_ctx* ctx, const float* d_x, const float* d_y, const float* d_z, int64_t n,
                                  double radius, float* d_nx, float* d_ny, float* d_nz, float* d_curvature) {
   PFX_API_BEGIN

@@ -230,6 +230,9 @@ void normals_lists_dev(pfx_ctx* ctx, const float* x, const float* y, const float
 void normals_chains_dev(pfx_ctx* ctx, pfx_ctx* owner, const uint8_t* mask, int want, const float vp[3], float* nx,
                         float* ny, float* nz, float* curv);
 void normals_release(pfx_ctx* ctx);
+// opt-in MFMA covariance (pfx_normals_fast.hip): not parity-exact
+void normals_fast_dev(pfx_ctx* ctx, const float* x, const float* y, const float* z, int64_t n, double r,
+                      const float vp[3], float* nx, float* ny, float* nz, float* curv);
 double cloud_resolution_dev(pfx_ctx* ctx, const float* x, const float* y, const float* z, int64_t n);
 int64_t iss_keypoints_dev(pfx_ctx* ctx, const float* x, const float* y, const float* z, int64_t n, double salient,
                           double non_max, int min_nb, double g21, double g32, int32_t* out, int64_t cap,

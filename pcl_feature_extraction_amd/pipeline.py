@@ -78,11 +78,14 @@ class OverlappedNarfFpfh:
         ctx_side.set_stream(self.s_side.cuda_stream)
         ctx_main.set_shared(True)  # NARF shares the device with the critical normal estimation
         self.pool = ThreadPoolExecutor(max_workers=1)
+        # opt-in: the MFMA-covariance normals (pfx_normals_fast_dev), not parity-exact
+        self.fast_normals = False
 
     def __call__(self, b: ScanBuffers, normal_radius: float = 0.05, feat_radius: float = 0.08, params=None,
                  cam=None):
         self.s_side.wait_stream(self.s_main)  # the scan was written on the main stream
-        fut = self.pool.submit(self.ctx_side.normals_dev, b.x, b.y, b.z, normal_radius, b.nx, b.ny, b.nz, b.curv)
+        est = self.ctx_side.normals_fast_dev if self.fast_normals else self.ctx_side.normals_dev
+        fut = self.pool.submit(est, b.x, b.y, b.z, normal_radius, b.nx, b.ny, b.nz, b.curv)
         try:
             kp = self.ctx.narf_keypoints_dev(b.x, b.y, b.z, params or narf_params(support_size=0.2),
                                              cam or camera())
