@@ -119,7 +119,9 @@ pfx_status pfx_ctx_synchronize(pfx_ctx* ctx);
  * and list set-up find free wave slots (1M-pt room: 161.4 -> 162.6 Mpoints/s; alone the
  * interest stage takes 0.63 instead of 0.47 ms, hence off by default). */
 pfx_status pfx_ctx_set_shared(pfx_ctx* ctx, int shared);
-/* Per-kernel HIP-event timing on the ctx stream (for bench.py's live roofline). */
+/* HIP-event timing on the ctx stream (for bench.py's live roofline): enable = 1 times every kernel
+ * group, 2 only the stage scopes (one event pair per stage call: "normals", "normals_fast", "iss",
+ * "harris3d", ...; the per-kernel pairs cost ~2 % of the headline step in host launch time), 0 off. */
 pfx_status pfx_ctx_set_timing(pfx_ctx* ctx, int enable);
 pfx_status pfx_ctx_reset_timing(pfx_ctx* ctx);
 /* Accumulated device time and launch count of the kernel `name`; syncs the stream. */

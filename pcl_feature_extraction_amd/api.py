@@ -107,8 +107,10 @@ class Context:
         concurrently (pfx_ctx_set_shared); results are unchanged."""
         self._check(self._lib.pfx_ctx_set_shared(self.h, 1 if shared else 0))
 
-    def set_timing(self, enable=True):
-        self._check(self._lib.pfx_ctx_set_timing(self.h, 1 if enable else 0))
+    def set_timing(self, enable=True, stages_only=False):
+        """HIP-event timers on this context's stream: every kernel group, or (stages_only) one event
+        pair per stage call (normals, normals_fast, shot, iss, ...: the live roofline's timer)."""
+        self._check(self._lib.pfx_ctx_set_timing(self.h, (2 if stages_only else 1) if enable else 0))
 
     def reset_timing(self):
         self._check(self._lib.pfx_ctx_reset_timing(self.h))

@@ -199,6 +199,7 @@ pfx_status pfx_ctx_set_timing(pfx_ctx* ctx, int enable) {
   check_ctx(ctx);
   harvest_timing(ctx);
   ctx->timer.enabled = enable != 0;
+  ctx->timer.stages_only = enable == 2;
   PFX_API_END(ctx)
 }
 

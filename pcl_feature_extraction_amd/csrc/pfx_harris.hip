@@ -529,7 +529,7 @@ int64_t harris3d_dev(pfx_ctx* ctx, const float* x, const float* y, const float* 
   if (n_corners) *n_corners = 0;
   if (n == 0) return 0;
   hipStream_t st = ctx->stream;
-  TimeScope total(ctx, "harris3d");
+  TimeScope total(ctx, "harris3d", true);
   // HarrisKeypoint3D::initCompute: NormalEstimation at the keypoint radius, viewpoint 0
   float* nx = ctx->buf("h3_nx").as<float>(n);
   float* ny = ctx->buf("h3_ny").as<float>(n);
@@ -560,7 +560,7 @@ int64_t harris6d_dev(pfx_ctx* ctx, const float* x, const float* y, const float* 
   if (n_corners) *n_corners = 0;
   if (n == 0) return 0;
   hipStream_t st = ctx->stream;
-  TimeScope total(ctx, "harris6d");
+  TimeScope total(ctx, "harris6d", true);
   // HarrisKeypoint6D::detectKeypoints: NormalEstimation at the keypoint radius, viewpoint 0
   float* nx = ctx->buf("h3_nx").as<float>(n);
   float* ny = ctx->buf("h3_ny").as<float>(n);

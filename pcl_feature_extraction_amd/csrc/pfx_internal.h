@@ -51,6 +51,7 @@ struct DevBuf {
 struct KernelTimer {
   struct Pending { hipEvent_t a, b; std::string name; };
   bool enabled = false;
+  bool stages_only = false;  // pfx_ctx_set_timing(ctx, 2): only the stage scopes (2 events per stage)
   std::vector<Pending> pending;
   std::vector<hipEvent_t> pool;
   std::map<std::string, std::pair<double, int64_t> > acc;
@@ -185,8 +186,8 @@ struct TimeScope {
   pfx_ctx* ctx;
   hipEvent_t a = nullptr, b = nullptr;
   std::string name;
-  TimeScope(pfx_ctx* c, std::string n) : ctx(c), name(std::move(n)) {
-    if (ctx->timer.enabled) {
+  TimeScope(pfx_ctx* c, std::string n, bool stage = false) : ctx(c), name(std::move(n)) {
+    if (ctx->timer.enabled && (stage || !ctx->timer.stages_only)) {
       a = ctx->timer.take();
       b = ctx->timer.take();
       PFX_HIP(hipEventRecord(a, ctx->stream));

@@ -555,7 +555,7 @@ double cloud_resolution_dev(pfx_ctx* ctx, const float* x, const float* y, const 
   if (!ctx->kp) ctx->kp = new KeypointState();
   Grid& G = ctx->kp->res;
   hipStream_t st = ctx->stream;
-  TimeScope total(ctx, "resolution");
+  TimeScope total(ctx, "resolution", true);
   float* term = ctx->buf("res_term").as<float>(n);
   int32_t* qa = ctx->buf("res_qa").as<int32_t>(n);
   int32_t* qb = ctx->buf("res_qb").as<int32_t>(n);
@@ -644,7 +644,7 @@ int64_t iss_keypoints_dev(pfx_ctx* ctx, const float* x, const float* y, const fl
   KeypointState& K = *ctx->kp;
   hipStream_t st = ctx->stream;
   if (n == 0) return 0;
-  TimeScope total(ctx, "iss");
+  TimeScope total(ctx, "iss", true);
   double* third = third_out ? third_out : ctx->buf("iss_third").as<double>(n);
   PFX_HIP(hipMemsetAsync(third, 0, sizeof(double) * n, st));
   build_grid(ctx, K.sal, x, y, z, n, salient);

@@ -312,7 +312,7 @@ void match_nearest_dev(pfx_ctx* ctx, const float* src, int64_t ns, int64_t ss, c
     if (nt && dt2s) PFX_HIP(hipMemsetAsync(dt2s, 0xff, sizeof(float) * nt, st));
     return;
   }
-  TimeScope total(ctx, "match");
+  TimeScope total(ctx, "match", true);
   const int Dp = (D + 31) / 32 * 32;  // K = 3 Dp: whole 32-deep LDS chunks
   const Prepared a = prep(ctx, "match_a", src, ns, ss, D, Dp, false);
   const Prepared b = prep(ctx, "match_b", tgt, nt, ts, D, Dp, true);

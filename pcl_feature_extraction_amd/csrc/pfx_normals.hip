@@ -600,7 +600,7 @@ void normals_lists_dev(pfx_ctx* ctx, const float* x, const float* y, const float
     return;
   }
   hipStream_t st = ctx->stream;
-  TimeScope total(ctx, "normals_lists_phase");
+  TimeScope total(ctx, "normals_lists_phase", true);
   build_grid(ctx, ctx->grid_a, x, y, z, n, r);
   k_nan_fill4<<<(unsigned)std::min<int64_t>(ceil_div(n, 256), 4096), 256, 0, st>>>(nx, ny, nz, curv, n);
   check_launch("k_nan_fill4");
@@ -708,7 +708,7 @@ void normals_chains_dev(pfx_ctx* ctx, pfx_ctx* owner, const uint8_t* mask, int w
 
 void normals_dev(pfx_ctx* ctx, const float* x, const float* y, const float* z, int64_t n, double r,
                  const float vp[3], float* nx, float* ny, float* nz, float* curv) {
-  TimeScope total(ctx, "normals");
+  TimeScope total(ctx, "normals", true);
   normals_lists_dev(ctx, x, y, z, n, r, nx, ny, nz, curv);
   if (n > 0) normals_chains_dev(ctx, ctx, nullptr, 0, vp, nx, ny, nz, curv);
 }

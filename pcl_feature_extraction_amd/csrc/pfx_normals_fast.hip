@@ -183,14 +183,14 @@ void normals_fast_dev(pfx_ctx* ctx, const float* x, const float* y, const float*
                       const float vp[3], float* nx, float* ny, float* nz, float* curv) {
   PFX_CHECK(r > 0.0, "normals_fast: radius must be > 0");
   if (n == 0) return;
-  TimeScope total(ctx, "normals_fast");
+  TimeScope total(ctx, "normals_fast", true);
   hipStream_t st = ctx->stream;
   build_grid(ctx, ctx->grid_a, x, y, z, n, r);
   if (ctx->normals) ctx->normals->ready = false;  // grid_a no longer matches held lists
   const Grid& G = ctx->grid_a;
   k_nan_fill4_fast<<<(unsigned)std::min<int64_t>(ceil_div(n, 256), 4096), 256, 0, st>>>(nx, ny, nz, curv, n);
   {
-    TimeScope ts(ctx, "normals_mfma");
+    TimeScope ts(ctx, "normals_mfma", true);
     // one wave per 16 grid points (all n: waves past the finite count return at once)
     k_normals_mfma<<<(unsigned)ceil_div(ceil_div(n, 16), 4), 256, 0, st>>>(view(G), (float)(r * r), vp[0], vp[1],
                                                                           vp[2], nx, ny, nz, curv);

@@ -270,7 +270,7 @@ int64_t ransac_rejector(pfx_ctx* ctx, const float* sx, const float* sy, const fl
     if (query[i] < 0 || query[i] >= ns || match[i] < 0 || match[i] >= nt)
       throw Error(PFX_ERR_INVALID, "ransac: correspondence index out of range");
   hipStream_t st = ctx->stream;
-  TimeScope total(ctx, "ransac");
+  TimeScope total(ctx, "ransac", true);
   auto up = [&](const char* name, const void* h, size_t bytes) {
     void* d = ctx->buf(name).get(bytes + 16);
     PFX_HIP(hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, st));

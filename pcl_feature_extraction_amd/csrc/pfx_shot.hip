@@ -471,7 +471,7 @@ void shot_dev(pfx_ctx* ctx, const float* sx, const float* sy, const float* sz, c
   unsigned long long* nbr = reinterpret_cast<unsigned long long*>(err + 2);
   PFX_HIP(hipMemsetAsync(err, 0, 4 * sizeof(int), st));
   {
-    TimeScope ts(ctx, "shot");
+    TimeScope ts(ctx, "shot", true);
     int32_t* over = ctx->buf("shot_over").as<int32_t>(nq);
     int* n_over = err + 1;
     const size_t lds_s = 2 * sizeof(uint64_t) * kCapSmall, lds = sizeof(uint64_t) * kCap;
