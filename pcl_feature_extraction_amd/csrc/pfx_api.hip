@@ -131,6 +131,7 @@ void pfx_ctx_destroy(pfx_ctx* ctx) {
     if (e) (void)hipEventDestroy(e);
   if (ctx->spin_ev) (void)hipEventDestroy(ctx->spin_ev);
   if (ctx->host_rb) (void)hipHostFree(ctx->host_rb);
+  if (ctx->host_scratch) (void)hipHostFree(ctx->host_scratch);
   if (ctx->fpfh_rb_mem) (void)hipHostFree(ctx->fpfh_rb_mem);
   delete ctx;
 }
@@ -595,11 +596,15 @@ extern "C" pfx_status pfx_gather_points_dev(pfx_ctx* ctx, const float* d_x, cons
   *n_out = (int64_t)keep.size();
   if (keep.empty()) return PFX_OK;
   int32_t* d_idx = ctx->buf("gather_idx").as<int32_t>(keep.size());
-  PFX_HIP(hipMemcpyAsync(d_idx, keep.data(), sizeof(int32_t) * keep.size(), hipMemcpyHostToDevice, ctx->stream));
+  // through the context's pinned block (an async DMA copy; the stream is synchronised first, so
+  // a previous call's copy out of that block has completed)
+  PFX_HIP(hipStreamSynchronize(ctx->stream));
+  int32_t* h_idx = static_cast<int32_t*>(ctx->pinned(sizeof(int32_t) * keep.size()));
+  std::memcpy(h_idx, keep.data(), sizeof(int32_t) * keep.size());
+  PFX_HIP(hipMemcpyAsync(d_idx, h_idx, sizeof(int32_t) * keep.size(), hipMemcpyHostToDevice, ctx->stream));
   k_gather_points<<<(unsigned)pfx::ceil_div((int64_t)keep.size(), 256), 256, 0, ctx->stream>>>(
       d_x, d_y, d_z, n, d_idx, (int64_t)keep.size(), d_kx, d_ky, d_kz);
   pfx::check_launch("k_gather_points");
-  PFX_HIP(hipStreamSynchronize(ctx->stream));  // `keep` is pageable host memory
   PFX_API_END(ctx)
 }
 

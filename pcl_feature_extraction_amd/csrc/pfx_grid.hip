@@ -96,16 +96,23 @@ __global__ void __launch_bounds__(256) k_bbox_reduce(uint32_t* __restrict__ mm, 
   if (t < 6) mm[nblocks * 6 + t] = s[t][0];
 }
 
+// oob (nullable, speculative bounds): counts the finite points outside [lo, hi] (clamped keys
+// are then not a valid grid; the caller rebuilds on exact bounds)
 __global__ void __launch_bounds__(256) k_cell_keys(const float* __restrict__ x, const float* __restrict__ y,
                                                    const float* __restrict__ z, int64_t n, double inv,
                                                    double ox, double oy, double oz, int32_t nx, int32_t ny,
                                                    int32_t nz, uint32_t* __restrict__ keys,
-                                                   uint32_t* __restrict__ vals) {
+                                                   uint32_t* __restrict__ vals, int* __restrict__ oob,
+                                                   double hx, double hy, double hz) {
   int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   if (i >= n) return;
   float px = x[i], py = y[i], pz = z[i];
   uint32_t key = (uint32_t)((int64_t)nx * ny * nz);
   if (isfinite(px) && isfinite(py) && isfinite(pz)) {
+    // (exactly the points the clamp below would move: cell index outside [0, dims))
+    if (oob && ((double)px < ox || (double)py < oy || (double)pz < oz || (double)px > hx || (double)py > hy ||
+                (double)pz > hz))
+      atomicAdd(oob, 1);
     int64_t ix = (int64_t)floor(((double)px - ox) * inv);
     int64_t iy = (int64_t)floor(((double)py - oy) * inv);
     int64_t iz = (int64_t)floor(((double)pz - oz) * inv);
@@ -185,7 +192,7 @@ void points_bbox(pfx_ctx* ctx, Grid& g, const float* d_x, const float* d_y, cons
 }
 
 void build_grid(pfx_ctx* ctx, Grid& g, const float* d_x, const float* d_y, const float* d_z,
-                int64_t n, double radius) {
+                int64_t n, double radius, bool use_hint) {
   PFX_CHECK(n >= 0 && n < (int64_t(1) << 31), "point count must be in [0, 2^31)");
   PFX_CHECK(radius > 0.0, "radius must be > 0");
   if (&g == &ctx->grid_b) {  // a grid prepared ahead for the next fpfh_dev no longer holds
@@ -198,7 +205,26 @@ void build_grid(pfx_ctx* ctx, Grid& g, const float* d_x, const float* d_y, const
   g.n = n;
   g.ux = d_x; g.uy = d_y; g.uz = d_z;
   double lo[3] = {0, 0, 0}, hi[3] = {0, 0, 0};
-  if (n > 0) bbox_dev(ctx, g, d_x, d_y, d_z, n, lo, hi);
+  g.oob = nullptr;
+  static const bool no_hint = getenv("PFX_GRID_NOHINT") != nullptr;  // A/B switch
+  if (use_hint && !no_hint && g.have_hint && n > 0) {
+    // speculative: the previous exact bounds, widened (no bounds pass, no host round trip)
+    for (int d = 0; d < 3; ++d) {
+      lo[d] = g.hint_lo[d];
+      hi[d] = g.hint_hi[d];
+    }
+    g.oob = g.b_oob.as<int>(1);
+  } else if (n > 0) {
+    bbox_dev(ctx, g, d_x, d_y, d_z, n, lo, hi);
+    // the hint for the next speculative build: 10 % wider on every side, plus two cells (scans of
+    // one sensor keep their extent)
+    for (int d = 0; d < 3; ++d) {
+      const double m = 0.1 * (hi[d] - lo[d]) + 2.0 * radius;
+      g.hint_lo[d] = lo[d] - m;
+      g.hint_hi[d] = hi[d] + m;
+    }
+    g.have_hint = true;
+  }
   double cell = radius * (1.0 + 1e-6);
   const double max_cells = double(1 << 26);
   int64_t dims[3];
@@ -250,9 +276,11 @@ void build_grid(pfx_ctx* ctx, Grid& g, const float* d_x, const float* d_y, const
     // occupied cell, then a suffix minimum fills the empty cells (no per-point atomics)
     k_fill_i32<<<(unsigned)std::min<int64_t>(ceil_div(C + 2, 256), 2048), 256, 0, st>>>(g.cell_start, C + 2,
                                                                                        (int32_t)n);
+    if (g.oob) k_fill_i32<<<1, 64, 0, st>>>(g.oob, 1, 0);
     if (n > 0) {
       k_cell_keys<<<(unsigned)ceil_div(n, 256), 256, 0, st>>>(d_x, d_y, d_z, n, inv, lo[0], lo[1], lo[2],
-                                                              g.nx, g.ny, g.nz, keys, vals);
+                                                              g.nx, g.ny, g.nz, keys, vals, g.oob, hi[0], hi[1],
+                                                              hi[2]);
       check_launch("k_cell_keys");
       PFX_HIP(rocprim::radix_sort_pairs<SortCfg>(tmp, sort_bytes, keys, keys2, vals,
                                         reinterpret_cast<uint32_t*>(g.perm), (size_t)n, 0, bits, st));

@@ -77,10 +77,18 @@ struct Grid {
   int32_t* perm = nullptr;                            // sorted position -> caller index
   int32_t* cell_start = nullptr;                      // ncells + 1 prefix (by linear cell key)
   const uint32_t* skeys = nullptr;                    // cell key of each sorted position
-  DevBuf b_sx, b_sy, b_sz, b_sp, b_perm, b_start, b_keys, b_keys2, b_vals, b_tmp, b_minmax;
+  DevBuf b_sx, b_sy, b_sz, b_sp, b_perm, b_start, b_keys, b_keys2, b_vals, b_tmp, b_minmax, b_oob;
+  // Speculative bounds (build_grid with use_hint): the last exact bounds of this grid, widened;
+  // when a build uses them, `oob` (device int) counts the finite points outside, and the grid is
+  // valid only if it stays 0 -- the caller checks it at its next readback and rebuilds exactly
+  bool have_hint = false;
+  double hint_lo[3] = {0, 0, 0}, hint_hi[3] = {0, 0, 0};
+  int* oob = nullptr;  // non-null iff the current build is speculative
   void release() {
     b_sx.release(); b_sy.release(); b_sz.release(); b_sp.release(); b_perm.release(); b_start.release();
-    b_keys.release(); b_keys2.release(); b_vals.release(); b_tmp.release(); b_minmax.release();
+    b_keys.release(); b_keys2.release(); b_vals.release(); b_tmp.release(); b_minmax.release(); b_oob.release();
+    have_hint = false;
+    oob = nullptr;
   }
 };
 
@@ -130,6 +138,7 @@ struct pfx_ctx {
   std::map<std::string, pfx::DevBuf> bufs;  // named scratch
   pfx::NarfState* narf = nullptr;
   pfx::NormalsState* normals = nullptr;  // neighbour lists between the two normal phases
+  bool normals_fork_hint = true;         // long-list chains on the side stream (last decision)
   pfx::KeypointState* kp = nullptr;      // grids + lists of the keypoint detectors
   pfx::DevBuf& buf(const char* name) { return bufs[name]; }
   // fpfh_dev's statistics / sticky error word, copied to pinned memory in stream order and read
@@ -177,6 +186,21 @@ struct pfx_ctx {
     if (!host_rb) PFX_HIP(hipHostMalloc(&host_rb, 4096, hipHostMallocDefault));
     return static_cast<T*>(host_rb);
   }
+  // grow-only pinned host block for larger per-call transfers (H2D of host-built index lists):
+  // pageable copies are staged through blit kernels that wait for CU slots on a busy device
+  void* host_scratch = nullptr;
+  size_t host_scratch_bytes = 0;
+  void* pinned(size_t need) {
+    if (need > host_scratch_bytes) {
+      if (host_scratch) {
+        PFX_HIP(hipStreamSynchronize(stream));  // a pending copy may still read the old block
+        PFX_HIP(hipHostFree(host_scratch));
+      }
+      host_scratch_bytes = need + need / 2 + 4096;
+      PFX_HIP(hipHostMalloc(&host_scratch, host_scratch_bytes, hipHostMallocDefault));
+    }
+    return host_scratch;
+  }
 };
 
 namespace pfx {
@@ -211,7 +235,7 @@ inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
 // grid building (pfx_grid.hip)
 void build_grid(pfx_ctx* ctx, Grid& g, const float* d_x, const float* d_y, const float* d_z,
-                int64_t n, double radius);
+                int64_t n, double radius, bool use_hint = false);
 // bounding box of the finite points (0 when there are none), synchronous
 void points_bbox(pfx_ctx* ctx, Grid& g, const float* d_x, const float* d_y, const float* d_z, int64_t n,
                  double lo[3], double hi[3]);

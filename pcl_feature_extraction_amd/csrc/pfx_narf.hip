@@ -40,7 +40,23 @@ struct NarfState {
   std::vector<float> h_interest, h_scs, h_range;
   std::vector<uint32_t> h_traits;
   bool have_debug = false;
+  // pinned host block of the readbacks (counters, NMS survivors, validity bits): async DMA copies,
+  // not pageable staging through a blit kernel (which waited ~1 ms for CU slots beside the
+  // normal estimation's list kernels and held the runtime lock the other host thread launches through)
+  void* pinned = nullptr;
+  size_t pinned_bytes = 0;
+  void* host(size_t need) {
+    if (need > pinned_bytes) {
+      if (pinned) PFX_HIP(hipHostFree(pinned));
+      pinned_bytes = need + need / 2 + 4096;
+      PFX_HIP(hipHostMalloc(&pinned, pinned_bytes, hipHostMallocDefault));
+    }
+    return pinned;
+  }
   void release() {
+    if (pinned) (void)hipHostFree(pinned);
+    pinned = nullptr;
+    pinned_bytes = 0;
     DevBuf* all[] = {&direct, &fill, &pts, &surf, &svalid, &sL, &sR, &sT, &sB, &uL, &uR, &uT, &uB, &shadow,
                      &traits, &rawdir, &dir, &scs, &scd, &interest, &cand, &counters, &rowp, &sat, &work, &fb1, &pk};
     for (auto* b : all) b->release();
@@ -1409,10 +1425,16 @@ int64_t narf_dev(pfx_ctx* ctx, const float* x, const float* y, const float* z, i
     PFX_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_ff_prof), z, sizeof(z)));
   }
 #endif
-  int h_cnt[4];
-  unsigned long long h_work[4];
-  PFX_HIP(hipMemcpyAsync(h_cnt, counters, sizeof(h_cnt), hipMemcpyDeviceToHost, st));
-  PFX_HIP(hipMemcpyAsync(h_work, work, sizeof(h_work), hipMemcpyDeviceToHost, st));
+  const int nwords = (npx + 31) / 32;
+  // pinned readback block: [4 counters | 4 work words | npx NMS survivors (float4) | npx indices | bits]
+  char* hb = static_cast<char*>(S.host(64 + (size_t)npx * (sizeof(float4) + sizeof(int)) + sizeof(uint32_t) * nwords));
+  int* h_cnt = reinterpret_cast<int*>(hb);
+  unsigned long long* h_work = reinterpret_cast<unsigned long long*>(hb + 16);
+  float4* h_pts = reinterpret_cast<float4*>(hb + 64);
+  int* h_cand = reinterpret_cast<int*>(hb + 64 + (size_t)npx * sizeof(float4));
+  uint32_t* h_valid = reinterpret_cast<uint32_t*>(hb + 64 + (size_t)npx * (sizeof(float4) + sizeof(int)));
+  PFX_HIP(hipMemcpyAsync(h_cnt, counters, 4 * sizeof(int), hipMemcpyDeviceToHost, st));
+  PFX_HIP(hipMemcpyAsync(h_work, work, 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
   PFX_HIP(hipStreamSynchronize(st));
   ctx->stats["narf_interest_grown"] = (int64_t)h_work[0];
   ctx->stats["narf_interest_fullimage"] = h_cnt[2];
@@ -1424,7 +1446,6 @@ int64_t narf_dev(pfx_ctx* ctx, const float* x, const float* y, const float* z, i
   if (h_cnt[1] & 2) throw Error(PFX_ERR_DEVICE, "narf: interest region left its window bound (internal error)");
   const int nc = h_cnt[0];
   // NMS survivors (point + strength) and the image's validity bits go to the host in one copy
-  const int nwords = (npx + 31) / 32;
   float4* cpts = S.rawdir.as<float4>(npx);  // rawdir is dead after k_border_dir_avg: reuse
   uint32_t* vbits = reinterpret_cast<uint32_t*>(S.sL.as<float>(npx));  // sL is dead after the update
   {
@@ -1433,15 +1454,14 @@ int64_t narf_dev(pfx_ctx* ctx, const float* x, const float* y, const float* z, i
     k_valid_bits<<<nblk(nwords), 256, 0, st>>>(P, npx, vbits);
     check_launch("k_gather_cand");
   }
-  std::vector<float4> h_pts(nc);
-  std::vector<uint32_t> h_valid(nwords);
-  if (nc > 0) PFX_HIP(hipMemcpyAsync(h_pts.data(), cpts, sizeof(float4) * nc, hipMemcpyDeviceToHost, st));
-  PFX_HIP(hipMemcpyAsync(h_valid.data(), vbits, sizeof(uint32_t) * nwords, hipMemcpyDeviceToHost, st));
+  if (nc > 0) {
+    PFX_HIP(hipMemcpyAsync(h_pts, cpts, sizeof(float4) * nc, hipMemcpyDeviceToHost, st));
+    PFX_HIP(hipMemcpyAsync(h_cand, cand, sizeof(int) * nc, hipMemcpyDeviceToHost, st));
+  }
+  PFX_HIP(hipMemcpyAsync(h_valid, vbits, sizeof(uint32_t) * nwords, hipMemcpyDeviceToHost, st));
   PFX_HIP(hipStreamSynchronize(st));
   // k_gather_cand wrote (x, y, z, strength) plus the pixel index in the sort key: restore raster order
   std::vector<std::pair<int, float4>> ordered(nc);
-  std::vector<int> h_cand(nc);
-  if (nc > 0) PFX_HIP(hipMemcpy(h_cand.data(), cand, sizeof(int) * nc, hipMemcpyDeviceToHost));
   for (int k = 0; k < nc; ++k) ordered[k] = std::make_pair(h_cand[k], h_pts[k]);
   std::sort(ordered.begin(), ordered.end(),
             [](const std::pair<int, float4>& a, const std::pair<int, float4>& b) { return a.first < b.first; });

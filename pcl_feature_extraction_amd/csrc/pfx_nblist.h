@@ -34,7 +34,12 @@ struct NbLists {
   const uint8_t* lg = nullptr;     // [nq] log2 of the entry stride
   const uint32_t* list = nullptr;  // [slots] run entries
   const uint32_t* skeys = nullptr; // cell key of each sorted position (the grid's)
+  // deferred builds (build_lists with defer): nq is an upper bound and the query count lives on
+  // the device until build_lists_check has run; kernels read it through nq_of()
+  const int64_t* nq_dev = nullptr;
 };
+
+__device__ __forceinline__ int64_t nq_of(const NbLists& L) { return L.nq_dev ? *L.nq_dev : L.nq; }
 
 // lists longer than this are handled by per-query kernels downstream (normals: k_normals_long)
 constexpr int kLongList = 1024;
@@ -50,7 +55,14 @@ struct NormalsState {
 };
 
 // mask (nullable): per *caller* index, queries are the masked points (in cell order).
+// defer: launch the list kernels and return without the host readback (out.nq = an upper bound,
+// out.nq_dev = the device count); consumers may be launched behind them in stream order, and
+// build_lists_check must follow.
 void build_lists(pfx_ctx* ctx, const Grid& g, const uint8_t* mask, double radius, bool sorted, NbLists& out,
-                 const char* tag);
+                 const char* tag, bool defer = false);
+// The deferred build's readback: true and `out` completed (exact nq, statistics) when the lists are
+// valid; false when they must be rebuilt synchronously (list buffer too small, first very long
+// lists, or a speculative grid with points outside its bounds) -- their consumers rerun too.
+bool build_lists_check(pfx_ctx* ctx, const Grid& g, NbLists& out, const char* tag);
 
 }  // namespace pfx

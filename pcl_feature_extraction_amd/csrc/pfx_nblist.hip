@@ -78,6 +78,18 @@ __global__ void k_list_init(int32_t* __restrict__ qpos, int64_t n, const int32_t
   if (i == 0 && nq_src) *d_nq = (int64_t)*nq_src;
 }
 
+// deferred builds: the query count the consumers see is 0 unless the lists are whole (every
+// entry inside the list buffer, no query left for the first very-long-list pass, no capacity
+// overflow, a speculative grid that held every point): an invalid build is then never read
+// (its offsets may point past the buffer) and build_lists_check reruns the exact path
+__global__ void k_defer_gate(const int* __restrict__ counters, const unsigned long long* __restrict__ cursor,
+                             unsigned long long cap, int have_huge, const int* __restrict__ oob,
+                             const int64_t* __restrict__ d_nq, int64_t* __restrict__ d_nq_eff) {
+  if (threadIdx.x != 0) return;
+  const bool ok = cursor[0] <= cap && (have_huge || counters[3] == 0) && counters[4] == 0 && (!oob || *oob == 0);
+  *d_nq_eff = ok ? *d_nq : 0;
+}
+
 __global__ void k_mask_flags(const int32_t* __restrict__ perm, const uint32_t* __restrict__ skeys, int64_t n,
                              uint64_t ncells, const uint8_t* __restrict__ mask, uint8_t* __restrict__ flags) {
   int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
@@ -904,10 +916,52 @@ __global__ void __launch_bounds__(256) k_nb_query(GridView g, const int32_t* __r
 
 std::string bname(const char* tag, const char* what) { return std::string(tag) + "_" + what; }
 
+// the pinned readback block of a list build
+struct ListsRb {
+  int cnt[14];
+  int oob;
+  int pad;
+  unsigned long long cur[4];
+  int64_t nq;
+};
+
 }  // namespace
 
+bool build_lists_check(pfx_ctx* ctx, const Grid& G, NbLists& out, const char* tag) {
+  hipStream_t st = ctx->stream;
+  auto B = [&](const char* what) -> DevBuf& { return ctx->bufs[bname(tag, what)]; };
+  ListsRb* rb = ctx->readback<ListsRb>();
+  PFX_HIP(hipMemcpyAsync(rb->cnt, B("counters").ptr, sizeof(rb->cnt), hipMemcpyDeviceToHost, st));
+  PFX_HIP(hipMemcpyAsync(rb->cur, B("cursor").ptr, sizeof(rb->cur), hipMemcpyDeviceToHost, st));
+  PFX_HIP(hipMemcpyAsync(&rb->nq, B("nq").ptr, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+  rb->oob = 0;
+  if (G.oob) PFX_HIP(hipMemcpyAsync(&rb->oob, G.oob, sizeof(int), hipMemcpyDeviceToHost, st));
+  ctx->sync_spin(st);
+  const int* h_cnt = rb->cnt;
+  const unsigned long long* h_cur = rb->cur;
+  const DevBuf& lb = B("list");
+  if (rb->oob > 0) return false;                                    // speculative grid too small
+  if (h_cur[0] > lb.bytes / sizeof(uint32_t)) return false;         // list buffer too small
+  if (!B("scratch").ptr && h_cnt[3] > 0) return false;              // first very long lists
+  if (h_cnt[4] > 0)
+    throw Error(PFX_ERR_CAPACITY, std::string(tag) + ": a query has " + std::to_string(h_cnt[4]) +
+                                      " neighbours (> " + std::to_string(kCapHuge) + " supported)");
+  out.nq = rb->nq;
+  out.nq_dev = nullptr;
+  out.total = (int64_t)h_cur[1];
+  out.long_total = (int64_t)h_cur[2];
+  out.long_nq = (int64_t)h_cur[3];
+  out.slots = (int64_t)h_cur[0];
+  ctx->stats[std::string(tag) + "_tiles_sparse"] = h_cnt[0];
+  ctx->stats[std::string(tag) + "_tiles_dense"] = h_cnt[1];
+  ctx->stats[std::string(tag) + "_single"] = h_cnt[2];
+  ctx->stats[std::string(tag) + "_huge"] = h_cnt[3];
+  ctx->stats[std::string(tag) + "_mid"] = h_cnt[12];
+  return true;
+}
+
 void build_lists(pfx_ctx* ctx, const Grid& G, const uint8_t* mask, double radius, bool sorted, NbLists& out,
-                 const char* tag) {
+                 const char* tag, bool defer) {
   hipStream_t st = ctx->stream;
   const int64_t n = G.n;
   GridView g = view(G);
@@ -998,8 +1052,7 @@ void build_lists(pfx_ctx* ctx, const Grid& G, const uint8_t* mask, double radius
       PFX_HIP(hipMemsetAsync(counters + 11, 0, 3 * sizeof(int), st));  // small queue, mid work + queue
     }
     // one synchronisation per call: counters, cursors and the query count in one pinned block
-    struct Rb { int cnt[14]; int pad[2]; unsigned long long cur[4]; int64_t nq; };
-    Rb* rb = ctx->readback<Rb>();
+    ListsRb* rb = ctx->readback<ListsRb>();
     auto read_back = [&] {
       PFX_HIP(hipMemcpyAsync(rb->cnt, counters, sizeof(rb->cnt), hipMemcpyDeviceToHost, st));
       PFX_HIP(hipMemcpyAsync(rb->cur, cursor, sizeof(rb->cur), hipMemcpyDeviceToHost, st));
@@ -1045,6 +1098,20 @@ void build_lists(pfx_ctx* ctx, const Grid& G, const uint8_t* mask, double radius
         if (hs.ptr) launch_huge();
       }
       check_launch("nblist lists");
+    }
+    if (defer && attempt == 0) {  // consumers are launched before the readback (build_lists_check)
+      int64_t* d_nq_eff = B("nq_eff").as<int64_t>(1);
+      k_defer_gate<<<1, 64, 0, st>>>(counters, cursor, lo.cap, hs.ptr ? 1 : 0, G.oob, d_nq, d_nq_eff);
+      check_launch("k_defer_gate");
+      out.nq = n;
+      out.nq_dev = d_nq_eff;
+      out.qpos = qpos;
+      out.off = off;
+      out.cnt = cnt;
+      out.lg = lgs;
+      out.list = lo.list;
+      out.skeys = G.skeys;
+      return;
     }
     read_back();
     if (!hs.ptr && rb->cnt[3] > 0) {  // very long lists, first time: allocate the scratch and sort them

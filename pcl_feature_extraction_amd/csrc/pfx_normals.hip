@@ -173,7 +173,7 @@ __device__ __forceinline__ void chain_wg(ChainLds<CAP>& S, const GridView& g, co
   constexpr int PO = CAP == kStageSmall ? 0 : 8;
   const long long pt0 = clock64();
 #endif
-  const bool valid = j < L.nq;
+  const bool valid = j < nq_of(L);
   int32_t p = 0;
   uint32_t key = 0, prev = kEmpty;
   int k = 0;
@@ -433,7 +433,7 @@ __global__ void __launch_bounds__(256) k_long_lists(GridView g, NbLists L, const
                                                     int32_t* __restrict__ longq, int* __restrict__ n_long) {
   const int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   bool push = false;
-  if (j < L.nq && L.cnt[j] > kLaneMax) push = !mask || ((mask[g.perm[L.qpos[j]]] != 0) == (want != 0));
+  if (j < nq_of(L) && L.cnt[j] > kLaneMax) push = !mask || ((mask[g.perm[L.qpos[j]]] != 0) == (want != 0));
   if (push) longq[wave_push_slot(n_long)] = (int32_t)j;
 }
 
@@ -636,7 +636,9 @@ void normals_chains_dev(pfx_ctx* ctx, pfx_ctx* owner, const uint8_t* mask, int w
   check_launch("k_long_lists");
   // (sized to what is resident at once: waves beyond it would wait for a second round)
   const int64_t lb = std::min<int64_t>(ceil_div(L.nq, 7 * 4), 256 * 4);
-  const bool fork = L.long_nq * 8 <= L.nq;
+  // (a deferred build has no count yet: the previous estimation's decision on this context)
+  const bool fork = L.nq_dev ? ctx->normals_fork_hint : L.long_nq * 8 <= L.nq;
+  if (!L.nq_dev) ctx->normals_fork_hint = fork;
   if (fork) {
     ctx->ensure_side();
     PFX_HIP(hipEventRecord(ctx->fork_ev[0], st));
@@ -706,9 +708,58 @@ void normals_chains_dev(pfx_ctx* ctx, pfx_ctx* owner, const uint8_t* mask, int w
 #endif
 }
 
+// The estimation with one host round trip: the grid on the previous call's widened bounds (no
+// bounds readback), then one readback validating the grid and the lists together before the
+// chains (a grid whose bounds missed a point, a list buffer that overflowed or the first very long
+// lists: the exact two-phase path reruns).  The chains are launched after the check so the host
+// returns while they run and the caller's next stage (FPFH) is queued behind them; launching them
+// before the check (PFX_NORMALS_DEFER=1) leaves the host waiting on the chains instead: measured
+// 170.6 vs 171.9 Mpoints/s (the exact bounds readback path, PFX_NORMALS_SYNC=1, 171.9).
 void normals_dev(pfx_ctx* ctx, const float* x, const float* y, const float* z, int64_t n, double r,
                  const float vp[3], float* nx, float* ny, float* nz, float* curv) {
   TimeScope total(ctx, "normals", true);
+  PFX_CHECK(r > 0.0, "normals: radius must be > 0");
+  PFX_CHECK(n >= 0, "normals: negative point count");
+  auto flag = [](const char* name) {
+    const char* e = getenv(name);
+    return e && *e && *e != '0';
+  };
+  static const bool sync_path = flag("PFX_NORMALS_SYNC");   // A/B switches
+  static const bool defer_chains = flag("PFX_NORMALS_DEFER");
+  if (n > 0 && !sync_path) {
+    if (!ctx->normals) ctx->normals = new NormalsState();
+    NormalsState& ns = *ctx->normals;
+    ns.ready = false;
+    ns.n = n;
+    ns.x = x;
+    ns.y = y;
+    ns.z = z;
+    ns.r = r;
+    ns.L = NbLists();
+    hipStream_t st = ctx->stream;
+    {
+      TimeScope phase(ctx, "normals_lists_phase", true);
+      build_grid(ctx, ctx->grid_a, x, y, z, n, r, /*use_hint=*/true);
+      k_nan_fill4<<<(unsigned)std::min<int64_t>(ceil_div(n, 256), 4096), 256, 0, st>>>(nx, ny, nz, curv, n);
+      check_launch("k_nan_fill4");
+      build_lists(ctx, ctx->grid_a, nullptr, r, true, ns.L, "normals", /*defer=*/true);
+    }
+    bool ok = true;
+    if (!defer_chains) ok = build_lists_check(ctx, ctx->grid_a, ns.L, "normals");
+    ns.ready = true;  // (the check below decides what stays when the chains go first)
+    if (ok) normals_chains_dev(ctx, ctx, nullptr, 0, vp, nx, ny, nz, curv);
+    if (defer_chains) ok = build_lists_check(ctx, ctx->grid_a, ns.L, "normals");
+    ctx->grid_a.oob = nullptr;
+    ctx->stats["normals_speculative_reruns"] += ok ? 0 : 1;
+    if (ok) {
+      ctx->stats["normals_neighbors"] = ns.L.total;
+      ctx->stats["normals_long_neighbors"] = ns.L.long_total;
+      ctx->stats["normals_long_queries"] = ns.L.long_nq;
+      ctx->stats["normals_queries"] = ns.L.nq;
+      ctx->normals_fork_hint = ns.L.long_nq * 8 <= ns.L.nq;
+      return;
+    }
+  }
   normals_lists_dev(ctx, x, y, z, n, r, nx, ny, nz, curv);
   if (n > 0) normals_chains_dev(ctx, ctx, nullptr, 0, vp, nx, ny, nz, curv);
 }

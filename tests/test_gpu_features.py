@@ -112,6 +112,32 @@ def test_normals_every_list_path(ctx):
         assert _nan_aware_equal(a, b)
 
 
+def test_normals_speculative_grid_and_list_check():
+    """normals_dev builds the grid on the previous call's widened bounds and validates grid and
+    lists in one readback (pfx_normals.hip normals_dev): a scan outside the hint, a list buffer
+    too small and the first very long lists each rerun the exact path, bit-exact either way."""
+    from pcl_feature_extraction_amd import Context
+    x, y, z = _cloud("underwater_source")
+    rng = np.random.default_rng(5)
+    blob = np.repeat(rng.normal(0, 0.004, (5500, 3)) + [x.mean(), y.mean(), z.mean()], 3, axis=0)  # k > 16384
+    with Context(0) as c:
+        def run(px, py, pz):
+            before = c.stat("normals_speculative_reruns")
+            g = c.normals(px, py, pz, 0.05)
+            o = O.normals(px, py, pz, 0.05)
+            for a, b in zip(g, o):
+                assert _nan_aware_equal(a, b)
+            return c.stat("normals_speculative_reruns") - before
+        assert run(x, y, z) in (0, 1)     # first call: exact bounds (a fresh list buffer may be short)
+        assert run(x, y, z) == 0          # inside the hint
+        sx = (x + 5.0).astype(np.float32)
+        assert run(sx, y, z) == 1         # outside the hint: rerun on exact bounds
+        assert run(sx, y, z) == 0
+        bx, by, bz = (np.concatenate([a, b]).astype(np.float32) for a, b in zip((sx, y, z), blob.T + [[5.0], [0], [0]]))
+        assert run(bx, by, bz) == 1       # first very long lists (scratch allocated by the rerun)
+        assert run(bx, by, bz) == 0
+
+
 def test_normals_empty_and_tiny(ctx):
     e = np.zeros(0, np.float32)
     g = ctx.normals(e, e, e, 0.05)
