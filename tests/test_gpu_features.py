@@ -121,13 +121,19 @@ def test_normals_speculative_grid_and_list_check():
     rng = np.random.default_rng(5)
     blob = np.repeat(rng.normal(0, 0.004, (5500, 3)) + [x.mean(), y.mean(), z.mean()], 3, axis=0)  # k > 16384
     with Context(0) as c:
+        def reruns():
+            try:
+                return c.stat("normals_speculative_reruns")
+            except Exception:  # (no normal estimation on this context yet)
+                return 0
+
         def run(px, py, pz):
-            before = c.stat("normals_speculative_reruns")
+            before = reruns()
             g = c.normals(px, py, pz, 0.05)
             o = O.normals(px, py, pz, 0.05)
             for a, b in zip(g, o):
                 assert _nan_aware_equal(a, b)
-            return c.stat("normals_speculative_reruns") - before
+            return reruns() - before
         assert run(x, y, z) in (0, 1)     # first call: exact bounds (a fresh list buffer may be short)
         assert run(x, y, z) == 0          # inside the hint
         sx = (x + 5.0).astype(np.float32)
