@@ -225,6 +225,98 @@ __device__ __forceinline__ bool pair_bins_fast(f3 p1, f3 n1, f3 p2, f3 n2, int& 
          bin_fast_f((f3a + 1.0f) * (0.5f * kBins), 1e-6f * 0.5f * kBins + kBinMapSlack, h3);
 }
 
+// pair_bins_fast for two pairs (p1, p2a) and (p1, p2b) at once: the same float operations
+// component by component, the element-wise arithmetic on packed FP32 (v_pk_mul/add_f32: one
+// instruction for both pairs, each half rounded exactly as the scalar op), the decisions,
+// transcendental approximations and bin maps per component.  p1 / n1 are the S point's
+// (wave-uniform, n1 finite: the caller checked).  ok[c] == false: pair c needs the exact path.
+typedef float fv2 __attribute__((ext_vector_type(2)));
+struct v32 { fv2 x, y, z; };
+__device__ __forceinline__ fv2 dot4v(const v32& a, const v32& b) { return (a.x * b.x + a.z * b.z) + (a.y * b.y + 0.0f); }
+__device__ __forceinline__ v32 cross3v(const v32& a, const v32& b) {
+  return v32{a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x};
+}
+__device__ __forceinline__ fv2 sel2(bool c0, bool c1, fv2 a, fv2 b) { return fv2{c0 ? a.x : b.x, c1 ? a.y : b.y}; }
+
+__device__ __forceinline__ void pair_bins_fast2(f3 p1, f3 n1, bool n1fin, const v32& p2, const v32& n2, int h1[2],
+                                                int h2[2], int h3[2], bool ok[2]) {
+  const int bz1 = bin_of(f1_scaled(0.0)), bz = bin_of((double)kBins * ((0.0 + 1.0) * 0.5));
+  const v32 dp0{p2.x - p1.x, p2.y - p1.y, p2.z - p1.z};
+  const fv2 s4 = (dp0.x * dp0.x + dp0.z * dp0.z) + (dp0.y * dp0.y + 0.0f);
+  const v32 n1v{fv2(n1.x), fv2(n1.y), fv2(n1.z)};
+  const fv2 d1 = dot4v(n1v, dp0), d2 = dot4v(n2, dp0);
+  bool sw[2], live[2];
+  fv2 rf4;
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    const bool fin = n1fin && isfinite(n2.x[c]) && isfinite(n2.y[c]) && isfinite(n2.z[c]);
+    const float ad1 = fabsf(d1[c]), ad2 = fabsf(d2[c]);
+    rf4[c] = __builtin_amdgcn_rsqf(s4[c]);
+    sw[c] = ad1 < ad2 * (1.0f - 4e-7f);
+    const bool decided = sw[c] || ad1 > ad2 * (1.0f + 4e-7f);
+    live[c] = fin && !(fmaxf(ad1, ad2) * rf4[c] < 2e-8f) && decided;
+  }
+  const fv2 f3a = sel2(sw[0], sw[1], -d2 * rf4, d1 * rf4);
+  const v32 n1c{sel2(sw[0], sw[1], n2.x, n1v.x), sel2(sw[0], sw[1], n2.y, n1v.y), sel2(sw[0], sw[1], n2.z, n1v.z)};
+  const v32 n2c{sel2(sw[0], sw[1], n1v.x, n2.x), sel2(sw[0], sw[1], n1v.y, n2.y), sel2(sw[0], sw[1], n1v.z, n2.z)};
+  const v32 dp{sel2(sw[0], sw[1], -dp0.x, dp0.x), sel2(sw[0], sw[1], -dp0.y, dp0.y), sel2(sw[0], sw[1], -dp0.z, dp0.z)};
+  const v32 v = cross3v(dp, n1c);
+  const fv2 sv = (v.x * v.x + v.z * v.z) + (v.y * v.y + 0.0f);
+  const fv2 rsv{__builtin_amdgcn_rsqf(sv.x), __builtin_amdgcn_rsqf(sv.y)};
+  const v32 vh{v.x * rsv, v.y * rsv, v.z * rsv};
+  const v32 w = cross3v(n1c, vh);
+  const fv2 f2a = dot4v(vh, n2c), y = dot4v(w, n2c), x = dot4v(n1c, n2c);
+  fv2 mn, rmx;
+  bool big[2];
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    const float ax = fabsf(x[c]), ay = fabsf(y[c]);
+    const float mx = fmaxf(ax, ay);
+    mn[c] = fminf(ax, ay);
+    big[c] = mx > 1e-20f;
+    rmx[c] = __builtin_amdgcn_rcpf(mx);
+  }
+  // atan_poly on both
+  const fv2 a = mn * rmx;
+  const fv2 z = a * a;
+  fv2 pp = fv2(-0.00405456405133009f);
+  pp = pp * z + 0.021862948313355446f;
+  pp = pp * z + -0.0559123195707798f;
+  pp = pp * z + 0.0964219719171524f;
+  pp = pp * z + -0.1390862911939621f;
+  pp = pp * z + 0.19946566224098206f;
+  pp = pp * z + -0.33329859375953674f;
+  pp = pp * z + 0.9999993443489075f;
+  fv2 t = pp * a;
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    float tc = t[c];
+    if (fabsf(y[c]) > fabsf(x[c])) tc = 1.57079637f - tc;
+    if (x[c] < 0.0f) tc = 3.14159274f - tc;
+    t[c] = y[c] < 0.0f ? -tc : tc;
+  }
+  const float d_pi = 1.0f / (2.0f * 3.14159265358979323846f);
+  const fv2 tol1 = (fv2(1e-6f) + 8e-6f * rmx) * (1.01f * (float)kBins * d_pi) + kBinMapSlack;
+  const fv2 b1 = (t + 3.14159265358979323846f) * ((float)kBins * d_pi);
+  const fv2 b2 = (f2a + 1.0f) * (0.5f * kBins), b3 = (f3a + 1.0f) * (0.5f * kBins);
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    if (s4[c] == 0.0f) {  // f4 == 0 in pair_bins
+      h1[c] = bz1; h2[c] = h3[c] = bz;
+      ok[c] = true;
+    } else if (!live[c]) {
+      ok[c] = false;
+    } else if (sv[c] == 0.0f) {  // v_norm == 0 in pair_bins
+      h1[c] = bz1; h2[c] = h3[c] = bz;
+      ok[c] = true;
+    } else {
+      ok[c] = big[c] && bin_fast_f(b1[c], tol1[c], h1[c]) &&
+              bin_fast_f(b2[c], 4e-6f * 0.5f * kBins + kBinMapSlack, h2[c]) &&
+              bin_fast_f(b3[c], 1e-6f * 0.5f * kBins + kBinMapSlack, h3[c]);
+    }
+  }
+}
+
 // the exact path out of line (rare), bins packed h1 | h2 << 8 | h3 << 16
 __device__ __attribute__((noinline)) int pair_bins_exact(float p1x, float p1y, float p1z, float n1x, float n1y,
                                                          float n1z, float p2x, float p2y, float p2z, float n2x,
@@ -333,7 +425,7 @@ __global__ void __launch_bounds__(256, PFX_SPFH_WPE) k_fpfh_spfh(GridView g, con
                                                       int* __restrict__ hcount, int* __restrict__ kcount,
                                                       int2* __restrict__ slowq, unsigned* __restrict__ n_slow,
                                                       unsigned slow_cap, unsigned long long* __restrict__ pairs) {
-  __shared__ uint32_t queue[4][128];
+  __shared__ uint32_t queue[4][192];  // < 128 pending + one 64-candidate push
   // 16 copies of each wave's counters (lane & 15): pairs of a planar patch pile into a few bins,
   // and same-address LDS atomics serialise
   __shared__ int hist[4][kHistCopies][kDesc];
@@ -356,25 +448,12 @@ __global__ void __launch_bounds__(256, PFX_SPFH_WPE) k_fpfh_spfh(GridView g, con
       R.start[r] = __builtin_amdgcn_readfirstlane(R.start[r]);
       R.pref[r + 1] = __builtin_amdgcn_readfirstlane(R.pref[r + 1]);
     }
+    const bool pn_fin = isfinite(pn.x) && isfinite(pn.y) && isfinite(pn.z);
     int k = 0, qn = 0;
-    auto process = [&](int nvalid) {
-      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      bool fast = true;
-      uint32_t q = 0;
-      if (lane < nvalid) {
-        q = queue[wv][lane];
-        const float4 qc = g.sp[q], qnv = snp[q];
-        int h1, h2, h3;
-        const f3 qp = mk3(qc.x, qc.y, qc.z), qn3 = mk3(qnv.x, qnv.y, qnv.z);
-        fast = pair_bins_fast(pp, pn, qp, qn3, h1, h2, h3);
-        if (fast) {
-          int* hc = hist[wv][lane & (kHistCopies - 1)];
-          atomicAdd(&hc[h1], 1);
-          atomicAdd(&hc[kBins + h2], 1);
-          atomicAdd(&hc[2 * kBins + h3], 1);
-        }
-      }
+    int* hc = hist[wv][lane & (kHistCopies - 1)];
+    // a pair the fast path cannot bin goes to the exact-pair queue (or, past its capacity, through
+    // the exact path right here, so no pass ever reruns)
+    auto defer = [&](bool fast, uint32_t q) {
       const uint64_t m = __ballot(!fast);
       if (m) {
         unsigned base = 0;
@@ -384,16 +463,46 @@ __global__ void __launch_bounds__(256, PFX_SPFH_WPE) k_fpfh_spfh(GridView g, con
         if (!fast) {
           if (slot < slow_cap) {
             slowq[slot] = make_int2((int)w, (int)q);
-          } else {  // queue full (rare): the exact path right here, so no pass ever reruns
+          } else {
             const float4 qc = g.sp[q], qnv = snp[q];
             const int hb = pair_bins_exact(pp.x, pp.y, pp.z, pn.x, pn.y, pn.z, qc.x, qc.y, qc.z, qnv.x, qnv.y, qnv.z);
-            int* hc = hist[wv][lane & (kHistCopies - 1)];
             atomicAdd(&hc[hb & 0xff], 1);
             atomicAdd(&hc[kBins + ((hb >> 8) & 0xff)], 1);
             atomicAdd(&hc[2 * kBins + (hb >> 16)], 1);
           }
         }
       }
+    };
+    // up to 128 queued pairs, two per lane (entries lane and lane + 64) on packed FP32
+    auto process = [&](int nvalid) {
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      const bool ina = lane < nvalid, inb = lane + 64 < nvalid;
+      const uint32_t qa = ina ? queue[wv][lane] : 0u, qb = inb ? queue[wv][lane + 64] : 0u;
+      bool fa = true, fb = true;
+      if (ina) {
+        const uint32_t qb2 = inb ? qb : qa;
+        const float4 ca = g.sp[qa], na = snp[qa], cb = g.sp[qb2], nb = snp[qb2];
+        const v32 p2{fv2{ca.x, cb.x}, fv2{ca.y, cb.y}, fv2{ca.z, cb.z}};
+        const v32 n2{fv2{na.x, nb.x}, fv2{na.y, nb.y}, fv2{na.z, nb.z}};
+        int h1[2], h2[2], h3[2];
+        bool ok[2];
+        pair_bins_fast2(pp, pn, pn_fin, p2, n2, h1, h2, h3, ok);
+        fa = ok[0];
+        fb = !inb || ok[1];
+        if (fa) {
+          atomicAdd(&hc[h1[0]], 1);
+          atomicAdd(&hc[kBins + h2[0]], 1);
+          atomicAdd(&hc[2 * kBins + h3[0]], 1);
+        }
+        if (inb && ok[1]) {
+          atomicAdd(&hc[h1[1]], 1);
+          atomicAdd(&hc[kBins + h2[1]], 1);
+          atomicAdd(&hc[2 * kBins + h3[1]], 1);
+        }
+      }
+      defer(fa, qa);
+      defer(fb, qb);
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
       __builtin_amdgcn_wave_barrier();
     };
@@ -414,13 +523,13 @@ __global__ void __launch_bounds__(256, PFX_SPFH_WPE) k_fpfh_spfh(GridView g, con
         const uint64_t m = __ballot(push);
         if (push) queue[wv][qn + __popcll(m & lanemask_lt())] = (uint32_t)pos;
         qn += __popcll(m);
-        if (qn >= 64) {
-          process(64);
-          const uint32_t rest = (lane + 64 < qn) ? queue[wv][lane + 64] : 0u;
+        if (qn >= 128) {
+          process(128);
+          const uint32_t rest = (lane + 128 < qn) ? queue[wv][lane + 128] : 0u;
           __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
           __builtin_amdgcn_wave_barrier();
-          if (lane + 64 < qn) queue[wv][lane] = rest;
-          qn -= 64;
+          if (lane + 128 < qn) queue[wv][lane] = rest;
+          qn -= 128;
         }
       }
     }

@@ -11,6 +11,7 @@ cut -c1-300 gpurun_out/bench_$TAG.json
 for w in shot match iss harris harris6d config1 fastnormals; do
   timeout -k 10 400 python bench.py --workload $w > gpurun_out/bench_${w}_$TAG.json 2> gpurun_out/bench_${w}_$TAG.err || { tail -30 gpurun_out/bench_${w}_$TAG.err; exit 1; }
 done
+timeout -k 10 400 python bench.py --scans 8 --steps 5 --warmup 2 --no-cpu-baseline > gpurun_out/bench_scans8_$TAG.json 2> gpurun_out/bench_scans8_$TAG.err || { tail -30 gpurun_out/bench_scans8_$TAG.err; exit 1; }
 timeout -k 10 400 python bench.py --workload dense --steps 3 --warmup 1 > gpurun_out/bench_dense_$TAG.json 2> gpurun_out/bench_dense_$TAG.err || { tail -30 gpurun_out/bench_dense_$TAG.err; exit 1; }
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof_$TAG -o run -- python3 $R/bench.py --steps 5 --warmup 2 --no-cpu-baseline > $R/gpurun_out/prof_$TAG.log 2>&1 || { tail -20 $R/gpurun_out/prof_$TAG.log; exit 1; }
