@@ -124,19 +124,21 @@ def cpu_baseline(x, y, z, workload, sample=None, reps=2):
                         f"anywhere in this pipeline"))
 
 
-def full_size_parity(outputs, kp, b, desc, rows, shot):
+def full_size_parity(outputs, kp, b, desc, rows, shot, normals_mask=None):
     """The last timed step's outputs against the CPU restatement's on the whole scan: bit-exact
-    (NaN positions equal) for keypoints, normals and descriptor rows."""
+    (NaN positions equal) for keypoints, normals and descriptor rows (normals_mask: the normals
+    compared only where it is set -- the demand-driven mode estimates no others)."""
     import numpy as np
     okp, onorm, odesc = outputs
     if shot:
         odesc = odesc[0]
+    sel = slice(None) if normals_mask is None else np.asarray(normals_mask) != 0
 
     def same(a, c):
         a, c = np.asarray(a, np.float32), np.asarray(c, np.float32)
         return bool(a.shape == c.shape and np.array_equal(np.nan_to_num(a, nan=7).view(np.uint32),
                                                           np.nan_to_num(c, nan=7).view(np.uint32)))
-    res = {"normals": all(same(t.cpu().numpy(), o) for t, o in zip((b.nx, b.ny, b.nz), onorm)),
+    res = {"normals": all(same(t.cpu().numpy()[sel], o[sel]) for t, o in zip((b.nx, b.ny, b.nz), onorm)),
            "descriptors": same(desc[:rows].cpu().numpy(), odesc)}
     if kp is not None:
         res["keypoints"] = bool(np.array_equal(np.asarray(kp), okp))
@@ -158,7 +160,7 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", choices=["fpfh", "shot", "match", "iss", "harris", "harris6d", "config1", "dense",
-                                           "fastnormals"],
+                                           "fastnormals", "demand"],
                     default="fpfh")
     ap.add_argument("--scans", type=int, default=0,
                     help="fpfh workload: scans per step (default 1 = configs[2] at --gpus 1, 8 = configs[4] at N > 1)")
@@ -241,6 +243,8 @@ def bench_scans(args, torch, dist, dev, world, rank, local):
     shot = args.workload == "shot"
     dense = args.workload == "dense"
     fast = args.workload == "fastnormals"
+    # opt-in: normals estimated only where FPFH reads them (same keypoints and descriptors)
+    demand = args.workload == "demand"
     npts = DENSE_POINTS if dense else N_POINTS
     if shot:
         n_scans, seeds = world, [3] if world == 1 else [300 + r for r in range(world)]
@@ -254,6 +258,9 @@ def bench_scans(args, torch, dist, dev, world, rank, local):
     ctx_n = Context(local)  # normal estimation overlapped with NARF on a second stream
     run_fpfh = OverlappedNarfFpfh(torch, ctx, ctx_n, dev)
     run_fpfh.fast_normals = fast
+    if demand:
+        run_fpfh.support_first = 1
+        run_fpfh.normals_scope = "support"
     # several scans on this rank (configs[4] at N < 8): the software-pipelined batch pass (scan
     # i's FPFH and scan i+1's NARF under scan i+1's normal estimation); one scan: the overlapped pass
     run_batch = (BatchNarfFpfh(torch, ctx, ctx_n, dev, side_stream=run_fpfh.s_side)
@@ -305,12 +312,14 @@ def bench_scans(args, torch, dist, dev, world, rank, local):
         blocks = []
         if w == 0 or run_batch is None:
             for b in scans:
-                if w == 0 and fast:  # the neighbour count of the scan, from one exact estimation
+                # the neighbour count of the scan, from one exact estimation (the fast mode has no
+                # lists; the support-first schedule's statistics cover its last subset only)
+                if w == 0 and (fast or (run_fpfh.support_first and not demand)):
                     ctx_n.normals_dev(b.x, b.y, b.z, 0.05, b.nx, b.ny, b.nz, b.curv)
                     nb_scan.append(ctx_n.stat("normals_neighbors"))
                     long_scan.append((ctx_n.stat("normals_long_neighbors"), ctx_n.stat("normals_long_queries")))
                 blocks.append(one_scan(b))
-                if w == 0 and not fast:
+                if w == 0 and not fast and (demand or not run_fpfh.support_first):
                     c = ctx if shot else ctx_n
                     nb_scan.append(c.stat("normals_neighbors"))
                     long_scan.append((c.stat("normals_long_neighbors"), c.stat("normals_long_queries")))
@@ -417,7 +426,7 @@ def bench_scans(args, torch, dist, dev, world, rank, local):
         deviation = fast_deviation(torch, fast_n, fast_d, b, k_exact, np.array_equal(np.asarray(kp_exact),
                                                                                      np.asarray(state["kp"])))
         run_fpfh.fast_normals = True
-    if rank == 0 and not shot:
+    if rank == 0 and not shot and not demand:  # (demand: the full estimation would overwrite the checked normals)
         b = scans[0]
         ctx_n.set_timing(True)
         ctx_n.reset_timing()
@@ -429,7 +438,7 @@ def bench_scans(args, torch, dist, dev, world, rank, local):
 
     if rank == 0:
         line = scans_line(args, world, n_scans, mine, shot, elapsed, timers, iso, nb_scan, long_scan, stat, npts,
-                          fast=fast, detail=detail, detail_steps=detail_steps)
+                          fast=fast, detail=detail, detail_steps=detail_steps, demand=demand)
         if deviation is not None:
             line["deviation_from_parity_path"] = deviation
         line["config"]["descriptor_rows"] = state["rows"]
@@ -451,12 +460,16 @@ def bench_scans(args, torch, dist, dev, world, rank, local):
                                           "opt-in mode departs from by design"}
         elif world == 1 and not args.no_cpu_baseline and not dense:
             x, y, z = host[0]
-            cb = cpu_baseline(x, y, z, args.workload, sample_np)
+            cb = cpu_baseline(x, y, z, "fpfh" if demand else args.workload, sample_np)
             cpu = {"value": round(npts / cb["seconds"] / 1e6, 6), "unit": "Mpoints/s",
                    "cores": cb["threads"], "kind": "port", "sample": cb["sample"], "runs_s": cb["runs"],
                    **host_info(),
                    "parity": full_size_parity(cb["outputs"], state["kp"], scans[0], sb.desc if shot else scans[0].desc,
-                                              state["rows"], shot)}
+                                              state["rows"], shot,
+                                              normals_mask=run_fpfh._support[:npts].cpu().numpy() if demand else None)}
+            if demand:
+                cpu["note"] = ("the reference's CPU path (every normal, as PCL computes them): the descriptors and "
+                               "keypoints are the outputs compared; normals compared on the support only")
         if dense:
             cpu = {"value": None, "note": "not run: the CPU restatement needs ~10 min per pass at this density "
                                           "(normals ~24.6G neighbour terms); see the configs[2] line"}
@@ -495,7 +508,7 @@ def fast_deviation(torch, fast_n, fast_d, b, k, same_kp):
 
 
 def scans_line(args, world, n_scans, mine, shot, elapsed, timers, iso, nb_scan, long_scan, stat, npts=N_POINTS,
-               fast=False, detail=None, detail_steps=1):
+               fast=False, detail=None, detail_steps=1, demand=False):
     """The contract line of bench_scans (rank 0), roofline over the neighbour-gather stage."""
     per_scan_calls = args.steps * len(mine)
     ms_per_step = elapsed / args.steps * 1e3
@@ -507,7 +520,8 @@ def scans_line(args, world, n_scans, mine, shot, elapsed, timers, iso, nb_scan, 
     # the WHOLE stage that produces them: grid build + FLANN-ordered list builders + ordered
     # covariance chains + long lists (timer "normals": HIP events around pfx_normals_dev on its
     # stream, inside the timed step, averaged per scan)
-    algo = nb * 12 + npts * 16
+    # (demand: the support's queries only -- the stage estimates no other normal)
+    algo = nb * 12 + (stat("normals_queries") if demand else npts) * 16
     stage_ms = timers["normals_fast" if fast else "normals"][0] / max(per_scan_calls, 1)
     stage_gbs = algo / (stage_ms / 1e3) / 1e9 if stage_ms > 0 else 0.0
     parts = ("grid_bbox", "grid_build", "normals_lists_small", "normals_lists_sparse", "normals_lists_dense",
@@ -571,7 +585,12 @@ def scans_line(args, world, n_scans, mine, shot, elapsed, timers, iso, nb_scan, 
         scaling = "weak"
     else:
         metric = "Mpoints/s through NARF keypoint + FPFH descriptor on 1M-pt cloud"
-        if n_scans == 1:
+        if n_scans == 1 and demand:
+            workload = ("configs[2] 1M-pt synthetic room, NARF(support 0.2) + FPFH(r 0.08) at the keypoints, normals "
+                        "(r 0.05) estimated only on the FPFH support (every point within 0.16 of a keypoint: a "
+                        "superset of the normals FPFHEstimation reads) -- same keypoints and descriptors; opt-in, "
+                        "not the contract line")
+        elif n_scans == 1:
             workload = ("configs[2] 1M-pt synthetic room, NARF(support 0.2) + normals(r 0.05) + FPFH(r 0.08) at "
                         "the keypoints")
         else:

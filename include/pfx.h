@@ -152,11 +152,30 @@ pfx_status pfx_normals_dev(pfx_ctx* ctx, const float* d_x, const float* d_y, con
  *   chains -- the normals of the points with (d_mask[i] != 0) == want (all when d_mask is
  *             null), on ctx's stream, from the lists held by `lists_ctx` (ctx itself or another
  *             context on the same device whose lists phase is ordered before this call).  Two
- *             chains calls with complementary masks may run concurrently on two contexts. */
+ *             chains calls with complementary masks may run concurrently on two contexts.
+ *             want = 3 / 2: workgroup partition -- every point of a block of 256 consecutive
+ *             (cell-ordered) queries that holds any masked point / holds none, so the two passes
+ *             stage each block's candidates once between them (the masked points are a subset
+ *             of pass 3's). */
 pfx_status pfx_normals_lists_dev(pfx_ctx* ctx, const float* d_x, const float* d_y, const float* d_z,
                                  int64_t n, double radius, float* d_nx, float* d_ny, float* d_nz,
                                  float* d_curvature);
 pfx_status pfx_normals_chains_dev(pfx_ctx* ctx, pfx_ctx* lists_ctx, const uint8_t* d_mask, int32_t want,
+                                  const float viewpoint[3], float* d_nx, float* d_ny, float* d_nz,
+                                  float* d_curvature);
+
+/* NormalEstimationOMP (tools.h:22-32) over a subset of the cloud: the points with
+ * (d_mask[i] != 0) == want get PCL's normal and curvature bit for bit (their neighbours are
+ * searched in the whole cloud); every other output entry is left untouched.  Two calls, want = 1
+ * then 0, give pfx_normals_dev's result.  Use: FPFH's support (pfx_fpfh_support_ball_dev) first,
+ * so FPFHEstimation starts on another stream while the rest is estimated -- the normals are
+ * Features::compute's intermediate (features.h:185-187), FPFH reads only the support's.
+ * pfx_normals_prepare_dev builds the cloud's grid ahead (coordinates only), e.g. while the mask
+ * is still being computed; pfx_normals_subset_dev builds it itself otherwise. */
+pfx_status pfx_normals_prepare_dev(pfx_ctx* ctx, const float* d_x, const float* d_y, const float* d_z,
+                                   int64_t n, double radius);
+pfx_status pfx_normals_subset_dev(pfx_ctx* ctx, const float* d_x, const float* d_y, const float* d_z,
+                                  int64_t n, double radius, const uint8_t* d_mask, int32_t want,
                                   const float viewpoint[3], float* d_nx, float* d_ny, float* d_nz,
                                   float* d_curvature);
 

@@ -100,6 +100,9 @@ _SIGS = {
     "pfx_fpfh_support_ball_dev": (c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_i64, c_dbl, c_vp]),
     "pfx_fpfh_prepare_queries_dev": (c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_i64, c_dbl]),
     "pfx_normals_lists_dev": (c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_dbl, c_vp, c_vp, c_vp, c_vp]),
+    "pfx_normals_prepare_dev": (c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_dbl]),
+    "pfx_normals_subset_dev": (c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_dbl, c_vp, ctypes.c_int32, c_vp, c_vp, c_vp,
+                                       c_vp, c_vp]),
     "pfx_normals_chains_dev": (c_int, [c_vp, c_vp, c_vp, ctypes.c_int32, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "pfx_shot": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_i64,
                          c_dbl, c_vp, c_vp]),

@@ -228,6 +228,18 @@ class Context:
         self._check(self._lib.pfx_normals_lists_dev(self.h, _ptr(x), _ptr(y), _ptr(z), x.numel(), float(r), _ptr(nx),
                                                     _ptr(ny), _ptr(nz), _ptr(curv)))
 
+    def normals_prepare_dev(self, x, y, z, r):
+        """The grid of the next normals_subset_dev calls on this cloud, built ahead (coordinates only)."""
+        self._check(self._lib.pfx_normals_prepare_dev(self.h, _ptr(x), _ptr(y), _ptr(z), x.numel(), float(r)))
+
+    def normals_subset_dev(self, x, y, z, r, mask, want, nx, ny, nz, curv, viewpoint=(0.0, 0.0, 0.0)):
+        """NormalEstimationOMP for the points with (mask != 0) == want only (uint8 device mask by
+        point); the other output entries are left untouched."""
+        vp = (ctypes.c_float * 3)(*viewpoint)
+        self._check(self._lib.pfx_normals_subset_dev(self.h, _ptr(x), _ptr(y), _ptr(z), x.numel(), float(r),
+                                                     _ptr(mask), int(want), vp, _ptr(nx), _ptr(ny), _ptr(nz),
+                                                     _ptr(curv)))
+
     def normals_chains_dev(self, lists_ctx, nx, ny, nz, curv, mask=None, want=1, viewpoint=(0.0, 0.0, 0.0)):
         """Phase 2 on this context's stream for the points with (mask != 0) == want (all if mask
         is None), from the lists held by `lists_ctx`."""

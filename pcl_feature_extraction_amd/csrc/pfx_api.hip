@@ -316,6 +316,29 @@ pfx_status pfx_normals_fast(pfx_ctx* ctx, const float* x, const float* y, const 
   PFX_API_END(ctx)
 }
 
+pfx_status pfx_normals_prepare_dev(pfx_ctx* ctx, const float* d_x, const float* d_y, const float* d_z, int64_t n,
+                                   double radius) {
+  PFX_API_BEGIN
+  check_ctx(ctx);
+  if (n < 0 || (n && (!d_x || !d_y || !d_z)))
+    throw Error(PFX_ERR_INVALID, "normals prepare: invalid arguments");
+  pfx::normals_prepare_dev(ctx, d_x, d_y, d_z, n, radius);
+  PFX_API_END(ctx)
+}
+
+pfx_status pfx_normals_subset_dev(pfx_ctx* ctx, const float* d_x, const float* d_y, const float* d_z, int64_t n,
+                                  double radius, const uint8_t* d_mask, int32_t want, const float viewpoint[3],
+                                  float* d_nx, float* d_ny, float* d_nz, float* d_curvature) {
+  PFX_API_BEGIN
+  check_ctx(ctx);
+  if (n < 0 || (n && (!d_x || !d_y || !d_z || !d_mask || !d_nx || !d_ny || !d_nz || !d_curvature)))
+    throw Error(PFX_ERR_INVALID, "normals subset: invalid arguments");
+  const float vp0[3] = {0.f, 0.f, 0.f};
+  pfx::normals_subset_dev(ctx, d_x, d_y, d_z, n, radius, d_mask, want, viewpoint ? viewpoint : vp0, d_nx, d_ny, d_nz,
+                          d_curvature);
+  PFX_API_END(ctx)
+}
+
 pfx_status pfx_normals_lists_dev(pfx_ctx* ctx, const float* d_x, const float* d_y, const float* d_z, int64_t n,
                                  double radius, float* d_nx, float* d_ny, float* d_nz, float* d_curvature) {
   PFX_API_BEGIN

@@ -202,6 +202,7 @@ void build_grid(pfx_ctx* ctx, Grid& g, const float* d_x, const float* d_y, const
     ctx->prep_nq = -1;
   }
   hipStream_t st = ctx->stream;
+  ++g.gen;
   g.n = n;
   g.ux = d_x; g.uy = d_y; g.uz = d_z;
   double lo[3] = {0, 0, 0}, hi[3] = {0, 0, 0};

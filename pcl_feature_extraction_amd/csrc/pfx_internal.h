@@ -84,11 +84,13 @@ struct Grid {
   bool have_hint = false;
   double hint_lo[3] = {0, 0, 0}, hint_hi[3] = {0, 0, 0};
   int* oob = nullptr;  // non-null iff the current build is speculative
+  uint64_t gen = 0;    // incremented by every build (consumers holding a grid check it)
   void release() {
     b_sx.release(); b_sy.release(); b_sz.release(); b_sp.release(); b_perm.release(); b_start.release();
     b_keys.release(); b_keys2.release(); b_vals.release(); b_tmp.release(); b_minmax.release(); b_oob.release();
     have_hint = false;
     oob = nullptr;
+    ++gen;
   }
 };
 
@@ -255,6 +257,10 @@ void normals_lists_dev(pfx_ctx* ctx, const float* x, const float* y, const float
 void normals_chains_dev(pfx_ctx* ctx, pfx_ctx* owner, const uint8_t* mask, int want, const float vp[3], float* nx,
                         float* ny, float* nz, float* curv);
 void normals_release(pfx_ctx* ctx);
+void normals_prepare_dev(pfx_ctx* ctx, const float* x, const float* y, const float* z, int64_t n, double r);
+void normals_subset_dev(pfx_ctx* ctx, const float* x, const float* y, const float* z, int64_t n, double r,
+                        const uint8_t* mask, int want, const float vp[3], float* nx, float* ny, float* nz,
+                        float* curv);
 // opt-in MFMA covariance (pfx_normals_fast.hip): not parity-exact
 void normals_fast_dev(pfx_ctx* ctx, const float* x, const float* y, const float* z, int64_t n, double r,
                       const float vp[3], float* nx, float* ny, float* nz, float* curv);

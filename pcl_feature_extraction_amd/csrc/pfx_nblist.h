@@ -52,14 +52,16 @@ struct NormalsState {
   const float *x = nullptr, *y = nullptr, *z = nullptr;  // the cloud and radius the lists belong to
   double r = 0.0;
   bool ready = false;
+  uint64_t grid_gen = 0;  // grid_a's build that indexes (x, y, z, n, r) (pfx_normals_prepare_dev)
 };
 
-// mask (nullable): per *caller* index, queries are the masked points (in cell order).
+// mask (nullable): per *caller* index, queries are the points with (mask != 0) == want (in cell
+// order).
 // defer: launch the list kernels and return without the host readback (out.nq = an upper bound,
 // out.nq_dev = the device count); consumers may be launched behind them in stream order, and
 // build_lists_check must follow.
 void build_lists(pfx_ctx* ctx, const Grid& g, const uint8_t* mask, double radius, bool sorted, NbLists& out,
-                 const char* tag, bool defer = false);
+                 const char* tag, bool defer = false, int want = 1);
 // The deferred build's readback: true and `out` completed (exact nq, statistics) when the lists are
 // valid; false when they must be rebuilt synchronously (list buffer too small, first very long
 // lists, or a speculative grid with points outside its bounds) -- their consumers rerun too.

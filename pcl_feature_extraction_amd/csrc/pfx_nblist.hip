@@ -91,9 +91,9 @@ __global__ void k_defer_gate(const int* __restrict__ counters, const unsigned lo
 }
 
 __global__ void k_mask_flags(const int32_t* __restrict__ perm, const uint32_t* __restrict__ skeys, int64_t n,
-                             uint64_t ncells, const uint8_t* __restrict__ mask, uint8_t* __restrict__ flags) {
+                             uint64_t ncells, const uint8_t* __restrict__ mask, int want, uint8_t* __restrict__ flags) {
   int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  if (i < n) flags[i] = ((uint64_t)skeys[i] < ncells) && mask[perm[i]];
+  if (i < n) flags[i] = ((uint64_t)skeys[i] < ncells) && ((mask[perm[i]] != 0) == (want != 0));
 }
 
 // segment (cell) start of each query position j, as (j if the cell changes at j else 0)
@@ -961,7 +961,7 @@ bool build_lists_check(pfx_ctx* ctx, const Grid& G, NbLists& out, const char* ta
 }
 
 void build_lists(pfx_ctx* ctx, const Grid& G, const uint8_t* mask, double radius, bool sorted, NbLists& out,
-                 const char* tag, bool defer) {
+                 const char* tag, bool defer, int want) {
   hipStream_t st = ctx->stream;
   const int64_t n = G.n;
   GridView g = view(G);
@@ -1003,7 +1003,7 @@ void build_lists(pfx_ctx* ctx, const Grid& G, const uint8_t* mask, double radius
     TimeScope ts(ctx, std::string(tag) + "_tiles");
     if (mask) {
       k_list_init<<<1, 256, 0, st>>>(nullptr, 0, nullptr, d_nq, counters, 14, cursor0);
-      k_mask_flags<<<nb, 256, 0, st>>>(G.perm, G.skeys, n, (uint64_t)G.ncells, mask, flags);
+      k_mask_flags<<<nb, 256, 0, st>>>(G.perm, G.skeys, n, (uint64_t)G.ncells, mask, want, flags);
       PFX_HIP(rocprim::select(tmp, t1, rocprim::counting_iterator<int32_t>(0), flags, qpos, d_nq, (size_t)n, st));
     } else {
       // every finite point, in cell order: sorted positions [0, cell_start[ncells])

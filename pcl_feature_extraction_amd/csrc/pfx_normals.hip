@@ -178,12 +178,17 @@ __device__ __forceinline__ void chain_wg(ChainLds<CAP>& S, const GridView& g, co
   uint32_t key = 0, prev = kEmpty;
   int k = 0;
   bool active = false;  // this pass computes the query (masked passes: mask[caller] == want)
+  bool sel = false;     // mask[caller] != 0
   if (valid) {
     p = L.qpos[j];
     key = L.skeys[p];
     k = L.cnt[j];
     if (tid > 0) prev = L.skeys[L.qpos[j - 1]];
-    active = !mask || ((mask[g.perm[p]] != 0) == (want != 0));
+    sel = mask && mask[g.perm[p]] != 0;
+    active = !mask || want >= 2 || (sel == ((want & 1) != 0));
+  }
+  if (want >= 2 && mask) {  // workgroup partition: all of a workgroup with any selected query
+    if ((__syncthreads_or(sel) != 0) != ((want & 1) != 0)) return;
   }
   if (!__syncthreads_or(active)) return;  // nothing of this pass in the workgroup
   // cell slots: first query of each distinct cell in the workgroup
@@ -428,12 +433,29 @@ __global__ void k_nan_fill4(float* __restrict__ a, float* __restrict__ b, float*
   }
 }
 
+// NaN (PCL's value for points without a normal) in the four outputs of the points with
+// (mask != 0) == want
+__global__ void k_nan_fill4_masked(float* __restrict__ a, float* __restrict__ b, float* __restrict__ c,
+                                   float* __restrict__ d, int64_t n, const uint8_t* __restrict__ mask, int want) {
+  const float v = __uint_as_float(0xffffffffu);
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    if ((mask[i] != 0) != (want != 0)) continue;
+    a[i] = v; b[i] = v; c[i] = v; d[i] = v;
+  }
+}
+
 // the lists longer than kLaneMax of this pass (mask[caller] == want), for k_normals_long
 __global__ void __launch_bounds__(256) k_long_lists(GridView g, NbLists L, const uint8_t* __restrict__ mask, int want,
                                                     int32_t* __restrict__ longq, int* __restrict__ n_long) {
   const int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   bool push = false;
-  if (j < nq_of(L) && L.cnt[j] > kLaneMax) push = !mask || ((mask[g.perm[L.qpos[j]]] != 0) == (want != 0));
+  if (want >= 2 && mask) {  // workgroup partition (blocks of 256 queries, as k_normals_chain's)
+    const bool sel = j < nq_of(L) && mask[g.perm[L.qpos[j]]] != 0;
+    const bool mine = (__syncthreads_or(sel) != 0) == ((want & 1) != 0);
+    push = mine && j < nq_of(L) && L.cnt[j] > kLaneMax;
+  } else if (j < nq_of(L) && L.cnt[j] > kLaneMax) {
+    push = !mask || ((mask[g.perm[L.qpos[j]]] != 0) == (want != 0));
+  }
   if (push) longq[wave_push_slot(n_long)] = (int32_t)j;
 }
 
@@ -762,6 +784,62 @@ void normals_dev(pfx_ctx* ctx, const float* x, const float* y, const float* z, i
   }
   normals_lists_dev(ctx, x, y, z, n, r, nx, ny, nz, curv);
   if (n > 0) normals_chains_dev(ctx, ctx, nullptr, 0, vp, nx, ny, nz, curv);
+}
+
+// The grid of a subset estimation built ahead (it needs only the coordinates): the normal-estimation
+// stream builds it while the subset mask is still being computed elsewhere.
+void normals_prepare_dev(pfx_ctx* ctx, const float* x, const float* y, const float* z, int64_t n, double r) {
+  PFX_CHECK(r > 0.0, "normals: radius must be > 0");
+  PFX_CHECK(n >= 0, "normals: negative point count");
+  if (!ctx->normals) ctx->normals = new NormalsState();
+  NormalsState& ns = *ctx->normals;
+  ns.ready = false;
+  ns.L = NbLists();
+  ns.n = n;
+  ns.x = x;
+  ns.y = y;
+  ns.z = z;
+  ns.r = r;
+  if (n == 0) return;
+  TimeScope ts(ctx, "normals_prepare", true);
+  build_grid(ctx, ctx->grid_a, x, y, z, n, r);
+  ns.grid_gen = ctx->grid_a.gen;
+}
+
+// Normal estimation of the points with (mask[i] != 0) == want only (PCL's values, bit for bit;
+// the other outputs are left untouched): lists of those points on the full cloud's grid, then
+// their chains.  Two calls with want = 1 and 0 give pfx_normals_dev's result, the first one's
+// points complete when its stream reaches the end of the call (FPFH's support first, so FPFH can
+// start while the rest is estimated).
+void normals_subset_dev(pfx_ctx* ctx, const float* x, const float* y, const float* z, int64_t n, double r,
+                        const uint8_t* mask, int want, const float vp[3], float* nx, float* ny, float* nz,
+                        float* curv) {
+  TimeScope total(ctx, "normals", true);
+  PFX_CHECK(r > 0.0, "normals: radius must be > 0");
+  PFX_CHECK(n >= 0, "normals: negative point count");
+  PFX_CHECK(mask != nullptr, "normals subset: null mask");
+  if (n == 0) return;
+  if (!ctx->normals) ctx->normals = new NormalsState();
+  NormalsState& ns = *ctx->normals;
+  const bool grid_ok = ns.grid_gen == ctx->grid_a.gen && ns.grid_gen != 0 && ns.x == x && ns.y == y && ns.z == z &&
+                       ns.n == n && ns.r == r;
+  if (!grid_ok) normals_prepare_dev(ctx, x, y, z, n, r);
+  ns.ready = false;
+  hipStream_t st = ctx->stream;
+  {
+    TimeScope phase(ctx, "normals_lists_phase", true);
+    k_nan_fill4_masked<<<(unsigned)std::min<int64_t>(ceil_div(n, 256), 4096), 256, 0, st>>>(nx, ny, nz, curv, n, mask,
+                                                                                           want);
+    check_launch("k_nan_fill4_masked");
+    build_lists(ctx, ctx->grid_a, mask, r, true, ns.L, "normals", /*defer=*/false, want);
+  }
+  ns.ready = true;
+  if (ns.L.nq > 0) normals_chains_dev(ctx, ctx, nullptr, 0, vp, nx, ny, nz, curv);
+  ns.ready = false;  // (the lists hold a subset: not the cloud's, nothing may reuse them)
+  ctx->stats["normals_queries"] = ns.L.nq;
+  ctx->stats["normals_neighbors"] = ns.L.total;
+  ctx->stats["normals_long_neighbors"] = ns.L.long_total;
+  ctx->stats["normals_long_queries"] = ns.L.long_nq;
 }
 
 }  // namespace pfx

@@ -80,10 +80,21 @@ class OverlappedNarfFpfh:
         self.pool = ThreadPoolExecutor(max_workers=1)
         # opt-in: the MFMA-covariance normals (pfx_normals_fast_dev), not parity-exact
         self.fast_normals = False
+        # FPFH's support first: normals of the points FPFH reads (pfx_fpfh_support_ball_dev), then
+        # FPFH on the main stream while the side stream estimates the rest (same results)
+        # (1: subset lists + chains, 2: every list, then the chains by workgroup partition)
+        self.support_first = int(os.environ.get("PFX_SUPPORT_FIRST", "0"))
+        # "support": with support_first = 1, estimate only the support's normals -- the step's
+        # outputs (keypoints, descriptors) are unchanged, as the normals are an intermediate of
+        # Features::compute (features.h:185-187); the other normal outputs are left unwritten
+        self.normals_scope = "all"
+        self._support = None
 
     def __call__(self, b: ScanBuffers, normal_radius: float = 0.05, feat_radius: float = 0.08, params=None,
                  cam=None):
         self.s_side.wait_stream(self.s_main)  # the scan was written on the main stream
+        if self.support_first and not self.fast_normals:
+            return self._support_first(b, normal_radius, feat_radius, params, cam)
         est = self.ctx_side.normals_fast_dev if self.fast_normals else self.ctx_side.normals_dev
         fut = self.pool.submit(est, b.x, b.y, b.z, normal_radius, b.nx, b.ny, b.nz, b.curv)
         try:
@@ -103,6 +114,75 @@ class OverlappedNarfFpfh:
         if k > 0:
             self.ctx.fpfh_dev(b.x, b.y, b.z, b.nx, b.ny, b.nz, b.kx[:k], b.ky[:k], b.kz[:k], feat_radius,
                               b.desc[:k])
+        return kp, k
+
+    def _support_first(self, b: ScanBuffers, normal_radius, feat_radius, params, cam):
+        """The normal estimation in two subsets (pfx_normals_subset_dev): the FPFH support -- every
+        point within 2 feat_radius of a keypoint, a superset of the normals FPFHEstimation reads --
+        as soon as NARF has found the keypoints, then the rest, concurrently with FPFH.  The side
+        stream builds the grid while NARF runs; both subsets finish inside the call."""
+        import threading
+        torch = self.torch
+        n = b.x.numel()
+        if self._support is None or self._support.numel() < n:
+            self._support = torch.empty(n, dtype=torch.uint8, device=b.x.device)
+        sup = self._support[:n]
+        mask_ready, sup_done = threading.Event(), threading.Event()
+        ev_mask, ev_sup = torch.cuda.Event(), torch.cuda.Event()
+        failed = []
+
+        cs = self.ctx_side
+        split = self.support_first == 2
+
+        def normals():
+            try:
+                if split:
+                    cs.normals_lists_dev(b.x, b.y, b.z, normal_radius, b.nx, b.ny, b.nz, b.curv)
+                else:
+                    cs.normals_prepare_dev(b.x, b.y, b.z, normal_radius)
+                mask_ready.wait()
+                if failed:
+                    return
+                self.s_side.wait_event(ev_mask)
+                if split:
+                    cs.normals_chains_dev(cs, b.nx, b.ny, b.nz, b.curv, mask=sup, want=3)
+                else:
+                    cs.normals_subset_dev(b.x, b.y, b.z, normal_radius, sup, 1, b.nx, b.ny, b.nz, b.curv)
+                ev_sup.record(self.s_side)
+            finally:
+                sup_done.set()
+            if split:
+                cs.normals_chains_dev(cs, b.nx, b.ny, b.nz, b.curv, mask=sup, want=2)
+            elif self.normals_scope != "support":
+                cs.normals_subset_dev(b.x, b.y, b.z, normal_radius, sup, 0, b.nx, b.ny, b.nz, b.curv)
+
+        fut = self.pool.submit(normals)
+        k = 0
+        try:
+            try:
+                kp = self.ctx.narf_keypoints_dev(b.x, b.y, b.z, params or narf_params(support_size=0.2),
+                                                 cam or camera())
+                k = self.ctx.gather_points_dev(b.x, b.y, b.z, kp, b.kx, b.ky, b.kz)
+                self.ctx.fpfh_prepare_dev(b.x, b.y, b.z, feat_radius)
+                if k > 0:
+                    self.ctx.fpfh_prepare_queries_dev(b.x, b.y, b.z, b.kx[:k], b.ky[:k], b.kz[:k], feat_radius)
+                    self.ctx.fpfh_support_ball_dev(b.x, b.y, b.z, b.kx[:k], b.ky[:k], b.kz[:k], feat_radius, sup)
+                else:
+                    sup.zero_()
+                ev_mask.record(self.s_main)
+            except BaseException:
+                failed.append(True)
+                raise
+            finally:
+                mask_ready.set()
+            sup_done.wait()
+            self.s_main.wait_event(ev_sup)
+            if k > 0:
+                self.ctx.fpfh_dev(b.x, b.y, b.z, b.nx, b.ny, b.nz, b.kx[:k], b.ky[:k], b.kz[:k], feat_radius,
+                                  b.desc[:k])
+        finally:
+            fut.result()
+        self.s_main.wait_stream(self.s_side)  # every normal belongs to the step
         return kp, k
 
     def check(self):

@@ -112,3 +112,67 @@ def test_support_ball_mask():
         expect[d2 <= lim] = 1
     assert np.array_equal(ball, expect)
     assert np.all(ball[exact == 1] == 1) and exact.sum() > 0
+
+
+def test_subset_normals_equal_full_estimation():
+    """pfx_normals_subset_dev with want = 1 then 0 (grid prepared ahead, a ragged random mask
+    incl. non-finite points) == pfx_normals_dev bit for bit; entries outside a subset untouched."""
+    import torch
+    from pcl_feature_extraction_amd import Context
+    from pcl_feature_extraction_amd.synth import synth_room
+    n = 120_000
+    x, y, z, _ = synth_room(n, 35)
+    x[::777] = np.nan
+    dev = torch.device("cuda", 0)
+    X, Y, Z = (torch.from_numpy(a).to(dev) for a in (x, y, z))
+    ref = [torch.empty(n, device=dev) for _ in range(4)]
+    out = [torch.full((n,), 5.0, device=dev) for _ in range(4)]
+    rng = np.random.default_rng(4)
+    m = (rng.random(n) < 0.3).astype(np.uint8)
+    M = torch.from_numpy(m).to(dev)
+    with Context(0) as a, Context(0) as b:
+        a.normals_dev(X, Y, Z, 0.05, *ref)
+        b.normals_prepare_dev(X, Y, Z, 0.05)
+        b.normals_subset_dev(X, Y, Z, 0.05, M, 1, *out)
+        b.synchronize()
+        half = out[0].cpu().numpy()
+        assert np.all(half[m == 0] == 5.0)  # untouched
+        b.normals_subset_dev(X, Y, Z, 0.05, M, 0, *out)
+        a.synchronize(); b.synchronize()
+    for r, o in zip(ref, out):
+        r, o = r.cpu().numpy(), o.cpu().numpy()
+        assert np.array_equal(np.nan_to_num(r, nan=7).view(np.uint32), np.nan_to_num(o, nan=7).view(np.uint32))
+
+
+@pytest.mark.parametrize("mode", [1, 2])
+def test_support_first_pass_matches_default(mode):
+    """OverlappedNarfFpfh with support_first (the support's normals -- subset lists and chains
+    (1), or every list then a workgroup-partitioned chain pass (2) -- then FPFH beside the rest)
+    gives the default schedule's keypoints, every normal and every descriptor bit for bit."""
+    import torch
+    from pcl_feature_extraction_amd import Context
+    from pcl_feature_extraction_amd.pipeline import OverlappedNarfFpfh, alloc
+    from pcl_feature_extraction_amd.synth import synth_room
+    n = 150_000
+    x, y, z, _ = synth_room(n, 22)
+    dev = torch.device("cuda", 0)
+    outs = []
+    for first in (0, mode):
+        b = alloc(torch, n, dev, max_keypoints=4096)
+        b.x.copy_(torch.from_numpy(x)); b.y.copy_(torch.from_numpy(y)); b.z.copy_(torch.from_numpy(z))
+        ctx, ctx_n = Context(0), Context(0)
+        ctx.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+        run = OverlappedNarfFpfh(torch, ctx, ctx_n, dev)
+        run.support_first = first
+        for _ in range(2):  # (the second pass reuses every buffer)
+            kp, k = run(b)
+        run.check()
+        run.close()
+        torch.cuda.synchronize(dev)
+        outs.append((np.asarray(kp), k, np.stack([t.cpu().numpy() for t in (b.nx, b.ny, b.nz, b.curv)]),
+                     b.desc[:k].cpu().numpy()))
+        ctx.close(); ctx_n.close()
+    (kp0, k0, n0, d0), (kp1, k1, n1, d1) = outs
+    assert np.array_equal(kp0, kp1) and k0 == k1 and k0 > 0
+    assert np.array_equal(np.nan_to_num(n0, nan=7).view(np.uint32), np.nan_to_num(n1, nan=7).view(np.uint32))
+    assert np.array_equal(np.nan_to_num(d0, nan=7).view(np.uint32), np.nan_to_num(d1, nan=7).view(np.uint32))
