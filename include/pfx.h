@@ -164,6 +164,18 @@ pfx_status pfx_normals_chains_dev(pfx_ctx* ctx, pfx_ctx* lists_ctx, const uint8_
                                   const float viewpoint[3], float* d_nx, float* d_ny, float* d_nz,
                                   float* d_curvature);
 
+/* pfx_normals_dev split at its one host round trip, so a consumer (FPFH) can be queued on another
+ * stream right behind the estimation: _launch queues grid, lists and chains with no host wait
+ * (the chains compute nothing unless the lists turn out whole); _finish validates them (host
+ * wait on ctx's stream) and, rarely -- a scan outside the previous scan's widened bounds, a list
+ * buffer to grow, the first very long lists -- reruns the exact path, stream-ordered on ctx's
+ * stream, and sets *rerun = 1: whatever read the outputs in between must then run again.
+ * Results after _finish are pfx_normals_dev's, bit for bit. */
+pfx_status pfx_normals_launch_dev(pfx_ctx* ctx, const float* d_x, const float* d_y, const float* d_z,
+                                  int64_t n, double radius, const float viewpoint[3], float* d_nx,
+                                  float* d_ny, float* d_nz, float* d_curvature);
+pfx_status pfx_normals_finish_dev(pfx_ctx* ctx, int32_t* rerun);
+
 /* NormalEstimationOMP (tools.h:22-32) over a subset of the cloud: the points with
  * (d_mask[i] != 0) == want get PCL's normal and curvature bit for bit (their neighbours are
  * searched in the whole cloud); every other output entry is left untouched.  Two calls, want = 1

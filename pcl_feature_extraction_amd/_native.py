@@ -101,6 +101,8 @@ _SIGS = {
     "pfx_fpfh_prepare_queries_dev": (c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp, c_i64, c_dbl]),
     "pfx_normals_lists_dev": (c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_dbl, c_vp, c_vp, c_vp, c_vp]),
     "pfx_normals_prepare_dev": (c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_dbl]),
+    "pfx_normals_launch_dev": (c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_dbl, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "pfx_normals_finish_dev": (c_int, [c_vp, c_vp]),
     "pfx_normals_subset_dev": (c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_dbl, c_vp, ctypes.c_int32, c_vp, c_vp, c_vp,
                                        c_vp, c_vp]),
     "pfx_normals_chains_dev": (c_int, [c_vp, c_vp, c_vp, ctypes.c_int32, c_vp, c_vp, c_vp, c_vp, c_vp]),

@@ -228,6 +228,20 @@ class Context:
         self._check(self._lib.pfx_normals_lists_dev(self.h, _ptr(x), _ptr(y), _ptr(z), x.numel(), float(r), _ptr(nx),
                                                     _ptr(ny), _ptr(nz), _ptr(curv)))
 
+    def normals_launch_dev(self, x, y, z, r, nx, ny, nz, curv, viewpoint=(0.0, 0.0, 0.0)):
+        """normals_dev with no host round trip (pfx_normals_launch_dev); normals_finish_dev must
+        follow before the outputs are trusted."""
+        vp = (ctypes.c_float * 3)(*viewpoint)
+        self._check(self._lib.pfx_normals_launch_dev(self.h, _ptr(x), _ptr(y), _ptr(z), x.numel(), float(r), vp,
+                                                     _ptr(nx), _ptr(ny), _ptr(nz), _ptr(curv)))
+
+    def normals_finish_dev(self) -> bool:
+        """Validates the launched estimation; True when it had to be rerun (consumers of its
+        outputs queued in between must run again)."""
+        rerun = ctypes.c_int32(0)
+        self._check(self._lib.pfx_normals_finish_dev(self.h, ctypes.byref(rerun)))
+        return bool(rerun.value)
+
     def normals_prepare_dev(self, x, y, z, r):
         """The grid of the next normals_subset_dev calls on this cloud, built ahead (coordinates only)."""
         self._check(self._lib.pfx_normals_prepare_dev(self.h, _ptr(x), _ptr(y), _ptr(z), x.numel(), float(r)))

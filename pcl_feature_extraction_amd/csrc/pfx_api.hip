@@ -316,6 +316,26 @@ pfx_status pfx_normals_fast(pfx_ctx* ctx, const float* x, const float* y, const 
   PFX_API_END(ctx)
 }
 
+pfx_status pfx_normals_launch_dev(pfx_ctx* ctx, const float* d_x, const float* d_y, const float* d_z, int64_t n,
+                                  double radius, const float viewpoint[3], float* d_nx, float* d_ny, float* d_nz,
+                                  float* d_curvature) {
+  PFX_API_BEGIN
+  check_ctx(ctx);
+  if (n < 0 || (n && (!d_x || !d_y || !d_z || !d_nx || !d_ny || !d_nz || !d_curvature)))
+    throw Error(PFX_ERR_INVALID, "normals: invalid arguments");
+  const float vp0[3] = {0.f, 0.f, 0.f};
+  pfx::normals_launch_dev(ctx, d_x, d_y, d_z, n, radius, viewpoint ? viewpoint : vp0, d_nx, d_ny, d_nz, d_curvature);
+  PFX_API_END(ctx)
+}
+
+pfx_status pfx_normals_finish_dev(pfx_ctx* ctx, int32_t* rerun) {
+  PFX_API_BEGIN
+  check_ctx(ctx);
+  const bool stood = pfx::normals_finish_dev(ctx);
+  if (rerun) *rerun = stood ? 0 : 1;
+  PFX_API_END(ctx)
+}
+
 pfx_status pfx_normals_prepare_dev(pfx_ctx* ctx, const float* d_x, const float* d_y, const float* d_z, int64_t n,
                                    double radius) {
   PFX_API_BEGIN

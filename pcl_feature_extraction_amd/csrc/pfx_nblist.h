@@ -53,6 +53,10 @@ struct NormalsState {
   double r = 0.0;
   bool ready = false;
   uint64_t grid_gen = 0;  // grid_a's build that indexes (x, y, z, n, r) (pfx_normals_prepare_dev)
+  // normals_launch_dev: the lists check still owed by normals_finish_dev, and the outputs to redo
+  bool pending = false;
+  float vp[3] = {0.f, 0.f, 0.f};
+  float *nx = nullptr, *ny = nullptr, *nz = nullptr, *curv = nullptr;
 };
 
 // mask (nullable): per *caller* index, queries are the points with (mask != 0) == want (in cell

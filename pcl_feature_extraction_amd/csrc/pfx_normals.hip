@@ -611,6 +611,7 @@ void normals_lists_dev(pfx_ctx* ctx, const float* x, const float* y, const float
   if (!ctx->normals) ctx->normals = new NormalsState();
   NormalsState& ns = *ctx->normals;
   ns.ready = false;
+  ns.pending = false;
   ns.n = n;
   ns.x = x;
   ns.y = y;
@@ -737,53 +738,114 @@ void normals_chains_dev(pfx_ctx* ctx, pfx_ctx* owner, const uint8_t* mask, int w
 // returns while they run and the caller's next stage (FPFH) is queued behind them; launching them
 // before the check (PFX_NORMALS_DEFER=1) leaves the host waiting on the chains instead: measured
 // 170.6 vs 171.9 Mpoints/s (the exact bounds readback path, PFX_NORMALS_SYNC=1, 171.9).
+namespace {
+bool env_flag(const char* name) {
+  const char* e = getenv(name);
+  return e && *e && *e != '0';
+}
+
+// grid on the hint, NaN fill, list kernels launched without their readback (the lists check
+// follows in the caller); false when the speculative form does not apply
+bool normals_speculative_lists(pfx_ctx* ctx, const float* x, const float* y, const float* z, int64_t n, double r,
+                               float* nx, float* ny, float* nz, float* curv) {
+  static const bool sync_path = env_flag("PFX_NORMALS_SYNC");  // A/B switch
+  if (n == 0 || sync_path) return false;
+  if (!ctx->normals) ctx->normals = new NormalsState();
+  NormalsState& ns = *ctx->normals;
+  ns.ready = false;
+  ns.pending = false;
+  ns.n = n;
+  ns.x = x;
+  ns.y = y;
+  ns.z = z;
+  ns.r = r;
+  ns.L = NbLists();
+  TimeScope phase(ctx, "normals_lists_phase", true);
+  build_grid(ctx, ctx->grid_a, x, y, z, n, r, /*use_hint=*/true);
+  k_nan_fill4<<<(unsigned)std::min<int64_t>(ceil_div(n, 256), 4096), 256, 0, ctx->stream>>>(nx, ny, nz, curv, n);
+  check_launch("k_nan_fill4");
+  build_lists(ctx, ctx->grid_a, nullptr, r, true, ns.L, "normals", /*defer=*/true);
+  return true;
+}
+
+// the lists check's verdict: statistics, or one exact rerun of lists and chains
+bool normals_conclude(pfx_ctx* ctx, bool ok, const float* x, const float* y, const float* z, int64_t n, double r,
+                      const float vp[3], float* nx, float* ny, float* nz, float* curv) {
+  NormalsState& ns = *ctx->normals;
+  ctx->grid_a.oob = nullptr;
+  ctx->stats["normals_speculative_reruns"] += ok ? 0 : 1;
+  if (ok) {
+    ctx->stats["normals_neighbors"] = ns.L.total;
+    ctx->stats["normals_long_neighbors"] = ns.L.long_total;
+    ctx->stats["normals_long_queries"] = ns.L.long_nq;
+    ctx->stats["normals_queries"] = ns.L.nq;
+    ctx->normals_fork_hint = ns.L.long_nq * 8 <= ns.L.nq;
+    return true;
+  }
+  normals_lists_dev(ctx, x, y, z, n, r, nx, ny, nz, curv);
+  normals_chains_dev(ctx, ctx, nullptr, 0, vp, nx, ny, nz, curv);
+  return false;
+}
+}  // namespace
+
+// The estimation with one host round trip: the grid on the previous call's widened bounds (no
+// bounds readback), then one readback validating the grid and the lists together before the
+// chains (a grid whose bounds missed a point, a list buffer that overflowed or the first very long
+// lists: the exact two-phase path reruns).  The chains are launched after the check so the host
+// returns while they run and the caller's next stage (FPFH) is queued behind them; launching them
+// before the check (PFX_NORMALS_DEFER=1) leaves the host waiting on the chains instead: measured
+// 170.6 vs 171.9 Mpoints/s (the exact bounds readback path, PFX_NORMALS_SYNC=1, 171.9).
+// normals_launch_dev + normals_finish_dev take the check off the caller's path altogether.
 void normals_dev(pfx_ctx* ctx, const float* x, const float* y, const float* z, int64_t n, double r,
                  const float vp[3], float* nx, float* ny, float* nz, float* curv) {
   TimeScope total(ctx, "normals", true);
   PFX_CHECK(r > 0.0, "normals: radius must be > 0");
   PFX_CHECK(n >= 0, "normals: negative point count");
-  auto flag = [](const char* name) {
-    const char* e = getenv(name);
-    return e && *e && *e != '0';
-  };
-  static const bool sync_path = flag("PFX_NORMALS_SYNC");   // A/B switches
-  static const bool defer_chains = flag("PFX_NORMALS_DEFER");
-  if (n > 0 && !sync_path) {
-    if (!ctx->normals) ctx->normals = new NormalsState();
+  static const bool defer_chains = env_flag("PFX_NORMALS_DEFER");  // A/B switch
+  if (normals_speculative_lists(ctx, x, y, z, n, r, nx, ny, nz, curv)) {
     NormalsState& ns = *ctx->normals;
-    ns.ready = false;
-    ns.n = n;
-    ns.x = x;
-    ns.y = y;
-    ns.z = z;
-    ns.r = r;
-    ns.L = NbLists();
-    hipStream_t st = ctx->stream;
-    {
-      TimeScope phase(ctx, "normals_lists_phase", true);
-      build_grid(ctx, ctx->grid_a, x, y, z, n, r, /*use_hint=*/true);
-      k_nan_fill4<<<(unsigned)std::min<int64_t>(ceil_div(n, 256), 4096), 256, 0, st>>>(nx, ny, nz, curv, n);
-      check_launch("k_nan_fill4");
-      build_lists(ctx, ctx->grid_a, nullptr, r, true, ns.L, "normals", /*defer=*/true);
-    }
     bool ok = true;
     if (!defer_chains) ok = build_lists_check(ctx, ctx->grid_a, ns.L, "normals");
     ns.ready = true;  // (the check below decides what stays when the chains go first)
     if (ok) normals_chains_dev(ctx, ctx, nullptr, 0, vp, nx, ny, nz, curv);
     if (defer_chains) ok = build_lists_check(ctx, ctx->grid_a, ns.L, "normals");
-    ctx->grid_a.oob = nullptr;
-    ctx->stats["normals_speculative_reruns"] += ok ? 0 : 1;
-    if (ok) {
-      ctx->stats["normals_neighbors"] = ns.L.total;
-      ctx->stats["normals_long_neighbors"] = ns.L.long_total;
-      ctx->stats["normals_long_queries"] = ns.L.long_nq;
-      ctx->stats["normals_queries"] = ns.L.nq;
-      ctx->normals_fork_hint = ns.L.long_nq * 8 <= ns.L.nq;
-      return;
-    }
+    normals_conclude(ctx, ok, x, y, z, n, r, vp, nx, ny, nz, curv);
+    return;
   }
   normals_lists_dev(ctx, x, y, z, n, r, nx, ny, nz, curv);
   if (n > 0) normals_chains_dev(ctx, ctx, nullptr, 0, vp, nx, ny, nz, curv);
+}
+
+// Launch half of a split estimation: grid, lists and chains are all queued with no host round
+// trip (the chains see a zero query count unless the lists are whole, k_defer_gate), so a
+// consumer can be queued behind them at once.  normals_finish_dev must follow before the outputs
+// are trusted: it validates and, rarely, reruns the exact path (the consumer then reruns too).
+void normals_launch_dev(pfx_ctx* ctx, const float* x, const float* y, const float* z, int64_t n, double r,
+                        const float vp[3], float* nx, float* ny, float* nz, float* curv) {
+  TimeScope total(ctx, "normals", true);
+  PFX_CHECK(r > 0.0, "normals: radius must be > 0");
+  PFX_CHECK(n >= 0, "normals: negative point count");
+  if (normals_speculative_lists(ctx, x, y, z, n, r, nx, ny, nz, curv)) {
+    NormalsState& ns = *ctx->normals;
+    ns.ready = true;
+    normals_chains_dev(ctx, ctx, nullptr, 0, vp, nx, ny, nz, curv);
+    ns.pending = true;
+    ns.vp[0] = vp[0]; ns.vp[1] = vp[1]; ns.vp[2] = vp[2];
+    ns.nx = nx; ns.ny = ny; ns.nz = nz; ns.curv = curv;
+    return;
+  }
+  normals_lists_dev(ctx, x, y, z, n, r, nx, ny, nz, curv);
+  if (n > 0) normals_chains_dev(ctx, ctx, nullptr, 0, vp, nx, ny, nz, curv);
+}
+
+// true when the launched estimation stood; false when it was rerun (exactly, stream-ordered on
+// ctx's stream: whatever consumed the outputs in between must run again)
+bool normals_finish_dev(pfx_ctx* ctx) {
+  NormalsState* ns = ctx->normals;
+  if (!ns || !ns->pending) return true;
+  ns->pending = false;
+  const bool ok = build_lists_check(ctx, ctx->grid_a, ns->L, "normals");
+  return normals_conclude(ctx, ok, ns->x, ns->y, ns->z, ns->n, ns->r, ns->vp, ns->nx, ns->ny, ns->nz, ns->curv);
 }
 
 // The grid of a subset estimation built ahead (it needs only the coordinates): the normal-estimation

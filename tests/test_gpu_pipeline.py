@@ -176,3 +176,44 @@ def test_support_first_pass_matches_default(mode):
     assert np.array_equal(kp0, kp1) and k0 == k1 and k0 > 0
     assert np.array_equal(np.nan_to_num(n0, nan=7).view(np.uint32), np.nan_to_num(n1, nan=7).view(np.uint32))
     assert np.array_equal(np.nan_to_num(d0, nan=7).view(np.uint32), np.nan_to_num(d1, nan=7).view(np.uint32))
+
+
+def test_split_check_pass_matches_default_with_reruns():
+    """OverlappedNarfFpfh with split_check (pfx_normals_launch_dev, FPFH queued behind it, then
+    pfx_normals_finish_dev): equal to the default schedule bit for bit on a sequence of scans
+    whose third one lies outside the second's widened bounds (the launched estimation is rerun
+    exactly and FPFH after it)."""
+    import torch
+    from pcl_feature_extraction_amd import Context
+    from pcl_feature_extraction_amd.pipeline import OverlappedNarfFpfh, alloc
+    from pcl_feature_extraction_amd.synth import synth_room
+    n = 150_000
+    x, y, z, _ = synth_room(n, 23)
+    x2, y2, z2, _ = synth_room(n, 24)
+    scans = [(x, y, z), (x2, y2, z2), (x2 + 5.0, y2, z2)]  # the third: a sensor moved by 5 m
+    dev = torch.device("cuda", 0)
+    res = {}
+    for split in (False, True):
+        b = alloc(torch, n, dev, max_keypoints=4096)
+        ctx, ctx_n = Context(0), Context(0)
+        ctx.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+        run = OverlappedNarfFpfh(torch, ctx, ctx_n, dev)
+        run.split_check = split
+        outs = []
+        for sx, sy, sz in scans:
+            for t, a in zip((b.x, b.y, b.z), (sx, sy, sz)):
+                t.copy_(torch.from_numpy(np.ascontiguousarray(a, np.float32)))
+            kp, k = run(b)
+            torch.cuda.synchronize(dev)
+            outs.append((np.asarray(kp), k, np.stack([t.cpu().numpy() for t in (b.nx, b.ny, b.nz, b.curv)]),
+                         b.desc[:k].cpu().numpy()))
+        run.check()
+        if split:
+            assert ctx_n.stat("normals_speculative_reruns") >= 1
+        run.close()
+        ctx.close(); ctx_n.close()
+        res[split] = outs
+    for (kp0, k0, n0, d0), (kp1, k1, n1, d1) in zip(res[False], res[True]):
+        assert np.array_equal(kp0, kp1) and k0 == k1
+        assert np.array_equal(np.nan_to_num(n0, nan=7).view(np.uint32), np.nan_to_num(n1, nan=7).view(np.uint32))
+        assert np.array_equal(np.nan_to_num(d0, nan=7).view(np.uint32), np.nan_to_num(d1, nan=7).view(np.uint32))
