@@ -118,14 +118,6 @@ __device__ __forceinline__ void shot_updates(f3 delta, double distance, double b
   vals[4] = (float)intWeight;
 }
 
-#ifdef PFX_SHOT_PROFILE
-__device__ unsigned long long g_shot_prof[8];
-#define PROF_T(v) long long v = (tid == 0) ? clock64() : 0
-#define PROF_ADD(i, a, b) if (tid == 0) atomicAdd(&g_shot_prof[i], (unsigned long long)((b) - (a)))
-#else
-#define PROF_T(v)
-#define PROF_ADD(i, a, b)
-#endif
 
 // the seven distinct LRF chains: cov (0,0) (0,1) (0,2) (1,1) (1,2) (2,2) and the weight sum
 constexpr int kChains = 7;
@@ -143,12 +135,346 @@ struct ShotLds {
   float hist[kLen];
   double cov[10];
   double axes[6];  // v1 (x axis), v3 (z axis)
+  int lrf_l[4];    // normalisation: per-wave smallest lsb exponent and largest square
+  float lrf_m[4];
   float rf[9];
   int n_invalid, zero_prefix, plusT, plusN, ok;
 };
 
-// CAP: LDS key capacity.  `list` (nullable): query subset with its device-side count; queries
-// with more than CAP neighbours go to `over` (or raise err when over == nullptr).
+// ---- the phases of one query, shared by the fused and the split kernels ----
+
+// A neighbour key's point: by caller index (the fused kernel) or, POS, by cell-sorted position --
+// the split kernels convert their keys once (ipos), after which every coordinate and normal of a
+// neighbourhood comes from a few contiguous runs (one float4 each) instead of six caller-order
+// gathers.
+template <bool POS>
+__device__ __forceinline__ float3 key_xyz(const GridView& g, int32_t p) {
+  if (POS) {
+    const float4 c = g.sp[p];
+    return make_float3(c.x, c.y, c.z);
+  }
+  return make_float3(g.ux[p], g.uy[p], g.uz[p]);
+}
+
+// SHOTLocalReferenceFrameEstimation's weighted double covariance over keys[0..k): S.cov (3x3
+// row-major + the weight sum at [9]), S.n_invalid (copies of the query), S.zero_prefix.
+// Every thread forms its neighbour's chain terms dist * (v_a * v_b) and dist exactly as the
+// reference loop does; lanes 0..6 then add them in neighbour order (the only sequential part).
+// An invalid neighbour (a copy of the query) contributes +0.0, which leaves a chain unchanged.
+template <bool POS, class Lds>
+__device__ __forceinline__ void shot_lrf(Lds& S, const GridView& g, const uint64_t* keys, int k, float cx,
+                                         float cy, float cz, double radius) {
+  const int tid = threadIdx.x;
+  if (tid == 0) {
+    S.n_invalid = 0; S.zero_prefix = 0; S.plusT = 0; S.plusN = 0;
+  }
+  double acc = 0.0;
+  for (int c0 = 0; c0 < k; c0 += kChunk) {
+    const int m = min(kChunk, k - c0);
+    __syncthreads();
+    if (tid < m) {
+      const uint64_t key = keys[c0 + tid];
+      const float3 c3 = key_xyz<POS>(g, key_idx(key));
+      const float px = c3.x, py = c3.y, pz = c3.z;
+      const bool valid = !(px == cx && py == cy && pz == cz);
+      const double vx = (double)(px - cx), vy = (double)(py - cy), vz = (double)(pz - cz);
+      const double dist = radius - sqrt((double)key_d2(key));
+      S.lrf[0][tid] = valid ? dist * (vx * vx) : 0.0;
+      S.lrf[1][tid] = valid ? dist * (vx * vy) : 0.0;
+      S.lrf[2][tid] = valid ? dist * (vx * vz) : 0.0;
+      S.lrf[3][tid] = valid ? dist * (vy * vy) : 0.0;
+      S.lrf[4][tid] = valid ? dist * (vy * vz) : 0.0;
+      S.lrf[5][tid] = valid ? dist * (vz * vz) : 0.0;
+      S.lrf[6][tid] = valid ? dist : 0.0;
+      if (!valid) atomicAdd(&S.n_invalid, 1);
+      if (key_d2(key) == 0.0f) atomicAdd(&S.zero_prefix, 1);
+    }
+    __syncthreads();
+    if (tid < kChains) {
+      const double* row = S.lrf[tid];
+      int t = 0;
+      for (; t + 8 <= m; t += 8) {
+        const double2 a = *reinterpret_cast<const double2*>(row + t);
+        const double2 b = *reinterpret_cast<const double2*>(row + t + 2);
+        const double2 c = *reinterpret_cast<const double2*>(row + t + 4);
+        const double2 e = *reinterpret_cast<const double2*>(row + t + 6);
+        acc = acc + a.x; acc = acc + a.y; acc = acc + b.x; acc = acc + b.y;
+        acc = acc + c.x; acc = acc + c.y; acc = acc + e.x; acc = acc + e.y;
+      }
+      for (; t < m; ++t) acc = acc + row[t];
+    }
+  }
+  __syncthreads();
+  if (tid < kChains) {  // chain -> cov[3a + b] (v_a v_b == v_b v_a exactly), cov[9] = weight sum
+    constexpr int kSlot[kChains][2] = {{0, 0}, {1, 3}, {2, 6}, {4, 4}, {5, 7}, {8, 8}, {9, 9}};
+    S.cov[kSlot[tid][0]] = acc;
+    S.cov[kSlot[tid][1]] = acc;
+  }
+  __syncthreads();
+}
+
+// `cov_m /= sum` (Eigen 3.2: times the reciprocal), SelfAdjointEigenSolver<Matrix3d>: axes = the
+// x (largest) and z (smallest) eigenvectors; false when the frame is undefined (PCL: NaN rows)
+__device__ __forceinline__ bool shot_eigen(const double cov[10], int valid, double axes[6]) {
+  if (valid < 5) return false;
+  double ev[3], V[3][3];
+  const double inv = 1.0 / cov[9];
+  eigen_selfadjoint3<true>(cov[0] * inv, cov[3] * inv, cov[4] * inv, cov[6] * inv, cov[7] * inv, cov[8] * inv, ev,
+                           V);
+  if (!(isfinite(ev[0]) && isfinite(ev[1]) && isfinite(ev[2]))) return false;
+  for (int i = 0; i < 3; ++i) { axes[i] = V[2][i]; axes[3 + i] = V[0][i]; }
+  return true;
+}
+
+// sign disambiguation of S.axes over the valid neighbours, then S.rf (x, y = z cross x, z)
+template <bool POS>
+__device__ __forceinline__ void shot_frame(ShotLds& S, const GridView& g, const uint64_t* keys, int k, int valid,
+                                           float cx, float cy, float cz) {
+  const int tid = threadIdx.x, lane = tid & 63;
+  {
+    const double v1x = S.axes[0], v1y = S.axes[1], v1z = S.axes[2];
+    const double v3x = S.axes[3], v3y = S.axes[4], v3z = S.axes[5];
+    int cT = 0, cN = 0;
+    for (int j = tid; j < k; j += 256) {
+      const float3 c3 = key_xyz<POS>(g, key_idx(keys[j]));
+      const float px = c3.x, py = c3.y, pz = c3.z;
+      if (px == cx && py == cy && pz == cz) continue;
+      const double vx = (double)(px - cx), vy = (double)(py - cy), vz = (double)(pz - cz);
+      if (((vx * v1x + vy * v1y) + vz * v1z) + 0.0 >= 0) ++cT;
+      if (((vx * v3x + vy * v3y) + vz * v3z) + 0.0 >= 0) ++cN;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) { cT += __shfl_xor(cT, o); cN += __shfl_xor(cN, o); }
+    if (lane == 0) { atomicAdd(&S.plusT, cT); atomicAdd(&S.plusN, cN); }
+  }
+  __syncthreads();
+  if (tid == 0) {
+    double ax[2][3] = {{S.axes[0], S.axes[1], S.axes[2]}, {S.axes[3], S.axes[4], S.axes[5]}};
+    const int counts[2] = {S.plusT, S.plusN};
+    // the valid neighbours in order: the d2 == 0 prefix holds every invalid one
+    const int zp = S.zero_prefix;
+    int valid_in_prefix = 0;
+    for (int j = 0; j < zp; ++j) {
+      const float3 c3 = key_xyz<POS>(g, key_idx(keys[j]));
+      if (!(c3.x == cx && c3.y == cy && c3.z == cz)) ++valid_in_prefix;
+    }
+    for (int w = 0; w < 2; ++w) {
+      int plus = 2 * counts[w] - valid;
+      if (plus == 0) {
+        const int median = valid / 2;
+        for (int i = -2; i <= 2; ++i) {
+          const int ne = median - i;
+          int j;
+          if (ne < valid_in_prefix) {
+            int seen = -1;
+            for (j = 0; j < zp; ++j) {
+              const float3 c3 = key_xyz<POS>(g, key_idx(keys[j]));
+              if (!(c3.x == cx && c3.y == cy && c3.z == cz) && ++seen == ne) break;
+            }
+          } else {
+            j = zp + (ne - valid_in_prefix);
+          }
+          const float3 c3 = key_xyz<POS>(g, key_idx(keys[j]));
+          const double vx = (double)(c3.x - cx), vy = (double)(c3.y - cy), vz = (double)(c3.z - cz);
+          if (((vx * ax[w][0] + vy * ax[w][1]) + vz * ax[w][2]) + 0.0 > 0) ++plus;
+        }
+        if (plus < 3)
+          for (int c = 0; c < 3; ++c) ax[w][c] *= -1;
+      } else if (plus < 0) {
+        for (int c = 0; c < 3; ++c) ax[w][c] *= -1;
+      }
+    }
+    const f3 x = mk3((float)ax[0][0], (float)ax[0][1], (float)ax[0][2]);
+    const f3 z = mk3((float)ax[1][0], (float)ax[1][1], (float)ax[1][2]);
+    const f3 y = cross3(z, x);
+    S.rf[0] = x.x; S.rf[1] = x.y; S.rf[2] = x.z;
+    S.rf[3] = y.x; S.rf[4] = y.y; S.rf[5] = y.z;
+    S.rf[6] = z.x; S.rf[7] = z.y; S.rf[8] = z.z;
+  }
+}
+
+// exponent of the least significant set bit of a finite nonzero float
+__device__ __forceinline__ int lsb_exp_f(float v) {
+  const uint32_t b = __float_as_uint(v);
+  const int e = (int)((b >> 23) & 0xff);
+  const uint32_t m = b & 0x7fffffu;
+  const uint32_t full = e ? (m | 0x800000u) : m;
+  return (e ? e : 1) - 150 + __builtin_ctz(full);
+}
+
+// the SHOT histogram from S.rf, normalizeHistogram, outputs
+// (POS: the normals come from snp, the cell-sorted float4 copy; else nx/ny/nz by caller index)
+template <bool POS>
+__device__ __forceinline__ void shot_hist(ShotLds& S, const GridView& g, const uint64_t* keys, int k, float cx,
+                                          float cy, float cz, const float* __restrict__ nx,
+                                          const float* __restrict__ ny, const float* __restrict__ nz,
+                                          const float4* __restrict__ snp, double radius, float* __restrict__ d,
+                                          float* __restrict__ rfo) {
+  const int tid = threadIdx.x, lane = tid & 63;
+  // Bin ownership for the histogram: thread j accumulates bins j and j + 256 in registers.
+  const int b0 = tid, b1 = tid + 256;
+  float h0 = 0.0f, h1 = 0.0f;
+  for (int i = tid; i < kLen; i += 256)
+    for (int w = 0; w < kMaskWords; ++w) S.upd.mask[i][w] = 0;
+  __syncthreads();
+  const f3 fx = mk3(S.rf[0], S.rf[1], S.rf[2]), fy = mk3(S.rf[3], S.rf[4], S.rf[5]),
+           fz = mk3(S.rf[6], S.rf[7], S.rf[8]);
+  // Each neighbour adds to at most one bin per update statement (its <= 5 bins are distinct),
+  // so PCL's sequential order restricted to one bin is neighbour order.  Per chunk: hit masks
+  // per bin -> counts -> offsets -> every update written to its bin's bucket at its rank among
+  // the bin's hits (a stable counting sort) -> each bin's owner adds its bucket in order.
+  for (int c0 = 0; c0 < k; c0 += kChunk) {
+    const int m = min(kChunk, k - c0);
+    int bins[5];
+    float vals[5];
+#pragma unroll
+    for (int s = 0; s < 5; ++s) bins[s] = -1;
+    if (tid < m) {
+      const uint64_t key = keys[c0 + tid];
+      const int32_t p = key_idx(key);
+      float pnx, pny, pnz;
+      if (POS) {
+        const float4 nv = snp[p];
+        pnx = nv.x; pny = nv.y; pnz = nv.z;
+      } else {
+        pnx = nx[p]; pny = ny[p]; pnz = nz[p];
+      }
+      const double distance = sqrt((double)key_d2(key));
+      if (isfinite(pnx) && isfinite(pny) && isfinite(pnz) && !(fabs(distance - 0.0) < 1E-15)) {
+        double cosd = dot4(mk3(pnx, pny, pnz), fz);
+        if (cosd > 1.0) cosd = 1.0;
+        if (cosd < -1.0) cosd = -1.0;
+        const double binDist = ((1.0 + cosd) * kBins) / 2;
+        const float3 c3 = key_xyz<POS>(g, p);
+        const f3 delta = mk3(c3.x - cx, c3.y - cy, c3.z - cz);
+        shot_updates(delta, distance, binDist, fx, fy, fz, radius, bins, vals);
+      }
+      const uint64_t bit = 1ull << (tid & 63);
+#pragma unroll
+      for (int s = 0; s < 5; ++s)
+        if (bins[s] >= 0) atomicOr(reinterpret_cast<unsigned long long*>(&S.upd.mask[bins[s]][tid >> 6]), bit);
+    }
+    __syncthreads();
+    // hit counts -> exclusive offsets (wave 0: 6 bins per lane, then a wave scan)
+    if (tid < 64) {
+      int c[6], tot = 0;
+#pragma unroll
+      for (int i = 0; i < 6; ++i) {
+        const int bb = tid * 6 + i;
+        c[i] = 0;
+        if (bb < kLen)
+          for (int w = 0; w < kMaskWords; ++w) c[i] += __popcll(S.upd.mask[bb][w]);
+        tot += c[i];
+      }
+      int incl = tot;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(incl, o);
+        if (lane >= o) incl += y;
+      }
+      int run = incl - tot;
+#pragma unroll
+      for (int i = 0; i < 6; ++i) {
+        const int bb = tid * 6 + i;
+        if (bb < kLen) S.upd.off[bb] = run;
+        run += c[i];
+      }
+    }
+    __syncthreads();
+    if (tid < m) {  // scatter: rank = hits of the bin from lower neighbours of the chunk
+      const int wq = tid >> 6;
+      const uint64_t below = lanemask_lt();
+#pragma unroll
+      for (int s = 0; s < 5; ++s) {
+        const int bb = bins[s];
+        if (bb < 0) continue;
+        int r = __popcll(S.upd.mask[bb][wq] & below);
+        for (int w = 0; w < wq; ++w) r += __popcll(S.upd.mask[bb][w]);
+        S.upd.val[S.upd.off[bb] + r] = vals[s];
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int o = 0; o < 2; ++o) {
+      const int b = o ? b1 : b0;
+      if (b < kLen) {
+        int cnt = 0;
+        for (int w = 0; w < kMaskWords; ++w) {
+          cnt += __popcll(S.upd.mask[b][w]);
+          S.upd.mask[b][w] = 0;  // ready for the next chunk
+        }
+        const float* v = S.upd.val + S.upd.off[b];
+        float h = o ? h1 : h0;
+        int i = 0;
+        for (; i + 4 <= cnt; i += 4) {
+          const float a0 = v[i], a1 = v[i + 1], a2 = v[i + 2], a3 = v[i + 3];
+          h = h + a0; h = h + a1; h = h + a2; h = h + a3;
+        }
+        for (; i < cnt; ++i) h = h + v[i];
+        if (o) h1 = h; else h0 = h;
+      }
+    }
+    __syncthreads();
+  }
+  S.hist[b0] = h0;
+  if (b1 < kLen) S.hist[b1] = h1;
+  __syncthreads();
+  // normalizeHistogram: acc_norm += shot[j] * shot[j] (float squares, double sum, in bin order).
+  // The squares are multiples of 2^L (L the smallest least-significant-bit exponent among the
+  // nonzero ones) and non-negative, so when 352 x the largest stays below 2^(L + 53) every
+  // partial sum is exact and any order gives PCL's value: a parallel sum; otherwise one lane
+  // runs the sequential loop.
+  {
+    float sq[2] = {h0 * h0, b1 < kLen ? h1 * h1 : 0.0f};
+    double part = (double)sq[0] + (double)sq[1];
+    float mx = fmaxf(sq[0], sq[1]);
+    int L = 1 << 20;
+    for (int o = 0; o < 2; ++o)
+      if (sq[o] != 0.0f && isfinite(sq[o])) L = min(L, lsb_exp_f(sq[o]));
+      else if (!(sq[o] == 0.0f)) L = -(1 << 20);  // non-finite: the sequential loop decides
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      part += __shfl_xor(part, o);
+      mx = fmaxf(mx, __shfl_xor(mx, o));
+      L = min(L, __shfl_xor(L, o));
+    }
+    if (lane == 0) {
+      S.axes[tid >> 6] = part;  // (axes are dead here: four wave partials)
+      S.lrf_l[tid >> 6] = L;
+      S.lrf_m[tid >> 6] = mx;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      const double tot = (S.axes[0] + S.axes[1]) + (S.axes[2] + S.axes[3]);
+      const int Lm = min(min(S.lrf_l[0], S.lrf_l[1]), min(S.lrf_l[2], S.lrf_l[3]));
+      const float mm = fmaxf(fmaxf(S.lrf_m[0], S.lrf_m[1]), fmaxf(S.lrf_m[2], S.lrf_m[3]));
+      double acc_norm;
+      if (mm == 0.0f) {
+        acc_norm = 0.0;
+      } else if (Lm > -(1 << 19) && (double)mm * kLen < ldexp(1.0, Lm + 53)) {
+        acc_norm = tot;
+      } else {
+        acc_norm = 0;
+        for (int j = 0; j < kLen; ++j) acc_norm += S.hist[j] * S.hist[j];
+      }
+      S.cov[0] = sqrt(acc_norm);
+    }
+    __syncthreads();
+  }
+  const float nrm = (float)S.cov[0];
+  for (int i = tid; i < kLen; i += 256) d[i] = S.hist[i] / nrm;
+  if (tid < 9) rfo[tid] = S.rf[tid];
+  __syncthreads();
+}
+
+__device__ __forceinline__ void shot_nan(float* __restrict__ d, float* __restrict__ rfo) {
+  for (int i = threadIdx.x; i < kLen; i += 256) d[i] = __builtin_nanf("");
+  if (threadIdx.x < 9) rfo[threadIdx.x] = __builtin_nanf("");
+}
+
+// Fused form (the lists longer than the split path's capacity): every phase of a query in one
+// workgroup.  CAP: LDS key capacity.  `list` (nullable): query subset with its device-side
+// count; queries with more than CAP neighbours go to `over` (or raise err when over == nullptr).
 template <int CAP>
 __global__ void __launch_bounds__(256) k_shot(GridView g, const float* __restrict__ nx,
                                               const float* __restrict__ ny, const float* __restrict__ nz,
@@ -162,7 +488,7 @@ __global__ void __launch_bounds__(256) k_shot(GridView g, const float* __restric
   __shared__ ShotLds S;
   __shared__ BucketLds SB;
   __shared__ int s_count;
-  const int tid = threadIdx.x, lane = tid & 63;
+  const int tid = threadIdx.x;
   const float rr = (float)(radius * radius);
   const int64_t count = list ? (int64_t)*n_list : nq;
   for (int64_t w = blockIdx.x; w < count; w += gridDim.x) {
@@ -171,16 +497,12 @@ __global__ void __launch_bounds__(256) k_shot(GridView g, const float* __restric
     float* rfo = rf_out + q * 9;
     const float cx = qx[q], cy = qy[q], cz = qz[q];
     if (!(isfinite(cx) && isfinite(cy) && isfinite(cz))) {
-      for (int i = tid; i < kLen; i += 256) d[i] = __builtin_nanf("");
-      if (tid < 9) rfo[tid] = __builtin_nanf("");
+      shot_nan(d, rfo);
       continue;
     }
-    PROF_T(t0);
     const int k = CAP == kCapSmall
                       ? sorted_neighbors_bucketed(g, cx, cy, cz, rr, keys, keys + CAP, CAP, &s_count, SB)
                       : sorted_neighbors(g, cx, cy, cz, rr, keys, CAP, &s_count);
-    PROF_T(t1);
-    PROF_ADD(0, t0, t1);
     if (k > CAP) {
       if (tid == 0) {
         if (over) over[atomicAdd(n_over, 1)] = (int32_t)q;
@@ -188,263 +510,151 @@ __global__ void __launch_bounds__(256) k_shot(GridView g, const float* __restric
       }
       continue;
     }
-    if (tid == 0) {
-      S.n_invalid = 0; S.zero_prefix = 0; S.plusT = 0; S.plusN = 0;
-      atomicAdd(nbr, (unsigned long long)k);
-    }
-    // ---- local reference frame: ordered double covariance ----
-    // Every thread forms its neighbour's chain terms dist * (v_a * v_b) and dist exactly as the
-    // reference loop does; lanes 0..6 then add them in neighbour order (the only sequential part).
-    // An invalid neighbour (a copy of the query) contributes +0.0, which leaves a chain unchanged.
-    double acc = 0.0;
-    for (int c0 = 0; c0 < k; c0 += kChunk) {
-      const int m = min(kChunk, k - c0);
-      __syncthreads();
-      if (tid < m) {
-        const uint64_t key = keys[c0 + tid];
-        const int32_t p = key_idx(key);
-        const float px = g.ux[p], py = g.uy[p], pz = g.uz[p];
-        const bool valid = !(px == cx && py == cy && pz == cz);
-        const double vx = (double)(px - cx), vy = (double)(py - cy), vz = (double)(pz - cz);
-        const double dist = radius - sqrt((double)key_d2(key));
-        S.lrf[0][tid] = valid ? dist * (vx * vx) : 0.0;
-        S.lrf[1][tid] = valid ? dist * (vx * vy) : 0.0;
-        S.lrf[2][tid] = valid ? dist * (vx * vz) : 0.0;
-        S.lrf[3][tid] = valid ? dist * (vy * vy) : 0.0;
-        S.lrf[4][tid] = valid ? dist * (vy * vz) : 0.0;
-        S.lrf[5][tid] = valid ? dist * (vz * vz) : 0.0;
-        S.lrf[6][tid] = valid ? dist : 0.0;
-        if (!valid) atomicAdd(&S.n_invalid, 1);
-        if (key_d2(key) == 0.0f) atomicAdd(&S.zero_prefix, 1);
-      }
-      __syncthreads();
-      if (tid < kChains) {
-        const double* row = S.lrf[tid];
-        int t = 0;
-        for (; t + 8 <= m; t += 8) {
-          const double2 a = *reinterpret_cast<const double2*>(row + t);
-          const double2 b = *reinterpret_cast<const double2*>(row + t + 2);
-          const double2 c = *reinterpret_cast<const double2*>(row + t + 4);
-          const double2 e = *reinterpret_cast<const double2*>(row + t + 6);
-          acc = acc + a.x; acc = acc + a.y; acc = acc + b.x; acc = acc + b.y;
-          acc = acc + c.x; acc = acc + c.y; acc = acc + e.x; acc = acc + e.y;
-        }
-        for (; t < m; ++t) acc = acc + row[t];
-      }
-    }
-    __syncthreads();
-    if (tid < kChains) {  // chain -> cov[3a + b] (v_a v_b == v_b v_a exactly), cov[9] = weight sum
-      constexpr int kSlot[kChains][2] = {{0, 0}, {1, 3}, {2, 6}, {4, 4}, {5, 7}, {8, 8}, {9, 9}};
-      S.cov[kSlot[tid][0]] = acc;
-      S.cov[kSlot[tid][1]] = acc;
-    }
-    __syncthreads();
-    PROF_T(t2);
-    PROF_ADD(1, t1, t2);
+    if (tid == 0) atomicAdd(nbr, (unsigned long long)k);
+    shot_lrf<false>(S, g, keys, k, cx, cy, cz, radius);
     const int valid = k - S.n_invalid;
     if (tid == 0) {
-      S.ok = 0;
-      if (valid >= 5) {
-        // `cov_m /= sum` (Eigen 3.2: times the reciprocal), SelfAdjointEigenSolver<Matrix3d>
-        double ev[3], V[3][3];
-        const double inv = 1.0 / S.cov[9];
-        eigen_selfadjoint3<true>(S.cov[0] * inv, S.cov[3] * inv, S.cov[4] * inv, S.cov[6] * inv, S.cov[7] * inv,
-                                 S.cov[8] * inv, ev, V);
-        if (isfinite(ev[0]) && isfinite(ev[1]) && isfinite(ev[2])) {
-          S.ok = 1;
-          for (int i = 0; i < 3; ++i) { S.axes[i] = V[2][i]; S.axes[3 + i] = V[0][i]; }
-        }
-      }
+      double cov[10], axes[6];
+      for (int i = 0; i < 10; ++i) cov[i] = S.cov[i];
+      S.ok = shot_eigen(cov, valid, axes) ? 1 : 0;
+      for (int i = 0; i < 6; ++i) S.axes[i] = axes[i];
     }
     __syncthreads();
     if (!S.ok) {
-      for (int i = tid; i < kLen; i += 256) d[i] = __builtin_nanf("");
-      if (tid < 9) rfo[tid] = __builtin_nanf("");
+      shot_nan(d, rfo);
       continue;
     }
-    // sign disambiguation: counts of non-negative projections over the valid neighbours
-    {
-      const double v1x = S.axes[0], v1y = S.axes[1], v1z = S.axes[2];
-      const double v3x = S.axes[3], v3y = S.axes[4], v3z = S.axes[5];
-      int cT = 0, cN = 0;
-      for (int j = tid; j < k; j += 256) {
-        const int32_t p = key_idx(keys[j]);
-        const float px = g.ux[p], py = g.uy[p], pz = g.uz[p];
-        if (px == cx && py == cy && pz == cz) continue;
-        const double vx = (double)(px - cx), vy = (double)(py - cy), vz = (double)(pz - cz);
-        if (((vx * v1x + vy * v1y) + vz * v1z) + 0.0 >= 0) ++cT;
-        if (((vx * v3x + vy * v3y) + vz * v3z) + 0.0 >= 0) ++cN;
+    shot_frame<false>(S, g, keys, k, valid, cx, cy, cz);
+    shot_hist<false>(S, g, keys, k, cx, cy, cz, nx, ny, nz, nullptr, radius, d, rfo);
+  }
+}
+
+// the split kernels' views of the surface: caller index -> cell-sorted position, and the normals
+// in cell order
+__global__ void k_shot_prep(const int32_t* __restrict__ perm, int64_t n, const float* __restrict__ nx,
+                            const float* __restrict__ ny, const float* __restrict__ nz, int32_t* __restrict__ ipos,
+                            float4* __restrict__ snp) {
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int32_t p = perm[i];
+  ipos[p] = (int32_t)i;
+  snp[i] = make_float4(nx[p], ny[p], nz[p], 0.0f);
+}
+
+// ---- split form: the single-lane eigen solve off the workgroups' critical path ----
+// Per query state between the three kernels.  status: 0 frame pending / defined, 1 done (NaN
+// written: non-finite query or no frame), 2 over the split capacity (the fused kernel's).
+struct ShotQuery {
+  double cov[10];
+  double axes[6];
+  int k, n_invalid, zero_prefix, status;
+};
+
+// the LDS of the LRF phase alone (kernel A: three workgroups per CU beside the sort's keys)
+struct LrfLds {
+  double lrf[kChains][kChunk];
+  double cov[10];
+  int n_invalid, zero_prefix, plusT, plusN;
+};
+
+// A: sort + LRF covariance, keys kept in global memory (stride kCapSmall)
+__global__ void __launch_bounds__(256) k_shot_lrf(GridView g, const float* __restrict__ qx,
+                                                  const float* __restrict__ qy, const float* __restrict__ qz,
+                                                  int64_t base, int64_t nq, int32_t* __restrict__ over,
+                                                  int* __restrict__ n_over,
+                                                  double radius, float* __restrict__ desc, float* __restrict__ rf_out,
+                                                  uint64_t* __restrict__ gkeys, ShotQuery* __restrict__ sq,
+                                                  const int32_t* __restrict__ ipos,
+                                                  unsigned long long* __restrict__ nbr) {
+  extern __shared__ __attribute__((aligned(16))) uint64_t keys[];  // kCapSmall + kCapSmall scratch
+  __shared__ LrfLds S;
+  __shared__ BucketLds SB;
+  __shared__ int s_count;
+  const int tid = threadIdx.x;
+  const float rr = (float)(radius * radius);
+  for (int64_t l = blockIdx.x; l < nq; l += gridDim.x) {  // l: index in the batch, q: caller's
+    const int64_t q = base + l;
+    const float cx = qx[q], cy = qy[q], cz = qz[q];
+    if (!(isfinite(cx) && isfinite(cy) && isfinite(cz))) {
+      shot_nan(desc + q * kLen, rf_out + q * 9);
+      if (tid == 0) sq[l].status = 1;
+      continue;
+    }
+    const int k = sorted_neighbors_bucketed(g, cx, cy, cz, rr, keys, keys + kCapSmall, kCapSmall, &s_count, SB);
+    if (k > kCapSmall) {
+      if (tid == 0) {
+        over[atomicAdd(n_over, 1)] = (int32_t)q;
+        sq[l].status = 2;
       }
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) { cT += __shfl_xor(cT, o); cN += __shfl_xor(cN, o); }
-      if (lane == 0) { atomicAdd(&S.plusT, cT); atomicAdd(&S.plusN, cN); }
+      continue;
+    }
+    if (tid == 0) atomicAdd(nbr, (unsigned long long)k);
+    // keys (d2, caller index) in FLANN order -> (d2, cell-sorted position), same order
+    uint64_t* gk = gkeys + l * kCapSmall;
+    for (int i = tid; i < k; i += 256) {
+      const uint64_t key = keys[i];
+      const uint64_t pk = (key & 0xffffffff00000000ull) | (uint32_t)ipos[key_idx(key)];
+      keys[i] = pk;
+      gk[i] = pk;
     }
     __syncthreads();
+    shot_lrf<true>(S, g, keys, k, cx, cy, cz, radius);
+    if (tid < 10) sq[l].cov[tid] = S.cov[tid];
     if (tid == 0) {
-      double ax[2][3] = {{S.axes[0], S.axes[1], S.axes[2]}, {S.axes[3], S.axes[4], S.axes[5]}};
-      const int counts[2] = {S.plusT, S.plusN};
-      // the valid neighbours in order: the d2 == 0 prefix holds every invalid one
-      const int zp = S.zero_prefix;
-      int valid_in_prefix = 0;
-      for (int j = 0; j < zp; ++j) {
-        const int32_t p = key_idx(keys[j]);
-        if (!(g.ux[p] == cx && g.uy[p] == cy && g.uz[p] == cz)) ++valid_in_prefix;
-      }
-      for (int w = 0; w < 2; ++w) {
-        int plus = 2 * counts[w] - valid;
-        if (plus == 0) {
-          const int median = valid / 2;
-          for (int i = -2; i <= 2; ++i) {
-            const int ne = median - i;
-            int j;
-            if (ne < valid_in_prefix) {
-              int seen = -1;
-              for (j = 0; j < zp; ++j) {
-                const int32_t p = key_idx(keys[j]);
-                if (!(g.ux[p] == cx && g.uy[p] == cy && g.uz[p] == cz) && ++seen == ne) break;
-              }
-            } else {
-              j = zp + (ne - valid_in_prefix);
-            }
-            const int32_t p = key_idx(keys[j]);
-            const double vx = (double)(g.ux[p] - cx), vy = (double)(g.uy[p] - cy), vz = (double)(g.uz[p] - cz);
-            if (((vx * ax[w][0] + vy * ax[w][1]) + vz * ax[w][2]) + 0.0 > 0) ++plus;
-          }
-          if (plus < 3)
-            for (int c = 0; c < 3; ++c) ax[w][c] *= -1;
-        } else if (plus < 0) {
-          for (int c = 0; c < 3; ++c) ax[w][c] *= -1;
-        }
-      }
-      const f3 x = mk3((float)ax[0][0], (float)ax[0][1], (float)ax[0][2]);
-      const f3 z = mk3((float)ax[1][0], (float)ax[1][1], (float)ax[1][2]);
-      const f3 y = cross3(z, x);
-      S.rf[0] = x.x; S.rf[1] = x.y; S.rf[2] = x.z;
-      S.rf[3] = y.x; S.rf[4] = y.y; S.rf[5] = y.z;
-      S.rf[6] = z.x; S.rf[7] = z.y; S.rf[8] = z.z;
-    }
-    // Bin ownership for the histogram: thread j accumulates bins j and j + 256 in registers.
-    const int b0 = tid, b1 = tid + 256;
-    float h0 = 0.0f, h1 = 0.0f;
-    for (int i = tid; i < kLen; i += 256)
-      for (int w = 0; w < kMaskWords; ++w) S.upd.mask[i][w] = 0;
-    __syncthreads();
-    PROF_T(t3);
-    PROF_ADD(2, t2, t3);
-    const f3 fx = mk3(S.rf[0], S.rf[1], S.rf[2]), fy = mk3(S.rf[3], S.rf[4], S.rf[5]),
-             fz = mk3(S.rf[6], S.rf[7], S.rf[8]);
-    // ---- SHOT histogram ----
-    // Each neighbour adds to at most one bin per update statement (its <= 5 bins are distinct),
-    // so PCL's sequential order restricted to one bin is neighbour order.  Per chunk: hit masks
-    // per bin -> counts -> offsets -> every update written to its bin's bucket at its rank among
-    // the bin's hits (a stable counting sort) -> each bin's owner adds its bucket in order.
-    for (int c0 = 0; c0 < k; c0 += kChunk) {
-      const int m = min(kChunk, k - c0);
-      PROF_T(t4);
-      int bins[5];
-      float vals[5];
-#pragma unroll
-      for (int s = 0; s < 5; ++s) bins[s] = -1;
-      if (tid < m) {
-        const uint64_t key = keys[c0 + tid];
-        const int32_t p = key_idx(key);
-        const float pnx = nx[p], pny = ny[p], pnz = nz[p];
-        const double distance = sqrt((double)key_d2(key));
-        if (isfinite(pnx) && isfinite(pny) && isfinite(pnz) && !(fabs(distance - 0.0) < 1E-15)) {
-          double cosd = dot4(mk3(pnx, pny, pnz), fz);
-          if (cosd > 1.0) cosd = 1.0;
-          if (cosd < -1.0) cosd = -1.0;
-          const double binDist = ((1.0 + cosd) * kBins) / 2;
-          const f3 delta = mk3(g.ux[p] - cx, g.uy[p] - cy, g.uz[p] - cz);
-          shot_updates(delta, distance, binDist, fx, fy, fz, radius, bins, vals);
-        }
-        const uint64_t bit = 1ull << (tid & 63);
-#pragma unroll
-        for (int s = 0; s < 5; ++s)
-          if (bins[s] >= 0) atomicOr(reinterpret_cast<unsigned long long*>(&S.upd.mask[bins[s]][tid >> 6]), bit);
-      }
-      __syncthreads();
-      PROF_T(t5);
-      PROF_ADD(3, t4, t5);
-      // hit counts -> exclusive offsets (wave 0: 6 bins per lane, then a wave scan)
-      if (tid < 64) {
-        int c[6], tot = 0;
-#pragma unroll
-        for (int i = 0; i < 6; ++i) {
-          const int bb = tid * 6 + i;
-          c[i] = 0;
-          if (bb < kLen)
-            for (int w = 0; w < kMaskWords; ++w) c[i] += __popcll(S.upd.mask[bb][w]);
-          tot += c[i];
-        }
-        int incl = tot;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-          const int y = __shfl_up(incl, o);
-          if (lane >= o) incl += y;
-        }
-        int run = incl - tot;
-#pragma unroll
-        for (int i = 0; i < 6; ++i) {
-          const int bb = tid * 6 + i;
-          if (bb < kLen) S.upd.off[bb] = run;
-          run += c[i];
-        }
-      }
-      __syncthreads();
-      if (tid < m) {  // scatter: rank = hits of the bin from lower neighbours of the chunk
-        const int wq = tid >> 6;
-        const uint64_t below = lanemask_lt();
-#pragma unroll
-        for (int s = 0; s < 5; ++s) {
-          const int bb = bins[s];
-          if (bb < 0) continue;
-          int r = __popcll(S.upd.mask[bb][wq] & below);
-          for (int w = 0; w < wq; ++w) r += __popcll(S.upd.mask[bb][w]);
-          S.upd.val[S.upd.off[bb] + r] = vals[s];
-        }
-      }
-      __syncthreads();
-#pragma unroll
-      for (int o = 0; o < 2; ++o) {
-        const int b = o ? b1 : b0;
-        if (b < kLen) {
-          int cnt = 0;
-          for (int w = 0; w < kMaskWords; ++w) {
-            cnt += __popcll(S.upd.mask[b][w]);
-            S.upd.mask[b][w] = 0;  // ready for the next chunk
-          }
-          const float* v = S.upd.val + S.upd.off[b];
-          float h = o ? h1 : h0;
-          int i = 0;
-          for (; i + 4 <= cnt; i += 4) {
-            const float a0 = v[i], a1 = v[i + 1], a2 = v[i + 2], a3 = v[i + 3];
-            h = h + a0; h = h + a1; h = h + a2; h = h + a3;
-          }
-          for (; i < cnt; ++i) h = h + v[i];
-          if (o) h1 = h; else h0 = h;
-        }
-      }
-      __syncthreads();
-      PROF_T(t6);
-      PROF_ADD(4, t5, t6);
-    }
-    S.hist[b0] = h0;
-    if (b1 < kLen) S.hist[b1] = h1;
-    __syncthreads();
-    PROF_T(t7);
-    if (tid == 0) {  // normalizeHistogram
-      double acc_norm = 0;
-      for (int j = 0; j < kLen; ++j) acc_norm += S.hist[j] * S.hist[j];
-      S.cov[0] = sqrt(acc_norm);
+      sq[l].k = k;
+      sq[l].n_invalid = S.n_invalid;
+      sq[l].zero_prefix = S.zero_prefix;
+      sq[l].status = 0;
     }
     __syncthreads();
-    const float nrm = (float)S.cov[0];
-    for (int i = tid; i < kLen; i += 256) d[i] = S.hist[i] / nrm;
-    if (tid < 9) rfo[tid] = S.rf[tid];
+  }
+}
+
+// B: one lane per query, SelfAdjointEigenSolver<Matrix3d>
+__global__ void __launch_bounds__(64) k_shot_eigen(ShotQuery* __restrict__ sq, int64_t nq) {
+  const int64_t q = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (q >= nq || sq[q].status != 0) return;
+  double cov[10], axes[6];
+  for (int i = 0; i < 10; ++i) cov[i] = sq[q].cov[i];
+  if (shot_eigen(cov, sq[q].k - sq[q].n_invalid, axes)) {
+    for (int i = 0; i < 6; ++i) sq[q].axes[i] = axes[i];
+  } else {
+    sq[q].status = 3;  // no frame: NaN rows (written by C)
+  }
+}
+
+// C: sign disambiguation, histogram, normalisation
+__global__ void __launch_bounds__(256) k_shot_hist(GridView g, const float* __restrict__ nx,
+                                                   const float* __restrict__ ny, const float* __restrict__ nz,
+                                                   const float* __restrict__ qx, const float* __restrict__ qy,
+                                                   const float* __restrict__ qz, int64_t base, int64_t nq,
+                                                   double radius, float* __restrict__ desc,
+                                                   float* __restrict__ rf_out, const uint64_t* __restrict__ gkeys,
+                                                   const ShotQuery* __restrict__ sq,
+                                                   const float4* __restrict__ snp) {
+  __shared__ ShotLds S;  // (the keys are read from global memory: eight workgroups per CU)
+  const int tid = threadIdx.x;
+  for (int64_t l = blockIdx.x; l < nq; l += gridDim.x) {
+    const int64_t q = base + l;
+    const int status = sq[l].status;
+    if (status == 1 || status == 2) continue;
+    float* d = desc + q * kLen;
+    float* rfo = rf_out + q * 9;
+    if (status == 3) {
+      shot_nan(d, rfo);
+      continue;
+    }
+    const int k = sq[l].k;
+    const uint64_t* keys = gkeys + l * kCapSmall;
+    if (tid < 6) S.axes[tid] = sq[l].axes[tid];
+    if (tid == 0) {
+      S.zero_prefix = sq[l].zero_prefix;
+      S.plusT = 0;
+      S.plusN = 0;
+    }
     __syncthreads();
-    PROF_T(t8);
-    PROF_ADD(5, t7, t8);
+    shot_frame<true>(S, g, keys, k, k - sq[l].n_invalid, qx[q], qy[q], qz[q]);
+    shot_hist<true>(S, g, keys, k, qx[q], qy[q], qz[q], nx, ny, nz, snp, radius, d, rfo);
   }
 }
 
@@ -476,9 +686,34 @@ void shot_dev(pfx_ctx* ctx, const float* sx, const float* sy, const float* sz, c
     int* n_over = err + 1;
     const size_t lds_s = 2 * sizeof(uint64_t) * kCapSmall, lds = sizeof(uint64_t) * kCap;
     PFX_HIP(hipFuncSetAttribute((const void*)k_shot<kCap>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    // lists <= kCapSmall: the split kernels in batches of kSplitBatch queries (sort + LRF
+    // covariance per workgroup, the eigen solve one lane per query, frame + histogram per
+    // workgroup); PFX_SHOT_FUSED=1: every phase in one workgroup per query (k_shot<kCapSmall>)
+    static const bool fused = [] {
+      const char* e = getenv("PFX_SHOT_FUSED");
+      return e && *e && *e != '0';
+    }();
     const unsigned blocks = (unsigned)std::min<int64_t>(nq, 256 * 10);
-    k_shot<kCapSmall><<<blocks, 256, lds_s, st>>>(g, snx, sny, snz, qx, qy, qz, nq, nullptr, nullptr, over, n_over,
-                                                   r, desc, rf, err, nbr);
+    if (fused) {
+      k_shot<kCapSmall><<<blocks, 256, lds_s, st>>>(g, snx, sny, snz, qx, qy, qz, nq, nullptr, nullptr, over, n_over,
+                                                     r, desc, rf, err, nbr);
+    } else {
+      constexpr int64_t kSplitBatch = 16384;
+      const int64_t bq = std::min<int64_t>(nq, kSplitBatch);
+      uint64_t* gkeys = ctx->buf("shot_keys").as<uint64_t>((size_t)bq * kCapSmall);
+      ShotQuery* sq = ctx->buf("shot_q").as<ShotQuery>((size_t)bq);
+      int32_t* ipos = ctx->buf("shot_ipos").as<int32_t>(ns);
+      float4* snp = ctx->buf("shot_snp").as<float4>(ns);
+      k_shot_prep<<<(unsigned)ceil_div(ns, 256), 256, 0, st>>>(ctx->grid_b.perm, ns, snx, sny, snz, ipos, snp);
+      for (int64_t q0 = 0; q0 < nq; q0 += kSplitBatch) {
+        const int64_t m = std::min<int64_t>(kSplitBatch, nq - q0);
+        const unsigned bl = (unsigned)std::min<int64_t>(m, 256 * 10);
+        k_shot_lrf<<<bl, 256, lds_s, st>>>(g, qx, qy, qz, q0, m, over, n_over, r, desc, rf, gkeys, sq, ipos, nbr);
+        k_shot_eigen<<<(unsigned)ceil_div(m, 64), 64, 0, st>>>(sq, m);
+        k_shot_hist<<<(unsigned)std::min<int64_t>(m, 256 * 16), 256, 0, st>>>(g, snx, sny, snz, qx, qy, qz, q0, m, r,
+                                                                           desc, rf, gkeys, sq, snp);
+      }
+    }
     // longer lists: grid sized for the worst case, the count stays on the device
     k_shot<kCap><<<(unsigned)std::min<int64_t>(nq, 256 * 2), 256, lds, st>>>(
         g, snx, sny, snz, qx, qy, qz, nq, over, n_over, nullptr, nullptr, r, desc, rf, err, nbr);
@@ -490,14 +725,6 @@ void shot_dev(pfx_ctx* ctx, const float* sx, const float* sy, const float* sz, c
   PFX_HIP(hipMemcpyAsync(&h_nbr, nbr, sizeof(h_nbr), hipMemcpyDeviceToHost, st));
   PFX_HIP(hipStreamSynchronize(st));
   ctx->stats["shot_neighbors"] = (int64_t)h_nbr;
-#ifdef PFX_SHOT_PROFILE
-  {
-    unsigned long long pr[8];
-    PFX_HIP(hipMemcpyFromSymbol(pr, HIP_SYMBOL(g_shot_prof), sizeof(pr)));
-    fprintf(stderr, "shot phase cycles (summed over queries): sort %llu lrf %llu frame %llu hist %llu apply %llu out %llu\n",
-            pr[0], pr[1], pr[2], pr[3], pr[4], pr[5]);
-  }
-#endif
   if (h > 0)
     throw Error(PFX_ERR_CAPACITY, "shot: a query has " + std::to_string(h) + " neighbours (> " +
                                       std::to_string(kCap) + " supported)");

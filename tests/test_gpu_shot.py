@@ -63,3 +63,19 @@ def test_shot_edge_cases(ctx):
     o = O.shot(x, y, z, nx, ny, nz, qx, qy, qz, 0.08)
     _check(g, o)
     assert np.isnan(g[0][-4:]).all()
+
+
+def test_shot_split_batches_and_long_lists(ctx):
+    """The split kernels (sort + LRF per workgroup, eigen one lane per query, frame + histogram
+    per workgroup) over more than one 16,384-query batch, with queries whose neighbourhoods
+    exceed the split path's 2,048 keys (the fused long-list kernel) in both batches."""
+    x, y, z = _cloud("indoor_source")
+    rng = np.random.default_rng(12)
+    blob = (rng.normal(0, 0.02, (3000, 3)) + [x[11], y[11], z[11]]).astype(np.float32)
+    x, y, z = (np.concatenate([a, b]).astype(np.float32) for a, b in zip((x, y, z), blob.T))
+    nx, ny, nz, _ = O.normals(x, y, z, 0.05)
+    n0 = len(x) - 3000
+    q = np.r_[rng.choice(n0, 16500), n0 + np.arange(0, 3000, 300), 11, n0 + 5].astype(np.int64)
+    g = ctx.shot(x, y, z, nx, ny, nz, x[q], y[q], z[q], 0.08)
+    o = O.shot(x, y, z, nx, ny, nz, x[q], y[q], z[q], 0.08)
+    assert _check(g, o) > 16000
