@@ -284,7 +284,7 @@ def bench_scans(args, torch, dist, dev, world, rank, local):
 
     def one_scan(b):
         if shot:
-            rows = narf_shot(ctx, b, sb, sample)
+            rows = run_fpfh.shot(b, sb, sample)  # (NARF || normals, then SHOT: as the headline's overlap)
             return sb.desc[:rows], None
         kp, k = run_fpfh(b)
         state["kp"] = kp
@@ -320,7 +320,7 @@ def bench_scans(args, torch, dist, dev, world, rank, local):
                     long_scan.append((ctx_n.stat("normals_long_neighbors"), ctx_n.stat("normals_long_queries")))
                 blocks.append(one_scan(b))
                 if w == 0 and not fast and (demand or not run_fpfh.support_first):
-                    c = ctx if shot else ctx_n
+                    c = ctx_n  # (the normal estimation runs on the side context in both passes)
                     nb_scan.append(c.stat("normals_neighbors"))
                     long_scan.append((c.stat("normals_long_neighbors"), c.stat("normals_long_queries")))
         else:

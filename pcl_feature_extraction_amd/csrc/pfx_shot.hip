@@ -673,9 +673,14 @@ void shot_dev(pfx_ctx* ctx, const float* sx, const float* sy, const float* sz, c
     PFX_HIP(hipStreamSynchronize(st));
     return;
   }
-  ctx->prep_x = nullptr;  // grid_b is rebuilt: a pending pfx_fpfh_prepare_dev no longer holds
+  // the surface grid prepared ahead (pfx_fpfh_prepare_dev: coordinates only, e.g. while the normals
+  // are estimated on another stream), else built here
+  const bool grid_ready = ctx->prep_x == sx && ctx->prep_n == ns && ctx->prep_r == r;
+  ctx->prep_x = nullptr;  // one-shot
   ctx->prep_n = -1;
-  build_grid(ctx, ctx->grid_b, sx, sy, sz, ns, r);
+  ctx->prep_qx = nullptr;
+  ctx->prep_nq = -1;
+  if (!grid_ready) build_grid(ctx, ctx->grid_b, sx, sy, sz, ns, r);
   GridView g = view(ctx->grid_b);
   int* err = ctx->buf("shot_err").as<int>(4);
   unsigned long long* nbr = reinterpret_cast<unsigned long long*>(err + 2);

@@ -219,6 +219,35 @@ class OverlappedNarfFpfh:
         self.s_main.wait_stream(self.s_side)  # every normal belongs to the step
         return kp, k
 
+    def shot(self, b: ScanBuffers, s, sample, normal_radius: float = 0.05, feat_radius: float = 0.08,
+             params=None, cam=None):
+        """narf_shot with the same overlap: the normal estimation on the side stream while NARF,
+        the keypoint gather, the sample's coordinates and the SHOT surface grid
+        (pfx_fpfh_prepare_dev's, which shot_dev takes over) run on the main stream; SHOT after an
+        event on the normals.  Same results as narf_shot; returns the number of rows."""
+        torch = self.torch
+        self.s_side.wait_stream(self.s_main)
+        fut = self.pool.submit(self.ctx_side.normals_dev, b.x, b.y, b.z, normal_radius, b.nx, b.ny, b.nz, b.curv)
+        try:
+            kp = self.ctx.narf_keypoints_dev(b.x, b.y, b.z, params or narf_params(support_size=0.2),
+                                             cam or camera())
+            k = self.ctx.gather_points_dev(b.x, b.y, b.z, kp, s.qx, s.qy, s.qz)
+            m = sample.numel()
+            with torch.cuda.stream(self.s_main):
+                torch.index_select(b.x, 0, sample, out=s.qx[k:k + m])
+                torch.index_select(b.y, 0, sample, out=s.qy[k:k + m])
+                torch.index_select(b.z, 0, sample, out=s.qz[k:k + m])
+            self.ctx.fpfh_prepare_dev(b.x, b.y, b.z, feat_radius)
+        finally:
+            fut.result()
+        ev = torch.cuda.Event()
+        ev.record(self.s_side)
+        self.s_main.wait_event(ev)
+        rows = k + m
+        self.ctx.shot_dev(b.x, b.y, b.z, b.nx, b.ny, b.nz, s.qx[:rows], s.qy[:rows], s.qz[:rows], feat_radius,
+                          s.desc[:rows], s.rf[:rows])
+        return rows
+
     def check(self):
         """Once per batch, outside any timed region: synchronises both contexts so errors the
         stream-ordered calls defer (an FPFH neighbourhood beyond capacity) are raised."""

@@ -217,3 +217,36 @@ def test_split_check_pass_matches_default_with_reruns():
         assert np.array_equal(kp0, kp1) and k0 == k1
         assert np.array_equal(np.nan_to_num(n0, nan=7).view(np.uint32), np.nan_to_num(n1, nan=7).view(np.uint32))
         assert np.array_equal(np.nan_to_num(d0, nan=7).view(np.uint32), np.nan_to_num(d1, nan=7).view(np.uint32))
+
+
+def test_overlapped_shot_matches_sequential():
+    """OverlappedNarfFpfh.shot (normals on the side stream beside NARF, SHOT's surface grid
+    prepared ahead) == pipeline.narf_shot on one stream, descriptors and frames bit for bit."""
+    import torch
+    from pcl_feature_extraction_amd import Context
+    from pcl_feature_extraction_amd.pipeline import OverlappedNarfFpfh, alloc, alloc_shot, narf_shot
+    from pcl_feature_extraction_amd.synth import synth_seabed
+    n = 150_000
+    x, y, z, _ = synth_seabed(n, 31)
+    dev = torch.device("cuda", 0)
+    sample = torch.from_numpy(np.sort(np.random.default_rng(2).choice(n, 500, replace=False))).to(dev)
+    outs = []
+    for overlapped in (False, True):
+        b = alloc(torch, n, dev, max_keypoints=4096)
+        s = alloc_shot(torch, 8192, dev)
+        b.x.copy_(torch.from_numpy(x)); b.y.copy_(torch.from_numpy(y)); b.z.copy_(torch.from_numpy(z))
+        ctx, ctx_n = Context(0), Context(0)
+        ctx.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+        if overlapped:
+            run = OverlappedNarfFpfh(torch, ctx, ctx_n, dev)
+            rows = run.shot(b, s, sample)
+            run.close()
+        else:
+            rows = narf_shot(ctx, b, s, sample)
+        torch.cuda.synchronize(dev)
+        outs.append((rows, s.desc[:rows].cpu().numpy(), s.rf[:rows].cpu().numpy()))
+        ctx.close(); ctx_n.close()
+    (r0, d0, f0), (r1, d1, f1) = outs
+    assert r0 == r1 and r0 >= 500
+    assert np.array_equal(np.nan_to_num(d0, nan=7).view(np.uint32), np.nan_to_num(d1, nan=7).view(np.uint32))
+    assert np.array_equal(np.nan_to_num(f0, nan=7).view(np.uint32), np.nan_to_num(f1, nan=7).view(np.uint32))
