@@ -225,9 +225,27 @@ class OverlappedNarfFpfh:
         the keypoint gather, the sample's coordinates and the SHOT surface grid
         (pfx_fpfh_prepare_dev's, which shot_dev takes over) run on the main stream; SHOT after an
         event on the normals.  Same results as narf_shot; returns the number of rows."""
+        import threading
         torch = self.torch
         self.s_side.wait_stream(self.s_main)
-        fut = self.pool.submit(self.ctx_side.normals_dev, b.x, b.y, b.z, normal_radius, b.nx, b.ny, b.nz, b.curv)
+        ev = torch.cuda.Event()
+        launched = threading.Event()
+
+        def est(*a):  # (as __call__'s split check: SHOT queued behind the launched estimation)
+            try:
+                self.ctx_side.normals_launch_dev(*a)
+                ev.record(self.s_side)
+            finally:
+                launched.set()
+            return self.ctx_side.normals_finish_dev()
+
+        fut = self.pool.submit(est, b.x, b.y, b.z, normal_radius, b.nx, b.ny, b.nz, b.curv)
+
+        def run_shot():
+            self.ctx.shot_dev(b.x, b.y, b.z, b.nx, b.ny, b.nz, s.qx[:rows], s.qy[:rows], s.qz[:rows], feat_radius,
+                              s.desc[:rows], s.rf[:rows])
+
+        rerun = False
         try:
             kp = self.ctx.narf_keypoints_dev(b.x, b.y, b.z, params or narf_params(support_size=0.2),
                                              cam or camera())
@@ -238,14 +256,15 @@ class OverlappedNarfFpfh:
                 torch.index_select(b.y, 0, sample, out=s.qy[k:k + m])
                 torch.index_select(b.z, 0, sample, out=s.qz[k:k + m])
             self.ctx.fpfh_prepare_dev(b.x, b.y, b.z, feat_radius)
+            rows = k + m
+            launched.wait()
+            self.s_main.wait_event(ev)
+            run_shot()
         finally:
-            fut.result()
-        ev = torch.cuda.Event()
-        ev.record(self.s_side)
-        self.s_main.wait_event(ev)
-        rows = k + m
-        self.ctx.shot_dev(b.x, b.y, b.z, b.nx, b.ny, b.nz, s.qx[:rows], s.qy[:rows], s.qz[:rows], feat_radius,
-                          s.desc[:rows], s.rf[:rows])
+            rerun = fut.result()
+        if rerun:  # the estimation was rerun exactly: SHOT again, behind it
+            self.s_main.wait_stream(self.s_side)
+            run_shot()
         return rows
 
     def check(self):
