@@ -623,8 +623,13 @@ __global__ void __launch_bounds__(64) k_shot_eigen(ShotQuery* __restrict__ sq, i
   }
 }
 
-// C: sign disambiguation, histogram, normalisation
-__global__ void __launch_bounds__(256) k_shot_hist(GridView g, const float* __restrict__ nx,
+// C: sign disambiguation, histogram, normalisation (workgroups per CU: the double-precision
+// interpolation of shot_updates wants ~195 VGPRs, i.e. two; held to three (168): SHOT stage 1.455
+// -> 1.247 ms on configs[3], four (128, with spills) 1.32)
+#ifndef PFX_SHOT_HIST_WG
+#define PFX_SHOT_HIST_WG 3
+#endif
+__global__ void __launch_bounds__(256, PFX_SHOT_HIST_WG) k_shot_hist(GridView g, const float* __restrict__ nx,
                                                    const float* __restrict__ ny, const float* __restrict__ nz,
                                                    const float* __restrict__ qx, const float* __restrict__ qy,
                                                    const float* __restrict__ qz, int64_t base, int64_t nq,
