@@ -573,7 +573,9 @@ def scans_line(args, world, n_scans, mine, shot, elapsed, timers, iso, nb_scan, 
         shot_gbs = sbytes / shot_s / 1e9 if shot_s > 0 else 0.0
         stage = roofline
         stage.pop("bound")
-        roofline = {"bound": "hbm", "kernel": "k_shot", "achieved": round(shot_gbs, 2), "peak": HBM_PEAK_GBS,
+        roofline = {"bound": "hbm", "kernel": "SHOT stage: k_shot_prep + k_shot_lrf + k_shot_eigen + k_shot_hist "
+                                              "(+ k_shot<16384> for lists over 2,048)",
+                    "achieved": round(shot_gbs, 2), "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": round(shot_gbs / HBM_PEAK_GBS, 5), "traffic": None,
                     "algorithmic_bytes_per_launch": int(sbytes), "avg_ms": round(shot_s * 1e3, 4),
                     "note": "sum_q |N_0.08(q)| x 24 B (xyz + normal) per launch (SURVEY 8(d)); VALU/LDS-atomic "
