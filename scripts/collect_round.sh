@@ -3,7 +3,7 @@
 # (referenced from DESIGN.md section 9: the evidence files each round commits)
 T=$1
 cp gpurun_out/bench_$T.json profiles/${T}_bench_fpfh_line.json
-for w in shot match iss harris harris6d config1 fastnormals scans8 dense; do cp gpurun_out/bench_${w}_$T.json profiles/${T}_bench_${w}_line.json; done
+for w in shot match iss harris harris6d config1 fastnormals demand scans8 dense; do cp gpurun_out/bench_${w}_$T.json profiles/${T}_bench_${w}_line.json; done
 cp gpurun_out/prof_$T/run_kernel_stats.csv profiles/${T}_kernel_stats.csv
 cp gpurun_out/prof_iss_$T/run_kernel_stats.csv profiles/${T}_iss_kernel_stats.csv
 cp gpurun_out/pmc_$T/summary.txt profiles/${T}_pmc_summary.txt

@@ -8,7 +8,7 @@ timeout -k 10 500 python -u -m pytest tests -x -q -m gpu --timeout 120 --timeout
 tail -1 gpurun_out/t_$TAG.log
 timeout -k 10 400 python bench.py > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err || { tail -30 gpurun_out/bench_$TAG.err; exit 1; }
 cut -c1-300 gpurun_out/bench_$TAG.json
-for w in shot match iss harris harris6d config1 fastnormals; do
+for w in shot match iss harris harris6d config1 fastnormals demand; do
   timeout -k 10 400 python bench.py --workload $w > gpurun_out/bench_${w}_$TAG.json 2> gpurun_out/bench_${w}_$TAG.err || { tail -30 gpurun_out/bench_${w}_$TAG.err; exit 1; }
 done
 timeout -k 10 400 python bench.py --scans 8 --steps 5 --warmup 2 --no-cpu-baseline > gpurun_out/bench_scans8_$TAG.json 2> gpurun_out/bench_scans8_$TAG.err || { tail -30 gpurun_out/bench_scans8_$TAG.err; exit 1; }
