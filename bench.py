@@ -236,8 +236,8 @@ def bench_scans(args, torch, dist, dev, world, rank, local):
 
     from pcl_feature_extraction_amd import Context
     from pcl_feature_extraction_amd.dist import gather_to_root, in_scan_order, owned_scans
-    from pcl_feature_extraction_amd.pipeline import (BatchNarfFpfh, OverlappedNarfFpfh, alloc, alloc_shot,
-                                                     keypoint_rows, narf_shot)
+    from pcl_feature_extraction_amd.pipeline import (BatchNarfFpfh, DeviceRows, OverlappedNarfFpfh, alloc,
+                                                     alloc_shot, narf_shot)
     from pcl_feature_extraction_amd.synth import ROOM_SCALE, synth_room, synth_seabed
 
     shot = args.workload == "shot"
@@ -281,6 +281,9 @@ def bench_scans(args, torch, dist, dev, world, rank, local):
         sb = alloc_shot(torch, 1 << 16, dev)
         sample = torch.from_numpy(sample_np.astype(np.int64)).to(dev)
     state = {"kp": None, "rows": 0, "gathered": None}
+    # descriptor rows' cloud indices to the device through pinned blocks (async: a pageable copy
+    # would hold the host until the scan's FPFH had finished, idling the device between steps)
+    dev_rows = DeviceRows(torch, dev, slots=2 * max(1, len(mine)))
 
     def one_scan(b):
         if shot:
@@ -288,15 +291,13 @@ def bench_scans(args, torch, dist, dev, world, rank, local):
             return sb.desc[:rows], None
         kp, k = run_fpfh(b)
         state["kp"] = kp
-        idx = torch.from_numpy(keypoint_rows(kp, npts).astype(np.int32)).to(dev, non_blocking=True)
-        return b.desc[:k], idx
+        return b.desc[:k], dev_rows(kp, npts)
 
     def batch_scans():
         blocks = []
         for b, (kp, k) in zip(scans, run_batch(scans)):
             state["kp"] = kp
-            idx = torch.from_numpy(keypoint_rows(kp, npts).astype(np.int32)).to(dev, non_blocking=True)
-            blocks.append((b.desc[:k], idx))
+            blocks.append((b.desc[:k], dev_rows(kp, npts)))
         return blocks
 
     def step():

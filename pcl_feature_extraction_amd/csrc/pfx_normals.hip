@@ -59,7 +59,7 @@ __device__ __forceinline__ void store_normal(const GridView& g, int32_t p, const
 // the grid columns around the query columns.  The workgroup collects those columns (LDS hash),
 // takes per column the z range its queries need, and stages the union (contiguous position
 // ranges of the cell-sorted packed copy) in LDS once; a per-cell table maps a list entry's run
-// to its LDS base.  The nine chains then read neighbour coordinates with ds_read_b128 instead
+// to its LDS base.  The nine chains then read neighbour coordinates from LDS (x, y as one ds_read_b64 over the 64 banks, z ds_read_b32) instead
 // of 64-address global gathers (the TA/L2 latency that bounded the previous version).
 // Fallbacks keep every list exact: union > kStageCap -> the same table with global bases;
 // > kMaxCells distinct cells -> per-lane run starts.
@@ -74,8 +74,9 @@ template <int CAP>
 struct ChainLds {
   static_assert(CAP * 3 >= 256 * 9, "lane-mode run tables live in the staging LDS");
   union {
-    struct {
-      float x[CAP], y[CAP], z[CAP];
+    struct {  // x, y as one 8-byte word (one ds_read_b64 per neighbour over 64 banks) + z
+      float2 xy[CAP];
+      float z[CAP];
     } c;
     struct {
       uint32_t key[kHash];
@@ -315,8 +316,7 @@ __device__ __forceinline__ void chain_wg(ChainLds<CAP>& S, const GridView& g, co
         for (int u = 0; u < 4; ++u) {
           const int i = i0 + u * 256 + tid;
           if (src[u] >= 0) {
-            S.u.c.x[i] = vx[u];
-            S.u.c.y[i] = vy[u];
+            S.u.c.xy[i] = make_float2(vx[u], vy[u]);
             S.u.c.z[i] = vz[u];
           }
         }
@@ -349,10 +349,12 @@ __device__ __forceinline__ void chain_wg(ChainLds<CAP>& S, const GridView& g, co
   for (int i = 0; i < 9; ++i) a[i] = 0.0f;
   if (staged) {
     const int32_t* tb = S.tbl + cs * 9;
-    const float *cxs = S.u.c.x, *cys = S.u.c.y, *czs = S.u.c.z;
+    const float2* cxy = S.u.c.xy;
+    const float* czs = S.u.c.z;
     run_chain<kBatch>(lst, lg, k, [&](uint32_t e) {
       const int32_t i = tb[entry_run(e)] + (int32_t)entry_off(e);
-      return make_float4(cxs[i], cys[i], czs[i], 0.f);
+      const float2 v = cxy[i];
+      return make_float4(v.x, v.y, czs[i], 0.f);
     }, a);
   } else if (indexed) {
     const int32_t* tb = S.tbl + cs * 9;
@@ -361,7 +363,7 @@ __device__ __forceinline__ void chain_wg(ChainLds<CAP>& S, const GridView& g, co
   } else {
     // too many cells for the shared table: each lane keeps its own nine run starts in the
     // (unused) staging LDS
-    int32_t* tb = reinterpret_cast<int32_t*>(S.u.c.x) + tid * 9;
+    int32_t* tb = reinterpret_cast<int32_t*>(S.u.c.xy) + tid * 9;
 #pragma unroll
     for (int r = 0; r < 9; ++r) {
       int32_t st, len;

@@ -92,6 +92,11 @@ class OverlappedNarfFpfh:
         # pfx_normals_finish_dev, FPFH queued in between; A/B 173.8 vs 172.1 Mpoints/s, 3 runs each;
         # PFX_NORMALS_SPLIT=0: pfx_normals_dev, whose check precedes the chains)
         self.split_check = os.environ.get("PFX_NORMALS_SPLIT", "1") == "1"
+        # split form: the estimation's ~50 launches issued by the calling thread before NARF's (no
+        # host round trip in them), the worker only waits for the check.  Two threads launching at
+        # once contend inside the HIP runtime (~60 us per launch in the API trace instead of ~7),
+        # which stretched the grid build at the head of the critical path.
+        self.launch_first = os.environ.get("PFX_NORMALS_LAUNCH_FIRST", "1") == "1"
         self._support = None
 
     def __call__(self, b: ScanBuffers, normal_radius: float = 0.05, feat_radius: float = 0.08, params=None,
@@ -101,7 +106,12 @@ class OverlappedNarfFpfh:
             return self._support_first(b, normal_radius, feat_radius, params, cam)
         ev = self.torch.cuda.Event()
         split = self.split_check and not self.fast_normals
-        if split:
+        if split and self.launch_first:
+            self.ctx_side.normals_launch_dev(b.x, b.y, b.z, normal_radius, b.nx, b.ny, b.nz, b.curv)
+            ev.record(self.s_side)
+            launched = None
+            fut = self.pool.submit(self.ctx_side.normals_finish_dev)
+        elif split:
             # the estimation queued with no host round trip, FPFH queued right behind it, and its
             # validation (pfx_normals_finish_dev) on the worker while FPFH is being queued
             import threading
@@ -117,7 +127,8 @@ class OverlappedNarfFpfh:
         else:
             launched = None
             est = self.ctx_side.normals_fast_dev if self.fast_normals else self.ctx_side.normals_dev
-        fut = self.pool.submit(est, b.x, b.y, b.z, normal_radius, b.nx, b.ny, b.nz, b.curv)
+        if not (split and self.launch_first):
+            fut = self.pool.submit(est, b.x, b.y, b.z, normal_radius, b.nx, b.ny, b.nz, b.curv)
         rerun = False
         try:
             kp = self.ctx.narf_keypoints_dev(b.x, b.y, b.z, params or narf_params(support_size=0.2),
@@ -129,7 +140,8 @@ class OverlappedNarfFpfh:
             if k > 0:  # FPFH's SPFH point set, also normals-free
                 self.ctx.fpfh_prepare_queries_dev(b.x, b.y, b.z, b.kx[:k], b.ky[:k], b.kz[:k], feat_radius)
             if split:
-                launched.wait()
+                if launched is not None:
+                    launched.wait()
                 self.s_main.wait_event(ev)
                 if k > 0:
                     self.ctx.fpfh_dev(b.x, b.y, b.z, b.nx, b.ny, b.nz, b.kx[:k], b.ky[:k], b.kz[:k], feat_radius,
@@ -358,6 +370,39 @@ def keypoint_rows(kp: np.ndarray, n: int) -> np.ndarray:
     """Cloud indices the descriptors belong to (keypoints.h:229 uses pixel index as cloud index)."""
     kp = np.asarray(kp)
     return kp[(kp >= 0) & (kp < n)]
+
+
+class DeviceRows:
+    """keypoint_rows on the device, staged through a ring of pinned host blocks so the copy is a
+    real async DMA.  (A pageable-memory copy blocks the host until its stream reaches it -- i.e.
+    until the scan's FPFH has finished -- so the next scan's launches were queued only after the
+    device had drained: ~0.25 ms of idle device per scan.)  A slot is reused `slots` calls later,
+    after its copy's event; the device block returned stays valid until then."""
+
+    def __init__(self, torch, device, slots: int = 2, cap: int = 1 << 16):
+        self.torch, self.device = torch, device
+        self.h = [torch.empty(cap, dtype=torch.int32, pin_memory=True) for _ in range(slots)]
+        self.d = [torch.empty(cap, dtype=torch.int32, device=device) for _ in range(slots)]
+        self.ev = [None] * slots
+        self.i = 0
+
+    def __call__(self, kp: np.ndarray, n: int):
+        rows = keypoint_rows(kp, n).astype(np.int32)
+        s = self.i
+        self.i = (s + 1) % len(self.h)
+        if self.ev[s] is not None:
+            self.ev[s].synchronize()
+        k = len(rows)
+        if k > self.h[s].numel():
+            self.h[s] = self.torch.empty(k, dtype=self.torch.int32, pin_memory=True)
+            self.d[s] = self.torch.empty(k, dtype=self.torch.int32, device=self.device)
+        self.h[s][:k].numpy()[:] = rows
+        out = self.d[s][:k]
+        out.copy_(self.h[s][:k], non_blocking=True)
+        ev = self.torch.cuda.Event()
+        ev.record()
+        self.ev[s] = ev
+        return out
 
 
 @dataclasses.dataclass
