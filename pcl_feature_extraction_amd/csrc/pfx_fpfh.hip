@@ -173,6 +173,15 @@ __device__ __forceinline__ bool bin_fast_f(float v, float tol, int& h) {
   return true;
 }
 
+// bin_fast_f without a branch: h is always written (clamped in float, so a NaN or huge value
+// converts safely); the result is only used when the return value is true
+__device__ __forceinline__ bool bin_fast_nb(float v, float tol, int& h) {
+  const float m = floorf(v);
+  const float fr = v - m;  // exact (|v| < 2^23)
+  h = (int)fminf(fmaxf(m, 0.0f), (float)(kBins - 1));
+  return (fr > tol) & (fr < 1.0f - tol);  // also false for NaN
+}
+
 __device__ __forceinline__ bool pair_bins_fast(f3 p1, f3 n1, f3 p2, f3 n2, int& h1, int& h2, int& h3) {
   f3 dp = sub3(p2, p1);
   const float s4 = sqn4(dp);
@@ -299,21 +308,20 @@ __device__ __forceinline__ void pair_bins_fast2(f3 p1, f3 n1, bool n1fin, const 
   const fv2 tol1 = (fv2(1e-6f) + 8e-6f * rmx) * (1.01f * (float)kBins * d_pi) + kBinMapSlack;
   const fv2 b1 = (t + 3.14159265358979323846f) * ((float)kBins * d_pi);
   const fv2 b2 = (f2a + 1.0f) * (0.5f * kBins), b3 = (f3a + 1.0f) * (0.5f * kBins);
+  // branch-free: every bin map evaluated, the outcome selected (short-circuit && and the
+  // if/else chain made the compiler nest exec-mask branches with register copies per level)
 #pragma unroll
   for (int c = 0; c < 2; ++c) {
-    if (s4[c] == 0.0f) {  // f4 == 0 in pair_bins
-      h1[c] = bz1; h2[c] = h3[c] = bz;
-      ok[c] = true;
-    } else if (!live[c]) {
-      ok[c] = false;
-    } else if (sv[c] == 0.0f) {  // v_norm == 0 in pair_bins
-      h1[c] = bz1; h2[c] = h3[c] = bz;
-      ok[c] = true;
-    } else {
-      ok[c] = big[c] && bin_fast_f(b1[c], tol1[c], h1[c]) &&
-              bin_fast_f(b2[c], 4e-6f * 0.5f * kBins + kBinMapSlack, h2[c]) &&
-              bin_fast_f(b3[c], 1e-6f * 0.5f * kBins + kBinMapSlack, h3[c]);
-    }
+    int a1, a2, a3;
+    const bool k1 = bin_fast_nb(b1[c], tol1[c], a1);
+    const bool k2 = bin_fast_nb(b2[c], 4e-6f * 0.5f * kBins + kBinMapSlack, a2);
+    const bool k3 = bin_fast_nb(b3[c], 1e-6f * 0.5f * kBins + kBinMapSlack, a3);
+    // f4 == 0, or v_norm == 0, in pair_bins: the zero-feature bins
+    const bool zero = (s4[c] == 0.0f) | (live[c] & (sv[c] == 0.0f));
+    ok[c] = zero | (live[c] & big[c] & k1 & k2 & k3);
+    h1[c] = zero ? bz1 : a1;
+    h2[c] = zero ? bz : a2;
+    h3[c] = zero ? bz : a3;
   }
 }
 

@@ -1,14 +1,10 @@
 set -o pipefail
-# headline A/B over an environment switch: bash scripts/gpu_ab_env.sh VAR "v1 v2" [pytest -k expr]
-VAR=$1; VALS=$2; K=$3
+# headline A/B over environment settings, 3 rounds: bash scripts/gpu_ab_env.sh "A=0 B=1" "A=1 B=1" ...
+# (each argument: one configuration, space-separated VAR=value pairs)
 mkdir -p gpurun_out
-if [ -n "$K" ]; then
-  timeout -k 10 400 python -u -m pytest tests -x -q -m gpu -k "$K" --timeout 200 --timeout-method thread > gpurun_out/t_env.log 2>&1 || { tail -30 gpurun_out/t_env.log; exit 1; }
-  tail -1 gpurun_out/t_env.log
-fi
 for i in 1 2 3; do
-for v in $VALS; do
-  env $VAR=$v timeout -k 10 300 python bench.py --no-cpu-baseline --no-e2e > gpurun_out/b_e.json 2> gpurun_out/b_e.err || { tail -20 gpurun_out/b_e.err; exit 1; }
-  echo "$VAR=$v $(python -c "import json; d=json.load(open('gpurun_out/b_e.json')); r=d['roofline']; print(d['value'], d['ms_per_step'], r['avg_ms'])")"
-done
+  for cfg in "$@"; do
+    env $cfg timeout -k 10 300 python bench.py --no-cpu-baseline --no-e2e > gpurun_out/b_env.json 2> gpurun_out/b_env.err || { tail -20 gpurun_out/b_env.err; exit 1; }
+    echo "[$cfg] $(python -c "import json; d=json.load(open('gpurun_out/b_env.json')); print(d['value'], d['ms_per_step'], d['roofline']['avg_ms'])")"
+  done
 done

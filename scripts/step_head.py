@@ -7,7 +7,7 @@ rows = list(csv.DictReader(open(sys.argv[1])))
 lim = float(sys.argv[2]) if len(sys.argv) > 2 else 900.0
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
 ends = [i for i, r in enumerate(rows) if "k_fpfh_weight<true>" in r["Kernel_Name"]]
-k0, k1 = ends[-4], ends[-3]
+k0, k1 = ends[-6], ends[-5]  # inside the timed region (5 timed steps, then 3 detail steps)
 t0, t1 = int(rows[k0]["End_Timestamp"]), int(rows[k1]["End_Timestamp"])
 for r in rows[k0 - 6:]:
     s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])

@@ -6,7 +6,7 @@ import sys
 rows = list(csv.DictReader(open(sys.argv[1])))
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
 ends = [i for i, r in enumerate(rows) if "k_fpfh_weight<true>" in r["Kernel_Name"]]
-k0, k1 = ends[-4], ends[-3]  # a step inside the timed region
+k0, k1 = ends[-6], ends[-5]  # a step inside the timed region (bench: 5 timed steps, then 3 with per-kernel timers)
 t0, t1 = int(rows[k0]["End_Timestamp"]), int(rows[k1]["End_Timestamp"])
 print("step us %.1f" % ((t1 - t0) / 1e3))
 for r in rows:
