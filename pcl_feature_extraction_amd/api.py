@@ -235,6 +235,11 @@ class Context:
         self._check(self._lib.pfx_normals_launch_dev(self.h, _ptr(x), _ptr(y), _ptr(z), x.numel(), float(r), vp,
                                                      _ptr(nx), _ptr(ny), _ptr(nz), _ptr(curv)))
 
+    def normals_gate_dev(self, event):
+        """The next normals launch on this context waits for `event` (a recorded torch.cuda.Event)
+        between its grid build and its list kernels (pfx_normals_gate_dev); None clears it."""
+        self._check(self._lib.pfx_normals_gate_dev(self.h, None if event is None else event.cuda_event))
+
     def normals_finish_dev(self) -> bool:
         """Validates the launched estimation; True when it had to be rerun (consumers of its
         outputs queued in between must run again)."""

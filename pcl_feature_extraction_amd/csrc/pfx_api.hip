@@ -328,6 +328,13 @@ pfx_status pfx_normals_launch_dev(pfx_ctx* ctx, const float* d_x, const float* d
   PFX_API_END(ctx)
 }
 
+pfx_status pfx_normals_gate_dev(pfx_ctx* ctx, void* hip_event) {
+  PFX_API_BEGIN
+  check_ctx(ctx);
+  ctx->lists_gate = static_cast<hipEvent_t>(hip_event);
+  PFX_API_END(ctx)
+}
+
 pfx_status pfx_normals_finish_dev(pfx_ctx* ctx, int32_t* rerun) {
   PFX_API_BEGIN
   check_ctx(ctx);

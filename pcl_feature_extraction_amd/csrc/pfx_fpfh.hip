@@ -906,10 +906,36 @@ void fpfh_prepare_dev(pfx_ctx* ctx, const float* sx, const float* sy, const floa
   ctx->prep_qx = nullptr;
   ctx->prep_nq = -1;
   if (ns == 0) return;
-  build_grid(ctx, ctx->grid_b, sx, sy, sz, ns, r);
+  // on the previous scan's widened bounds (no bounds readback, so the call queues without a host
+  // wait); the first consumer validates it (fpfh_validate_grid) and rebuilds exactly if needed
+  build_grid(ctx, ctx->grid_b, sx, sy, sz, ns, r, /*use_hint=*/true);
+  if (ctx->grid_b.oob) {
+    if (!ctx->grid_b_hoob) PFX_HIP(hipHostMalloc((void**)&ctx->grid_b_hoob, 64, hipHostMallocDefault));
+    if (!ctx->grid_b_oob_ev) PFX_HIP(hipEventCreateWithFlags(&ctx->grid_b_oob_ev, hipEventDisableTiming));
+    PFX_HIP(hipMemcpyAsync(ctx->grid_b_hoob, ctx->grid_b.oob, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+    PFX_HIP(hipEventRecord(ctx->grid_b_oob_ev, ctx->stream));
+  }
   ctx->prep_x = sx;
   ctx->prep_n = ns;
   ctx->prep_r = r;
+}
+
+bool fpfh_validate_grid(pfx_ctx* ctx) {
+  Grid& G = ctx->grid_b;
+  if (!G.oob) return false;
+  G.oob = nullptr;
+  PFX_HIP(hipEventSynchronize(ctx->grid_b_oob_ev));
+  if (*ctx->grid_b_hoob == 0) return false;
+  ctx->stats["fpfh_speculative_reruns"] += 1;
+  // exact rebuild (bounds readback; refreshes the hint); the preparation still describes it
+  const float* x = ctx->prep_x;
+  const int64_t n = ctx->prep_n;
+  const double r = ctx->prep_r;
+  build_grid(ctx, G, G.ux, G.uy, G.uz, G.n, r);
+  ctx->prep_x = x;
+  ctx->prep_n = n;
+  ctx->prep_r = r;
+  return true;
 }
 
 // S of the next fpfh_dev (input != surface) marked and compacted ahead of time: it needs only the
@@ -921,6 +947,7 @@ void fpfh_prepare_queries_dev(pfx_ctx* ctx, const float* sx, const float* sy, co
   ctx->prep_nq = -1;
   if (ns == 0 || nq == 0) return;
   if (!(ctx->prep_x == sx && ctx->prep_n == ns && ctx->prep_r == r)) fpfh_prepare_dev(ctx, sx, sy, sz, ns, r);
+  fpfh_validate_grid(ctx);
   hipStream_t st = ctx->stream;
   const Grid& G = ctx->grid_b;
   uint8_t* flags = ctx->buf("fpfh_flags").as<uint8_t>(ns);
@@ -949,6 +976,7 @@ void fpfh_support_mask_dev(pfx_ctx* ctx, const float* sx, const float* sy, const
   PFX_HIP(hipMemsetAsync(mask, 0, ns, st));
   if (nq == 0) return;
   if (!(ctx->prep_x == sx && ctx->prep_n == ns && ctx->prep_r == r)) fpfh_prepare_dev(ctx, sx, sy, sz, ns, r);
+  fpfh_validate_grid(ctx);
   TimeScope ts(ctx, "fpfh_support");
   const Grid& G = ctx->grid_b;
   const GridView g = view(G);
@@ -978,6 +1006,7 @@ void fpfh_support_ball_dev(pfx_ctx* ctx, const float* sx, const float* sy, const
   PFX_HIP(hipMemsetAsync(mask, 0, ns, st));
   if (nq == 0) return;
   if (!(ctx->prep_x == sx && ctx->prep_n == ns && ctx->prep_r == r)) fpfh_prepare_dev(ctx, sx, sy, sz, ns, r);
+  fpfh_validate_grid(ctx);
   TimeScope ts(ctx, "fpfh_support");
   // (2r)^2 with a relative margin far above the float rounding of the squared distance
   const float rr4 = (float)(4.0 * r * r * (1.0 + 1e-5));
@@ -1002,8 +1031,9 @@ void fpfh_dev(pfx_ctx* ctx, const float* sx, const float* sy, const float* sz, c
   }
   const bool grid_ready = ctx->prep_x == sx && ctx->prep_n == ns && ctx->prep_r == r;
   if (!grid_ready) build_grid(ctx, ctx->grid_b, sx, sy, sz, ns, r);
+  const bool rebuilt = grid_ready && fpfh_validate_grid(ctx);
   // S marked ahead (fpfh_prepare_queries_dev on this grid and these queries)?
-  const bool s_ready = grid_ready && !same && ctx->prep_qx == qx && ctx->prep_nq == nq;
+  const bool s_ready = grid_ready && !rebuilt && !same && ctx->prep_qx == qx && ctx->prep_nq == nq;
   ctx->prep_x = nullptr;  // one-shot
   ctx->prep_n = -1;
   ctx->prep_qx = nullptr;

@@ -137,9 +137,14 @@ struct pfx_ctx {
   const float* prep_qx = nullptr;
   int64_t prep_nq = -1;
   const uint8_t* fpfh_support = nullptr;  // pfx_fpfh_support_mask_dev -> next pfx_fpfh_dev
+  // a speculative grid_b (pfx_fpfh_prepare_dev on the previous scan's widened bounds): its
+  // out-of-bounds count, copied to pinned memory in stream order, checked by the first consumer
+  int* grid_b_hoob = nullptr;
+  hipEvent_t grid_b_oob_ev = nullptr;
   std::map<std::string, pfx::DevBuf> bufs;  // named scratch
   pfx::NarfState* narf = nullptr;
   pfx::NormalsState* normals = nullptr;  // neighbour lists between the two normal phases
+  hipEvent_t lists_gate = nullptr;       // pfx_normals_gate_dev: waited for before the next list kernels
   bool normals_fork_hint = true;         // long-list chains on the side stream (last decision)
   pfx::KeypointState* kp = nullptr;      // grids + lists of the keypoint detectors
   pfx::DevBuf& buf(const char* name) { return bufs[name]; }
@@ -298,6 +303,9 @@ void fpfh_dev(pfx_ctx* ctx, const float* sx, const float* sy, const float* sz, c
               const float* qz, int64_t nq, int same, double r, float* out,
               bool reuse_normal_lists = false);
 void fpfh_prepare_dev(pfx_ctx* ctx, const float* sx, const float* sy, const float* sz, int64_t ns, double r);
+// a prepared speculative grid_b checked (one pinned read, normally long complete) and rebuilt
+// exactly when a point fell outside its bounds; true when it was rebuilt
+bool fpfh_validate_grid(pfx_ctx* ctx);
 void fpfh_prepare_queries_dev(pfx_ctx* ctx, const float* sx, const float* sy, const float* sz, int64_t ns,
                               const float* qx, const float* qy, const float* qz, int64_t nq, double r);
 void shot_dev(pfx_ctx* ctx, const float* sx, const float* sy, const float* sz, const float* snx,

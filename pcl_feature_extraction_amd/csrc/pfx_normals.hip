@@ -599,6 +599,14 @@ __global__ void __launch_bounds__(256) k_normals_long(GridView g, NbLists L, con
 }  // namespace
 
 
+// pfx_normals_gate_dev: the caller's event, once, between the grid and the list kernels
+static void wait_lists_gate(pfx_ctx* ctx) {
+  if (!ctx->lists_gate) return;
+  hipEvent_t e = ctx->lists_gate;
+  ctx->lists_gate = nullptr;
+  PFX_HIP(hipStreamWaitEvent(ctx->stream, e, 0));
+}
+
 void normals_release(pfx_ctx* ctx) {
   delete ctx->normals;
   ctx->normals = nullptr;
@@ -629,6 +637,7 @@ void normals_lists_dev(pfx_ctx* ctx, const float* x, const float* y, const float
   build_grid(ctx, ctx->grid_a, x, y, z, n, r);
   k_nan_fill4<<<(unsigned)std::min<int64_t>(ceil_div(n, 256), 4096), 256, 0, st>>>(nx, ny, nz, curv, n);
   check_launch("k_nan_fill4");
+  wait_lists_gate(ctx);
   build_lists(ctx, ctx->grid_a, nullptr, r, true, ns.L, "normals");
   ctx->stats["normals_neighbors"] = ns.L.total;
   ctx->stats["normals_long_neighbors"] = ns.L.long_total;
@@ -766,6 +775,7 @@ bool normals_speculative_lists(pfx_ctx* ctx, const float* x, const float* y, con
   build_grid(ctx, ctx->grid_a, x, y, z, n, r, /*use_hint=*/true);
   k_nan_fill4<<<(unsigned)std::min<int64_t>(ceil_div(n, 256), 4096), 256, 0, ctx->stream>>>(nx, ny, nz, curv, n);
   check_launch("k_nan_fill4");
+  wait_lists_gate(ctx);
   build_lists(ctx, ctx->grid_a, nullptr, r, true, ns.L, "normals", /*defer=*/true);
   return true;
 }

@@ -681,6 +681,7 @@ void shot_dev(pfx_ctx* ctx, const float* sx, const float* sy, const float* sz, c
   // the surface grid prepared ahead (pfx_fpfh_prepare_dev: coordinates only, e.g. while the normals
   // are estimated on another stream), else built here
   const bool grid_ready = ctx->prep_x == sx && ctx->prep_n == ns && ctx->prep_r == r;
+  if (grid_ready) fpfh_validate_grid(ctx);  // (a speculative prepared grid: exact after this)
   ctx->prep_x = nullptr;  // one-shot
   ctx->prep_n = -1;
   ctx->prep_qx = nullptr;

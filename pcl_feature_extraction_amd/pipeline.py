@@ -97,6 +97,11 @@ class OverlappedNarfFpfh:
         # once contend inside the HIP runtime (~60 us per launch in the API trace instead of ~7),
         # which stretched the grid build at the head of the critical path.
         self.launch_first = os.environ.get("PFX_NORMALS_LAUNCH_FIRST", "1") == "1"
+        # with launch_first: FPFH's surface grid (it needs only the cloud) queued before NARF, so
+        # after NARF's host selection only the keypoint gather and the S marking remain before SPFH
+        # (1: after the estimation's launch; 2: before it, with the estimation's list kernels gated
+        # on it -- pfx_normals_gate_dev -- so it never queues behind them; 0: after NARF)
+        self.prep_first = int(os.environ.get("PFX_PREP_FIRST", "2"))
         self._support = None
 
     def __call__(self, b: ScanBuffers, normal_radius: float = 0.05, feat_radius: float = 0.08, params=None,
@@ -107,10 +112,17 @@ class OverlappedNarfFpfh:
         ev = self.torch.cuda.Event()
         split = self.split_check and not self.fast_normals
         if split and self.launch_first:
+            if self.prep_first == 2:
+                self.ctx.fpfh_prepare_dev(b.x, b.y, b.z, feat_radius)
+                gate = self.torch.cuda.Event()
+                gate.record(self.s_main)
+                self.ctx_side.normals_gate_dev(gate)
             self.ctx_side.normals_launch_dev(b.x, b.y, b.z, normal_radius, b.nx, b.ny, b.nz, b.curv)
             ev.record(self.s_side)
             launched = None
             fut = self.pool.submit(self.ctx_side.normals_finish_dev)
+            if self.prep_first == 1:
+                self.ctx.fpfh_prepare_dev(b.x, b.y, b.z, feat_radius)
         elif split:
             # the estimation queued with no host round trip, FPFH queued right behind it, and its
             # validation (pfx_normals_finish_dev) on the worker while FPFH is being queued
@@ -136,7 +148,8 @@ class OverlappedNarfFpfh:
             k = self.ctx.gather_points_dev(b.x, b.y, b.z, kp, b.kx, b.ky, b.kz)
             # the FPFH surface grid (normals-free) after NARF: the step's first milliseconds
             # belong to the normal-estimation grid and NARF, the critical and the longer path
-            self.ctx.fpfh_prepare_dev(b.x, b.y, b.z, feat_radius)
+            if not (split and self.launch_first and self.prep_first):  # (already queued)
+                self.ctx.fpfh_prepare_dev(b.x, b.y, b.z, feat_radius)
             if k > 0:  # FPFH's SPFH point set, also normals-free
                 self.ctx.fpfh_prepare_queries_dev(b.x, b.y, b.z, b.kx[:k], b.ky[:k], b.kz[:k], feat_radius)
             if split:

@@ -333,3 +333,40 @@ def test_fpfh_dev_does_not_reuse_lists_of_rewritten_buffers():
     ref = O.fpfh(xb, yb, zb, onb[0], onb[1], onb[2], xb, yb, zb, 0.05, same_as_surface=True)
     assert _nan_aware_equal(gb, ref)
     assert _nan_aware_equal(gb2, ref)
+
+
+def test_fpfh_speculative_surface_grid():
+    """pfx_fpfh_prepare_dev builds FPFH's surface grid on the previous scan's widened bounds (no
+    bounds readback); its first consumer validates the grid and rebuilds it exactly when a point
+    lies outside.  Descriptors through the prepared path equal the host API's on a fresh context
+    for a first scan (exact build), a scan inside the bounds (speculative grid kept) and a scan
+    moved by 3 m (speculative grid rebuilt)."""
+    import torch
+    from pcl_feature_extraction_amd import Context
+    x, y, z = _cloud("indoor_source")
+    dev = torch.device("cuda", 0)
+    scans = [(x, y, z), (x + 0.01, y, z), (x + 3.0, y, z)]
+    q = np.arange(0, len(x), 97)
+    with Context(0) as ctx:
+        ctx.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+        for i, (sx, sy, sz) in enumerate(scans):
+            sx, sy, sz = (np.ascontiguousarray(a, np.float32) for a in (sx, sy, sz))
+            t = [torch.from_numpy(a).to(dev) for a in (sx, sy, sz)]
+            nrm = [torch.empty_like(t[0]) for _ in range(4)]
+            qs = [a[q].contiguous() for a in t]
+            out = torch.empty((len(q), 33), dtype=torch.float32, device=dev)
+            ctx.fpfh_prepare_dev(*t, 0.08)
+            ctx.normals_dev(*t, 0.05, *nrm)
+            ctx.fpfh_prepare_queries_dev(*t, *qs, 0.08)
+            ctx.fpfh_dev(*t, *nrm[:3], *qs, 0.08, out)
+            torch.cuda.synchronize(dev)
+            got = out.cpu().numpy()
+            with Context(0) as fresh:
+                n_h = fresh.normals(sx, sy, sz, 0.05)
+                ref = fresh.fpfh(sx, sy, sz, n_h[0], n_h[1], n_h[2], sx[q], sy[q], sz[q], 0.08)
+            assert _nan_aware_equal(got, ref), i
+            try:
+                reruns = ctx.stat("fpfh_speculative_reruns")
+            except Exception:  # (no rerun yet: the statistic does not exist)
+                reruns = 0
+            assert reruns == (1 if i == 2 else 0), (i, reruns)
