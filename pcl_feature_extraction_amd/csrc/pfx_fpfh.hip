@@ -661,10 +661,25 @@ __global__ void __launch_bounds__(kWT) k_fpfh_weight(GridView g, const float* __
     float* rb1 = GLOBAL ? rb0 : rb0 + kChunkW * RS;
     const int nch = (k + kChunkW - 1) / kChunkW;
     auto stage = [&](int c, float* rbuf, int t0, int nt) {
-      const int c0 = c * kChunkW, m = min(kChunkW, k - c0);
-      for (int e = t0; e < m * kDesc; e += nt) {
+      const int c0 = c * kChunkW, m = min(kChunkW, k - c0), tot = m * kDesc;
+      // every row load first (clamped index: all issued back to back), then the LDS stores -- a
+      // load-then-store loop waited for each load in turn, one global latency per element a
+      // thread stages, on the critical path of the slowest query's chunk sequence
+      constexpr int PER = (kChunkW * kDesc + (kWT - 64) - 1) / (kWT - 64);
+      float v[PER];
+#pragma unroll
+      for (int u = 0; u < PER; ++u) {
+        const int e = min(t0 + u * nt, tot - 1);
         const int j = e / kDesc, b = e - j * kDesc;
-        rbuf[j * RS + b] = spfh[(int64_t)key_idx(keys[c0 + j]) * kDesc + b];
+        v[u] = spfh[(int64_t)key_idx(keys[c0 + j]) * kDesc + b];
+      }
+#pragma unroll
+      for (int u = 0; u < PER; ++u) {
+        const int e = t0 + u * nt;
+        if (e < tot) {
+          const int j = e / kDesc, b = e - j * kDesc;
+          rbuf[j * RS + b] = v[u];
+        }
       }
       for (int j = t0; j < m; j += nt) {
         const float d2 = key_d2(keys[c0 + j]);

@@ -58,19 +58,20 @@ __device__ __forceinline__ void query_runs(const GridView& g, float qx, float qy
   cz = cz < -2 ? -2 : (cz > g.nz + 1 ? g.nz + 1 : cz);
   int64_t z0 = cz - 1 < 0 ? 0 : cz - 1;
   int64_t z1 = cz + 1 >= g.nz ? g.nz - 1 : cz + 1;
+  // branch-free: all 18 cell_start loads issued together (clamped to a valid address, results
+  // selected), not one dependent round trip per run behind a branch
+  const bool zok = finite && z0 <= z1;
   int32_t acc = 0;
 #pragma unroll
   for (int r = 0; r < 9; ++r) {
-    int64_t ix = cx + (r / 3) - 1, iy = cy + (r % 3) - 1;
-    int32_t s = 0, len = 0;
-    if (finite && ix >= 0 && ix < g.nx && iy >= 0 && iy < g.ny && z0 <= z1) {
-      int64_t base = (ix * g.ny + iy) * g.nz;
-      s = g.cell_start[base + z0];
-      len = g.cell_start[base + z1 + 1] - s;
-    }
-    R.start[r] = s;
+    const int64_t ix = cx + (r / 3) - 1, iy = cy + (r % 3) - 1;
+    const bool ok = zok && ix >= 0 && ix < g.nx && iy >= 0 && iy < g.ny;
+    const int64_t base = ok ? (ix * g.ny + iy) * g.nz : 0;
+    const int32_t a = g.cell_start[base + (ok ? z0 : 0)];
+    const int32_t b = g.cell_start[base + (ok ? z1 + 1 : 0)];
+    R.start[r] = ok ? a : 0;
     R.pref[r] = acc;
-    acc += len;
+    acc += ok ? b - a : 0;
   }
   R.pref[9] = acc;
 }
@@ -80,13 +81,13 @@ __device__ __forceinline__ void block_run(const GridView& g, uint32_t key, int r
   const int64_t iz = key % g.nz, iy = (key / g.nz) % g.ny, ix = key / ((uint64_t)g.nz * g.ny);
   const int64_t bx = ix + (r / 3) - 1, by = iy + (r % 3) - 1;
   const int64_t z0 = iz - 1 < 0 ? 0 : iz - 1, z1 = iz + 1 >= g.nz ? g.nz - 1 : iz + 1;
-  s = 0;
-  len = 0;
-  if (bx >= 0 && bx < g.nx && by >= 0 && by < g.ny) {
-    const int64_t base = (bx * g.ny + by) * g.nz;
-    s = g.cell_start[base + z0];
-    len = g.cell_start[base + z1 + 1] - s;
-  }
+  // branch-free (clamped address, selected result): block_runs' loads are issued together
+  const bool ok = bx >= 0 && bx < g.nx && by >= 0 && by < g.ny;
+  const int64_t base = ok ? (bx * g.ny + by) * g.nz : 0;
+  const int32_t a = g.cell_start[base + (ok ? z0 : 0)];
+  const int32_t b = g.cell_start[base + (ok ? z1 + 1 : 0)];
+  s = ok ? a : 0;
+  len = ok ? b - a : 0;
 }
 
 __device__ __forceinline__ int block_runs(const GridView& g, uint32_t key, Runs& R) {
