@@ -178,8 +178,12 @@ struct ListOut {
 
 // Candidate coordinates of a tile: staged in LDS, or read from the packed grid copy (L2).
 struct CandLds {
-  const float *cx, *cy, *cz;
-  __device__ __forceinline__ void get(int t, float& x, float& y, float& z) const { x = cx[t]; y = cy[t]; z = cz[t]; }
+  const float2* cxy;
+  const float* cz;
+  __device__ __forceinline__ void get(int t, float& x, float& y, float& z) const {
+    const float2 v = cxy[t];
+    x = v.x; y = v.y; z = cz[t];
+  }
 };
 struct CandGlobal {
   const float4* sp;
@@ -470,12 +474,13 @@ struct Stager {
   }
   // unconditional (slots >= T get don't-care values; the arrays hold PT * 256): a conditional
   // store lets the compiler sink each load into its own branch and wait for it there
-  __device__ __forceinline__ void store(float* cx, float* cy, float* cz, int32_t* s_qp, int qn) const {
+  __device__ __forceinline__ void store(float2* cxy, float* cz, int32_t* s_qp, int qn) const {
     const int tid = threadIdx.x;
 #pragma unroll
     for (int u = 0; u < PT; ++u) {
       const int t = tid + 256 * u;
-      cx[t] = x[u]; cy[t] = y[u]; cz[t] = z[u];
+      cxy[t] = make_float2(x[u], y[u]);
+      cz[t] = z[u];
     }
     if (tid < qn) s_qp[tid] = qp;
   }
@@ -491,11 +496,13 @@ __global__ void __launch_bounds__(256, TCAP <= kTcapSmall ? 4 : (STAGE ? 3 : 2))
   constexpr int Q = kQ, QW = Q / 4;  // queries per tile / per wave
   constexpr int U = 2;               // candidates per lane in flight in the test loop
   constexpr int SCAP = STAGE ? Stager<TCAP, STAGE>::PT * 256 : 1;
-  __shared__ float cx[SCAP], cy[SCAP], cz[SCAP];
+  __shared__ float2 cxy[SCAP];
+  __shared__ float cz[SCAP];
   // dense tiles: the test loop reads candidates from LDS chunks of CH staged by the whole
   // workgroup (one latency round and one run search per candidate, not per wave and candidate)
   constexpr int CH = STAGE ? 1 : 1024;
-  __shared__ float hx[CH], hy[CH], hz[CH];
+  __shared__ float2 hxy[CH];
+  __shared__ float hz[CH];
   __shared__ uint16_t lists[Q][LCAP + 2];  // +2: odd dword row stride (no bank conflicts)
   __shared__ uint32_t sd[4][LCAP];
   __shared__ uint16_t stt[4][LCAP];
@@ -527,7 +534,7 @@ __global__ void __launch_bounds__(256, TCAP <= kTcapSmall ? 4 : (STAGE ? 3 : 2))
       s_chunk = next_chunk;
       next_chunk = atomicAdd(next_tile, chunk);
     }
-    sg.store(cx, cy, cz, s_qp, qn);
+    sg.store(cxy, cz, s_qp, qn);
     __syncthreads();
   }
   while (i < ntiles) {
@@ -553,7 +560,8 @@ __global__ void __launch_bounds__(256, TCAP <= kTcapSmall ? 4 : (STAGE ? 3 : 2))
         const int32_t p = s_qp[j];
         if (STAGE) {  // a query lies in its own cell, i.e. in run 4 of its block
           const int t = R.pref[4] + (p - R.start[4]);
-          qx[u] = cx[t]; qy[u] = cy[t]; qz[u] = cz[t];
+          const float2 v = cxy[t];
+          qx[u] = v.x; qy[u] = v.y; qz[u] = cz[t];
         } else {
           const float4 c = g.sp[p];
           qx[u] = c.x; qy[u] = c.y; qz[u] = c.z;
@@ -570,14 +578,12 @@ __global__ void __launch_bounds__(256, TCAP <= kTcapSmall ? 4 : (STAGE ? 3 : 2))
         __syncthreads();  // the previous chunk's readers are done
 #pragma unroll
         for (int u = 0; u < CPT; ++u) {
-          hx[tid + 256 * u] = cc[u].x;
-          hy[tid + 256 * u] = cc[u].y;
+          hxy[tid + 256 * u] = make_float2(cc[u].x, cc[u].y);
           hz[tid + 256 * u] = cc[u].z;
         }
         __syncthreads();
       }
-      const float* Xs = STAGE ? cx : hx - c0;
-      const float* Ys = STAGE ? cy : hy - c0;
+      const float2* XYs = STAGE ? cxy : hxy - c0;
       const float* Zs = STAGE ? cz : hz - c0;
       for (int t0 = c0; t0 < cend; t0 += 64 * U) {
         float px[U], py[U], pz[U];
@@ -586,7 +592,8 @@ __global__ void __launch_bounds__(256, TCAP <= kTcapSmall ? 4 : (STAGE ? 3 : 2))
           const int t = t0 + 64 * v + lane;
           px[v] = py[v] = pz[v] = 0.f;
           if (t < cend) {
-            px[v] = Xs[t]; py[v] = Ys[t]; pz[v] = Zs[t];
+            const float2 xy = XYs[t];
+            px[v] = xy.x; py[v] = xy.y; pz[v] = Zs[t];
           }
         }
 #pragma unroll
@@ -643,7 +650,7 @@ __global__ void __launch_bounds__(256, TCAP <= kTcapSmall ? 4 : (STAGE ? 3 : 2))
         const int k = cursor[u];
         if (ok && j < qn && k <= LCAP && k > 1) {  // wave-uniform
           if (STAGE) {
-            const CandLds cand{cx, cy, cz};
+            const CandLds cand{cxy, cz};
             sort_list<NB, CandLds, (TCAP <= kTcapSmall)>(lists[j], k, qx[u], qy[u], qz[u], cand, bscale, sd[wv],
                                                          stt[wv], bcount[wv], bpos[wv], g, R, lane);
           } else {
@@ -684,7 +691,7 @@ __global__ void __launch_bounds__(256, TCAP <= kTcapSmall ? 4 : (STAGE ? 3 : 2))
       arena_base += need;
       arena_left -= need;
     }
-    if (ni < ntiles) sg.store(cx, cy, cz, s_qp, qn_n);
+    if (ni < ntiles) sg.store(cxy, cz, s_qp, qn_n);
     __syncthreads();
     const int64_t base = (int64_t)s_base;
     if (tid < qn && s_k[tid] <= LCAP) out.off[start + tid] = base + tid;
