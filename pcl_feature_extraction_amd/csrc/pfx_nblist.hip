@@ -26,6 +26,7 @@ constexpr int kArena = 16384;   // list entries per arena reservation of a tile 
 constexpr int kArenaQuery = 16384;  // ... of a per-query workgroup (lists of 1k-4k entries)
 constexpr int kTcapSmall = 384, kTcapSparse = 1280, kTcapDense = 8000;
 constexpr int kCapQuery = 4096, kBucketsQuery = 1024;
+constexpr int kCapMid8 = 8192, kBucketsMid8 = 1024;  // 72 KB of LDS: two workgroups per CU
 constexpr int kCapMid = 16384, kBucketsMid = 2048;  // 144 KB of LDS: one workgroup per CU
 constexpr int kCapHuge = 1 << 18, kBucketsHuge = 4096, kHugeBlocks = 256;  // 1 GB scratch, allocated on demand
 
@@ -925,7 +926,7 @@ std::string bname(const char* tag, const char* what) { return std::string(tag) +
 
 // the pinned readback block of a list build
 struct ListsRb {
-  int cnt[14];
+  int cnt[16];
   int oob;
   int pad;
   unsigned long long cur[4];
@@ -994,9 +995,10 @@ void build_lists(pfx_ctx* ctx, const Grid& G, const uint8_t* mask, double radius
   // counters: 0 sparse tiles, 1 dense tiles, 2 per-query work, 3 huge work, 4 max k over cap,
   // 5 / 7 sparse / dense tile queue heads, 6 per-query work queued by the classifier (restored
   // for a rerun), 8 / 9 per-query / huge work queue heads, 10 small tiles, 11 their queue head,
-  // 12 mid work (lists of 4k-16k entries), 13 its queue head
-  int* counters = B("counters").as<int>(14);
+  // 12 mid work (lists of 8k-16k entries), 13 its queue head, 14 mid8 work (4k-8k), 15 its head
+  int* counters = B("counters").as<int>(16);
   int32_t* mid = B("mid").as<int32_t>(n);
+  int32_t* mid8 = B("mid8").as<int32_t>(n);
   unsigned long long* cursor = B("cursor").as<unsigned long long>(4);
   size_t t1 = 0, t2 = 0, t3 = 0;
   PFX_HIP(rocprim::select(nullptr, t1, rocprim::counting_iterator<int32_t>(0), flags, qpos, d_nq, (size_t)n, st));
@@ -1009,12 +1011,12 @@ void build_lists(pfx_ctx* ctx, const Grid& G, const uint8_t* mask, double radius
   {
     TimeScope ts(ctx, std::string(tag) + "_tiles");
     if (mask) {
-      k_list_init<<<1, 256, 0, st>>>(nullptr, 0, nullptr, d_nq, counters, 14, cursor0);
+      k_list_init<<<1, 256, 0, st>>>(nullptr, 0, nullptr, d_nq, counters, 16, cursor0);
       k_mask_flags<<<nb, 256, 0, st>>>(G.perm, G.skeys, n, (uint64_t)G.ncells, mask, want, flags);
       PFX_HIP(rocprim::select(tmp, t1, rocprim::counting_iterator<int32_t>(0), flags, qpos, d_nq, (size_t)n, st));
     } else {
       // every finite point, in cell order: sorted positions [0, cell_start[ncells])
-      k_list_init<<<nb, 256, 0, st>>>(qpos, n, G.cell_start + G.ncells, d_nq, counters, 14, cursor0);
+      k_list_init<<<nb, 256, 0, st>>>(qpos, n, G.cell_start + G.ncells, d_nq, counters, 16, cursor0);
     }
     k_seg_marks<<<nb, 256, 0, st>>>(qpos, G.skeys, d_nq, seg);
     PFX_HIP(rocprim::inclusive_scan(tmp, t2, seg, seg, (size_t)n, rocprim::maximum<int32_t>(), st));
@@ -1027,6 +1029,10 @@ void build_lists(pfx_ctx* ctx, const Grid& G, const uint8_t* mask, double radius
   const size_t lds_q = sizeof(uint32_t) * 2 * kCapQuery;
   PFX_HIP(hipFuncSetAttribute((const void*)k_nb_query<kCapQuery, kBucketsQuery, false>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_q));
+  static const bool use_mid8 = getenv("PFX_LIST_MID8") != nullptr && *getenv("PFX_LIST_MID8") == '1';
+  const size_t lds_m8 = sizeof(uint32_t) * 2 * kCapMid8;
+  PFX_HIP(hipFuncSetAttribute((const void*)k_nb_query<kCapMid8, kBucketsMid8, false>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_m8));
   const size_t lds_m = sizeof(uint32_t) * 2 * kCapMid;
   PFX_HIP(hipFuncSetAttribute((const void*)k_nb_query<kCapMid, kBucketsMid, false>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_m));
@@ -1056,7 +1062,7 @@ void build_lists(pfx_ctx* ctx, const Grid& G, const uint8_t* mask, double radius
       PFX_HIP(hipMemcpyAsync(counters + 2, counters + 6, sizeof(int), hipMemcpyDeviceToDevice, st));
       PFX_HIP(hipMemsetAsync(counters + 3, 0, 3 * sizeof(int), st));  // huge, max k, sparse queue
       PFX_HIP(hipMemsetAsync(counters + 7, 0, 3 * sizeof(int), st));  // dense, query, huge queues
-      PFX_HIP(hipMemsetAsync(counters + 11, 0, 3 * sizeof(int), st));  // small queue, mid work + queue
+      PFX_HIP(hipMemsetAsync(counters + 11, 0, 5 * sizeof(int), st));  // small queue, mid / mid8 work + queues
     }
     // one synchronisation per call: counters, cursors and the query count in one pinned block
     ListsRb* rb = ctx->readback<ListsRb>();
@@ -1094,9 +1100,16 @@ void build_lists(pfx_ctx* ctx, const Grid& G, const uint8_t* mask, double radius
       {
         TimeScope t3(ctx, std::string(tag) + "_lists_query");
         k_nb_query<kCapQuery, kBucketsQuery, false><<<256 * 4, 256, lds_q, st>>>(
-            g, qpos, G.skeys, single, counters + 2, rr, (float)kBucketsQuery / rr, isort, lo, mid, counters + 12,
-            counters + 4, nullptr, counters + 8);
-        // lists of 4k-16k entries (dense clouds); the count stays on the device
+            g, qpos, G.skeys, single, counters + 2, rr, (float)kBucketsQuery / rr, isort, lo,
+            use_mid8 ? mid8 : mid, counters + (use_mid8 ? 14 : 12), counters + 4, nullptr, counters + 8);
+        // opt-in (PFX_LIST_MID8=1, not yet measured on hardware): lists of 4k-8k entries (dense
+        // clouds: ~14 % of the 10M-pt room's queries, 31 % of its entries) in two 72 KB
+        // workgroups per CU instead of the 16k tier's one; the count stays on the device
+        if (use_mid8)
+          k_nb_query<kCapMid8, kBucketsMid8, false><<<256 * 2, 256, lds_m8, st>>>(
+              g, qpos, G.skeys, mid8, counters + 14, rr, (float)kBucketsMid8 / rr, isort, lo, mid, counters + 12,
+              counters + 4, nullptr, counters + 15);
+        // lists of up to 16k entries, one 144 KB workgroup per CU
         k_nb_query<kCapMid, kBucketsMid, false><<<256, 256, lds_m, st>>>(
             g, qpos, G.skeys, mid, counters + 12, rr, (float)kBucketsMid / rr, isort, lo, huge, counters + 3,
             counters + 4, nullptr, counters + 13);
@@ -1137,7 +1150,7 @@ void build_lists(pfx_ctx* ctx, const Grid& G, const uint8_t* mask, double radius
       // unused arena tails (scheduling-dependent, at most one arena per launched workgroup), so
       // this run's demand plus the tail bound always fits the rebuild.
       const size_t tails = (size_t)(256 * 4 * 2 + 256 * 3 * 4 + 256 * 2 * 4) * kArena +
-                           (size_t)(256 * 4 + 256 + kHugeBlocks) * kArenaQuery;
+                           (size_t)(256 * 4 + 256 * 2 + 256 + kHugeBlocks) * kArenaQuery;
       lb.release();
       lb.get(sizeof(uint32_t) * ((size_t)h_cur[0] + tails + ((size_t)1 << 20)));
       continue;
@@ -1158,6 +1171,7 @@ void build_lists(pfx_ctx* ctx, const Grid& G, const uint8_t* mask, double radius
     ctx->stats[std::string(tag) + "_single"] = h_cnt[2];
     ctx->stats[std::string(tag) + "_huge"] = h_cnt[3];
     ctx->stats[std::string(tag) + "_mid"] = h_cnt[12];
+    ctx->stats[std::string(tag) + "_mid8"] = h_cnt[14];
 #ifdef PFX_SHOT_PROFILE
     {
       unsigned long long pr[16];
