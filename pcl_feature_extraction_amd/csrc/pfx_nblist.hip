@@ -1029,7 +1029,7 @@ void build_lists(pfx_ctx* ctx, const Grid& G, const uint8_t* mask, double radius
   const size_t lds_q = sizeof(uint32_t) * 2 * kCapQuery;
   PFX_HIP(hipFuncSetAttribute((const void*)k_nb_query<kCapQuery, kBucketsQuery, false>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_q));
-  static const bool use_mid8 = getenv("PFX_LIST_MID8") != nullptr && *getenv("PFX_LIST_MID8") == '1';
+  static const bool use_mid8 = !(getenv("PFX_LIST_MID8") && *getenv("PFX_LIST_MID8") == '0');  // A/B switch
   const size_t lds_m8 = sizeof(uint32_t) * 2 * kCapMid8;
   PFX_HIP(hipFuncSetAttribute((const void*)k_nb_query<kCapMid8, kBucketsMid8, false>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_m8));
@@ -1102,9 +1102,10 @@ void build_lists(pfx_ctx* ctx, const Grid& G, const uint8_t* mask, double radius
         k_nb_query<kCapQuery, kBucketsQuery, false><<<256 * 4, 256, lds_q, st>>>(
             g, qpos, G.skeys, single, counters + 2, rr, (float)kBucketsQuery / rr, isort, lo,
             use_mid8 ? mid8 : mid, counters + (use_mid8 ? 14 : 12), counters + 4, nullptr, counters + 8);
-        // opt-in (PFX_LIST_MID8=1, not yet measured on hardware): lists of 4k-8k entries (dense
-        // clouds: ~14 % of the 10M-pt room's queries, 31 % of its entries) in two 72 KB
-        // workgroups per CU instead of the 16k tier's one; the count stays on the device
+        // lists of 4k-8k entries (dense clouds: ~14 % of the 10M-pt room's queries, 31 % of its
+        // entries) in two 72 KB workgroups per CU instead of the 16k tier's one (10M-pt dense
+        // variant: per-query lists 750 -> 650 ms, 1066 -> 968 ms per step; PFX_LIST_MID8=0 turns
+        // it off); the count stays on the device
         if (use_mid8)
           k_nb_query<kCapMid8, kBucketsMid8, false><<<256 * 2, 256, lds_m8, st>>>(
               g, qpos, G.skeys, mid8, counters + 14, rr, (float)kBucketsMid8 / rr, isort, lo, mid, counters + 12,

@@ -92,8 +92,8 @@ def test_normals_edge_cases(ctx):
 
 def test_normals_every_list_path(ctx):
     """Densities that route queries through every neighbour-list path (pfx_nblist.hip): sparse
-    and dense tiles, the per-query LDS kernels (k > 1024, k > 4096) and the global-scratch kernel
-    (k > 16384),
+    and dense tiles, the per-query LDS kernels (k > 1024, k > 4096, k > 8192) and the
+    global-scratch kernel (k > 16384),
     plus lane-per-query and nine-lanes-per-query chains; duplicates exercise the index tie-break."""
     rng = np.random.default_rng(23)
     sparse = np.c_[rng.uniform(0, 1, (4000, 2)), np.full(4000, 1.0)]
@@ -105,7 +105,8 @@ def test_normals_every_list_path(ctx):
     pts = np.concatenate([sparse, dense, denser, blob, mid, huge]).astype(np.float32)
     x, y, z = pts[:, 0].copy(), pts[:, 1].copy(), pts[:, 2].copy()
     g = ctx.normals(x, y, z, 0.05)
-    for nm in ["normals_tiles_sparse", "normals_tiles_dense", "normals_single", "normals_mid", "normals_huge"]:
+    for nm in ["normals_tiles_sparse", "normals_tiles_dense", "normals_single", "normals_mid8", "normals_mid",
+               "normals_huge"]:
         assert ctx.stat(nm) > 0, nm
     o = O.normals(x, y, z, 0.05)
     for a, b in zip(g, o):
