@@ -424,8 +424,11 @@ __global__ void k_all_finite(const uint32_t* __restrict__ skeys, int64_t n, uint
 // fast path.  Pairs the fast path cannot bin with certainty go to a global queue for
 // k_fpfh_exact (no call to the double-precision path here: fewer registers, more waves); the
 // integer bin counts and |N| go to hcount / kcount, k_fpfh_finalize turns them into PCL's floats.
+// register budget: 7 waves per SIMD (73 VGPRs; the grid below keeps 16 waves per CU resident):
+// fewer spills of the packed-pair code than at 8 (64 VGPRs): SPFH 0.91 -> 0.89 ms, headline
+// 182.8 -> 185.0 Mpoints/s over three A/B rounds (6: 183.9, 8 + one run loop: 184.1)
 #ifndef PFX_SPFH_WPE
-#define PFX_SPFH_WPE 8
+#define PFX_SPFH_WPE 7
 #endif
 __global__ void __launch_bounds__(256, PFX_SPFH_WPE) k_fpfh_spfh(GridView g, const float4* __restrict__ snp,
                                                       const int32_t* __restrict__ slist,
