@@ -84,10 +84,11 @@ __global__ void k_list_init(int32_t* __restrict__ qpos, int64_t n, const int32_t
 // overflow, a speculative grid that held every point): an invalid build is then never read
 // (its offsets may point past the buffer) and build_lists_check reruns the exact path
 __global__ void k_defer_gate(const int* __restrict__ counters, const unsigned long long* __restrict__ cursor,
-                             unsigned long long cap, int have_huge, const int* __restrict__ oob,
+                             unsigned long long cap, int have_huge, int ran_mids, const int* __restrict__ oob,
                              const int64_t* __restrict__ d_nq, int64_t* __restrict__ d_nq_eff) {
   if (threadIdx.x != 0) return;
-  const bool ok = cursor[0] <= cap && (have_huge || counters[3] == 0) && counters[4] == 0 && (!oob || *oob == 0);
+  const bool ok = cursor[0] <= cap && (have_huge || counters[3] == 0) && counters[4] == 0 && (!oob || *oob == 0) &&
+                  ((ran_mids & 1) || counters[14] == 0) && ((ran_mids & 2) || counters[12] == 0);
   *d_nq_eff = ok ? *d_nq : 0;
 }
 
@@ -935,6 +936,25 @@ struct ListsRb {
 
 }  // namespace
 
+// The 4k-8k and 8k-16k per-query tiers need 72 / 144 KB of LDS per workgroup, so even an empty
+// launch waits until whole CUs are free of the concurrent NARF stream's workgroups (150-200 us on
+// the headline's critical path, whose lists never reach these tiers).  A tier is launched while
+// one of the last 16 builds of this (context, tag) had work for it (always on the first build);
+// a skipped tier that turns out to have work is launched after the readback (or, for a deferred
+// build, the lists are rebuilt exactly), so results never depend on the hint.
+static bool mid_tier_wanted(pfx_ctx* ctx, const char* tag, const char* which) {
+  const auto it = ctx->stats.find(std::string(tag) + which);
+  return it == ctx->stats.end() || it->second > 0;
+}
+static void note_mid_tiers(pfx_ctx* ctx, const char* tag, const int* h_cnt) {
+  for (int t = 0; t < 2; ++t) {
+    const std::string key = std::string(tag) + (t ? "_hint_mid" : "_hint_mid8");
+    const int work = t ? h_cnt[12] : h_cnt[14];
+    int64_t& v = ctx->stats[key];
+    v = work > 0 ? 16 : std::max<int64_t>(0, v - 1);
+  }
+}
+
 bool build_lists_check(pfx_ctx* ctx, const Grid& G, NbLists& out, const char* tag) {
   hipStream_t st = ctx->stream;
   auto B = [&](const char* what) -> DevBuf& { return ctx->bufs[bname(tag, what)]; };
@@ -951,6 +971,9 @@ bool build_lists_check(pfx_ctx* ctx, const Grid& G, NbLists& out, const char* ta
   if (rb->oob > 0) return false;                                    // speculative grid too small
   if (h_cur[0] > lb.bytes / sizeof(uint32_t)) return false;         // list buffer too small
   if (!B("scratch").ptr && h_cnt[3] > 0) return false;              // first very long lists
+  const int ran = (int)ctx->stats[std::string(tag) + "_ran_mid_tiers"];
+  note_mid_tiers(ctx, tag, h_cnt);
+  if ((!(ran & 1) && h_cnt[14] > 0) || (!(ran & 2) && h_cnt[12] > 0)) return false;  // a skipped tier had work
   if (h_cnt[4] > 0)
     throw Error(PFX_ERR_CAPACITY, std::string(tag) + ": a query has " + std::to_string(h_cnt[4]) +
                                       " neighbours (> " + std::to_string(kCapHuge) + " supported)");
@@ -1073,6 +1096,22 @@ void build_lists(pfx_ctx* ctx, const Grid& G, const uint8_t* mask, double radius
       ctx->sync_spin(st);
     };
     DevBuf& hs = B("scratch");
+    auto launch_mid8 = [&] {
+      k_nb_query<kCapMid8, kBucketsMid8, false><<<256 * 2, 256, lds_m8, st>>>(
+          g, qpos, G.skeys, mid8, counters + 14, rr, (float)kBucketsMid8 / rr, isort, lo, mid, counters + 12,
+          counters + 4, nullptr, counters + 15);
+      check_launch("nblist 8k lists");
+    };
+    auto launch_mid = [&] {
+      k_nb_query<kCapMid, kBucketsMid, false><<<256, 256, lds_m, st>>>(
+          g, qpos, G.skeys, mid, counters + 12, rr, (float)kBucketsMid / rr, isort, lo, huge, counters + 3,
+          counters + 4, nullptr, counters + 13);
+      check_launch("nblist 16k lists");
+    };
+    // (see mid_tier_wanted; a rerun launches every tier)
+    const int ran_mids = attempt ? 3 : ((use_mid8 && mid_tier_wanted(ctx, tag, "_hint_mid8") ? 1 : 0) |
+                                        (mid_tier_wanted(ctx, tag, "_hint_mid") ? 2 : 0) | (use_mid8 ? 0 : 1));
+    ctx->stats[std::string(tag) + "_ran_mid_tiers"] = ran_mids;
     auto launch_huge = [&] {
       k_nb_query<kCapHuge, kBucketsHuge, true><<<kHugeBlocks, 256, 0, st>>>(
           g, qpos, G.skeys, huge, counters + 3, rr, (float)kBucketsHuge / rr, isort, lo, nullptr, nullptr, counters + 4,
@@ -1106,14 +1145,9 @@ void build_lists(pfx_ctx* ctx, const Grid& G, const uint8_t* mask, double radius
         // entries) in two 72 KB workgroups per CU instead of the 16k tier's one (10M-pt dense
         // variant: per-query lists 750 -> 650 ms, 1066 -> 968 ms per step; PFX_LIST_MID8=0 turns
         // it off); the count stays on the device
-        if (use_mid8)
-          k_nb_query<kCapMid8, kBucketsMid8, false><<<256 * 2, 256, lds_m8, st>>>(
-              g, qpos, G.skeys, mid8, counters + 14, rr, (float)kBucketsMid8 / rr, isort, lo, mid, counters + 12,
-              counters + 4, nullptr, counters + 15);
+        if (use_mid8 && (ran_mids & 1)) launch_mid8();
         // lists of up to 16k entries, one 144 KB workgroup per CU
-        k_nb_query<kCapMid, kBucketsMid, false><<<256, 256, lds_m, st>>>(
-            g, qpos, G.skeys, mid, counters + 12, rr, (float)kBucketsMid / rr, isort, lo, huge, counters + 3,
-            counters + 4, nullptr, counters + 13);
+        if (ran_mids & 2) launch_mid();
         // beyond 16k entries: once the 1 GB scratch exists the launch is unconditional (count on
         // the device); the first time, the readback below decides
         if (hs.ptr) launch_huge();
@@ -1122,7 +1156,7 @@ void build_lists(pfx_ctx* ctx, const Grid& G, const uint8_t* mask, double radius
     }
     if (defer && attempt == 0) {  // consumers are launched before the readback (build_lists_check)
       int64_t* d_nq_eff = B("nq_eff").as<int64_t>(1);
-      k_defer_gate<<<1, 64, 0, st>>>(counters, cursor, lo.cap, hs.ptr ? 1 : 0, G.oob, d_nq, d_nq_eff);
+      k_defer_gate<<<1, 64, 0, st>>>(counters, cursor, lo.cap, hs.ptr ? 1 : 0, ran_mids, G.oob, d_nq, d_nq_eff);
       check_launch("k_defer_gate");
       out.nq = n;
       out.nq_dev = d_nq_eff;
@@ -1135,6 +1169,15 @@ void build_lists(pfx_ctx* ctx, const Grid& G, const uint8_t* mask, double radius
       return;
     }
     read_back();
+    if ((!(ran_mids & 1) && rb->cnt[14] > 0) || (!(ran_mids & 2) && rb->cnt[12] > 0)) {
+      // a skipped per-query tier had work: run it and the tiers after it (each launch takes its
+      // queue from where an earlier launch stopped, so only the new entries are listed)
+      if (!(ran_mids & 1) && rb->cnt[14] > 0) launch_mid8();
+      launch_mid();
+      if (hs.ptr) launch_huge();
+      read_back();
+    }
+    note_mid_tiers(ctx, tag, rb->cnt);
     if (!hs.ptr && rb->cnt[3] > 0) {  // very long lists, first time: allocate the scratch and sort them
       hs.get(sizeof(uint32_t) * (size_t)kHugeBlocks * 4 * kCapHuge);
       launch_huge();
