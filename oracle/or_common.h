@@ -14,9 +14,17 @@
 //
 //  Floating-point contract (every oracle TU is built with -O2 -ffp-contract=off, x86-64
 //  SSE2, no -march): IEEE binary32/64, left-to-right evaluation, no FMA.  Eigen 3.2
-//  evaluation orders are restated explicitly:
-//    * fixed-size 3-vectors (not vectorised):    dot/squaredNorm = (x + y) + z
+//  evaluation orders are restated explicitly (one model everywhere, round 4):
+//    * reductions (dot / sum / squaredNorm / norm) of a fixed-size expression without packet
+//      access -- Vector3f, Map<Vector3f>, a 3-element block -- go through Redux.h's
+//      DefaultTraversal + CompleteUnrolling, i.e. redux_novec_unroller, which splits at
+//      HalfLength = Length / 2:  sum of 3 terms = x + (y + z)            (dot3 / sqn3)
 //    * aligned 4-vectors (SSE2 packet predux):   dot/squaredNorm = (x + z) + (y + w)
+//    * small fixed-size matrix * vector products (Affine3f * Vector3f, Matrix3f * Vector3f) are
+//      CoeffBasedProduct coefficients (product_coeff_impl, DefaultTraversal): left to right,
+//      ((m0 v0 + m1 v1) + m2 v2)                                         (mv3)
+//    * scalar code written out in PCL (squaredEuclideanDistance, flipNormalTowardsViewpoint):
+//      left to right as written.
 //  Transcendentals: atan2f and acosf are glibc's (sysdeps/ieee754/flt-32/e_atan2f.c,
 //  s_atanf.c, e_acosf.c: the fdlibm float routines, unchanged from the ROS-Indigo-era glibc
 //  2.19 to 2.35), restated below and PINNED against the host libm bit for bit
@@ -173,9 +181,11 @@ inline V3 sub(V3 a, V3 b) { return v3(a.x - b.x, a.y - b.y, a.z - b.z); }
 inline V3 add(V3 a, V3 b) { return v3(a.x + b.x, a.y + b.y, a.z + b.z); }
 inline V3 mul(V3 a, float s) { return v3(a.x * s, a.y * s, a.z * s); }
 inline V3 divs(V3 a, float s) { return v3(a.x / s, a.y / s, a.z / s); }
-// Vector3f (unvectorised): ((a0 b0 + a1 b1) + a2 b2)
-inline float dot3(V3 a, V3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
-inline float sqn3(V3 a) { return a.x * a.x + a.y * a.y + a.z * a.z; }
+// Vector3f reductions (unvectorised, redux_novec_unroller<0,3>): a0 b0 + (a1 b1 + a2 b2)
+inline float dot3(V3 a, V3 b) { return a.x * b.x + (a.y * b.y + a.z * b.z); }
+inline float sqn3(V3 a) { return a.x * a.x + (a.y * a.y + a.z * a.z); }
+// one row of a small fixed-size matrix * Vector3f (CoeffBasedProduct): ((m0 v0 + m1 v1) + m2 v2)
+inline float mv3(V3 row, V3 v) { return (row.x * v.x + row.y * v.y) + row.z * v.z; }
 // Vector4f with w == 0 (SSE2 predux): ((a0 b0 + a2 b2) + (a1 b1 + 0))
 inline float dot4(V3 a, V3 b) { return (a.x * b.x + a.z * b.z) + (a.y * b.y + 0.0f); }
 inline float sqn4(V3 a) { return (a.x * a.x + a.z * a.z) + (a.y * a.y + 0.0f); }

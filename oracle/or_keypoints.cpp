@@ -253,7 +253,7 @@ int orc_iss_keypoints(const float* x, const float* y, const float* z, i64 n, dou
 //  refineCorners: up to 10 times, over the corner's current r-ball (finite normals),
 //    NNT += n n^T, NNTp += (n n^T) p (Matrix3f * Vector3f: ((m0 p0 + m1 p1) + m2 p2)),
 //    invert3x3SymMatrix (common/eigen.hpp: adjugate / det, det != 0), corner = NNTInv * NNTp,
-//    until |corner - previous|^2 <= 1e-6.
+//    until |corner - previous|^2 <= 1e-6 (a Vector3f squaredNorm: dx^2 + (dy^2 + dz^2)).
 //  Restatement choices (unpinned): neighbour order = FLANN's sorted (d2, index) order -- PCL's
 //  NormalEstimation and HarrisKeypoint3D search an unsorted search::KdTree(false), i.e. the
 //  kd-tree traversal order, which changes float sums in the last bits; corners in index order
@@ -429,7 +429,7 @@ int harris_finish(const float* x, const float* y, const float* z, i64 n, double 
             px = q[0]; py = q[1]; pz = q[2];
           }
           const float dx = px - ox, dy = py - oy, dz = pz - oz;
-          diff = (dx * dx + dy * dy) + dz * dz;
+          diff = dx * dx + (dy * dy + dz * dz);  // (Map - Map).squaredNorm (): Redux.h x + (y + z)
         } while (diff > 1e-6 && ++iterations < 10);
         cx[(size_t)c] = px; cy[(size_t)c] = py; cz[(size_t)c] = pz;
       }

@@ -16,6 +16,14 @@
 //      (planar images have no angular resolution).
 //    * VectorAverage covariance is used as a full symmetric matrix.
 //    * histogram cell of a NaN / negative angle -> 0 (UB in PCL).
+//  Round 4 (one Eigen 3.2 model, or_common.h): Vector3f dot / squaredNorm / norm / normalized()
+//  reduce as x + (y + z) (range = transformedPoint.norm () in getImagePoint, the viewing
+//  direction and normal flip of getSurfaceInformation, eigen33's cross-product lengths, the
+//  border-direction cosines and normalize (), getTransFromUnitVectorsZY, the greedy selection's
+//  squaredNorm); the viewer-frame rotation of nkdGetDirectionAngle is an Affine3f * Vector3f
+//  product (left to right); get3dDirection intersects the neighbour pixel's viewing ray with
+//  the local plane (normal_no_jumps, neighborhood_mean_no_jumps) as PCL 1.7 does (rounds 1-3
+//  projected along the normal through the point).
 //  Single-threaded except the per-pixel interest loop (OpenMP, order-free).
 // =====================================================================================
 #include "or_common.h"
@@ -168,6 +176,8 @@ void createRangeImage(const float* X, const float* Y, const float* Z, i64 n, con
 }
 
 // ---- VectorAverage3f (common/impl/vector_average.hpp) -------------------------------------
+// add(): `covariance_(i, j) = (1.0f-alpha)*(covariance_(i, j) + alpha*diff[i]*diff[j])` -- the
+// product parses left to right, (alpha * diff[i]) * diff[j] (round 4; was alpha * (d_i d_j))
 struct VecAvg {
   int n = 0;
   float acc_w = 0.0f;
@@ -181,7 +191,7 @@ struct VecAvg {
     mean = orc::add(mean, v3(alpha * diff.x, alpha * diff.y, alpha * diff.z));
     float d[3] = {diff.x, diff.y, diff.z};
     for (int i = 0; i < 3; ++i)
-      for (int j = i; j < 3; ++j) cov[i][j] = (1.0f - alpha) * (cov[i][j] + alpha * (d[i] * d[j]));
+      for (int j = i; j < 3; ++j) cov[i][j] = (1.0f - alpha) * (cov[i][j] + alpha * d[i] * d[j]);
   }
   void pca(float evals[3], V3 evecs[3]) const {
     float m[3][3];
@@ -194,6 +204,7 @@ struct VecAvg {
 struct Surface {
   bool valid = false;
   V3 normal_no_jumps;
+  V3 mean_no_jumps;  // LocalSurface::neighborhood_mean_no_jumps (get3dDirection's plane)
   float max_nb_d2 = 0.0f;
 };
 
@@ -239,6 +250,7 @@ bool surfaceInformation(const RangeImage& ri, int x, int y, int radius, const P4
   V3 view = normalized3(sub(ri.sensorPos(), v3(point.x, point.y, point.z)));
   if (dot3(normal, view) < 0.0f) normal = mul(normal, -1.0f);
   s.normal_no_jumps = normal;
+  s.mean_no_jumps = va.mean;  // `mean = vector_average.getMean ()`
   s.valid = true;
   return true;
 }
@@ -456,13 +468,17 @@ struct Border {
     V3 nbp = ri.calc3D((float)(x + dx), (float)(y + dy), point.range);
     const Surface& s = surf[(size_t)y * w + x];
     if (s.valid) {
-      V3 nrm = s.normal_no_jumps;
-      float d = dot3(sub(nbp, pt), nrm);
-      V3 proj = sub(nbp, mul(nrm, d));
-      direction = sub(proj, pt);
-    } else {
-      direction = sub(nbp, pt);
+      // "Get the point that lies on the local plane approximation": the viewing ray through the
+      // neighbour pixel meets the plane (normal_no_jumps, neighborhood_mean_no_jumps)
+      //   lambda = n.dot(mean - sensor) / n.dot(viewing_direction)
+      //   neighbor_point = lambda * viewing_direction + sensor_pos
+      const V3 sensor = ri.sensorPos();
+      const V3 vd = sub(nbp, sensor);
+      const V3 nrm = s.normal_no_jumps;
+      const float lambda = dot3(nrm, sub(s.mean_no_jumps, sensor)) / dot3(nrm, vd);
+      nbp = add(mul(vd, lambda), sensor);
     }
+    direction = sub(nbp, pt);
     direction = normalize3(direction);  // `direction.normalize ()`
     return true;
   }
@@ -642,8 +658,8 @@ void interestImage(const RangeImage& ri, const Border& B, const Params& P, std::
           float neg = 1.0f - 0.5f * scs * std::max(1.0f - distance_factor / P.optimal_distance_to_high_surface_change, 0.0f);
           neg = neg * neg;
           const float pos = (pixelDistance < 2.0) ? scs : scs * (1.0f - distance_factor);
-          // nkdGetDirectionAngle
-          V3 rot = v3(0.0f + dot3(tmp0, dir), 0.0f + dot3(tmp1, dir), 0.0f + dot3(tmp2, dir));
+          // nkdGetDirectionAngle: (rotation * direction).head<2> (), Affine3f * Vector3f (mv3 rows)
+          V3 rot = v3(0.0f + mv3(tmp0, dir), 0.0f + mv3(tmp1, dir), 0.0f + mv3(tmp2, dir));
           float inv = std::sqrt(rot.x * rot.x + rot.y * rot.y);
           float dvx = rot.x * (1.0f / inv);  // Vector2f::normalize (): times the reciprocal
           float angle = 0.5f * normAngle(2.0f * acosf_glibc(dvx));
@@ -753,7 +769,7 @@ void interestImageSparse(const RangeImage& ri, const Border& B, const Params& P,
         const float scs = B.scs[(size_t)index2];
         if (scs < P.min_surface_change_score) continue;
         const V3 dir = B.scd[(size_t)index2];
-        V3 rot = v3(0.0f + dot3(tmp0, dir), 0.0f + dot3(tmp1, dir), 0.0f + dot3(tmp2, dir));
+        V3 rot = v3(0.0f + mv3(tmp0, dir), 0.0f + mv3(tmp1, dir), 0.0f + mv3(tmp2, dir));
         float inv = std::sqrt(rot.x * rot.x + rot.y * rot.y);
         float dvx = rot.x * (1.0f / inv);
         float angle = 0.5f * normAngle(2.0f * acosf_glibc(dvx));
@@ -850,7 +866,7 @@ void interestImageSeeded(const RangeImage& ri, const Border& B, const Params& P,
           float neg = 1.0f - 0.5f * scs * std::max(1.0f - distance_factor / P.optimal_distance_to_high_surface_change, 0.0f);
           neg = neg * neg;
           const float pos = (pixelDistance < 2.0) ? scs : scs * (1.0f - distance_factor);
-          V3 rot = v3(0.0f + dot3(tmp0, dir), 0.0f + dot3(tmp1, dir), 0.0f + dot3(tmp2, dir));
+          V3 rot = v3(0.0f + mv3(tmp0, dir), 0.0f + mv3(tmp1, dir), 0.0f + mv3(tmp2, dir));
           float inv = std::sqrt(rot.x * rot.x + rot.y * rot.y);
           float dvx = rot.x * (1.0f / inv);
           float angle = 0.5f * normAngle(2.0f * acosf_glibc(dvx));

@@ -214,7 +214,8 @@ double orc_ransac_sample_threshold(const float* x, const float* y, const float* 
   float ev[3];
   orc::computeRoots(Sm, ev);
   for (int k = 0; k < 3; ++k) ev[k] *= scale;
-  const float ssum = (std::sqrt(ev[0]) + std::sqrt(ev[1])) + std::sqrt(ev[2]);
+  // `eigen_values.array ().sqrt ().sum ()` on a Vector3f: Redux.h's unrolled x + (y + z)
+  const float ssum = std::sqrt(ev[0]) + (std::sqrt(ev[1]) + std::sqrt(ev[2]));
   double t = (double)ssum / 3.0;
   return t * t;
 }

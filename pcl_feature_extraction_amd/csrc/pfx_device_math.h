@@ -4,8 +4,9 @@
 // (SURVEY.md Appendix A), so results are bit-identical to the CPU restatement:
 //   * compiled with -ffp-contract=off (no v_fma contraction), default IEEE div/sqrt
 //     (v_div_fixup / corrected v_sqrt sequences), f32 denormals on;
-//   * Eigen fixed-size Vector3f reductions: (x + y) + z; aligned Vector4f (SSE2 predux):
-//     (x + z) + (y + w);
+//   * Eigen 3.2 fixed-size Vector3f reductions (Redux.h redux_novec_unroller, HalfLength split):
+//     x + (y + z); aligned Vector4f (SSE2 predux): (x + z) + (y + w); a row of a small
+//     fixed-size matrix * vector product (CoeffBasedProduct): ((m0 v0 + m1 v1) + m2 v2);
 //   * atan2f / acosf: glibc's fdlibm float routines (e_atan2f.c, s_atanf.c, e_acosf.c) restated
 //     operation for operation (the oracle's are pinned bit for bit against the host libm);
 //     cosf / sinf as the correctly rounded result, evaluated in f64 (ocml) and rounded once;
@@ -23,8 +24,9 @@ __device__ __forceinline__ f3 sub3(f3 a, f3 b) { return mk3(a.x - b.x, a.y - b.y
 __device__ __forceinline__ f3 add3(f3 a, f3 b) { return mk3(a.x + b.x, a.y + b.y, a.z + b.z); }
 __device__ __forceinline__ f3 scale3(f3 a, float s) { return mk3(a.x * s, a.y * s, a.z * s); }
 __device__ __forceinline__ f3 div3(f3 a, float s) { return mk3(a.x / s, a.y / s, a.z / s); }
-__device__ __forceinline__ float dot3(f3 a, f3 b) { return (a.x * b.x + a.y * b.y) + a.z * b.z; }
-__device__ __forceinline__ float sqn3(f3 a) { return (a.x * a.x + a.y * a.y) + a.z * a.z; }
+__device__ __forceinline__ float dot3(f3 a, f3 b) { return a.x * b.x + (a.y * b.y + a.z * b.z); }
+__device__ __forceinline__ float sqn3(f3 a) { return a.x * a.x + (a.y * a.y + a.z * a.z); }
+__device__ __forceinline__ float mv3(f3 row, f3 v) { return (row.x * v.x + row.y * v.y) + row.z * v.z; }
 __device__ __forceinline__ float dot4(f3 a, f3 b) { return (a.x * b.x + a.z * b.z) + (a.y * b.y + 0.0f); }
 __device__ __forceinline__ float sqn4(f3 a) { return (a.x * a.x + a.z * a.z) + (a.y * a.y + 0.0f); }
 __device__ __forceinline__ f3 cross3(f3 a, f3 b) {

@@ -422,7 +422,7 @@ __global__ void __launch_bounds__(256) k_harris_refine(GridView g, const int32_t
       py = __shfl(py, 0);
       pz = __shfl(pz, 0);
       const float dx = px - ox, dy = py - oy, dz = pz - oz;
-      const float diff = (dx * dx + dy * dy) + dz * dz;
+      const float diff = dx * dx + (dy * dy + dz * dz);  // Vector3f squaredNorm (Redux.h x + (y + z))
       wave_lds_sync();  // the key region is rewritten by the next ball
       if (!(diff > 1e-6)) break;
     }

@@ -35,7 +35,7 @@ enum {
 
 struct NarfState {
   int w = 0, h = 0;
-  DevBuf direct, fill, pts, surf, svalid, sL, sR, sT, sB, uL, uR, uT, uB, shadow, traits, rawdir, dir, scs, scd,
+  DevBuf direct, fill, pts, surf, smean, svalid, sL, sR, sT, sB, uL, uR, uT, uB, shadow, traits, rawdir, dir, scs, scd,
       interest, cand, counters, rowp, sat, work, fb1, pk;
   std::vector<float> h_interest, h_scs, h_range;
   std::vector<uint32_t> h_traits;
@@ -57,7 +57,7 @@ struct NarfState {
     if (pinned) (void)hipHostFree(pinned);
     pinned = nullptr;
     pinned_bytes = 0;
-    DevBuf* all[] = {&direct, &fill, &pts, &surf, &svalid, &sL, &sR, &sT, &sB, &uL, &uR, &uT, &uB, &shadow,
+    DevBuf* all[] = {&direct, &fill, &pts, &surf, &smean, &svalid, &sL, &sR, &sT, &sB, &uL, &uR, &uT, &uB, &shadow,
                      &traits, &rawdir, &dir, &scs, &scd, &interest, &cand, &counters, &rowp, &sat, &work, &fb1, &pk};
     for (auto* b : all) b->release();
   }
@@ -168,12 +168,13 @@ struct VecAvg {
     f3 d = sub3(s, mean);
     mean = add3(mean, mk3(alpha * d.x, alpha * d.y, alpha * d.z));
     float om = 1.0f - alpha;
-    c00 = om * (c00 + alpha * (d.x * d.x));
-    c01 = om * (c01 + alpha * (d.x * d.y));
-    c02 = om * (c02 + alpha * (d.x * d.z));
-    c11 = om * (c11 + alpha * (d.y * d.y));
-    c12 = om * (c12 + alpha * (d.y * d.z));
-    c22 = om * (c22 + alpha * (d.z * d.z));
+    // `(1.0f-alpha)*(covariance_(i, j) + alpha*diff[i]*diff[j])`: (alpha * d_i) * d_j
+    c00 = om * (c00 + alpha * d.x * d.x);
+    c01 = om * (c01 + alpha * d.x * d.y);
+    c02 = om * (c02 + alpha * d.x * d.z);
+    c11 = om * (c11 + alpha * d.y * d.y);
+    c12 = om * (c12 + alpha * d.y * d.z);
+    c22 = om * (c22 + alpha * d.z * d.z);
   }
   __device__ void pca(float ev[3], f3 evec[3]) const {
     Sym3 m;
@@ -185,8 +186,9 @@ struct VecAvg {
 };
 
 // RangeImage::getSurfaceInformation (no-jumps part), radius/step from the border parameters
+// surf = (normal_no_jumps, max_neighbor_distance_squared), smean = neighborhood_mean_no_jumps
 __global__ void k_surface(Img I, const float4* __restrict__ P, int radius, int step, int no_of_closest,
-                          float4* __restrict__ surf, uint8_t* __restrict__ svalid) {
+                          float4* __restrict__ surf, float4* __restrict__ smean, uint8_t* __restrict__ svalid) {
   int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= I.w * I.h) return;
   svalid[i] = 0;
@@ -224,6 +226,7 @@ __global__ void k_surface(Img I, const float4* __restrict__ P, int radius, int s
   f3 view = normalized3(sub3(sensor, mk3(point.x, point.y, point.z)));
   if (dot3(normal, view) < 0.0f) normal = scale3(normal, -1.0f);
   surf[i] = make_float4(normal.x, normal.y, normal.z, maxd2);
+  smean[i] = make_float4(va.mean.x, va.mean.y, va.mean.z, 0.0f);
   svalid[i] = 1;
 }
 
@@ -418,9 +421,9 @@ __global__ void k_classify(Img I, int prb, const float* __restrict__ sL, const f
   if (own) atomicOr(&traits[i], own);
 }
 
-// get3dDirection for obstacle borders; rawdir.w = 1 if valid
+// RangeImageBorderExtractor::get3dDirection for obstacle borders; rawdir.w = 1 if valid
 __global__ void k_border_dir_raw(Img I, const float4* __restrict__ P, const float4* __restrict__ surf,
-                                 const uint8_t* __restrict__ svalid, const uint32_t* __restrict__ traits,
+                                 const float4* __restrict__ smean, const uint8_t* __restrict__ svalid, const uint32_t* __restrict__ traits,
                                  float4* __restrict__ rawdir) {
   int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= I.w * I.h) return;
@@ -437,17 +440,17 @@ __global__ void k_border_dir_raw(Img I, const float4* __restrict__ P, const floa
       float4 point = P[i];
       f3 pt = mk3(point.x, point.y, point.z);
       f3 nbp = calc3d(I, (float)(x + dx), (float)(y + dy), point.w);
-      f3 d;
       if (svalid[i]) {
-        float4 s = surf[i];
-        f3 nrm = mk3(s.x, s.y, s.z);
-        float k = dot3(sub3(nbp, pt), nrm);
-        f3 proj = sub3(nbp, scale3(nrm, k));
-        d = sub3(proj, pt);
-      } else {
-        d = sub3(nbp, pt);
+        // the neighbour pixel's viewing ray meets the local plane (normal_no_jumps,
+        // neighborhood_mean_no_jumps): lambda = n.(mean - sensor) / n.(nbp - sensor)
+        const float4 s = surf[i], m = smean[i];
+        const f3 nrm = mk3(s.x, s.y, s.z);
+        const f3 sensor = mk3(I.to_world.m[3], I.to_world.m[7], I.to_world.m[11]);
+        const f3 vd = sub3(nbp, sensor);
+        const float lambda = dot3(nrm, sub3(mk3(m.x, m.y, m.z), sensor)) / dot3(nrm, vd);
+        nbp = add3(scale3(vd, lambda), sensor);
       }
-      d = normalize3(d);  // get3dDirection: `direction.normalize ()`
+      f3 d = normalize3(sub3(nbp, pt));  // get3dDirection: `direction.normalize ()`
       out = make_float4(d.x, d.y, d.z, 1.0f);
     }
   }
@@ -686,7 +689,8 @@ __device__ __forceinline__ void contribute(const InterestParams& ip, float sc, f
   const float df = ip.radius_reciprocal * distance;
   const float neg = negative_score(ip, sc, df);
   const float pos = (pd < 2.0f) ? sc : sc * (1.0f - df);
-  const f3 rot = mk3(0.0f + dot3(tmp0, dir), 0.0f + dot3(tmp1, dir), 0.0f + dot3(tmp2, dir));
+  // (rotation * direction).head<2> (): Affine3f * Vector3f, rows left to right
+  const f3 rot = mk3(0.0f + mv3(tmp0, dir), 0.0f + mv3(tmp1, dir), 0.0f + mv3(tmp2, dir));
   const float nrm = sqrtf(rot.x * rot.x + rot.y * rot.y);
   const float dvx = rot.x * (1.0f / nrm);  // Vector2f::normalize (): times the reciprocal
   const int cell = angle_cell(dvx, ip.d90, ip.d180);
@@ -1309,6 +1313,7 @@ int64_t narf_dev(pfx_ctx* ctx, const float* x, const float* y, const float* z, i
   float4* P = S.pts.as<float4>(npx);
   range_image_dev(ctx, x, y, z, n, cam, P);
   float4* surf = S.surf.as<float4>(npx);
+  float4* smean = S.smean.as<float4>(npx);
   uint8_t* svalid = S.svalid.as<uint8_t>(npx);
   float *sL = S.sL.as<float>(npx), *sR = S.sR.as<float>(npx), *sT = S.sT.as<float>(npx), *sB = S.sB.as<float>(npx);
   float *uL = S.uL.as<float>(npx), *uR = S.uR.as<float>(npx), *uT = S.uT.as<float>(npx), *uB = S.uB.as<float>(npx);
@@ -1325,7 +1330,7 @@ int64_t narf_dev(pfx_ctx* ctx, const float* x, const float* y, const float* z, i
     TimeScope ts(ctx, "narf_border");
     const int step = (p.pixel_radius_plane_extraction / 2) + 1;
     const int nn = (int)std::pow((double)(p.pixel_radius_plane_extraction / step + 1), 2.0);
-    k_surface<<<nblk(npx), 256, 0, st>>>(I, P, p.pixel_radius_plane_extraction, step, nn, surf, svalid);
+    k_surface<<<nblk(npx), 256, 0, st>>>(I, P, p.pixel_radius_plane_extraction, step, nn, surf, smean, svalid);
     k_border_scores<<<nblk(npx), 256, 0, st>>>(I, P, surf, svalid, p.pixel_radius_borders, sL, sR, sT, sB);
     k_update_scores<<<nblk(npx), 256, 0, st>>>(I, p.minimum_border_probability, sL, sR, sT, sB, uL, uR, uT, uB);
     PFX_HIP(hipMemsetAsync(sh, 0xff, sizeof(int4) * npx, st));
@@ -1335,7 +1340,7 @@ int64_t narf_dev(pfx_ctx* ctx, const float* x, const float* y, const float* z, i
     k_shadow_lt<<<nblk(npx), 256, 0, st>>>(I, P, p.pixel_radius_borders, p.minimum_border_probability, uL, uR, uT,
                                            uB, sh);
     k_classify<<<nblk(npx), 256, 0, st>>>(I, p.pixel_radius_borders, uL, uR, uT, uB, sh, traits);
-    k_border_dir_raw<<<nblk(npx), 256, 0, st>>>(I, P, surf, svalid, traits, rawdir);
+    k_border_dir_raw<<<nblk(npx), 256, 0, st>>>(I, P, surf, smean, svalid, traits, rawdir);
     const float deg = 0.017453292519943295769236907684886127134428718885417f;
     const float min_cos = (float)std::cos((double)(120.0f * deg));
     const float thr = 0.95f * p.minimum_border_probability;
@@ -1481,7 +1486,8 @@ int64_t narf_dev(pfx_ctx* ctx, const float* x, const float* y, const float* z, i
     bool too_close = false;
     for (const HostInterestPoint& b : accepted) {
       float dx = a.x - b.x, dy = a.y - b.y, dz = a.z - b.z;
-      if (dx * dx + dy * dy + dz * dz < min_d2) { too_close = true; break; }
+      // (a - b).squaredNorm () on Vector3f maps: dx^2 + (dy^2 + dz^2)
+      if (dx * dx + (dy * dy + dz * dz) < min_d2) { too_close = true; break; }
     }
     if (too_close) continue;
     accepted.push_back(a);

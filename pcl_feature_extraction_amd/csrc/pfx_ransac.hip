@@ -195,7 +195,8 @@ __global__ void k_ransac_threshold(const float* __restrict__ x, const float* __r
   float ev[3];
   computeRoots(c00 / scale, c01 / scale, c02 / scale, c11 / scale, c12 / scale, c22 / scale, ev);
   for (int k = 0; k < 3; ++k) ev[k] *= scale;
-  const float ssum = (sqrtf(ev[0]) + sqrtf(ev[1])) + sqrtf(ev[2]);
+  // `eigen_values.array ().sqrt ().sum ()` on a Vector3f: Redux.h's unrolled x + (y + z)
+  const float ssum = sqrtf(ev[0]) + (sqrtf(ev[1]) + sqrtf(ev[2]));
   const double t = (double)ssum / 3.0;
   *out = t * t;
 }
