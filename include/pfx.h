@@ -70,7 +70,14 @@ typedef struct pfx_narf_params {
   float min_interest_value;                      /* 0.45                    */
   float min_surface_change_score;                /* 0.2                     */
   int32_t do_non_maximum_suppression;            /* 1                       */
-  int32_t calculate_sparse_interest_image;       /* 1 (same keypoints) */
+  /* 1 (PCL's default).  Either value computes NarfKeypoint's COMPLETE interest formula
+   * (calculateCompleteInterestImage); 1 only skips pixels that provably cannot reach
+   * min_interest_value, so 0 and 1 give the same keypoints.  PCL 1.7's own sparse heuristics
+   * (calculateSparseInterestImage, source absent here) are NOT reproduced: parity with that
+   * mode is unpinned, with a measured sensitivity of 1-2 keypoints per reference cloud
+   * (DESIGN.md section 5).  pfx_ctx_last_stats(ctx, "narf_interest_formula") = 0 after every
+   * NARF call (0 = complete formula). */
+  int32_t calculate_sparse_interest_image;
   int32_t no_of_polynomial_approximations_per_point; /* 0 (only 0 supported) */
   int32_t add_points_on_straight_edges;          /* 0 (only 0 supported)    */
   /* RangeImageBorderExtractor::Parameters */
@@ -127,8 +134,10 @@ pfx_status pfx_ctx_reset_timing(pfx_ctx* ctx);
 /* Accumulated device time and launch count of the kernel `name`; syncs the stream. */
 pfx_status pfx_ctx_kernel_time(pfx_ctx* ctx, const char* name, double* total_ms,
                                int64_t* launches);
-/* Count of neighbours gathered by the last normals call (sum over queries of |N_r(q)|) --
- * the per-launch unit count for the neighbour-gather roofline. */
+/* Statistics of the last calls on ctx, by name: e.g. "normals_neighbors" (sum over queries of
+ * |N_r(q)| of the last normals call -- the per-launch unit count for the neighbour-gather
+ * roofline), "narf_keypoints", "narf_interest_formula" (0 = NarfKeypoint's complete formula, the
+ * only one implemented; see pfx_narf_params.calculate_sparse_interest_image). */
 pfx_status pfx_ctx_last_stats(pfx_ctx* ctx, const char* what, int64_t* value);
 
 /* ---- radius search (FLANN semantics) ---------------------------------------------- */

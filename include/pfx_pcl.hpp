@@ -481,6 +481,10 @@ class NarfKeypoint {
     int no_of_polynomial_approximations_per_point = 0;
     int max_no_of_threads = 1;
     bool use_recursive_scale_reduction = false;
+    // PCL's default (true).  Both values compute the COMPLETE interest formula here (true only
+    // prunes pixels that cannot reach min_interest_value: same keypoints); PCL 1.7's sparse
+    // heuristics are not reproduced -- unpinned, measured sensitivity 1-2 keypoints per reference
+    // cloud (pfx.h)
     bool calculate_sparse_interest_image = true;
   };
   explicit NarfKeypoint(RangeImageBorderExtractor* border_extractor = nullptr, float support_size = -1.0f)

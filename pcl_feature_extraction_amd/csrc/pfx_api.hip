@@ -171,6 +171,10 @@ void* pfx_ctx_get_stream(pfx_ctx* ctx) {
 pfx_status pfx_ctx_trim(pfx_ctx* ctx) {
   PFX_API_BEGIN
   check_ctx(ctx);
+  // a split estimation still owes its lists check (normals_launch_dev): conclude it first, so
+  // the outputs it launched are validated (and rerun if needed) before its state goes
+  pfx::normals_finish_dev(ctx);
+  ctx->lists_gate = nullptr;  // a borrowed event the next call must not wait on
   PFX_HIP(hipStreamSynchronize(ctx->stream));
   pfx::fpfh_resolve(ctx);
   pfx::narf_release(ctx);

@@ -1505,6 +1505,9 @@ int64_t narf_dev(pfx_ctx* ctx, const float* x, const float* y, const float* z, i
   S.have_debug = true;
   ctx->stats["narf_candidates"] = nc;
   ctx->stats["narf_keypoints"] = (int64_t)out.size();
+  // which interest formula ran: 0 = NarfKeypoint::calculateCompleteInterestImage (both values of
+  // calculate_sparse_interest_image; PCL's sparse heuristics are not reproduced -- pfx.h)
+  ctx->stats["narf_interest_formula"] = 0;
   return (int64_t)out.size();
 }
 

@@ -1170,12 +1170,17 @@ void build_lists(pfx_ctx* ctx, const Grid& G, const uint8_t* mask, double radius
     }
     read_back();
     if ((!(ran_mids & 1) && rb->cnt[14] > 0) || (!(ran_mids & 2) && rb->cnt[12] > 0)) {
-      // a skipped per-query tier had work: run it and the tiers after it (each launch takes its
-      // queue from where an earlier launch stopped, so only the new entries are listed)
+      // a skipped per-query tier had work: run it and the tiers after it.  A launch that drained
+      // its queue left the head at count + gridDim (every workgroup's last fetch overshoots), so
+      // the head of each tier that already ran is first set back to the count it drained: the
+      // relaunch then takes exactly the entries the catch-up launches append
+      if (ran_mids & 2) PFX_HIP(hipMemcpyAsync(counters + 13, counters + 12, sizeof(int), hipMemcpyDeviceToDevice, st));
+      if (hs.ptr) PFX_HIP(hipMemcpyAsync(counters + 9, counters + 3, sizeof(int), hipMemcpyDeviceToDevice, st));
       if (!(ran_mids & 1) && rb->cnt[14] > 0) launch_mid8();
       launch_mid();
       if (hs.ptr) launch_huge();
       read_back();
+      ++ctx->stats[std::string(tag) + "_tier_catchups"];
     }
     note_mid_tiers(ctx, tag, rb->cnt);
     if (!hs.ptr && rb->cnt[3] > 0) {  // very long lists, first time: allocate the scratch and sort them

@@ -607,6 +607,15 @@ static void wait_lists_gate(pfx_ctx* ctx) {
   PFX_HIP(hipStreamWaitEvent(ctx->stream, e, 0));
 }
 
+// The gate is borrowed for one normal-estimation call: whichever way the call ends (no points,
+// no list build, an error before the wait), the event is dropped with it, so no later call waits
+// on an event the caller may have destroyed.
+struct GateScope {
+  pfx_ctx* ctx;
+  explicit GateScope(pfx_ctx* c) : ctx(c) {}
+  ~GateScope() { ctx->lists_gate = nullptr; }
+};
+
 void normals_release(pfx_ctx* ctx) {
   delete ctx->normals;
   ctx->normals = nullptr;
@@ -616,6 +625,7 @@ void normals_release(pfx_ctx* ctx) {
 // NaN-filled (non-finite points are not queries: PCL writes NaN).
 void normals_lists_dev(pfx_ctx* ctx, const float* x, const float* y, const float* z, int64_t n, double r,
                        float* nx, float* ny, float* nz, float* curv) {
+  GateScope gate_scope(ctx);
   PFX_CHECK(r > 0.0, "normals: radius must be > 0");
   PFX_CHECK(n >= 0, "normals: negative point count");
   if (!ctx->normals) ctx->normals = new NormalsState();
@@ -810,6 +820,7 @@ bool normals_conclude(pfx_ctx* ctx, bool ok, const float* x, const float* y, con
 // normals_launch_dev + normals_finish_dev take the check off the caller's path altogether.
 void normals_dev(pfx_ctx* ctx, const float* x, const float* y, const float* z, int64_t n, double r,
                  const float vp[3], float* nx, float* ny, float* nz, float* curv) {
+  GateScope gate_scope(ctx);
   TimeScope total(ctx, "normals", true);
   PFX_CHECK(r > 0.0, "normals: radius must be > 0");
   PFX_CHECK(n >= 0, "normals: negative point count");
@@ -834,6 +845,7 @@ void normals_dev(pfx_ctx* ctx, const float* x, const float* y, const float* z, i
 // are trusted: it validates and, rarely, reruns the exact path (the consumer then reruns too).
 void normals_launch_dev(pfx_ctx* ctx, const float* x, const float* y, const float* z, int64_t n, double r,
                         const float vp[3], float* nx, float* ny, float* nz, float* curv) {
+  GateScope gate_scope(ctx);
   TimeScope total(ctx, "normals", true);
   PFX_CHECK(r > 0.0, "normals: radius must be > 0");
   PFX_CHECK(n >= 0, "normals: negative point count");
@@ -888,6 +900,7 @@ void normals_prepare_dev(pfx_ctx* ctx, const float* x, const float* y, const flo
 void normals_subset_dev(pfx_ctx* ctx, const float* x, const float* y, const float* z, int64_t n, double r,
                         const uint8_t* mask, int want, const float vp[3], float* nx, float* ny, float* nz,
                         float* curv) {
+  GateScope gate_scope(ctx);
   TimeScope total(ctx, "normals", true);
   PFX_CHECK(r > 0.0, "normals: radius must be > 0");
   PFX_CHECK(n >= 0, "normals: negative point count");

@@ -12,7 +12,7 @@ i=0
 for P in "$P1" "$P2" "$P3" "$P4"; do
   i=$((i+1))
   timeout -k 10 300 rocprofv3 --kernel-trace --pmc $P --output-format csv -d $R/gpurun_out/pmc_$TAG/p$i -o run -- \
-    python3 $R/bench.py --steps 1 --warmup 1 --no-cpu-baseline > $R/gpurun_out/pmc_$TAG/p$i.log 2>&1 || exit 1
+    python3 $R/bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-e2e > $R/gpurun_out/pmc_$TAG/p$i.log 2>&1 || exit 1
 done
 python3 $R/scripts/pmc_summary.py $R/gpurun_out/pmc_$TAG k_normals_chain,k_normals_chain_big $R/gpurun_out/pmc_$TAG/pmc_normals_chain.json > $R/gpurun_out/pmc_$TAG/summary.txt
 # the whole neighbour-gather stage (grid kernels excluded: shared with the FPFH grid in the step)

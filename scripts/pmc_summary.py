@@ -64,8 +64,14 @@ if len(sys.argv) > 3:
                 per[k]["SQ_WAIT_ANY_frac"] = a["SQ_WAIT_ANY"] / a["SQ_WAVE_CYCLES"]
             if a.get("SQ_ACTIVE_INST_LDS"):
                 per[k]["lds_conflict_per_active"] = a.get("SQ_LDS_BANK_CONFLICT", 0.0) / a["SQ_ACTIVE_INST_LDS"]
+    # the build the counters describe: bench.py reports whether its own libpfx.so is that build
+    import hashlib
+    import os
+    lib = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "pcl_feature_extraction_amd",
+                       "libpfx.so")
+    lib_sha16 = hashlib.sha256(open(lib, "rb").read()).hexdigest()[:16] if os.path.exists(lib) else None
     with open(dest, "w") as f:
-        json.dump({"kernel": " + ".join(found), "hbm_bytes_per_launch": int(fetch + write),
+        json.dump({"kernel": " + ".join(found), "hbm_bytes_per_launch": int(fetch + write), "libpfx_sha16": lib_sha16,
                    "stage_hbm_bytes_per_launch": int(fetch + write),
                    "fetch_bytes_x2": int(fetch), "write_bytes": int(write), "kernels": per,
                    "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes, FETCH x2 "

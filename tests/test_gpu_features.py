@@ -113,6 +113,84 @@ def test_normals_every_list_path(ctx):
         assert _nan_aware_equal(a, b)
 
 
+def _every_list_cloud():
+    rng = np.random.default_rng(23)
+    sparse = np.c_[rng.uniform(0, 1, (4000, 2)), np.full(4000, 1.0)]
+    dense = np.c_[rng.uniform(2, 2.3, (9000, 2)), np.full(9000, 1.0)]
+    mid8 = np.repeat(rng.normal(0, 0.004, (1700, 3)) + [6, 6, 1], 3, axis=0)   # k = 5100 (4k-8k tier)
+    mid = np.repeat(rng.normal(0, 0.004, (3500, 3)) + [7, 7, 1], 3, axis=0)    # k = 10500 (8k-16k tier)
+    huge = np.repeat(rng.normal(0, 0.004, (5500, 3)) + [8, 8, 1], 3, axis=0)   # k = 16500 (global scratch)
+    return sparse, dense, mid8, mid, huge
+
+
+def _xyz(*parts):
+    pts = np.concatenate(parts).astype(np.float32)
+    return pts[:, 0].copy(), pts[:, 1].copy(), pts[:, 2].copy()
+
+
+def test_list_tier_hints_every_path_fresh_context():
+    """The 4k-8k / 8k-16k per-query list tiers launch only while a recent build of the (context,
+    tag) had work for them (pfx_nblist.hip mid_tier_wanted).  On a fresh context, once the hints
+    have decayed (17 builds without such lists), a cloud that needs the skipped tiers must still
+    come out exact on every path: the non-deferred catch-up with the global scratch already
+    allocated (the huge tier, which already ran on an empty queue, restarts at the count it drained --
+    ADVICE r03 high: the lists the catch-up appends were never fetched), with one or both tiers
+    skipped, and the deferred check's exact rebuild.  (Lists over 4k always pass through the 4k-8k
+    queue, so that hint cannot decay while the 8k-16k one is on.)"""
+    import torch
+    from pcl_feature_extraction_amd import Context
+    sparse, dense, mid8, mid, huge = _every_list_cloud()
+    ex, ey, ez = _xyz(sparse, dense, mid8, mid, huge)
+    ref = O.normals(ex, ey, ez, 0.05)
+    dev = torch.device("cuda", 0)
+
+    def dev_arrays(x, y, z):
+        t = [torch.from_numpy(a).to(dev) for a in (x, y, z)]
+        o = [torch.empty(len(x), dtype=torch.float32, device=dev) for _ in range(4)]
+        torch.cuda.synchronize()  # (the context runs on its own stream)
+        return t, o
+
+    with Context(0) as c:
+        def lists_only(x, y, z):  # a non-deferred build of tag "normals" (pfx_normals_lists_dev)
+            (tx, ty, tz), o = dev_arrays(x, y, z)
+            c.normals_lists_dev(tx, ty, tz, 0.05, *o)
+            c.synchronize()
+
+        def every_two_phase():
+            (tx, ty, tz), o = dev_arrays(ex, ey, ez)
+            c.normals_lists_dev(tx, ty, tz, 0.05, *o)
+            c.normals_chains_dev(c, *o)
+            c.synchronize()
+            for a, b in zip(o, ref):
+                assert _nan_aware_equal(a.cpu().numpy(), b)
+
+        def catchups():
+            try:
+                return c.stat("normals_tier_catchups")
+            except Exception:
+                return 0
+
+        every_two_phase()                          # first build: every tier, scratch allocated
+        assert c.stat("normals_huge") > 0 and c.stat("normals_mid") > 0 and c.stat("normals_mid8") > 0
+        sx, sy, sz = _xyz(sparse, mid8)
+        for _ in range(17):
+            lists_only(sx, sy, sz)                 # the 8k-16k hint decays, the 4k-8k one stays
+        before = catchups()
+        every_two_phase()                          # 8k-16k skipped: catch-up of it, then huge again
+        assert catchups() == before + 1
+        px, py, pz = _xyz(sparse)
+        for _ in range(17):
+            lists_only(px, py, pz)                 # both hints decay
+        before = catchups()
+        every_two_phase()                          # both skipped: catch-up of every per-query tier
+        assert catchups() == before + 1
+        for _ in range(17):
+            lists_only(px, py, pz)
+        g = c.normals(ex, ey, ez, 0.05)            # deferred build (normals_dev): check + exact rebuild
+        for a, b in zip(g, ref):
+            assert _nan_aware_equal(a, b)
+
+
 def test_normals_speculative_grid_and_list_check():
     """normals_dev builds the grid on the previous call's widened bounds and validates grid and
     lists in one readback (pfx_normals.hip normals_dev): a scan outside the hint, a list buffer

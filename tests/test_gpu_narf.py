@@ -64,6 +64,9 @@ def test_narf_keypoints_bit_exact(ctx, name):
     assert np.array_equal(kp, okp)
     assert len(kp) > 0
     assert np.all(np.diff(kp) > 0)  # ascending pixel indices
+    # the boundary reports which interest formula ran: the complete one, in both modes
+    # (PCL's own sparse heuristics are not reproduced; pfx.h pfx_narf_params)
+    assert ctx.stat("narf_interest_formula") == 0
 
 
 def test_narf_empty_cloud(ctx):
