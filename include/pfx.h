@@ -450,6 +450,14 @@ const char* pfx_batch_last_error(const pfx_batch* batch);
  * copied out in scan order: rows[s] = K_s, scan s's rows start at sum_{t<s} K_t of desc
  * (cap_rows x 33) and idx (cap_rows).  Results equal the per-scan entry points bit for bit.
  * PFX_ERR_CAPACITY (rows filled in) when sum K_s > cap_rows. */
+/* The batch's host-side plan (no device work; pfx_batch_narf_fpfh follows it): scan s runs on
+ * device device_of_scan[s] = s % n_devices as that device's slot slot_of_scan[s] = s / n_devices
+ * (its scans pipelined in slot order), and given each scan's descriptor rows K_s, its rows land at
+ * row_offset[s] = sum_{t<s} K_t of the gathered output (row_offset has n_scans + 1 entries: the last
+ * is the total).  Any output pointer may be NULL.  PFX_ERR_INVALID for n_scans < 0,
+ * n_devices <= 0 or a negative K_s. */
+pfx_status pfx_batch_plan(int n_scans, int n_devices, const int64_t* rows_per_scan, int32_t* device_of_scan,
+                          int32_t* slot_of_scan, int64_t* row_offset);
 pfx_status pfx_batch_narf_fpfh(pfx_batch* batch, int n_scans, const float* const* x, const float* const* y,
                                const float* const* z, const int64_t* n, const pfx_camera* cam,
                                const pfx_narf_params* params, double normal_radius, double feature_radius,

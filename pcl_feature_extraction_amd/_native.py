@@ -147,6 +147,7 @@ _SIGS = {
                                        ctypes.c_int32, ctypes.c_int32, c_vp, c_i64, c_i64p, c_vp, c_vp, c_i64p, c_vp,
                                        c_vp]),
     "pfx_batch_create": (c_int, [c_vp, c_int, ctypes.POINTER(c_vp)]),
+    "pfx_batch_plan": (c_int, [c_int, c_int, c_vp, c_vp, c_vp, c_vp]),
     "pfx_batch_destroy": (None, [c_vp]),
     "pfx_batch_last_error": (ctypes.c_char_p, [c_vp]),
     "pfx_batch_narf_fpfh": (c_int, [c_vp, c_int, c_vp, c_vp, c_vp, c_vp, ctypes.POINTER(Camera),

@@ -484,6 +484,21 @@ class Context:
         return keep[: nk.value].copy(), T.reshape(4, 4)
 
 
+def batch_plan(n_scans, n_devices, rows_per_scan=None):
+    """pfx_batch_plan (host only, no device): (device_of_scan, slot_of_scan, row_offset[n_scans + 1])
+    of the batch's round-robin deal and scan-order gather layout."""
+    lib = N.lib()
+    dev = np.zeros(max(n_scans, 1), np.int32)
+    slot = np.zeros(max(n_scans, 1), np.int32)
+    off = np.zeros(n_scans + 1, np.int64)
+    rows = None if rows_per_scan is None else np.ascontiguousarray(rows_per_scan, np.int64)
+    st = lib.pfx_batch_plan(int(n_scans), int(n_devices), None if rows is None else _ptr(rows), _ptr(dev), _ptr(slot),
+                            _ptr(off))
+    if st != 0:
+        raise N.PfxError(st, "pfx_batch_plan")
+    return dev[:n_scans], slot[:n_scans], off
+
+
 class Batch:
     """pfx_batch: the multi-GPU scan batch of one process; scan s on devices[s % G],
     results gathered on devices[0] over RCCL and returned in scan order."""

@@ -15,6 +15,7 @@
 // sequential, a spatial split of the normals would need an r-halo).
 #include <rccl/rccl.h>
 
+#include <algorithm>
 #include <condition_variable>
 #include <exception>
 #include <mutex>
@@ -35,6 +36,10 @@ namespace {
 
 void ok(pfx_ctx* ctx, pfx_status st) {
   if (st != PFX_OK) throw Error(st, pfx_last_error(ctx));
+}
+
+void plan_ok(pfx_status st) {
+  if (st != PFX_OK) throw Error(st, "batch: invalid scan / device counts for the plan");
 }
 
 struct ScanSlot {
@@ -214,6 +219,23 @@ void destroy(pfx_batch* b) {
 
 extern "C" {
 
+pfx_status pfx_batch_plan(int n_scans, int n_devices, const int64_t* rows_per_scan, int32_t* device_of_scan,
+                          int32_t* slot_of_scan, int64_t* row_offset) {
+  if (n_scans < 0 || n_devices <= 0) return PFX_ERR_INVALID;
+  int64_t acc = 0;
+  if (row_offset) row_offset[0] = 0;
+  for (int s = 0; s < n_scans; ++s) {
+    if (device_of_scan) device_of_scan[s] = s % n_devices;  // round-robin deal
+    if (slot_of_scan) slot_of_scan[s] = s / n_devices;
+    if (rows_per_scan) {
+      if (rows_per_scan[s] < 0) return PFX_ERR_INVALID;
+      acc += rows_per_scan[s];
+    }
+    if (row_offset) row_offset[s + 1] = acc;  // scan-order layout of the gathered rows
+  }
+  return PFX_OK;
+}
+
 pfx_status pfx_batch_create(const int* devices, int n_devices, pfx_batch** out) {
   if (!out) return PFX_ERR_INVALID;
   *out = nullptr;
@@ -276,17 +298,18 @@ pfx_status pfx_batch_narf_fpfh(pfx_batch* b, int n_scans, const float* const* x,
       if (n[s] < 0 || (n[s] && (!x[s] || !y[s] || !z[s])))
         throw Error(PFX_ERR_INVALID, "batch_narf_fpfh: invalid scan " + std::to_string(s));
     const int G = (int)b->devs.size();
-    // deal the scans round-robin (scan s on device s % G), slots reused across calls
-    for (int d = 0; d < G; ++d) {
-      Device& D = b->devs[(size_t)d];
-      size_t m = 0;
-      for (int s = d; s < n_scans; s += G) ++m;
-      if (D.slots.size() < m) D.slots.resize(m);
-      D.active = m;
-      for (size_t i = 0; i < m; ++i) {
-        D.slots[i].scan = d + (int)i * G;
-        D.slots[i].rows = 0;
-      }
+    // deal the scans (pfx_batch_plan: scan s on device s % G as its slot s / G), slots reused
+    // across calls
+    std::vector<int32_t> dev_of((size_t)n_scans), slot_of((size_t)n_scans);
+    plan_ok(pfx_batch_plan(n_scans, G, nullptr, dev_of.data(), slot_of.data(), nullptr));
+    for (Device& D : b->devs) D.active = 0;
+    for (int s = 0; s < n_scans; ++s) {
+      Device& D = b->devs[(size_t)dev_of[(size_t)s]];
+      const size_t i = (size_t)slot_of[(size_t)s];
+      if (D.slots.size() <= i) D.slots.resize(i + 1);
+      D.active = std::max(D.active, i + 1);
+      D.slots[i].scan = s;
+      D.slots[i].rows = 0;
     }
     std::vector<std::exception_ptr> errs((size_t)G);
     std::vector<std::thread> th;
@@ -301,11 +324,11 @@ pfx_status pfx_batch_narf_fpfh(pfx_batch* b, int n_scans, const float* const* x,
     for (auto& t : th) t.join();
     for (auto& e : errs)
       if (e) std::rethrow_exception(e);
-    // scan-order row offsets on the first device
+    // scan-order row offsets on the first device (pfx_batch_plan)
     std::vector<int64_t> off((size_t)n_scans + 1, 0), k((size_t)n_scans, 0);
     for (Device& D : b->devs)
       for (size_t i = 0; i < D.active; ++i) k[(size_t)D.slots[i].scan] = D.slots[i].rows;
-    for (int s = 0; s < n_scans; ++s) off[(size_t)s + 1] = off[(size_t)s] + k[(size_t)s];
+    plan_ok(pfx_batch_plan(n_scans, G, k.data(), nullptr, nullptr, off.data()));
     const int64_t total = off[(size_t)n_scans];
     for (int s = 0; s < n_scans; ++s) rows[s] = k[(size_t)s];
     if (total > cap_rows)

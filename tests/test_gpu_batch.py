@@ -5,8 +5,9 @@ torch.distributed process group (RCCL) -- the per-scan loop of evaluation.cpp:27
 
 Bar: every gathered scan's (K_s x 33 descriptors, K_s cloud indices) equals a single-scan
 pipeline.narf_fpfh run on fresh contexts bit for bit, and two scans equal the CPU restatement
-(oracle/, parity vs real PCL unpinned: DESIGN.md).  N per scan is reduced to 200k points to keep
-the suite short; the full-size batch runs in bench.py (`--scans 8`)."""
+(oracle/, parity vs real PCL unpinned: DESIGN.md) -- at 200k points per scan (every scan against a
+fresh single-scan pass), and at configs[4]'s own 1M points per scan (both batch paths, two scans
+against the oracle)."""
 import os
 import socket
 
@@ -93,3 +94,64 @@ def test_config4_batch_gather_matches_single_scan_and_oracle():
         od = O.fpfh(x, y, z, nx, ny, nz, x[rows], y[rows], z[rows], 0.08, threads=16)
         assert np.array_equal(_bits(got[s][0]), _bits(od)), s
         assert np.array_equal(got[s][1], rows.astype(np.int32)), s
+
+
+N_FULL = 1_000_000
+
+
+def test_config4_full_size_batch_both_paths_and_oracle():
+    """configs[4] at its own size on the one GPU: the 8 x 1M-point room scans (seeds 100-107)
+    through bench.py's batch path (BatchNarfFpfh + dist.gather_to_root over RCCL at world 1) and
+    through the C-ABI batch (pfx_batch_narf_fpfh: host scans in, scan-order rows out): both agree
+    bit for bit on every scan, and scans 0 and 5 equal the CPU restatement at full size
+    (keypoints, descriptor rows, cloud indices)."""
+    import torch
+    import torch.distributed as dist
+    from pcl_feature_extraction_amd import Batch, Context
+    from pcl_feature_extraction_amd.dist import gather_to_root, in_scan_order
+    from pcl_feature_extraction_amd.pipeline import BatchNarfFpfh, alloc, keypoint_rows
+    from pcl_feature_extraction_amd.synth import synth_room
+
+    dev = torch.device("cuda", 0)
+    clouds = [tuple(np.ascontiguousarray(a) for a in synth_room(N_FULL, s)[:3]) for s in SEEDS]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    try:
+        scans = []
+        for c in clouds:
+            b = alloc(torch, N_FULL, dev, max_keypoints=4096)
+            for t, a in zip((b.x, b.y, b.z), c):
+                t.copy_(torch.from_numpy(a))
+            scans.append(b)
+        ctx, ctx_n = Context(0), Context(0)
+        run = BatchNarfFpfh(torch, ctx, ctx_n, dev)
+        res = run(scans)
+        run.check()
+        blocks = [(b.desc[:k], torch.from_numpy(keypoint_rows(kp, N_FULL).astype(np.int32)).to(dev))
+                  for b, (kp, k) in zip(scans, res)]
+        got = in_scan_order(gather_to_root(torch, dist, blocks, 33, dev, len(SEEDS)), len(SEEDS), 1)
+        torch.cuda.synchronize(dev)
+        got = [(d.cpu().numpy(), i.cpu().numpy()) for d, i in got]
+        kps = [np.asarray(kp) for kp, _ in res]
+        run.close()
+        ctx.close()
+        ctx_n.close()
+        del scans, blocks
+    finally:
+        dist.destroy_process_group()
+    with Batch([0]) as bt:
+        cab = bt.narf_fpfh(clouds)
+    assert len(cab) == len(SEEDS)
+    for s in range(len(SEEDS)):
+        assert len(got[s][1]) > 0, s
+        assert np.array_equal(cab[s][1], got[s][1]), s
+        assert np.array_equal(_bits(cab[s][0]), _bits(got[s][0])), s
+    for s in (0, 5):
+        x, y, z = clouds[s]
+        okp = O.narf_keypoints(x, y, z, threads=16)
+        assert np.array_equal(kps[s], okp), s
+        nx, ny, nz, _ = O.normals(x, y, z, 0.05, threads=16)
+        rows = keypoint_rows(okp, N_FULL)
+        od = O.fpfh(x, y, z, nx, ny, nz, x[rows], y[rows], z[rows], 0.08, threads=16)
+        assert np.array_equal(got[s][1], rows.astype(np.int32)), s
+        assert np.array_equal(_bits(got[s][0]), _bits(od)), s
