@@ -22,6 +22,7 @@ namespace pfx {
 namespace {
 
 constexpr int kQ = 16;  // tile: consecutive queries of one cell
+typedef float pf2 __attribute__((ext_vector_type(2)));  // packed f32 pair (v_pk_add_f32 / v_pk_mul_f32)
 constexpr int kArena = 16384;   // list entries per arena reservation of a tile workgroup (> a typical tile)
 constexpr int kArenaQuery = 16384;  // ... of a per-query workgroup (lists of 1k-4k entries)
 constexpr int kTcapSmall = 384, kTcapSparse = 1280, kTcapDense = 8000;
@@ -505,7 +506,10 @@ __global__ void __launch_bounds__(256, TCAP <= kTcapSmall ? 4 : (STAGE ? 3 : 2))
   constexpr int CH = STAGE ? 1 : 1024;
   __shared__ float2 hxy[CH];
   __shared__ float hz[CH];
-  __shared__ uint16_t lists[Q][LCAP + 2];  // +2: odd dword row stride (no bank conflicts)
+  // the tile's lists (+2: odd dword row stride, no bank conflicts), then the test's trash slots
+  // (a miss stores its candidate to its lane's slot: the test loop has no branch)
+  __shared__ uint16_t lists_flat[Q * (LCAP + 2) + 4 * 64];
+  uint16_t(*lists)[LCAP + 2] = reinterpret_cast<uint16_t(*)[LCAP + 2]>(lists_flat);
   __shared__ uint32_t sd[4][LCAP];
   __shared__ uint16_t stt[4][LCAP];
   __shared__ int bcount[4][NB], bpos[4][NB];
@@ -513,7 +517,10 @@ __global__ void __launch_bounds__(256, TCAP <= kTcapSmall ? 4 : (STAGE ? 3 : 2))
   __shared__ int32_t s_qp[Q];
   __shared__ unsigned long long s_base;
   __shared__ int s_chunk;
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (SGPR): per-query branches are scalar
+  const uint32_t trash_at = (uint32_t)(Q * (LCAP + 2) + 64 * wv + lane);
+  const uint32_t wrow = (uint32_t)(wv * (LCAP + 2));  // the wave's first list row (its queries: wv + 4 u)
   const int ntiles = *ntiles_ptr;
   unsigned long long wg_total = 0, arena_base = 0, arena_left = 0;  // thread 0's
   int next_chunk = 0;                                                // thread 0's
@@ -551,22 +558,26 @@ __global__ void __launch_bounds__(256, TCAP <= kTcapSmall ? 4 : (STAGE ? 3 : 2))
     }
     const int recv = rec_load(rec_base, rec_step, ni, ni < ntiles);
     // [B] test
-    float qx[QW], qy[QW], qz[QW];
+    pf2 qxy[QW];
+    float qz[QW];
     int cursor[QW];
 #pragma unroll
     for (int u = 0; u < QW; ++u) {
       const int j = wv + 4 * u;
       cursor[u] = 0;
-      qx[u] = qy[u] = qz[u] = 0.f;
+      qxy[u] = pf2{0.f, 0.f};
+      qz[u] = 0.f;
       if (j < qn) {
         const int32_t p = s_qp[j];
         if (STAGE) {  // a query lies in its own cell, i.e. in run 4 of its block
           const int t = R.pref[4] + (p - R.start[4]);
           const float2 v = cxy[t];
-          qx[u] = v.x; qy[u] = v.y; qz[u] = cz[t];
+          qxy[u] = pf2{v.x, v.y};
+          qz[u] = cz[t];
         } else {
           const float4 c = g.sp[p];
-          qx[u] = c.x; qy[u] = c.y; qz[u] = c.z;
+          qxy[u] = pf2{c.x, c.y};
+          qz[u] = c.z;
         }
       }
     }
@@ -587,30 +598,44 @@ __global__ void __launch_bounds__(256, TCAP <= kTcapSmall ? 4 : (STAGE ? 3 : 2))
       }
       const float2* XYs = STAGE ? cxy : hxy - c0;
       const float* Zs = STAGE ? cz : hz - c0;
+      // Branch-free test (round 4): candidate reads are unconditional (index clamped into the
+      // staging array), a slot past the block gets the threshold -1 (never a hit), and every lane
+      // stores -- a hit to its compacted slot, a miss to its own trash slot -- through one
+      // v_cndmask of the two element offsets; FLANN's d2 = (dx^2 + dy^2) + dz^2 (dx = q - p; the
+      // 0 + dx^2 of L2_Simple is exact) with x, y on packed f32.  The branchy form compiled into
+      // ~30 instructions and two exec-mask branches per candidate and query.
       for (int t0 = c0; t0 < cend; t0 += 64 * U) {
-        float px[U], py[U], pz[U];
+        pf2 pxy[U];
+        float pz[U], rrv[U];
 #pragma unroll
         for (int v = 0; v < U; ++v) {
           const int t = t0 + 64 * v + lane;
-          px[v] = py[v] = pz[v] = 0.f;
-          if (t < cend) {
-            const float2 xy = XYs[t];
-            px[v] = xy.x; py[v] = xy.y; pz[v] = Zs[t];
-          }
+          const int tr = STAGE ? min(t, SCAP - 1) : t;  // (dense chunks: t - c0 < CH always)
+          const float2 xy = XYs[tr];
+          pxy[v] = pf2{xy.x, xy.y};
+          pz[v] = Zs[tr];
+          rrv[v] = t < cend ? rr : -1.0f;
         }
 #pragma unroll
         for (int v = 0; v < U; ++v) {
           const int t = t0 + 64 * v + lane;
-          const bool in = t < cend;
 #pragma unroll
           for (int u = 0; u < QW; ++u) {
             const int j = wv + 4 * u;
-            const bool hit = in && j < qn && flann_d2(qx[u], qy[u], qz[u], px[v], py[v], pz[v]) < rr;
-            const uint64_t m = __ballot(hit);
-            if (hit) {
-              const int slot = cursor[u] + __popcll(m & lanemask_lt());
-              if (slot < LCAP) lists[j][slot] = (uint16_t)t;
-            }
+            if (j >= qn) continue;  // wave-uniform
+            const pf2 dxy = qxy[u] - pxy[v];
+            const pf2 sq = dxy * dxy;
+            const float dz = qz[u] - pz[v];
+            const bool hit = (sq.x + sq.y) + dz * dz < rrv[v];
+            const uint64_t m = __builtin_amdgcn_ballot_w64(hit);
+            const int slot = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                           __builtin_amdgcn_mbcnt_lo((uint32_t)m, (uint32_t)cursor[u]));
+            // (an overflowing list -- it goes to the per-query path -- keeps writing its row's pad
+            // slot).  The select as bit arithmetic: a plain ?: let the compiler sink the slot
+            // computation into an exec-masked if/else around every store.
+            const uint32_t hit_at = (uint32_t)(min(slot, LCAP) + wrow) + (uint32_t)(4 * u * (LCAP + 2));
+            const uint32_t sel = 0u - (uint32_t)hit;
+            lists_flat[trash_at ^ ((trash_at ^ hit_at) & sel)] = (uint16_t)t;
             cursor[u] += __popcll(m);
           }
         }
@@ -653,11 +678,11 @@ __global__ void __launch_bounds__(256, TCAP <= kTcapSmall ? 4 : (STAGE ? 3 : 2))
         if (ok && j < qn && k <= LCAP && k > 1) {  // wave-uniform
           if (STAGE) {
             const CandLds cand{cxy, cz};
-            sort_list<NB, CandLds, (TCAP <= kTcapSmall)>(lists[j], k, qx[u], qy[u], qz[u], cand, bscale, sd[wv],
+            sort_list<NB, CandLds, (TCAP <= kTcapSmall)>(lists[j], k, qxy[u].x, qxy[u].y, qz[u], cand, bscale, sd[wv],
                                                          stt[wv], bcount[wv], bpos[wv], g, R, lane);
           } else {
             const CandGlobal cand{g.sp, &R};
-            sort_list<NB>(lists[j], k, qx[u], qy[u], qz[u], cand, bscale, sd[wv], stt[wv], bcount[wv], bpos[wv],
+            sort_list<NB>(lists[j], k, qxy[u].x, qxy[u].y, qz[u], cand, bscale, sd[wv], stt[wv], bcount[wv], bpos[wv],
                           g, R, lane);
           }
         }
