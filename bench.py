@@ -51,11 +51,11 @@ CYCLE_SEEDS = [2, 100, 101, 102]  # the headline's distinct scans: configs[2]'s 
 
 VERBOSE_TIMERS = ["grid_bbox", "grid_build", "normals", "normals_fast", "normals_mfma", "normals_lists_phase", "normals_tiles", "normals_lists",
                   "normals_lists_small", "normals_lists_sparse",
-                  "normals_lists_dense", "normals_lists_query", "normals_chain", "normals_chain_big", "normals_long", "range_image",
+                  "normals_lists_dense", "normals_lists_wide", "normals_lists_query", "normals_chain", "normals_chain_big", "normals_long", "range_image",
                   "narf_border", "narf_interest", "narf_nms", "narf_gather", "fpfh_mark", "fpfh_spfh",
                   "fpfh_support", "fpfh_weight", "shot"]
 VERBOSE_STATS = ["normals_neighbors", "normals_queries", "normals_tiles_sparse", "normals_tiles_dense",
-                 "normals_single", "normals_huge", "normals_long_lists", "normals_chain_wg_staged",
+                 "normals_single", "normals_wide", "normals_huge", "normals_long_lists", "normals_chain_wg_staged",
                  "normals_chain_wg_table", "normals_chain_wg_lane", "normals_chain_wg_deferred", "fpfh_spfh_points", "fpfh_spfh_pairs", "fpfh_spfh_exact_pairs", "narf_candidates", "narf_keypoints",
                  "narf_interest_fullimage", "narf_interest_grown", "narf_interest_window_px",
                  "narf_interest_visits", "narf_interest_queue_grown", "fpfh_weight_kmax", "fpfh_weight_sequential",
@@ -637,7 +637,7 @@ def scans_line(args, world, n_scans, scans_here, shot, elapsed, timers, iso, nb_
     stage_ms = timers["normals_fast" if fast else "normals"][0] / max(per_scan_calls, 1)
     stage_gbs = algo / (stage_ms / 1e3) / 1e9 if stage_ms > 0 else 0.0
     parts = ("grid_bbox", "grid_build", "normals_lists_small", "normals_lists_sparse", "normals_lists_dense",
-             "normals_lists_query", "normals_chain", "normals_chain_big", "normals_long")
+             "normals_lists_wide", "normals_lists_query", "normals_chain", "normals_chain_big", "normals_long")
     # per-kernel breakdown: extra steps with every kernel timer on (after the timed region)
     detail_calls = max(detail_steps * scans_here, 1)
     kernels = {nm: round(detail[nm][0] / detail_calls, 4) for nm in parts}
@@ -976,7 +976,7 @@ def bench_harris(args, torch, dev, world, rank, local, six=False):
             kname = "k_harris_response + k_harris_nms"
         achieved = algo / resp_s / 1e9 if resp_s > 0 else 0.0
         names = (tag, "normals_lists_phase", "grid_bbox", "grid_build", "normals_tiles", "normals_lists_small",
-                 "normals_lists_sparse", "normals_lists_dense", "normals_lists_query", "normals_chain",
+                 "normals_lists_sparse", "normals_lists_dense", "normals_lists_wide", "normals_lists_query", "normals_chain",
                  "normals_chain_big", "normals_long", tag + "_refine")
         names += ("harris6d_gradient", "harris6d_response") if six else ("harris3d_response",)
         stages = {nm: round(ctx.kernel_time(nm)[0] / args.steps, 4) for nm in names}
@@ -1059,7 +1059,7 @@ def bench_config1(args, torch, dev, world, rank, local):
         ctx.close()
         return
     names = ("normals", "fpfh_mark", "fpfh_spfh", "fpfh_weight", "grid_build", "normals_lists_small",
-             "normals_lists_sparse", "normals_lists_dense", "normals_lists_query", "normals_chain",
+             "normals_lists_sparse", "normals_lists_dense", "normals_lists_wide", "normals_lists_query", "normals_chain",
              "normals_chain_big", "normals_long")
     stages = {nm: round(ctx.kernel_time(nm)[0] / args.steps, 4) for nm in names}
     ctx.set_timing(False)

@@ -30,6 +30,16 @@ constexpr int kCapQuery = 4096, kBucketsQuery = 1024;
 constexpr int kCapMid8 = 8192, kBucketsMid8 = 1024;  // 72 KB of LDS: two workgroups per CU
 constexpr int kCapMid = 16384, kBucketsMid = 2048;  // 144 KB of LDS: one workgroup per CU
 constexpr int kCapHuge = 1 << 18, kBucketsHuge = 4096, kHugeBlocks = 256;  // 1 GB scratch, allocated on demand
+constexpr int kNCounters = 20;
+
+// The lists of a wide tile are written unsorted to HBM by a test pass and ordered in place by the
+// per-query tiers: work items j | kListMode (the tier by k: <= 4096, <= 8192, <= 16384, beyond);
+// queue 0 also takes the test-mode items of the lists that overflow a tile kernel.
+constexpr int32_t kListMode = 1 << 30;
+struct TierQ {
+  int32_t* q[4];
+  int* n[4];
+};
 
 // Tile record (written by k_tile_class, one per tile, in class order): the 9 candidate runs of
 // the tile's 3x3x3 block, its first query (index into qpos) and query count.  A workgroup loads
@@ -72,8 +82,9 @@ __device__ __forceinline__ void wave_sync() {
 // qpos = 0..n-1 with the query count = the finite points (cell_start[ncells])
 __global__ void k_list_init(int32_t* __restrict__ qpos, int64_t n, const int32_t* __restrict__ nq_src,
                             int64_t* __restrict__ d_nq, int* __restrict__ counters, int ncounters,
-                            unsigned long long* __restrict__ cursor) {
+                            unsigned long long* __restrict__ cursor, TierQ tq, TierQ* __restrict__ tq_dev) {
   const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (i == 0) *tq_dev = tq;
   if (qpos && i < n) qpos[i] = (int32_t)i;
   if (i < ncounters) counters[i] = 0;
   if (i < 4) cursor[i] = 0ull;
@@ -114,17 +125,17 @@ __global__ void k_tile_flags(const int32_t* __restrict__ seg, const int64_t* __r
   flags[j] = (j < *nq_ptr) && ((j - seg[j]) % kQ == 0);
 }
 
-// candidate-block class of a tile: small, sparse, dense, or every query to the per-query path.
-// The tile's record goes to its class's region of `recs` (slots reserved with one atomic per
-// wave and class): small at [0, n), sparse at [n, 2n) upward, dense at [n, 2n) downward from
-// 2n - 1 (sparse + dense <= tiles <= n, so the two never meet).
+// candidate-block class of a tile: small, sparse, dense or wide.  The tile's record goes to its class's region of
+// `recs` (slots reserved with one atomic per wave and class): small at [0, n) upward, wide at
+// [0, n) downward from n - 1, sparse at [n, 2n) upward, dense at [n, 2n) downward from 2n - 1
+// (each pair shares <= n tiles, so they never meet); a wide tile also gets its work entry.
 __global__ void __launch_bounds__(256) k_tile_class(GridView g, const int32_t* __restrict__ qpos,
                                                     const uint32_t* __restrict__ skeys,
                                                     const int64_t* __restrict__ nq_ptr,
                                                     const int32_t* __restrict__ tiles,
                                                     const int64_t* __restrict__ ntiles_ptr,
                                                     int32_t* __restrict__ recs, int64_t n,
-                                                    int32_t* __restrict__ single, int* __restrict__ counts) {
+                                                    int32_t* __restrict__ wide, int* __restrict__ counts) {
   const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   const int64_t ntiles = *ntiles_ptr;
   const int lane = threadIdx.x & 63;
@@ -137,36 +148,24 @@ __global__ void __launch_bounds__(256) k_tile_class(GridView g, const int32_t* _
     qn = (int)(next - start < kQ ? next - start : kQ);
     const int T = block_runs(g, skeys[qpos[start]], R);
     // 3: small tiles (<= kTcapSmall candidates, so no list can exceed them: a low-LDS kernel
-    // with more workgroups per CU), 0: sparse, 1: dense, 2: per query
+    // with more workgroups per CU), 0: sparse, 1: dense, 2: wide (k_nb_wide: any block size)
     cls = T <= kTcapSmall ? 3 : (T <= kTcapSparse ? 0 : (T <= kTcapDense ? 1 : 2));
   }
 #pragma unroll
   for (int c = 0; c < 4; ++c) {
-    if (c == 2) continue;
     const uint64_t m = __ballot(cls == c);
     if (!m) continue;
     int base = 0;
-    const int ci = c == 3 ? 10 : c;
+    const int ci = c == 3 ? 10 : (c == 2 ? 16 : c);
     if (lane == __builtin_ctzll(m)) base = atomicAdd(&counts[ci], __popcll(m));
     base = __shfl(base, __builtin_ctzll(m));
     if (cls == c) {
       const int64_t slot = base + __popcll(m & lanemask_lt());
-      const int64_t at = c == 3 ? slot : (c == 0 ? n + slot : 2 * n - 1 - slot);
+      // small at [0, n) upward, wide at [0, n) downward from n - 1
+      const int64_t at = c == 3 ? slot : (c == 0 ? n + slot : (c == 1 ? 2 * n - 1 - slot : n - 1 - slot));
       rec_write(recs + at * kRecInts, R, start, qn);
+      if (c == 2) wide[slot] = (int32_t)at;
     }
-  }
-  int v = cls == 2 ? qn : 0, inc = v;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const int x = __shfl_up(inc, o);
-    if (lane >= o) inc += x;
-  }
-  const int total = __shfl(inc, 63);
-  if (total) {
-    int base = 0;
-    if (lane == 63) base = atomicAdd(&counts[2], total);
-    base = __shfl(base, 63) + inc - v;
-    for (int j = 0; j < v; ++j) single[base + j] = start + j;
   }
 }
 
@@ -198,7 +197,7 @@ struct CandGlobal {
 };
 
 #ifdef PFX_SHOT_PROFILE
-__device__ unsigned long long g_tile_prof[16];
+__device__ unsigned long long g_tile_prof[24];
 #define TPROF_T(v) long long v = (threadIdx.x == 0) ? clock64() : 0
 #define TPROF_ADD(i, a, b) if (threadIdx.x == 0) atomicAdd(&g_tile_prof[i], (unsigned long long)((b) - (a)))
 #else
@@ -456,6 +455,77 @@ __device__ __forceinline__ void sort_list(uint16_t* L, int k, float qx, float qy
 // so the one global-latency round of a tile (staging loads, list stores) is shared.  Tiles come
 // from a dynamic queue `chunk` at a time; thread 0 keeps the next chunk's base fetched one chunk
 // ahead and publishes it in [D].
+// (the kernels get the queues through one pointer to a device copy: eight pointers as kernel
+// arguments pushed the tile kernels into spilling scalar registers)
+__device__ __forceinline__ void push_sort(const TierQ* tq, int32_t j, int k) {
+  const int t = k <= kCapQuery ? 0 : (k <= kCapMid8 ? 1 : (k <= kCapMid ? 2 : 3));
+  tq->q[t][atomicAdd(tq->n[t], 1)] = j | kListMode;
+}
+
+// One pass of a tile's candidates against the wave's queries u (act[u], wave-uniform): hits are
+// counted in cursor[u] and, with STORE, written to glist[gb[u] + slot] as run entries (in
+// candidate order).  STAGE: the candidates are staged in cxy / cz; otherwise they stream through
+// hxy / hz in chunks of kChunkWide (the whole workgroup takes part: barriers inside).
+constexpr int kChunkWide = 1024;
+template <bool STAGE, int SCAP, bool STORE>
+__device__ __forceinline__ void tile_pass(const GridView& g, const Runs& R, int T, const float2* cxy, const float* cz,
+                                          float2* hxy, float* hz, const pf2* qxy, const float* qz, const bool* act,
+                                          const int64_t* gb, int* cursor, uint32_t* __restrict__ glist, float rr) {
+  constexpr int CH = kChunkWide, U = 2, QW = 4;
+  const int tid = threadIdx.x, lane = tid & 63;
+#pragma unroll
+  for (int u = 0; u < QW; ++u) cursor[u] = 0;
+  for (int c0 = 0; c0 < T; c0 += (STAGE ? T : CH)) {
+    const int cend = STAGE ? T : min(T, c0 + CH);
+    if (!STAGE) {
+      float4 cc[CH / 256];
+#pragma unroll
+      for (int u = 0; u < CH / 256; ++u) cc[u] = g.sp[run_pos(R, min(c0 + tid + 256 * u, T - 1))];
+      __syncthreads();  // the previous chunk's readers are done
+#pragma unroll
+      for (int u = 0; u < CH / 256; ++u) {
+        hxy[tid + 256 * u] = make_float2(cc[u].x, cc[u].y);
+        hz[tid + 256 * u] = cc[u].z;
+      }
+      __syncthreads();
+    }
+    const float2* XYs = STAGE ? cxy : hxy - c0;
+    const float* Zs = STAGE ? cz : hz - c0;
+    for (int t0 = c0; t0 < cend; t0 += 64 * U) {
+      pf2 pxy[U];
+      float pz[U], rrv[U];
+#pragma unroll
+      for (int v = 0; v < U; ++v) {
+        const int t = t0 + 64 * v + lane;
+        const int tr = STAGE ? min(t, SCAP - 1) : t;  // (chunks: CH is a multiple of 64 U)
+        const float2 xy = XYs[tr];
+        pxy[v] = pf2{xy.x, xy.y};
+        pz[v] = Zs[tr];
+        rrv[v] = t < cend ? rr : -1.0f;
+      }
+#pragma unroll
+      for (int v = 0; v < U; ++v) {
+        const int t = t0 + 64 * v + lane;
+#pragma unroll
+        for (int u = 0; u < QW; ++u) {
+          if (!act[u]) continue;  // wave-uniform
+          const pf2 dxy = qxy[u] - pxy[v];
+          const pf2 sq = dxy * dxy;
+          const float dz = qz[u] - pz[v];
+          const bool hit = (sq.x + sq.y) + dz * dz < rrv[v];
+          const uint64_t m = __builtin_amdgcn_ballot_w64(hit);
+          if (STORE && hit) {
+            const int slot = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                           __builtin_amdgcn_mbcnt_lo((uint32_t)m, (uint32_t)cursor[u]));
+            glist[gb[u] + slot] = run_entry(R, t);
+          }
+          cursor[u] += __popcll(m);
+        }
+      }
+    }
+  }
+}
+
 template <int TCAP, bool STAGE>
 struct Stager {
   static constexpr int PT = STAGE ? (TCAP + 255) / 256 : 0;
@@ -494,7 +564,7 @@ __global__ void __launch_bounds__(256, TCAP <= kTcapSmall ? 4 : (STAGE ? 3 : 2))
                                                  const int32_t* __restrict__ rec_base, int rec_step,
                                                  const int* __restrict__ ntiles_ptr,
                                                  float rr, float bscale, int sorted, ListOut out,
-                                                 int32_t* __restrict__ single, int* __restrict__ n_single,
+                                                 const TierQ* __restrict__ tq,
                                                  int* __restrict__ next_tile, int chunk) {
   constexpr int Q = kQ, QW = Q / 4;  // queries per tile / per wave
   constexpr int U = 2;               // candidates per lane in flight in the test loop
@@ -650,7 +720,7 @@ __global__ void __launch_bounds__(256, TCAP <= kTcapSmall ? 4 : (STAGE ? 3 : 2))
     }
     __syncthreads();
     TPROF_T(p1);
-    TPROF_ADD(STAGE ? 1 : 5, p0, p1);
+    TPROF_ADD(TCAP <= kTcapSmall ? 17 : (STAGE ? 1 : 5), p0, p1);
     // [C] list slots, sort
     int lg = 0;
     while ((1 << lg) < qn) ++lg;
@@ -663,11 +733,14 @@ __global__ void __launch_bounds__(256, TCAP <= kTcapSmall ? 4 : (STAGE ? 3 : 2))
       for (int j = 0; j < qn; ++j) wg_total += s_k[j] <= LCAP ? (unsigned long long)s_k[j] : 0ull;
     if (tid < qn) {
       const int k = s_k[tid];
-      if (k > LCAP) {
-        single[wave_push_slot(n_single)] = start + tid;  // the per-query path writes its descriptor
-      } else {
+      if (k <= LCAP) {
         out.cnt[start + tid] = k;
         out.lg[start + tid] = (uint8_t)lg;
+      } else {
+        // the per-query kernel (test + sort): measured against a second tile pass writing these
+        // lists unsorted for a sort-only per-query pass, that pass cost more (room: dense tiles
+        // +0.22 ms against 0.07 saved; dense variant: no change)
+        tq->q[0][wave_push_slot(tq->n[0])] = start + tid;
       }
     }
     if (sorted) {
@@ -690,7 +763,7 @@ __global__ void __launch_bounds__(256, TCAP <= kTcapSmall ? 4 : (STAGE ? 3 : 2))
     }
     __syncthreads();
     TPROF_T(p2);
-    TPROF_ADD(STAGE ? 2 : 6, p1, p2);
+    TPROF_ADD(TCAP <= kTcapSmall ? 18 : (STAGE ? 2 : 6), p1, p2);
     // [D] one latency round: the next tile's staging loads, the list-slot reservation and the
     // queue fetch; their results land in LDS, then this tile's lists are written (stores in
     // flight until the next tile's round)
@@ -735,13 +808,125 @@ __global__ void __launch_bounds__(256, TCAP <= kTcapSmall ? 4 : (STAGE ? 3 : 2))
     }
     __syncthreads();  // lists and s_k read before the next tile's test overwrites them
     TPROF_T(p3);
-    TPROF_ADD(STAGE ? 3 : 7, p2, p3);
+    TPROF_ADD(TCAP <= kTcapSmall ? 19 : (STAGE ? 3 : 7), p2, p3);
     i = ni;
     R = Rn;
     start = start_n;
     qn = qn_n;
   }
   if (tid == 0 && wg_total) atomicAdd(out.cursor + 1, wg_total);
+}
+
+// ---- wide tiles (round 4) ----------------------------------------------------------------
+// Every query of a tile whose 3x3x3 block has 8000 < T <= 65535 candidates (k_tile_class): one
+// workgroup per tile (dynamic queue) streams the block through LDS in chunks shared by the
+// tile's (up to 16) queries -- the per-query kernel read the block once per query, with a run
+// search per candidate -- in a count pass and a pass writing the hits unsorted to their slots in
+// HBM; the per-query tiers then order each list in place (kListMode work items, no test).
+__global__ void __launch_bounds__(256) k_nb_wide(GridView g, const int32_t* __restrict__ qpos,
+                                                 const int32_t* __restrict__ recs, const int32_t* __restrict__ work,
+                                                 const int* __restrict__ n_ptr, float rr, int sorted, ListOut out,
+                                                 const TierQ* __restrict__ tq, int* __restrict__ next_work) {
+  constexpr int QW = 4;
+  __shared__ float2 hxy[kChunkWide];
+  __shared__ float hz[kChunkWide];
+  __shared__ int s_k[kQ];
+  __shared__ int32_t s_qp[kQ];
+  __shared__ int s_w;
+  __shared__ unsigned long long s_base;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int count = *n_ptr;
+  if (count == 0) return;  // (the room has no wide tiles: an empty launch costs only its dispatch)
+  // thread 0's: list slots from a per-workgroup arena, totals added once per workgroup
+  unsigned long long wg_total = 0, wg_long = 0, wg_long_n = 0, arena_base = 0, arena_left = 0;
+  for (;;) {
+    if (tid == 0) s_w = atomicAdd(next_work, 1);
+    __syncthreads();
+    const int w = __builtin_amdgcn_readfirstlane(s_w);
+    __syncthreads();
+    if (w >= count) break;
+    Runs R;
+    int32_t start;
+    int qn;
+    rec_unpack(rec_load(recs, kRecInts, work[w], true), R, start, qn);
+    const int T = R.pref[9];
+    if (tid < qn) s_qp[tid] = qpos[start + tid];
+    __syncthreads();
+    pf2 qxy[QW];
+    float qz[QW];
+    bool act[QW];
+    int cursor[QW];
+    int64_t gb[QW];
+#pragma unroll
+    for (int u = 0; u < QW; ++u) {
+      const int j = wv + 4 * u;
+      act[u] = j < qn;
+      qxy[u] = pf2{0.f, 0.f};
+      qz[u] = 0.f;
+      gb[u] = 0;
+      if (act[u]) {
+        const float4 c = g.sp[s_qp[j]];
+        qxy[u] = pf2{c.x, c.y};
+        qz[u] = c.z;
+      }
+    }
+    tile_pass<false, 1, false>(g, R, T, nullptr, nullptr, hxy, hz, qxy, qz, act, gb, cursor, nullptr, rr);
+    if (lane == 0) {
+#pragma unroll
+      for (int u = 0; u < QW; ++u)
+        if (act[u]) s_k[wv + 4 * u] = cursor[u];
+    }
+    __syncthreads();
+    int need = 0;
+    for (int j = 0; j < qn; ++j) need += s_k[j];
+    need = __builtin_amdgcn_readfirstlane(need);
+    if (tid == 0) {
+      if ((unsigned long long)need > arena_left) {
+        const unsigned long long res = need > kArenaQuery ? (unsigned long long)need : (unsigned long long)kArenaQuery;
+        arena_base = atomicAdd(out.cursor, res);
+        arena_left = res;
+      }
+      s_base = arena_base;
+      arena_base += need;
+      arena_left -= need;
+      wg_total += need;
+      for (int j = 0; j < qn; ++j)
+        if (s_k[j] > kLongList) {
+          wg_long += (unsigned long long)s_k[j];
+          ++wg_long_n;
+        }
+    }
+    __syncthreads();
+    const int64_t base = (int64_t)s_base;
+    const bool fits = (unsigned long long)(base + need) <= out.cap;
+    if (fits) {
+#pragma unroll
+      for (int u = 0; u < QW; ++u) {
+        int pre = 0;
+        for (int j = 0; j < wv + 4 * u && j < qn; ++j) pre += s_k[j];
+        gb[u] = base + pre;
+      }
+      tile_pass<false, 1, true>(g, R, T, nullptr, nullptr, hxy, hz, qxy, qz, act, gb, cursor, out.list, rr);
+    }
+    if (tid < qn) {
+      int pre = 0;
+      for (int j = 0; j < tid; ++j) pre += s_k[j];
+      const int k = s_k[tid];
+      out.off[start + tid] = base + pre;
+      out.cnt[start + tid] = k;
+      out.lg[start + tid] = 0;
+      if (fits && sorted && k > 1) push_sort(tq, start + tid, k);
+    }
+    __syncthreads();  // s_k / s_qp are rewritten by the next tile
+  }
+  if (tid == 0) {
+    if (wg_total) atomicAdd(out.cursor + 1, wg_total);
+    if (wg_long_n) {
+      atomicAdd(out.cursor + 2, wg_long);
+      atomicAdd(out.cursor + 3, wg_long_n);
+    }
+  }
 }
 
 // One 256-thread workgroup per query: candidates streamed from L2/HBM, the list bucket-sorted
@@ -775,6 +960,7 @@ __global__ void __launch_bounds__(256) k_nb_query(GridView g, const int32_t* __r
   uint32_t* spv = base_arr + 3 * CAP;
   const int tid = threadIdx.x;
   const int count = *n_ptr;
+  if (count == 0) return;  // an empty tier costs only its dispatch (the queue head stays 0)
   __shared__ int s_w;
   // thread 0's: list slots from a per-workgroup arena and the totals added once per workgroup
   // (one same-address atomic per query made the cursors the bottleneck of this kernel)
@@ -785,7 +971,9 @@ __global__ void __launch_bounds__(256) k_nb_query(GridView g, const int32_t* __r
     const int w = s_w;
     __syncthreads();
     if (w >= count) break;
-    const int32_t j = work[w];
+    const int32_t jw = work[w];
+    const bool from_list = (jw & kListMode) != 0;  // the list is in place, unsorted: sort only
+    const int32_t j = jw & (kListMode - 1);
     const int32_t qp = qpos[j];
     const float4 q = g.sp[qp];
     Runs R;
@@ -793,7 +981,42 @@ __global__ void __launch_bounds__(256) k_nb_query(GridView g, const int32_t* __r
     if (tid == 0) s_count = 0;
     for (int b = tid; b < NB; b += 256) bcount[b] = 0;
     __syncthreads();
-    for (int t0 = 0; t0 < R.pref[9]; t0 += 4 * 256) {  // 4 candidates per thread in flight
+    TPROF_T(q0);
+    if (from_list) {
+      // entries -> positions and d2, four per thread in flight (a list past the buffer's end is
+      // left alone: the build reruns with a larger buffer)
+      const int kl = out.cnt[j];
+      const int64_t lo = out.off[j];
+      const int kk = (unsigned long long)(lo + kl) <= out.cap && kl <= CAP ? kl : 0;
+      if (tid == 0) {
+        s_count = kk;
+        s_base = (unsigned long long)lo;
+        if (kl > CAP) atomicMax(err, kl);
+      }
+      for (int e0 = tid; e0 < kk; e0 += 4 * 256) {
+        int32_t pos[4];
+        float4 c[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const uint32_t en = out.list[lo + min(e0 + 256 * u, kk - 1)];
+          const int r = entry_run(en);
+          int32_t st = R.start[0];
+#pragma unroll
+          for (int v = 1; v < 9; ++v) st = r == v ? R.start[v] : st;
+          pos[u] = st + (int32_t)entry_off(en);
+          c[u] = g.sp[pos[u]];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int e = e0 + 256 * u;
+          if (e < kk) {
+            hits[e] = (uint32_t)pos[u];
+            hd[e] = __float_as_uint(flann_d2(q.x, q.y, q.z, c[u].x, c[u].y, c[u].z));
+          }
+        }
+      }
+    }
+    for (int t0 = 0; !from_list && t0 < R.pref[9]; t0 += 4 * 256) {  // 4 candidates per thread in flight
       float4 c[4];
       int32_t pos[4];
 #pragma unroll
@@ -820,6 +1043,8 @@ __global__ void __launch_bounds__(256) k_nb_query(GridView g, const int32_t* __r
       }
     }
     __syncthreads();
+    TPROF_T(q1);
+    if (!GLOBAL && CAP == kCapQuery) { TPROF_ADD(20, q0, q1); }
     const int k = s_count;
     if (k > CAP) {
       if (tid == 0) {
@@ -829,7 +1054,7 @@ __global__ void __launch_bounds__(256) k_nb_query(GridView g, const int32_t* __r
       __syncthreads();
       continue;
     }
-    if (tid == 0) {
+    if (tid == 0 && !from_list) {
       const unsigned long long need = (unsigned long long)k;
       if (need > arena_left) {
         const unsigned long long res = need > (unsigned long long)kArenaQuery ? need : (unsigned long long)kArenaQuery;
@@ -907,6 +1132,8 @@ __global__ void __launch_bounds__(256) k_nb_query(GridView g, const int32_t* __r
           if (fits) out.list[off + st + rank] = pos_entry(R, (int32_t)p);
         }
         __syncthreads();
+        TPROF_T(q2);
+        if (CAP == kCapQuery) { TPROF_ADD(21, q1, q2); TPROF_ADD(22, 0, (long long)k); TPROF_ADD(23, 0, (long long)R.pref[9]); }
         continue;
       } else {
         for (int e = tid; e < k; e += 256) {
@@ -952,7 +1179,7 @@ std::string bname(const char* tag, const char* what) { return std::string(tag) +
 
 // the pinned readback block of a list build
 struct ListsRb {
-  int cnt[16];
+  int cnt[kNCounters];
   int oob;
   int pad;
   unsigned long long cur[4];
@@ -1013,6 +1240,7 @@ bool build_lists_check(pfx_ctx* ctx, const Grid& G, NbLists& out, const char* ta
   ctx->stats[std::string(tag) + "_single"] = h_cnt[2];
   ctx->stats[std::string(tag) + "_huge"] = h_cnt[3];
   ctx->stats[std::string(tag) + "_mid"] = h_cnt[12];
+  ctx->stats[std::string(tag) + "_wide"] = h_cnt[16];
   return true;
 }
 
@@ -1041,10 +1269,12 @@ void build_lists(pfx_ctx* ctx, const Grid& G, const uint8_t* mask, double radius
   int32_t* cnt = B("cnt").as<int32_t>(n);
   uint8_t* lgs = B("lg").as<uint8_t>(n);
   // counters: 0 sparse tiles, 1 dense tiles, 2 per-query work, 3 huge work, 4 max k over cap,
-  // 5 / 7 sparse / dense tile queue heads, 6 per-query work queued by the classifier (restored
-  // for a rerun), 8 / 9 per-query / huge work queue heads, 10 small tiles, 11 their queue head,
-  // 12 mid work (lists of 8k-16k entries), 13 its queue head, 14 mid8 work (4k-8k), 15 its head
-  int* counters = B("counters").as<int>(16);
+  // 5 / 7 sparse / dense tile queue heads, 6 unused, 8 / 9 per-query / huge work queue heads,
+  // 10 small tiles, 11 their queue head,
+  // 12 mid work (lists of 8k-16k entries), 13 its queue head, 14 mid8 work (4k-8k), 15 its head,
+  // 16 wide-tile work (queued by the classifier), 17 its queue head
+  int* counters = B("counters").as<int>(kNCounters);
+  int32_t* wq = B("wide").as<int32_t>((size_t)n);  // wide-tile work: record indices
   int32_t* mid = B("mid").as<int32_t>(n);
   int32_t* mid8 = B("mid8").as<int32_t>(n);
   unsigned long long* cursor = B("cursor").as<unsigned long long>(4);
@@ -1056,28 +1286,33 @@ void build_lists(pfx_ctx* ctx, const Grid& G, const uint8_t* mask, double radius
   void* tmp = B("tmp").get(std::max(t1, std::max(t2, t3)) + 16);
   const unsigned nb = (unsigned)ceil_div(n, 256);
   unsigned long long* cursor0 = B("cursor").as<unsigned long long>(4);
+  // sort-only work (kListMode) of the lists the tile kernels write unsorted, by length; the
+  // kernels read the queues from a device copy written by k_list_init
+  static const bool use_mid8 = !(getenv("PFX_LIST_MID8") && *getenv("PFX_LIST_MID8") == '0');  // A/B switch
+  const TierQ tq{{single, use_mid8 ? mid8 : mid, mid, huge},
+                 {counters + 2, counters + (use_mid8 ? 14 : 12), counters + 12, counters + 3}};
+  TierQ* tq_dev = static_cast<TierQ*>(B("tierq").get(sizeof(TierQ)));
   {
     TimeScope ts(ctx, std::string(tag) + "_tiles");
     if (mask) {
-      k_list_init<<<1, 256, 0, st>>>(nullptr, 0, nullptr, d_nq, counters, 16, cursor0);
+      k_list_init<<<1, 256, 0, st>>>(nullptr, 0, nullptr, d_nq, counters, kNCounters, cursor0, tq, tq_dev);
       k_mask_flags<<<nb, 256, 0, st>>>(G.perm, G.skeys, n, (uint64_t)G.ncells, mask, want, flags);
       PFX_HIP(rocprim::select(tmp, t1, rocprim::counting_iterator<int32_t>(0), flags, qpos, d_nq, (size_t)n, st));
     } else {
       // every finite point, in cell order: sorted positions [0, cell_start[ncells])
-      k_list_init<<<nb, 256, 0, st>>>(qpos, n, G.cell_start + G.ncells, d_nq, counters, 16, cursor0);
+      k_list_init<<<nb, 256, 0, st>>>(qpos, n, G.cell_start + G.ncells, d_nq, counters, kNCounters, cursor0, tq,
+                                      tq_dev);
     }
     k_seg_marks<<<nb, 256, 0, st>>>(qpos, G.skeys, d_nq, seg);
     PFX_HIP(rocprim::inclusive_scan(tmp, t2, seg, seg, (size_t)n, rocprim::maximum<int32_t>(), st));
     k_tile_flags<<<nb, 256, 0, st>>>(seg, d_nq, flags, n);
     PFX_HIP(rocprim::select(tmp, t3, rocprim::counting_iterator<int32_t>(0), flags, tiles, d_ntiles, (size_t)n, st));
-    k_tile_class<<<nb, 256, 0, st>>>(g, qpos, G.skeys, d_nq, tiles, d_ntiles, recs, n, single, counters);
+    k_tile_class<<<nb, 256, 0, st>>>(g, qpos, G.skeys, d_nq, tiles, d_ntiles, recs, n, wq, counters);
     check_launch("nblist tiles");
-    PFX_HIP(hipMemcpyAsync(counters + 6, counters + 2, sizeof(int), hipMemcpyDeviceToDevice, st));
   }
   const size_t lds_q = sizeof(uint32_t) * 2 * kCapQuery;
   PFX_HIP(hipFuncSetAttribute((const void*)k_nb_query<kCapQuery, kBucketsQuery, false>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_q));
-  static const bool use_mid8 = !(getenv("PFX_LIST_MID8") && *getenv("PFX_LIST_MID8") == '0');  // A/B switch
   const size_t lds_m8 = sizeof(uint32_t) * 2 * kCapMid8;
   PFX_HIP(hipFuncSetAttribute((const void*)k_nb_query<kCapMid8, kBucketsMid8, false>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_m8));
@@ -1107,10 +1342,11 @@ void build_lists(pfx_ctx* ctx, const Grid& G, const uint8_t* mask, double radius
     ListOut lo{off, cnt, lgs, static_cast<uint32_t*>(lb.ptr), cursor, lb.bytes / sizeof(uint32_t)};
     if (attempt) {  // (the first attempt's cursors were zeroed by k_list_init)
       PFX_HIP(hipMemsetAsync(cursor, 0, 4 * sizeof(unsigned long long), st));
-      PFX_HIP(hipMemcpyAsync(counters + 2, counters + 6, sizeof(int), hipMemcpyDeviceToDevice, st));
+      PFX_HIP(hipMemsetAsync(counters + 2, 0, sizeof(int), st));  // per-query work
       PFX_HIP(hipMemsetAsync(counters + 3, 0, 3 * sizeof(int), st));  // huge, max k, sparse queue
       PFX_HIP(hipMemsetAsync(counters + 7, 0, 3 * sizeof(int), st));  // dense, query, huge queues
       PFX_HIP(hipMemsetAsync(counters + 11, 0, 5 * sizeof(int), st));  // small queue, mid / mid8 work + queues
+      PFX_HIP(hipMemsetAsync(counters + 17, 0, sizeof(int), st));  // wide queue (its work: the classifier's)
     }
     // one synchronisation per call: counters, cursors and the query count in one pinned block
     ListsRb* rb = ctx->readback<ListsRb>();
@@ -1148,18 +1384,25 @@ void build_lists(pfx_ctx* ctx, const Grid& G, const uint8_t* mask, double radius
       {
         TimeScope t0(ctx, std::string(tag) + "_lists_small");
         k_nb_tile<kTcapSmall, 256, kTcapSmall, true><<<256 * 4 * 2, 256, 0, st>>>(
-            g, qpos, recs, kRecInts, counters + 10, rr, 256.0f / rr, isort, lo, single, counters + 2, counters + 11,
+            g, qpos, recs, kRecInts, counters + 10, rr, 256.0f / rr, isort, lo, tq_dev, counters + 11,
             ch_small);
       }
       {
         TimeScope t1(ctx, std::string(tag) + "_lists_sparse");
         k_nb_tile<512, 256, kTcapSparse, true><<<256 * 3 * 4, 256, 0, st>>>(
-            g, qpos, recs + (size_t)n * kRecInts, kRecInts, counters + 0, rr, 256.0f / rr, isort, lo, single, counters + 2, counters + 5, ch_sparse);
+            g, qpos, recs + (size_t)n * kRecInts, kRecInts, counters + 0, rr, 256.0f / rr, isort, lo, tq_dev, counters + 5,
+            ch_sparse);
       }
       {
         TimeScope t2(ctx, std::string(tag) + "_lists_dense");
         k_nb_tile<1024, 256, kTcapDense, false><<<256 * 2 * 4, 256, 0, st>>>(
-            g, qpos, recs + (size_t)(2 * n - 1) * kRecInts, -kRecInts, counters + 1, rr, 256.0f / rr, isort, lo, single, counters + 2, counters + 7, ch_dense);
+            g, qpos, recs + (size_t)(2 * n - 1) * kRecInts, -kRecInts, counters + 1, rr, 256.0f / rr, isort, lo, tq_dev,
+            counters + 7, ch_dense);
+      }
+      {
+        TimeScope t4(ctx, std::string(tag) + "_lists_wide");
+        k_nb_wide<<<256 * 4, 256, 0, st>>>(g, qpos, recs, wq, counters + 16, rr, isort, lo, tq_dev, counters + 17);
+        check_launch("nblist wide tiles");
       }
       {
         TimeScope t3(ctx, std::string(tag) + "_lists_query");
@@ -1224,7 +1467,7 @@ void build_lists(pfx_ctx* ctx, const Grid& G, const uint8_t* mask, double radius
       // unused arena tails (scheduling-dependent, at most one arena per launched workgroup), so
       // this run's demand plus the tail bound always fits the rebuild.
       const size_t tails = (size_t)(256 * 4 * 2 + 256 * 3 * 4 + 256 * 2 * 4) * kArena +
-                           (size_t)(256 * 4 + 256 * 2 + 256 + kHugeBlocks) * kArenaQuery;
+                           (size_t)(256 * 4 + 256 * 4 + 256 * 2 + 256 + kHugeBlocks) * kArenaQuery;
       lb.release();
       lb.get(sizeof(uint32_t) * ((size_t)h_cur[0] + tails + ((size_t)1 << 20)));
       continue;
@@ -1245,15 +1488,21 @@ void build_lists(pfx_ctx* ctx, const Grid& G, const uint8_t* mask, double radius
     ctx->stats[std::string(tag) + "_single"] = h_cnt[2];
     ctx->stats[std::string(tag) + "_huge"] = h_cnt[3];
     ctx->stats[std::string(tag) + "_mid"] = h_cnt[12];
+    ctx->stats[std::string(tag) + "_wide"] = h_cnt[16];
     ctx->stats[std::string(tag) + "_mid8"] = h_cnt[14];
 #ifdef PFX_SHOT_PROFILE
     {
-      unsigned long long pr[16];
+      unsigned long long pr[24];
       PFX_HIP(hipMemcpyFromSymbol(pr, HIP_SYMBOL(g_tile_prof), sizeof(pr)));
       fprintf(stderr, "%s wave_sort cycles (wave 0): count %llu scan %llu scatter %llu rank %llu\n", tag, pr[8],
               pr[9], pr[10], pr[11]);
       fprintf(stderr, "%s tile cycles: sparse stage %llu test %llu sort %llu write %llu | dense - %llu test %llu "
-              "sort %llu write %llu (cumulative)\n", tag, pr[0], pr[1], pr[2], pr[3], pr[4], pr[5], pr[6], pr[7]);
+              "sort %llu write %llu | small - %llu test %llu sort %llu write %llu (cumulative)\n", tag, pr[0], pr[1], pr[2],
+              pr[3], pr[4], pr[5], pr[6], pr[7], pr[16], pr[17], pr[18], pr[19]);
+      fprintf(stderr, "%s query cycles: test %llu sort+write %llu | entries %llu candidates %llu\n", tag, pr[20],
+              pr[21], pr[22], pr[23]);
+      static const unsigned long long zero[24] = {};
+      PFX_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_tile_prof), zero, sizeof(zero)));
     }
 #endif
     return;

@@ -104,21 +104,22 @@ __device__ __forceinline__ int block_runs(const GridView& g, uint32_t key, Runs&
   return acc;
 }
 
+// position of candidate t of the block: t + (start[r] - pref[r]) for its run r -- one compare and
+// one select per run boundary (the differences are per-block scalars when R is uniform)
 __device__ __forceinline__ int32_t run_pos(const Runs& R, int32_t t) {
-  int32_t p = R.start[0] + t;
+  int32_t d = R.start[0] - R.pref[0];
 #pragma unroll
-  for (int r = 1; r < 9; ++r)
-    if (t >= R.pref[r]) p = R.start[r] + (t - R.pref[r]);
-  return p;
+  for (int r = 1; r < 9; ++r) d = t >= R.pref[r] ? R.start[r] - R.pref[r] : d;
+  return t + d;
 }
 
-// run entry (pfx_nblist.h) of candidate t of the block: (run << 28) | offset within the run
+// run entry (pfx_nblist.h) of candidate t of the block: (run << 28) | offset within the run,
+// = t + ((r << 28) - pref[r]) in wrapping u32 (the offset is < 2^28)
 __device__ __forceinline__ uint32_t run_entry(const Runs& R, int32_t t) {
-  uint32_t e = (uint32_t)(t - R.pref[0]);
+  uint32_t d = 0u - (uint32_t)R.pref[0];
 #pragma unroll
-  for (int r = 1; r < 9; ++r)
-    if (t >= R.pref[r]) e = ((uint32_t)r << 28) | (uint32_t)(t - R.pref[r]);
-  return e;
+  for (int r = 1; r < 9; ++r) d = t >= R.pref[r] ? ((uint32_t)r << 28) - (uint32_t)R.pref[r] : d;
+  return (uint32_t)t + d;
 }
 
 // Gather the neighbours of q into keys[0..min(k,cap)) (unsorted); returns k (may exceed cap).

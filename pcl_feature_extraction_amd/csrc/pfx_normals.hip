@@ -129,7 +129,9 @@ __device__ __forceinline__ void run_chain(const uint32_t* lst, int lg, int k, Fe
   // Branch-free batches: entry loads use a clamped index and padded terms are exact zeros
   // (accumulators are never -0, so + 0.0f is the identity).  Two entry buffers alternate
   // without register copies (a copy of a pending load forces a vmcnt wait), so one batch of
-  // entry loads is always in flight behind the batch being summed.
+  // entry loads is always in flight behind the batch being summed.  (Measured and rejected in
+  // round 4: 32-bit element offsets, chains 0.50 -> 0.54-0.62 ms; an all-zero coordinate slot
+  // fetched by the padded steps instead of three coordinate selects, no change.)
   const int last = k - 1;
   auto at = [&](int m) { return lst[(int64_t)(m < last ? m : last) << lg]; };
   uint32_t eA[KB], eB[KB];
@@ -415,14 +417,18 @@ __global__ void __launch_bounds__(256, 1) k_normals_chain_big(GridView g, NbList
 // long lists: nine lanes per query (one chain each), seven queries per wave.  The chains of a
 // list are strictly sequential, so the kernel's time is the longest list's chain; a batch of
 // global gathers per few steps put one memory latency on that chain every batch.  Here the wave
-// gathers kLB (64) steps of its seven lists at a time into LDS (seven coordinate loads per lane,
+// gathers kLB (32) steps of its seven lists at a time into LDS (seven coordinate loads per lane,
 // issued one batch ahead, with the list entries two batches ahead), and the chains read LDS
-// (four steps per ds_read_b128): one latency per 64 steps instead of per 16.
+// (four steps per ds_read_b128): one latency per 32 steps instead of per 16.
 // Persistent waves (grid-stride over groups of seven queries): the queue length is only known
 // on the device, and a grid sized for the worst case spends its time dispatching empty waves.
 constexpr int kPerWave = 7, kLB = 32;
+// rows padded by one float4 (a 144-B stride): the 21 rows a chain step reads (7 queries x 3
+// planes, one ds_read_b128 per lane at the same step) spread over the LDS banks instead of
+// piling onto two bank groups (a 128-B stride: 9.4 conflict cycles per LDS instruction, r03 PMC)
+constexpr int kLBPad = kLB + 4;
 struct LongLds {
-  float c[2][3][kPerWave][kLB];  // double-buffered x | y | z per query and step (5.3 KB)
+  float c[2][3][kPerWave][kLBPad];  // double-buffered x | y | z per query and step (6 KB)
   int32_t rtab[kPerWave * 9];
 };
 

@@ -30,11 +30,16 @@ for name, gen, seed in (("room", synth_room, 2), ("seabed", synth_seabed, 3)):
         for _ in range(steps):
             ctx.normals_dev(b.x, b.y, b.z, 0.05, b.nx, b.ny, b.nz, b.curv)
         torch.cuda.synchronize()
-        names = ["grid_build", "normals", "normals_lists_small", "normals_lists_sparse", "normals_lists_dense", "normals_lists_query",
+        names = ["grid_build", "normals", "normals_lists_small", "normals_lists_sparse", "normals_lists_dense", "normals_lists_wide", "normals_lists_query",
                  "normals_chain", "normals_chain_big", "normals_long"]
         t = {n: round(ctx.kernel_time(n)[0] / steps, 4) for n in names}
         nb = ctx.stat("normals_neighbors")
         chain = t["normals_chain"] + t["normals_chain_big"]
         gbs = (nb * 12 + len(x) * 16) / (chain / 1e3) / 1e9
-        st = {k: ctx.stat("normals_" + k) for k in ("single", "mid", "huge")}
+        def stat(k):
+            try:
+                return ctx.stat("normals_" + k)
+            except Exception:  # (a library build without that statistic)
+                return None
+        st = {k: stat(k) for k in ("wide", "single", "mid", "huge")}
         print(name, json.dumps(t), json.dumps(st), "chain GB/s %.0f frac %.3f" % (gbs, gbs / 8000.0), flush=True)

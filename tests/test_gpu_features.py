@@ -92,21 +92,23 @@ def test_normals_edge_cases(ctx):
 
 def test_normals_every_list_path(ctx):
     """Densities that route queries through every neighbour-list path (pfx_nblist.hip): sparse
-    and dense tiles, the per-query LDS kernels (k > 1024, k > 4096, k > 8192) and the
-    global-scratch kernel (k > 16384),
-    plus lane-per-query and nine-lanes-per-query chains; duplicates exercise the index tie-break."""
+    and dense tiles, the lists that overflow a tile (k > 512 / 1024: the per-query kernel's test
+    and sort), wide tiles (blocks of > 8000 candidates: lists written unsorted, then sorted in place
+    by the per-query tiers, k <= 4096, <= 8192, <= 16384 in LDS, beyond in global scratch), plus
+    lane-per-query and nine-lanes-per-query chains; duplicates exercise the index tie-break."""
     rng = np.random.default_rng(23)
     sparse = np.c_[rng.uniform(0, 1, (4000, 2)), np.full(4000, 1.0)]
     dense = np.c_[rng.uniform(2, 2.3, (9000, 2)), np.full(9000, 1.0)]          # k ~ 400..800
     denser = np.c_[rng.uniform(3, 3.1, (9000, 2)), np.full(9000, 1.0)]         # k ~ 1800..7000
     blob = rng.normal(0, 0.01, (1500, 3)) + [4, 4, 1]                          # k ~ 900..1500
     mid = np.repeat(rng.normal(0, 0.004, (1700, 3)) + [6, 6, 1], 3, axis=0)   # k = 5100, ties
+    mid16 = np.repeat(rng.normal(0, 0.004, (3500, 3)) + [7, 7, 1], 3, axis=0)  # k = 10500 (8k-16k)
     huge = np.repeat(rng.normal(0, 0.004, (5500, 3)) + [8, 8, 1], 3, axis=0)  # k = 16500 > 16384
-    pts = np.concatenate([sparse, dense, denser, blob, mid, huge]).astype(np.float32)
+    pts = np.concatenate([sparse, dense, denser, blob, mid, mid16, huge]).astype(np.float32)
     x, y, z = pts[:, 0].copy(), pts[:, 1].copy(), pts[:, 2].copy()
     g = ctx.normals(x, y, z, 0.05)
-    for nm in ["normals_tiles_sparse", "normals_tiles_dense", "normals_single", "normals_mid8", "normals_mid",
-               "normals_huge"]:
+    for nm in ["normals_tiles_sparse", "normals_tiles_dense", "normals_wide", "normals_single", "normals_mid8",
+               "normals_mid", "normals_huge"]:
         assert ctx.stat(nm) > 0, nm
     o = O.normals(x, y, z, 0.05)
     for a, b in zip(g, o):
