@@ -16,5 +16,5 @@ for P in "$P1" "$P2" "$P3" "$P4"; do
 done
 python3 $R/scripts/pmc_summary.py $R/gpurun_out/pmc_$TAG k_normals_chain,k_normals_chain_big $R/gpurun_out/pmc_$TAG/pmc_normals_chain.json > $R/gpurun_out/pmc_$TAG/summary.txt
 # the whole neighbour-gather stage (grid kernels excluded: shared with the FPFH grid in the step)
-python3 $R/scripts/pmc_summary.py $R/gpurun_out/pmc_$TAG k_tile_class,k_nb_tile,k_nb_query,k_normals_chain,k_normals_chain_big,k_normals_long $R/gpurun_out/pmc_$TAG/pmc_normals_stage.json > /dev/null
+python3 $R/scripts/pmc_summary.py $R/gpurun_out/pmc_$TAG k_tile_class,k_nb_tile,k_nb_wide,k_nb_query,k_normals_chain,k_normals_chain_big,k_normals_long $R/gpurun_out/pmc_$TAG/pmc_normals_stage.json > /dev/null
 cat $R/gpurun_out/pmc_$TAG/summary.txt
