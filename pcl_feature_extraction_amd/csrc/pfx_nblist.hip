@@ -100,7 +100,8 @@ __global__ void k_defer_gate(const int* __restrict__ counters, const unsigned lo
                              const int64_t* __restrict__ d_nq, int64_t* __restrict__ d_nq_eff) {
   if (threadIdx.x != 0) return;
   const bool ok = cursor[0] <= cap && (have_huge || counters[3] == 0) && counters[4] == 0 && (!oob || *oob == 0) &&
-                  ((ran_mids & 1) || counters[14] == 0) && ((ran_mids & 2) || counters[12] == 0);
+                  ((ran_mids & 1) || counters[14] == 0) && ((ran_mids & 2) || counters[12] == 0) &&
+                  ((ran_mids & 4) || counters[16] == 0);
   *d_nq_eff = ok ? *d_nq : 0;
 }
 
@@ -1199,9 +1200,10 @@ static bool mid_tier_wanted(pfx_ctx* ctx, const char* tag, const char* which) {
   return it == ctx->stats.end() || it->second > 0;
 }
 static void note_mid_tiers(pfx_ctx* ctx, const char* tag, const int* h_cnt) {
-  for (int t = 0; t < 2; ++t) {
-    const std::string key = std::string(tag) + (t ? "_hint_mid" : "_hint_mid8");
-    const int work = t ? h_cnt[12] : h_cnt[14];
+  static const char* const keys[3] = {"_hint_mid8", "_hint_mid", "_hint_wide"};
+  for (int t = 0; t < 3; ++t) {
+    const std::string key = std::string(tag) + keys[t];
+    const int work = h_cnt[t == 0 ? 14 : (t == 1 ? 12 : 16)];
     int64_t& v = ctx->stats[key];
     v = work > 0 ? 16 : std::max<int64_t>(0, v - 1);
   }
@@ -1225,7 +1227,8 @@ bool build_lists_check(pfx_ctx* ctx, const Grid& G, NbLists& out, const char* ta
   if (!B("scratch").ptr && h_cnt[3] > 0) return false;              // first very long lists
   const int ran = (int)ctx->stats[std::string(tag) + "_ran_mid_tiers"];
   note_mid_tiers(ctx, tag, h_cnt);
-  if ((!(ran & 1) && h_cnt[14] > 0) || (!(ran & 2) && h_cnt[12] > 0)) return false;  // a skipped tier had work
+  if ((!(ran & 1) && h_cnt[14] > 0) || (!(ran & 2) && h_cnt[12] > 0) || (!(ran & 4) && h_cnt[16] > 0))
+    return false;  // a skipped tier had work
   if (h_cnt[4] > 0)
     throw Error(PFX_ERR_CAPACITY, std::string(tag) + ": a query has " + std::to_string(h_cnt[4]) +
                                       " neighbours (> " + std::to_string(kCapHuge) + " supported)");
@@ -1338,7 +1341,7 @@ void build_lists(pfx_ctx* ctx, const Grid& G, const uint8_t* mask, double radius
   const int ch_small = env_or("PFX_TILE_CHUNK_S", chunk_all ? chunk_all : 4),
             ch_sparse = env_or("PFX_TILE_CHUNK_P", chunk_all ? chunk_all : std::max(2, heavy)),
             ch_dense = env_or("PFX_TILE_CHUNK_D", chunk_all ? chunk_all : std::max(1, heavy));
-  for (int attempt = 0; attempt < 2; ++attempt) {
+  for (int attempt = 0; attempt < 3; ++attempt) {
     ListOut lo{off, cnt, lgs, static_cast<uint32_t*>(lb.ptr), cursor, lb.bytes / sizeof(uint32_t)};
     if (attempt) {  // (the first attempt's cursors were zeroed by k_list_init)
       PFX_HIP(hipMemsetAsync(cursor, 0, 4 * sizeof(unsigned long long), st));
@@ -1370,8 +1373,10 @@ void build_lists(pfx_ctx* ctx, const Grid& G, const uint8_t* mask, double radius
       check_launch("nblist 16k lists");
     };
     // (see mid_tier_wanted; a rerun launches every tier)
-    const int ran_mids = attempt ? 3 : ((use_mid8 && mid_tier_wanted(ctx, tag, "_hint_mid8") ? 1 : 0) |
-                                        (mid_tier_wanted(ctx, tag, "_hint_mid") ? 2 : 0) | (use_mid8 ? 0 : 1));
+    // (bit 4: the wide-tile kernel -- an empty launch of it also waits for whole CUs beside NARF)
+    const int ran_mids = attempt ? 7 : ((use_mid8 && mid_tier_wanted(ctx, tag, "_hint_mid8") ? 1 : 0) |
+                                        (mid_tier_wanted(ctx, tag, "_hint_mid") ? 2 : 0) | (use_mid8 ? 0 : 1) |
+                                        (mid_tier_wanted(ctx, tag, "_hint_wide") ? 4 : 0));
     ctx->stats[std::string(tag) + "_ran_mid_tiers"] = ran_mids;
     auto launch_huge = [&] {
       k_nb_query<kCapHuge, kBucketsHuge, true><<<kHugeBlocks, 256, 0, st>>>(
@@ -1401,8 +1406,10 @@ void build_lists(pfx_ctx* ctx, const Grid& G, const uint8_t* mask, double radius
       }
       {
         TimeScope t4(ctx, std::string(tag) + "_lists_wide");
-        k_nb_wide<<<256 * 4, 256, 0, st>>>(g, qpos, recs, wq, counters + 16, rr, isort, lo, tq_dev, counters + 17);
-        check_launch("nblist wide tiles");
+        if (ran_mids & 4) {
+          k_nb_wide<<<256 * 4, 256, 0, st>>>(g, qpos, recs, wq, counters + 16, rr, isort, lo, tq_dev, counters + 17);
+          check_launch("nblist wide tiles");
+        }
       }
       {
         TimeScope t3(ctx, std::string(tag) + "_lists_query");
@@ -1437,6 +1444,11 @@ void build_lists(pfx_ctx* ctx, const Grid& G, const uint8_t* mask, double radius
       return;
     }
     read_back();
+    if (!(ran_mids & 4) && rb->cnt[16] > 0) {  // skipped wide tiles had work: rerun with every tier
+      note_mid_tiers(ctx, tag, rb->cnt);
+      ++ctx->stats[std::string(tag) + "_tier_catchups"];
+      continue;
+    }
     if ((!(ran_mids & 1) && rb->cnt[14] > 0) || (!(ran_mids & 2) && rb->cnt[12] > 0)) {
       // a skipped per-query tier had work: run it and the tiers after it.  A launch that drained
       // its queue left the head at count + gridDim (every workgroup's last fetch overshoots), so
