@@ -26,7 +26,10 @@ namespace pfx {
 namespace {
 
 constexpr int kBatch = 8;      // neighbour entries per half-batch (two in flight)
-constexpr int kLaneMax = 2 * kLongList;  // longer lists go to k_normals_long (measured: 1024 0.90, 1536 0.78, 2048 0.75, 4096 0.84 ms for the chain stage of the room)
+#ifndef PFX_LANE_MAX
+#define PFX_LANE_MAX (2 * kLongList)
+#endif
+constexpr int kLaneMax = PFX_LANE_MAX;  // longer lists go to k_normals_long (measured: 1024 0.90, 1536 0.78, 2048 0.75, 4096 0.84 ms for the chain stage of the room)
 
 __device__ __forceinline__ void chain_add(float a[9], float x, float y, float z) {
   a[0] = a[0] + x * x;
