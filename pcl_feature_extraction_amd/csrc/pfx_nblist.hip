@@ -1011,8 +1011,11 @@ __global__ void __launch_bounds__(256) k_nb_query(GridView g, const int32_t* __r
         for (int u = 0; u < 4; ++u) {
           const int e = e0 + 256 * u;
           if (e < kk) {
+            const float d2 = flann_d2(q.x, q.y, q.z, c[u].x, c[u].y, c[u].z);
             hits[e] = (uint32_t)pos[u];
-            hd[e] = __float_as_uint(flann_d2(q.x, q.y, q.z, c[u].x, c[u].y, c[u].z));
+            hd[e] = __float_as_uint(d2);
+            const int b = (int)(d2 * bscale);
+            if (sorted) atomicAdd(&bcount[b < NB ? b : NB - 1], 1);
           }
         }
       }
@@ -1026,21 +1029,32 @@ __global__ void __launch_bounds__(256) k_nb_query(GridView g, const int32_t* __r
         pos[u] = t < R.pref[9] ? run_pos(R, t) : -1;
         c[u] = g.sp[pos[u] < 0 ? 0 : pos[u]];
       }
+      // one slot reservation per wave and round (the four ballots' total) instead of one per
+      // ballot, and the sort's bucket counts taken here instead of in a pass over the hits
+      float d2[4];
+      uint64_t m[4];
+      int tot = 0;
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        const float d2 = flann_d2(q.x, q.y, q.z, c[u].x, c[u].y, c[u].z);
-        const bool hit = pos[u] >= 0 && d2 < rr;
-        const uint64_t m = __ballot(hit);
-        int base = 0;
-        if ((tid & 63) == 0 && m) base = atomicAdd(&s_count, __popcll(m));
-        base = __shfl(base, 0);
-        if (hit) {
-          const int slot = base + __popcll(m & lanemask_lt());
+        d2[u] = flann_d2(q.x, q.y, q.z, c[u].x, c[u].y, c[u].z);
+        m[u] = __ballot(pos[u] >= 0 && d2[u] < rr);
+        tot += __popcll(m[u]);
+      }
+      int base = 0;
+      if ((tid & 63) == 0 && tot) base = atomicAdd(&s_count, tot);
+      base = __shfl(base, 0);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if ((m[u] >> (tid & 63)) & 1) {
+          const int slot = base + __popcll(m[u] & lanemask_lt());
           if (slot < CAP) {
             hits[slot] = (uint32_t)pos[u];
-            hd[slot] = __float_as_uint(d2);
+            hd[slot] = __float_as_uint(d2[u]);
+            const int b = (int)(d2[u] * bscale);
+            if (sorted) atomicAdd(&bcount[b < NB ? b : NB - 1], 1);
           }
         }
+        base += __popcll(m[u]);
       }
     }
     __syncthreads();
@@ -1074,12 +1088,7 @@ __global__ void __launch_bounds__(256) k_nb_query(GridView g, const int32_t* __r
       out.cnt[j] = k;
       out.lg[j] = 0;
     }
-    if (sorted && k > 1) {
-      for (int e = tid; e < k; e += 256) {
-        const int b = (int)(__uint_as_float(hd[e]) * bscale);
-        atomicAdd(&bcount[b < NB ? b : NB - 1], 1);
-      }
-      __syncthreads();
+    if (sorted && k > 1) {  // (the bucket counts were taken with the hits)
       if (tid < 64) {  // one wave scans the counts
         constexpr int PER = NB / 64;
         int s = 0;
