@@ -29,7 +29,12 @@ constexpr int kBatch = 8;      // neighbour entries per half-batch (two in fligh
 #ifndef PFX_LANE_MAX
 #define PFX_LANE_MAX (2 * kLongList)
 #endif
-constexpr int kLaneMax = PFX_LANE_MAX;  // longer lists go to k_normals_long (measured: 1024 0.90, 1536 0.78, 2048 0.75, 4096 0.84 ms for the chain stage of the room)
+// lists longer than the lane cap go to k_normals_long.  Room (few long lists): 2048 (measured:
+// 1024 0.90, 1536 0.78, 2048 0.75, 4096 0.84 ms for the chain stage; round 4: 1024 / 1536 slower
+// again).  Dense clouds (many long lists, the non-forked schedule): 4096 -- the dense 10M variant's
+// long-list chains 140 -> 91 ms against chain_big 17 -> 28 ms (14.0 -> 14.7 Mpoints/s).
+constexpr int kLaneMax = PFX_LANE_MAX;
+constexpr int kLaneMaxDense = 2 * kLaneMax;
 
 __device__ __forceinline__ void chain_add(float a[9], float x, float y, float z) {
   a[0] = a[0] + x * x;
@@ -172,7 +177,7 @@ __device__ __forceinline__ void chain_wg(ChainLds<CAP>& S, const GridView& g, co
                                          float* __restrict__ ny, float* __restrict__ nz, float* __restrict__ curv,
                                          int32_t* __restrict__ longq, int* __restrict__ n_long,
                                          int* __restrict__ modes, int64_t* __restrict__ deferq,
-                                         const uint8_t* __restrict__ mask, int want) {
+                                         const uint8_t* __restrict__ mask, int want, int lane_max) {
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int64_t j = j0 + tid;
 #ifdef PFX_SHOT_PROFILE
@@ -220,20 +225,30 @@ __device__ __forceinline__ void chain_wg(ChainLds<CAP>& S, const GridView& g, co
       S.u.h.b[s] = -1;
     }
     __syncthreads();
-    // touched columns and the z range each needs
-    for (int i = tid; i < ncell * 9; i += 256) {
-      const CellXYZ c = cell_of(g, S.ckey[i / 9]);
-      const int r = i % 9, X = c.x + r / 3 - 1, Y = c.y + r % 3 - 1;
-      if (X < 0 || X >= g.nx || Y < 0 || Y >= g.ny) continue;
-      const uint32_t col = (uint32_t)X * (uint32_t)g.ny + (uint32_t)Y;
-      uint32_t h = col_hash(col);
-      for (;;) {
-        const uint32_t old = atomicCAS(&S.u.h.key[h], kEmpty, col);
-        if (old == kEmpty || old == col) break;
-        h = (h + 1) & (kHash - 1);
+    // touched columns and the z range each needs; each (cell, run)'s run start is loaded here
+    // already (the run table below needs it: one global round less in the prologue)
+    constexpr int kIt = (kMaxCells * 9 + 255) / 256;
+    int32_t pre_sr[kIt];
+#pragma unroll
+    for (int it = 0; it < kIt; ++it) {
+      const int i = tid + 256 * it;
+      pre_sr[it] = 0;
+      if (i < ncell * 9) {
+        const CellXYZ c = cell_of(g, S.ckey[i / 9]);
+        const int r = i % 9, X = c.x + r / 3 - 1, Y = c.y + r % 3 - 1;
+        if (X >= 0 && X < g.nx && Y >= 0 && Y < g.ny) {
+          const uint32_t col = (uint32_t)X * (uint32_t)g.ny + (uint32_t)Y;
+          pre_sr[it] = g.cell_start[(int64_t)col * g.nz + (c.z > 0 ? c.z - 1 : 0)];
+          uint32_t h = col_hash(col);
+          for (;;) {
+            const uint32_t old = atomicCAS(&S.u.h.key[h], kEmpty, col);
+            if (old == kEmpty || old == col) break;
+            h = (h + 1) & (kHash - 1);
+          }
+          atomicMin(&S.u.h.a[h], c.z > 0 ? c.z - 1 : 0);
+          atomicMax(&S.u.h.b[h], c.z + 1 < g.nz ? c.z + 1 : g.nz - 1);
+        }
       }
-      atomicMin(&S.u.h.a[h], c.z > 0 ? c.z - 1 : 0);
-      atomicMax(&S.u.h.b[h], c.z + 1 < g.nz ? c.z + 1 : g.nz - 1);
     }
     __syncthreads();
     // position range of every touched column, LDS bases by a block scan
@@ -275,13 +290,16 @@ __device__ __forceinline__ void chain_wg(ChainLds<CAP>& S, const GridView& g, co
     }
     __syncthreads();
     // run table: list entry (r, off) of a query of cell cs -> tbl[cs * 9 + r] + off
-    for (int i = tid; i < ncell * 9; i += 256) {
+#pragma unroll
+    for (int it = 0; it < kIt; ++it) {
+      const int i = tid + 256 * it;
+      if (i >= ncell * 9) continue;
       const CellXYZ c = cell_of(g, S.ckey[i / 9]);
       const int r = i % 9, X = c.x + r / 3 - 1, Y = c.y + r % 3 - 1;
       int32_t t = 0;
       if (X >= 0 && X < g.nx && Y >= 0 && Y < g.ny) {
         const uint32_t col = (uint32_t)X * (uint32_t)g.ny + (uint32_t)Y;
-        const int32_t s_r = g.cell_start[(int64_t)col * g.nz + (c.z > 0 ? c.z - 1 : 0)];
+        const int32_t s_r = pre_sr[it];
         t = s_r;
         if (staged) {
           uint32_t h = col_hash(col);
@@ -309,20 +327,15 @@ __device__ __forceinline__ void chain_wg(ChainLds<CAP>& S, const GridView& g, co
           }
           src[u] = i < total ? S.ostart[lo] + (i - S.obase[lo]) : -1;
         }
-        float vx[4], vy[4], vz[4];
+        float4 v[4];  // (the packed copy: one load per point instead of three)
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const int32_t q = src[u] < 0 ? 0 : src[u];
-          vx[u] = g.sx[q];
-          vy[u] = g.sy[q];
-          vz[u] = g.sz[q];
-        }
+        for (int u = 0; u < 4; ++u) v[u] = g.sp[src[u] < 0 ? 0 : src[u]];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
           const int i = i0 + u * 256 + tid;
           if (src[u] >= 0) {
-            S.u.c.xy[i] = make_float2(vx[u], vy[u]);
-            S.u.c.z[i] = vz[u];
+            S.u.c.xy[i] = make_float2(v[u].x, v[u].y);
+            S.u.c.z[i] = v[u].z;
           }
         }
       }
@@ -339,14 +352,14 @@ __device__ __forceinline__ void chain_wg(ChainLds<CAP>& S, const GridView& g, co
     atomicAdd(&g_chain_prof[PO + 0], (unsigned long long)(pt1 - pt0));
     atomicAdd(&g_chain_prof[PO + 4], 1ull);
   }
-  int wk = (active && k <= kLaneMax) ? k : 0;
+  int wk = (active && k <= lane_max) ? k : 0;
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) wk = max(wk, __shfl_xor(wk, o));
   const uint64_t wm = __ballot(active && k == wk);
   const bool rec = wm && lane == __builtin_ctzll(wm);
 #endif
   if (!active) return;
-  if (k > kLaneMax) return;  // listed by k_long_lists, chained by k_normals_long
+  if (k > lane_max) return;  // listed by k_long_lists, chained by k_normals_long
   const uint32_t* lst = L.list + L.off[j];
   const int lg = L.lg[j];
   float a[9];
@@ -393,10 +406,11 @@ __global__ void __launch_bounds__(256, 3) k_normals_chain(GridView g, NbLists L,
                                                           float* __restrict__ nz, float* __restrict__ curv,
                                                           int32_t* __restrict__ longq, int* __restrict__ n_long,
                                                           int* __restrict__ modes, int64_t* __restrict__ deferq,
-                                                          const uint8_t* __restrict__ mask, int want) {
+                                                          const uint8_t* __restrict__ mask, int want,
+                                                          int lane_max) {
   __shared__ ChainLds<kStageSmall> S;
   chain_wg<kStageSmall, true>(S, g, L, (int64_t)blockIdx.x * 256, vpx, vpy, vpz, nx, ny, nz, curv,
-                              longq, n_long, modes, deferq, mask, want);
+                              longq, n_long, modes, deferq, mask, want, lane_max);
 }
 
 // the deferred (dense) workgroups: one 144 KB workgroup per CU, persistent over the queue
@@ -406,14 +420,15 @@ __global__ void __launch_bounds__(256, 1) k_normals_chain_big(GridView g, NbList
                                                               float* __restrict__ curv, int32_t* __restrict__ longq,
                                                               int* __restrict__ n_long, int* __restrict__ modes,
                                                               const int64_t* __restrict__ deferq,
-                                                              const uint8_t* __restrict__ mask, int want) {
+                                                              const uint8_t* __restrict__ mask, int want,
+                                                              int lane_max) {
   extern __shared__ __attribute__((aligned(16))) unsigned char dyn[];
   ChainLds<kStageBig>& S = *reinterpret_cast<ChainLds<kStageBig>*>(dyn);
   const int count = modes[3];
   for (int w = blockIdx.x; w < count; w += gridDim.x) {
     __syncthreads();  // the previous workgroup's chains have finished reading the LDS
     chain_wg<kStageBig, false>(S, g, L, deferq[w], vpx, vpy, vpz, nx, ny, nz, curv, longq, n_long, modes, nullptr,
-                               mask, want);
+                               mask, want, lane_max);
   }
 }
 
@@ -457,14 +472,15 @@ __global__ void k_nan_fill4_masked(float* __restrict__ a, float* __restrict__ b,
 
 // the lists longer than kLaneMax of this pass (mask[caller] == want), for k_normals_long
 __global__ void __launch_bounds__(256) k_long_lists(GridView g, NbLists L, const uint8_t* __restrict__ mask, int want,
+                                                    int lane_max,
                                                     int32_t* __restrict__ longq, int* __restrict__ n_long) {
   const int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   bool push = false;
   if (want >= 2 && mask) {  // workgroup partition (blocks of 256 queries, as k_normals_chain's)
     const bool sel = j < nq_of(L) && mask[g.perm[L.qpos[j]]] != 0;
     const bool mine = (__syncthreads_or(sel) != 0) == ((want & 1) != 0);
-    push = mine && j < nq_of(L) && L.cnt[j] > kLaneMax;
-  } else if (j < nq_of(L) && L.cnt[j] > kLaneMax) {
+    push = mine && j < nq_of(L) && L.cnt[j] > lane_max;
+  } else if (j < nq_of(L) && L.cnt[j] > lane_max) {
     push = !mask || ((mask[g.perm[L.qpos[j]]] != 0) == (want != 0));
   }
   if (push) longq[wave_push_slot(n_long)] = (int32_t)j;
@@ -685,13 +701,14 @@ void normals_chains_dev(pfx_ctx* ctx, pfx_ctx* owner, const uint8_t* mask, int w
   // device mostly idle) k_normals_long runs on a side stream concurrently with the short-list
   // chains, which leave them out; when most lists are long (dense clouds) the two kernels would
   // only crowd each other, so it runs after them on the same stream
-  k_long_lists<<<(unsigned)nb, 256, 0, st>>>(view(G), L, mask, want, longq, n_long);
-  check_launch("k_long_lists");
-  // (sized to what is resident at once: waves beyond it would wait for a second round)
-  const int64_t lb = std::min<int64_t>(ceil_div(L.nq, 7 * 4), 256 * 4);
   // (a deferred build has no count yet: the previous estimation's decision on this context)
   const bool fork = L.nq_dev ? ctx->normals_fork_hint : L.long_nq * 8 <= L.nq;
   if (!L.nq_dev) ctx->normals_fork_hint = fork;
+  const int lane_max = fork ? kLaneMax : kLaneMaxDense;
+  k_long_lists<<<(unsigned)nb, 256, 0, st>>>(view(G), L, mask, want, lane_max, longq, n_long);
+  check_launch("k_long_lists");
+  // (sized to what is resident at once: waves beyond it would wait for a second round)
+  const int64_t lb = std::min<int64_t>(ceil_div(L.nq, 7 * 4), 256 * 4);
   if (fork) {
     ctx->ensure_side();
     PFX_HIP(hipEventRecord(ctx->fork_ev[0], st));
@@ -708,7 +725,7 @@ void normals_chains_dev(pfx_ctx* ctx, pfx_ctx* owner, const uint8_t* mask, int w
     {
       TimeScope ts(ctx, "normals_chain");
       k_normals_chain<<<(unsigned)nb, 256, 0, st>>>(view(G), L, vp[0], vp[1], vp[2], nx, ny, nz, curv, longq, n_long,
-                                                    n_long + 1, deferq, mask, want);
+                                                    n_long + 1, deferq, mask, want, lane_max);
       check_launch("k_normals_chain");
     }
     static std::once_flag attr;  // contexts may run on several host threads
@@ -721,7 +738,7 @@ void normals_chains_dev(pfx_ctx* ctx, pfx_ctx* owner, const uint8_t* mask, int w
     TimeScope tb(ctx, "normals_chain_big");
     k_normals_chain_big<<<256, 256, sizeof(ChainLds<kStageBig>), st>>>(view(G), L, vp[0], vp[1], vp[2], nx, ny, nz,
                                                                          curv, longq, n_long, n_long + 1, deferq,
-                                                                         mask, want);
+                                                                         mask, want, lane_max);
     check_launch("k_normals_chain_big");
   }
   {
