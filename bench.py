@@ -784,12 +784,18 @@ def bench_match(args, torch, dev, world, rank, local):
         elapsed = float(t.item())
     ns, nt = len(src), len(tgt)
     if rank == 0:
-        # MFMA work per step: two tile passes over the padded (ns x nt) grid, K = 3 x 352 (bf16 split)
+        # MFMA work per step: one tile pass over the padded (ns x nt) grid, K = 3 x 352 (bf16 split);
+        # the candidate test runs over the pruned pair list the pass emits (a second contraction only
+        # when that list overflows: match_filter, counted if it ran)
+        # plus the seeding pass over the cross of the first 4 row / column tiles (match_seed)
         pad = lambda v: (v + 127) // 128 * 128  # noqa: E731
-        flops = 2 * 2.0 * pad(ns) * pad(nt) * 3 * 352
         tb, nb = ctx.kernel_time("match_bound")
-        tf, _ = ctx.kernel_time("match_filter")
-        tiles_s = (tb + tf) / max(nb, 1) / 1e3
+        tf, nf = ctx.kernel_time("match_filter")
+        tsd, nsd = ctx.kernel_time("match_seed")
+        gx, gy = pad(nt) // 128, pad(ns) // 128
+        seed_tiles = 4 * gx + 4 * (gy - 4) if (gx > 16 and gy > 16) else 0
+        flops = ((1 + nf / max(nb, 1)) * pad(ns) * pad(nt) + (nsd / max(nb, 1)) * seed_tiles * 128 * 128) * 2.0 * 3 * 352
+        tiles_s = (tb + tf + tsd) / max(nb, 1) / 1e3
         achieved = flops / tiles_s / 1e12 if tiles_s > 0 else 0.0
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
@@ -805,6 +811,12 @@ def bench_match(args, torch, dev, world, rank, local):
                    "sample": (f"the same {ns} x {nt} SHOT-352 sets through the CPU restatement (oracle/or_match.cpp: "
                               f"exhaustive L2_Simple 1-NN both directions, OpenMP), {csec:.1f}s"),
                    "parity": {"correspondences": same}}
+        def stat(nm):
+            try:
+                return ctx.stat(nm)
+            except Exception:  # a library build without that statistic
+                return None
+
         line = {
             "metric": "Mpairs/s descriptor matching (Features::findCorrespondences, SHOT-352 mutual 1-NN)",
             "value": round(world * ns * nt * args.steps / elapsed / 1e6, 3),
@@ -815,16 +827,18 @@ def bench_match(args, torch, dev, world, rank, local):
             "config": {"workload": "SURVEY 8(f) F1: mutual nearest SHOT-352 descriptors of two 1M-pt scans",
                        "source_rows": ns, "target_rows": nt, "correspondences": int(npairs),
                        "parallelism": f"replica x{world}"},
-            "roofline": {"bound": "mfma", "kernel": "k_match_tiles<0> + k_match_tiles<1>", "achieved": round(achieved, 2),
+            "roofline": {"bound": "mfma", "kernel": ("k_match_tiles<0,seed> + " if nsd else "") + "k_match_tiles<0>"
+                         + (" + k_match_tiles<1>" if nf else ""), "achieved": round(achieved, 2),
                          "peak": BF16_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": round(achieved / BF16_PEAK_TFLOPS, 5),
                          "traffic": None, "flops_per_step": flops, "avg_tiles_ms": round(tiles_s * 1e3, 4),
-                         "candidates": {"rows": ctx.stat("match_candidates_rows"),
-                                        "cols": ctx.stat("match_candidates_cols")}},
+                         "candidates": {"pairs_emitted": stat("match_pairs_emitted"),
+                                        "rows": stat("match_candidates_rows"),
+                                        "cols": stat("match_candidates_cols")}},
             "cpu_baseline": cpu,
         }
         if os.environ.get("PFX_BENCH_VERBOSE"):
             rep = {nm: round(ctx.kernel_time(nm)[0] / args.steps, 4)
-                   for nm in ("match", "match_bound", "match_filter", "match_exact")}
+                   for nm in ("match", "match_seed", "match_bound", "match_filter", "match_exact")}
             print("per-step kernel ms:", json.dumps(rep), file=sys.stderr, flush=True)
         print(json.dumps(line), flush=True)
     ctx.close()

@@ -101,15 +101,57 @@ struct Side {
   int64_t n;
 };
 
-// PASS 0: row / column upper bounds.  PASS 1: candidates.
-template <int PASS>
-__global__ void __launch_bounds__(256) k_match_tiles(Side A, Side B, int D, int Dp, float c1, float c2,
+// PASS 0: row / column upper bounds, and the pruned pair list: after a tile's atomicMin the
+// running bound of a row (column) is >= its final U, so a pair with d^ - e above the running
+// bound of both its row and its column can never be a candidate; the rest (a few dozen per row:
+// the tiles that lowered a bound) are emitted as (row, col, d^ - e) and tested against the final
+// bounds by k_match_exact_emit -- no second contraction.  PASS 1 (the fallback when the pair
+// list overflows): the contraction again, candidates against the final bounds.
+// EMIT = false (PASS 0 only): bounds alone, over the seeding cross (cross = 1: the first <= 4 row
+// tiles x every column tile and the first <= 4 column tiles x the other row tiles), so that the
+// emitting pass starts from bounds near final ones instead of from +inf.
+// Three waves per SIMD requested: the accumulators then live in VGPRs (no AGPR copies), 126 VGPRs,
+// four workgroups per CU -- 0.41 -> 0.34 ms for the 10k x 10k bound pass.
+template <int PASS, bool EMIT>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) k_match_tiles(Side A, Side B, int D, int Dp, float c1, float c2,
                                                      uint32_t* __restrict__ Urow, uint32_t* __restrict__ Ucol,
                                                      int2* __restrict__ crow, int2* __restrict__ ccol,
-                                                     unsigned* __restrict__ ncand, unsigned cap) {
+                                                     unsigned* __restrict__ ncand, unsigned cap,
+                                                     int4* __restrict__ emit, unsigned* __restrict__ nemit,
+                                                     unsigned ecap, int gx, int gy, int group, int cross) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int64_t r0 = (int64_t)blockIdx.y * kTile + (wv >> 1) * 64;
-  const int64_t q0 = (int64_t)blockIdx.x * kTile + (wv & 1) * 64;
+  // XCD-aware tile order: workgroups are dealt round-robin over the 8 XCDs, so XCD x gets the
+  // flat ids x, x + 8, ...; it is handed the x-th contiguous eighth of a grouped tile sequence
+  // (group row tiles at a time, column-major inside the group) -- its in-flight tiles then share
+  // a few A and B panels in its own L2 instead of streaming every B panel from the MALL.
+  int ty, tx;
+  {
+    const int bid = blockIdx.x, T = gx * gy;
+    int seq = bid;
+    if (cross) {
+      const int sr = min(4, gy), sc = min(4, gx);
+      if (seq < sr * gx) {
+        ty = seq % sr;
+        tx = seq / sr;
+      } else {
+        seq -= sr * gx;
+        ty = sr + seq / sc;
+        tx = seq % sc;
+      }
+    } else if (group > 0) {
+      const int xcd = bid & 7, slot = bid >> 3, q = T >> 3, r = T & 7;
+      seq = xcd * q + min(xcd, r) + slot;
+      const int g = seq / (group * gx), idx = seq - g * group * gx;
+      const int rows = min(group, gy - g * group);
+      tx = idx / rows;
+      ty = g * group + (idx - tx * rows);
+    } else {
+      ty = seq / gx;
+      tx = seq - ty * gx;
+    }
+  }
+  const int64_t r0 = (int64_t)ty * kTile + (wv >> 1) * 64;
+  const int64_t q0 = (int64_t)tx * kTile + (wv & 1) * 64;
   const int KP = 3 * Dp;
   const int h = lane >> 5, l32 = lane & 31;
   f32x16 acc[2][2];
@@ -128,7 +170,7 @@ __global__ void __launch_bounds__(256) k_match_tiles(Side A, Side B, int D, int 
   __shared__ __attribute__((aligned(16))) uint16_t sa[2][kTile * RS];
   __shared__ __attribute__((aligned(16))) uint16_t sb[2][kTile * RS];
   const int tid = threadIdx.x;
-  const int64_t ra0 = (int64_t)blockIdx.y * kTile, qb0 = (int64_t)blockIdx.x * kTile;
+  const int64_t ra0 = (int64_t)ty * kTile, qb0 = (int64_t)tx * kTile;
   uint4 va0, va1, vb0, vb1;
   // 128 rows x 64 B per operand = 512 16-B pieces: thread t moves pieces t and t + 256
   const int row0 = tid >> 2, row1 = (tid + 256) >> 2, part = tid & 3;
@@ -181,30 +223,57 @@ __global__ void __launch_bounds__(256) k_match_tiles(Side A, Side B, int D, int 
     cn2[b] = B.n2[q];
     cnr[b] = B.nrm[q];
     cval[b] = B.valid[q] != 0;
-    ucol[b] = PASS ? Ucol[q] : kInfBits;
+    ucol[b] = Ucol[q];  // PASS 0: the running bound before this tile (>= the final one)
   }
   float cmin[2] = {__uint_as_float(kInfBits), __uint_as_float(kInfBits)};
+  // PASS 0: pairs are staged per wave in LDS (free after the main loop: 512 pairs per wave) and
+  // flushed with one global atomic per wave; a full stage spills straight to the global list
+  constexpr unsigned kStage = 512;
+  int4* stage = reinterpret_cast<int4*>(wv < 2 ? &sa[0][0] : &sb[0][0]) + (wv & 1) * kStage;
+  unsigned staged = 0;  // wave-uniform
+  // the wave's 64 rows (n2, norm, valid, running bound) staged in LDS by one load per lane: the
+  // emission branches would otherwise serialise the per-row global loads (one L2 trip per row)
+  float4* rowd = reinterpret_cast<float4*>(reinterpret_cast<char*>(wv < 2 ? &sa[0][0] : &sb[0][0]) + 16384) +
+                 (wv & 1) * 64;
+  if (PASS == 0 && EMIT) {
+    const int64_t rl = r0 + lane;
+    rowd[lane] = make_float4(A.n2[rl], A.nrm[rl], A.valid[rl] ? 1.f : 0.f, __uint_as_float(Urow[rl]));
+  }
 #pragma unroll
   for (int a = 0; a < 2; ++a) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      const int64_t row = r0 + 32 * a + (r & 3) + 8 * (r >> 2) + 4 * h;
-      const float rn2 = A.n2[row], rnr = A.nrm[row];
-      const bool rval = A.valid[row] != 0;
-      const uint32_t urow = PASS ? Urow[row] : kInfBits;
+      const int rr = 32 * a + (r & 3) + 8 * (r >> 2) + 4 * h;
+      const int64_t row = r0 + rr;
+      float rn2, rnr;
+      bool rval;
+      uint32_t urow;
+      if (PASS == 0 && EMIT) {
+        const float4 rd = rowd[rr];
+        rn2 = rd.x;
+        rnr = rd.y;
+        rval = rd.z != 0.f;
+        urow = __float_as_uint(rd.w);
+      } else {
+        rn2 = A.n2[row];
+        rnr = A.nrm[row];
+        rval = A.valid[row] != 0;
+        urow = Urow[row];
+      }
       float rmin = __uint_as_float(kInfBits);
+      float dh[2], e[2];
 #pragma unroll
       for (int b = 0; b < 2; ++b) {
-        const float dh = (rn2 + cn2[b]) - 2.0f * acc[a][b][r];
+        dh[b] = (rn2 + cn2[b]) - 2.0f * acc[a][b][r];
         const float s = rnr + cnr[b];
-        const float e = 1.5f * (c1 * (s * s) + c2 * (rnr * cnr[b])) + 1e-30f;
+        e[b] = 1.5f * (c1 * (s * s) + c2 * (rnr * cnr[b])) + 1e-30f;
         const bool ok = rval && cval[b];
         if (PASS == 0) {
-          const float ub = ok ? fmaxf(dh + e, 0.f) : __uint_as_float(kInfBits);
+          const float ub = ok ? fmaxf(dh[b] + e[b], 0.f) : __uint_as_float(kInfBits);
           rmin = fminf(rmin, ub);
           cmin[b] = fminf(cmin[b], ub);
         } else if (ok) {
-          const float lb = dh - e;
+          const float lb = dh[b] - e[b];
           const int64_t col = q0 + 32 * b + l32;
           if (lb <= __uint_as_float(urow)) {
             const unsigned slot = atomicAdd(&ncand[0], 1u);
@@ -220,6 +289,31 @@ __global__ void __launch_bounds__(256) k_match_tiles(Side A, Side B, int D, int 
 #pragma unroll
         for (int o = 16; o > 0; o >>= 1) rmin = fminf(rmin, __shfl_xor(rmin, o));
         if (l32 == 0 && rmin < __uint_as_float(kInfBits) && row < A.n) atomicMin(&Urow[row], __float_as_uint(rmin));
+        // any ub of a row (column) bounds its final U from above: the row's threshold is the
+        // running bound read before the tile or this wave's 64-column minimum, the column's the
+        // running bound or the minimum over the rows this lane has passed (this one included)
+        if (!EMIT) continue;
+        const float trow = fminf(__uint_as_float(urow), rmin);
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+          const float lb = dh[b] - e[b];
+          const bool em = rval && cval[b] && (lb <= trow || lb <= fminf(__uint_as_float(ucol[b]), cmin[b]));
+          const uint64_t m = __ballot(em);
+          if (m) {
+            const unsigned k = (unsigned)__popcll(m), pre = (unsigned)__popcll(m & ((1ull << lane) - 1ull));
+            const int4 pr = make_int4((int)row, (int)(q0 + 32 * b + l32), __float_as_int(lb), 0);
+            if (staged + k <= kStage) {
+              if (em) stage[staged + pre] = pr;
+              staged += k;
+            } else {
+              const int first = __ffsll((long long)m) - 1;
+              unsigned base = 0;
+              if (lane == first) base = atomicAdd(nemit, k);
+              base = __shfl(base, first);
+              if (em && base + pre < ecap) emit[base + pre] = pr;
+            }
+          }
+        }
       }
     }
   }
@@ -230,25 +324,94 @@ __global__ void __launch_bounds__(256) k_match_tiles(Side A, Side B, int D, int 
       const int64_t q = q0 + 32 * b + l32;
       if (h == 0 && v < __uint_as_float(kInfBits) && q < B.n) atomicMin(&Ucol[q], __float_as_uint(v));
     }
+    if (staged) {
+      unsigned base = 0;
+      if (lane == 0) base = atomicAdd(nemit, staged);
+      base = __shfl(base, 0);
+      for (unsigned i = lane; i < staged; i += 64)
+        if (base + i < ecap) emit[base + i] = stage[i];
+    }
   }
 }
 
-// one lane per candidate (i, j): FLANN L2_Simple in the reference order, 64-bit min key
-__global__ void __launch_bounds__(256) k_match_exact(const float* __restrict__ A, int64_t sa,
-                                                     const float* __restrict__ B, int64_t sb, int D,
-                                                     const int2* __restrict__ cand, const unsigned* __restrict__ ncand,
-                                                     unsigned long long* __restrict__ best) {
-  const unsigned n = *ncand;
-  for (unsigned t = blockIdx.x * 256 + threadIdx.x; t < n; t += gridDim.x * 256) {
-    const int2 c = cand[t];
-    const float* a = A + (int64_t)c.x * sa;
-    const float* b = B + (int64_t)c.y * sb;
-    float result = 0.0f;
+// L2_Simple in the reference order (oracle/or_match.cpp): a sequential fp32 sum, no FMA
+template <bool VEC>
+__device__ __forceinline__ float l2_simple(const float* __restrict__ a, const float* __restrict__ b, int D) {
+  float result = 0.0f;
+  if (VEC) {  // 16-B loads, the same sequential sum
+#pragma unroll 4
+    for (int k = 0; k < D; k += 4) {
+      const float4 x = *reinterpret_cast<const float4*>(a + k), y = *reinterpret_cast<const float4*>(b + k);
+      const float d0 = x.x - y.x, d1 = x.y - y.y, d2 = x.z - y.z, d3 = x.w - y.w;
+      result = result + d0 * d0;
+      result = result + d1 * d1;
+      result = result + d2 * d2;
+      result = result + d3 * d3;
+    }
+  } else {
     for (int k = 0; k < D; ++k) {
       const float diff = a[k] - b[k];
       result = result + diff * diff;
     }
-    atomicMin(&best[c.x], ((unsigned long long)__float_as_uint(result) << 32) | (uint32_t)c.y);
+  }
+  return result;
+}
+
+// The candidate test of the pruned pairs against the final bounds, fused with the exact pass:
+// a pair is a candidate of its row iff d^ - e <= U_row, of its column iff d^ - e <= U_col (the
+// tests k_match_tiles<1> makes); (a - b)^2 == (b - a)^2 in fp32, so one L2_Simple serves both.
+template <bool VEC>
+__global__ void __launch_bounds__(256) k_match_exact_emit(const float* __restrict__ A, int64_t sa,
+                                                          const float* __restrict__ B, int64_t sb, int D,
+                                                          const int4* __restrict__ emit,
+                                                          const unsigned* __restrict__ nemit, unsigned ecap,
+                                                          const uint32_t* __restrict__ Urow,
+                                                          const uint32_t* __restrict__ Ucol,
+                                                          unsigned* __restrict__ ncand,
+                                                          unsigned long long* __restrict__ bs,
+                                                          unsigned long long* __restrict__ bt) {
+  const unsigned n = min(*nemit, ecap);
+  unsigned nr = 0, nc = 0;
+  for (unsigned t = blockIdx.x * 256 + threadIdx.x; t < n; t += gridDim.x * 256) {
+    const int4 p = emit[t];
+    const float lb = __int_as_float(p.z);
+    const bool pr = lb <= __uint_as_float(Urow[p.x]), pc = lb <= __uint_as_float(Ucol[p.y]);
+    if (!(pr || pc)) continue;
+    const float d = l2_simple<VEC>(A + (int64_t)p.x * sa, B + (int64_t)p.y * sb, D);
+    if (pr) atomicMin(&bs[p.x], ((unsigned long long)__float_as_uint(d) << 32) | (uint32_t)p.y);
+    if (pc) atomicMin(&bt[p.y], ((unsigned long long)__float_as_uint(d) << 32) | (uint32_t)p.x);
+    nr += pr;
+    nc += pc;
+  }
+  // candidate counts (statistics): one atomic per wave
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    nr += __shfl_xor(nr, o);
+    nc += __shfl_xor(nc, o);
+  }
+  if ((threadIdx.x & 63) == 0 && (nr | nc)) {
+    atomicAdd(&ncand[0], nr);
+    atomicAdd(&ncand[1], nc);
+  }
+}
+
+template <bool VEC>
+__global__ void __launch_bounds__(256) k_match_exact(const float* __restrict__ A, int64_t sa,
+                                                     const float* __restrict__ B, int64_t sb, int D,
+                                                     const int2* __restrict__ crow, const int2* __restrict__ ccol,
+                                                     const unsigned* __restrict__ ncand, unsigned cap,
+                                                     unsigned long long* __restrict__ bs,
+                                                     unsigned long long* __restrict__ bt) {
+  // both directions in one launch (row candidates, then column candidates); counts past the
+  // buffer are clamped here and rerun by the host with a larger buffer
+  const unsigned n0 = min(ncand[0], cap), n1 = min(ncand[1], cap);
+  for (unsigned t = blockIdx.x * 256 + threadIdx.x; t < n0 + n1; t += gridDim.x * 256) {
+    const bool fwd = t < n0;
+    const int2 c = fwd ? crow[t] : ccol[t - n0];
+    const float* a = fwd ? A + (int64_t)c.x * sa : B + (int64_t)c.x * sb;
+    const float* b = fwd ? B + (int64_t)c.y * sb : A + (int64_t)c.y * sa;
+    const float result = l2_simple<VEC>(a, b, D);
+    atomicMin(fwd ? &bs[c.x] : &bt[c.x], ((unsigned long long)__float_as_uint(result) << 32) | (uint32_t)c.y);
   }
 }
 
@@ -320,32 +483,79 @@ void match_nearest_dev(pfx_ctx* ctx, const float* src, int64_t ns, int64_t ss, c
   uint32_t* Ucol = ctx->buf("match_ucol").as<uint32_t>(b.n_pad);
   unsigned long long* bs = ctx->buf("match_bs").as<unsigned long long>(ns);
   unsigned long long* bt = ctx->buf("match_bt").as<unsigned long long>(nt);
-  unsigned* ncand = ctx->buf("match_ncand").as<unsigned>(2);
+  unsigned* ncand = ctx->buf("match_ncand").as<unsigned>(3);
   PFX_HIP(hipMemsetAsync(Urow, 0x7f, sizeof(uint32_t) * a.n_pad, st));  // 0x7f7f7f7f: above any bound
   PFX_HIP(hipMemsetAsync(Ucol, 0x7f, sizeof(uint32_t) * b.n_pad, st));
-  PFX_HIP(hipMemsetAsync(bs, 0xff, sizeof(unsigned long long) * ns, st));
-  PFX_HIP(hipMemsetAsync(bt, 0xff, sizeof(unsigned long long) * nt, st));
   const float u = 5.9604645e-8f;  // 2^-24
   const float c1 = (2.0f * (float)D + 6.1f) * u, c2 = 12.2f * (float)D * u + 6.2f / 65536.0f;
-  const dim3 grid((unsigned)(b.n_pad / kTile), (unsigned)(a.n_pad / kTile));
+  const int gx = (int)(b.n_pad / kTile), gy = (int)(a.n_pad / kTile);
+  const unsigned grid = (unsigned)gx * (unsigned)gy;
+  static const int group = getenv("PFX_MATCH_GROUP") ? atoi(getenv("PFX_MATCH_GROUP")) : 8;
+  const bool vec = D % 4 == 0 && ss % 4 == 0 && ts % 4 == 0 && ((uintptr_t)src & 15) == 0 && ((uintptr_t)tgt & 15) == 0;
+  unsigned* h = ctx->readback<unsigned>();
+  // the pruned pair list: a few dozen pairs per row normally (PFX_MATCH_RECOMPUTE=1 forces the
+  // two-contraction fallback)
+  static const bool recompute = getenv("PFX_MATCH_RECOMPUTE") && *getenv("PFX_MATCH_RECOMPUTE") == '1';
+  const unsigned ecap = recompute ? 0u : (unsigned)std::min<int64_t>(64 * (ns + nt) + (1 << 16), int64_t(1) << 28);
+  int4* emit = ctx->buf("match_emit").as<int4>(std::max(ecap, 1u));
+  unsigned* nemit = ncand + 2;
+  PFX_HIP(hipMemsetAsync(ncand, 0, 3 * sizeof(unsigned), st));
+  PFX_HIP(hipMemsetAsync(bs, 0xff, sizeof(unsigned long long) * ns, st));
+  PFX_HIP(hipMemsetAsync(bt, 0xff, sizeof(unsigned long long) * nt, st));
+  if (gx > 16 && gy > 16) {  // seed the bounds (a tenth of the tiles at 10k x 10k)
+    TimeScope ts0(ctx, "match_seed");
+    const unsigned ncross = (unsigned)(4 * gx + 4 * (gy - 4));
+    k_match_tiles<0, false><<<ncross, 256, 0, st>>>(a.side, b.side, D, Dp, c1, c2, Urow, Ucol, nullptr, nullptr,
+                                                    nullptr, 0, nullptr, nullptr, 0, gx, gy, 0, 1);
+    check_launch("k_match_tiles<0, false>");
+  }
   {
     TimeScope ts1(ctx, "match_bound");
-    k_match_tiles<0><<<grid, 256, 0, st>>>(a.side, b.side, D, Dp, c1, c2, Urow, Ucol, nullptr, nullptr, nullptr, 0);
-    check_launch("k_match_tiles<0>");
+    k_match_tiles<0, true><<<grid, 256, 0, st>>>(a.side, b.side, D, Dp, c1, c2, Urow, Ucol, nullptr, nullptr, nullptr,
+                                                 0, emit, nemit, ecap, gx, gy, group, 0);
+    check_launch("k_match_tiles<0, true>");
   }
+  {
+    TimeScope ts3(ctx, "match_exact");
+    auto* ke = vec ? k_match_exact_emit<true> : k_match_exact_emit<false>;
+    ke<<<1024, 256, 0, st>>>(src, ss, tgt, ts, D, emit, nemit, ecap, Urow, Ucol, ncand, bs, bt);
+    check_launch("k_match_exact_emit");
+  }
+  k_match_finish<<<(unsigned)ceil_div(ns, 256), 256, 0, st>>>(bs, ns, s2t, ds2t);
+  if (t2s) k_match_finish<<<(unsigned)ceil_div(nt, 256), 256, 0, st>>>(bt, nt, t2s, dt2s);
+  check_launch("k_match_finish");
+  PFX_HIP(hipMemcpyAsync(h, ncand, 3 * sizeof(unsigned), hipMemcpyDeviceToHost, st));
+  PFX_HIP(hipStreamSynchronize(st));  // the one host round trip of a normal call
+  ctx->stats["match_pairs_emitted"] = h[2];
+  ctx->stats["match_candidates_rows"] = h[0];
+  ctx->stats["match_candidates_cols"] = h[1];
+  if (h[2] <= ecap) return;
+  // fallback: the pair list overflowed (near-duplicate descriptors) -- the contraction again,
+  // candidates against the final bounds, exact pass over the candidate lists
   DevBuf& cb = ctx->buf("match_cand");
   unsigned cap = (unsigned)std::min<int64_t>(std::max<int64_t>(8 * (ns + nt), 1 << 20), int64_t(1) << 30);
   for (int attempt = 0; attempt < 2; ++attempt) {
     int2* crow = static_cast<int2*>(cb.get(sizeof(int2) * 2 * (size_t)cap));
     int2* ccol = crow + cap;
     PFX_HIP(hipMemsetAsync(ncand, 0, 2 * sizeof(unsigned), st));
+    PFX_HIP(hipMemsetAsync(bs, 0xff, sizeof(unsigned long long) * ns, st));
+    PFX_HIP(hipMemsetAsync(bt, 0xff, sizeof(unsigned long long) * nt, st));
     {
       TimeScope ts2(ctx, "match_filter");
-      k_match_tiles<1><<<grid, 256, 0, st>>>(a.side, b.side, D, Dp, c1, c2, Urow, Ucol, crow, ccol, ncand, cap);
+      k_match_tiles<1, false><<<grid, 256, 0, st>>>(a.side, b.side, D, Dp, c1, c2, Urow, Ucol, crow, ccol, ncand,
+                                                    cap, nullptr, nullptr, 0, gx, gy, group, 0);
       check_launch("k_match_tiles<1>");
     }
-    unsigned h[2];
-    PFX_HIP(hipMemcpyAsync(h, ncand, sizeof(h), hipMemcpyDeviceToHost, st));
+    {
+      TimeScope ts3(ctx, "match_exact");
+      auto* ke = vec ? k_match_exact<true> : k_match_exact<false>;
+      ke<<<1024, 256, 0, st>>>(src, ss, tgt, ts, D, crow, ccol, ncand, cap, bs, bt);
+      check_launch("k_match_exact");
+    }
+    k_match_finish<<<(unsigned)ceil_div(ns, 256), 256, 0, st>>>(bs, ns, s2t, ds2t);
+    if (t2s) k_match_finish<<<(unsigned)ceil_div(nt, 256), 256, 0, st>>>(bt, nt, t2s, dt2s);
+    check_launch("k_match_finish");
+    PFX_HIP(hipMemcpyAsync(h, ncand, 2 * sizeof(unsigned), hipMemcpyDeviceToHost, st));
     PFX_HIP(hipStreamSynchronize(st));
     ctx->stats["match_candidates_rows"] = h[0];
     ctx->stats["match_candidates_cols"] = h[1];
@@ -354,17 +564,8 @@ void match_nearest_dev(pfx_ctx* ctx, const float* src, int64_t ns, int64_t ss, c
       cap = std::max(h[0], h[1]);
       continue;
     }
-    TimeScope ts3(ctx, "match_exact");
-    const unsigned g0 = (unsigned)std::max<int64_t>(1, std::min<int64_t>(ceil_div(h[0], 256), 8192));
-    const unsigned g1 = (unsigned)std::max<int64_t>(1, std::min<int64_t>(ceil_div(h[1], 256), 8192));
-    k_match_exact<<<g0, 256, 0, st>>>(src, ss, tgt, ts, D, crow, ncand, bs);
-    k_match_exact<<<g1, 256, 0, st>>>(tgt, ts, src, ss, D, ccol, ncand + 1, bt);
-    check_launch("k_match_exact");
     break;
   }
-  k_match_finish<<<(unsigned)ceil_div(ns, 256), 256, 0, st>>>(bs, ns, s2t, ds2t);
-  if (t2s) k_match_finish<<<(unsigned)ceil_div(nt, 256), 256, 0, st>>>(bt, nt, t2s, dt2s);
-  check_launch("k_match_finish");
 }
 
 int64_t correspondences_dev(pfx_ctx* ctx, const float* src, int64_t ns, int64_t ss, const float* tgt, int64_t nt,

@@ -103,3 +103,15 @@ def test_nearest_host_api(ctx):
     idx, dist = ctx.nearest_descriptors(src, tgt)
     oi, od = O.nearest_descriptor(src, tgt)
     assert np.array_equal(idx, oi) and _same(dist, od)
+
+
+def test_match_pair_list_overflow(ctx):
+    """Near-duplicate sets (two distinct rows, 1000 copies each): every same-class pair ties, the
+    bound pass's pruned pair list overflows, and the two-contraction fallback (candidates against
+    the final bounds) must give the same answer."""
+    rng = np.random.default_rng(21)
+    base = shot_like(rng, 2)
+    src = base[rng.integers(0, 2, 2000)]
+    tgt = base[rng.integers(0, 2, 2000)]
+    _check(ctx, src, tgt)
+    assert ctx.stat("match_pairs_emitted") > 64 * (len(src) + len(tgt)) + 65536
