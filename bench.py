@@ -647,6 +647,10 @@ def scans_line(args, world, n_scans, scans_here, shot, elapsed, timers, iso, nb_
              "algorithmic_bytes_per_launch": int(chain_algo), "ms": chain_ms,
              "achieved": round(chain_algo / (chain_ms / 1e3) / 1e9, 2) if chain_ms > 0 else None}
     chain["frac"] = round(chain["achieved"] / HBM_PEAK_GBS, 5) if chain["achieved"] else None
+    if chain["frac"] and chain["frac"] > 1:
+        chain["note"] = ("above 1: the chains read each neighbour from the LDS-staged cell that many queries share, "
+                         "so the algorithmic gather bytes exceed what HBM delivers -- these neighbourhoods are not "
+                         "HBM-bound (the configs[2] line is the HBM-roofline case)")
     # the committed PMC summary was collected on configs[2]'s scan: only that line may cite it
     pmc = (load_pmc("pmc_normals_stage.json") or {}) if (npts == N_POINTS and not fast) else {}
     roofline = {"bound": "hbm", "kernel": "normals stage: grid + k_nb_tile/k_nb_query list builders + "

@@ -13,9 +13,14 @@
 //              a_hi.b_hi + a_hi.b_lo + a_lo.b_hi (error <= 3.1 2^-16 |a||b|).
 //   2. bound:  128x128 workgroup tiles of d^ = |a|^2 + |b|^2 - 2 a.b on v_mfma_f32_32x32x16_bf16;
 //              with the rigorous error bound e(a, b) (below) |d^ - L2_Simple(a, b)| <= e, every
-//              row keeps U_i = min_j (d^_ij + e_ij) and every column U_j likewise.
-//   3. filter: the tiles again; (i, j) is a candidate of row i iff d^_ij - e_ij <= U_i (the true
-//              minimiser always is), of column j iff d^_ij - e_ij <= U_j.
+//              row keeps U_i = min_j (d^_ij + e_ij) and every column U_j likewise.  A seeding
+//              launch over a cross of tiles (4 row tiles x all, all x 4 column tiles) first
+//              brings the bounds near their final values.
+//   3. prune:  the same launch emits (i, j, d^_ij - e_ij) for the pairs whose d^ - e is within the
+//              running bound of the row or the column (running bounds only fall, so no candidate
+//              is missed); (i, j) is a candidate of row i iff d^_ij - e_ij <= U_i (the true
+//              minimiser always is), of column j iff d^_ij - e_ij <= U_j, tested on that list.
+//              A list overflow falls back to a second contraction that tests every pair.
 //   4. exact:  one lane per candidate evaluates L2_Simple in the reference's order and keeps the
 //              minimum of the 64-bit key (float bits << 32 | row) -- ties go to the lowest row.
 //   5. mutual: target2source[source2target[c]] == c, compacted in source order.
@@ -51,6 +56,13 @@ __device__ __forceinline__ uint16_t bf16_rne(float f) {
 }
 __device__ __forceinline__ float bf16_val(uint16_t h) { return __uint_as_float((uint32_t)h << 16); }
 
+#ifndef PFX_MATCH_KC
+#define PFX_MATCH_KC 32
+#endif
+constexpr int kKC = PFX_MATCH_KC;  // K per LDS stage
+// packed row length: the three Dp-long parts, zero-padded to whole K stages
+__host__ __device__ inline int kp_of(int Dp) { return (3 * Dp + kKC - 1) / kKC * kKC; }
+
 // one wave per row: validity, fp32 squared norm, packed bf16 split (pad rows/dims are zero)
 __global__ void __launch_bounds__(256) k_match_prep(const float* __restrict__ X, int64_t n, int64_t stride, int D,
                                                     int Dp, int64_t n_pad, int is_target,
@@ -59,8 +71,9 @@ __global__ void __launch_bounds__(256) k_match_prep(const float* __restrict__ X,
   const int lane = threadIdx.x & 63;
   const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (i >= n_pad) return;
-  const int KP = 3 * Dp;
+  const int KP = kp_of(Dp);
   uint16_t* row = P + i * KP;
+  for (int k = 3 * Dp + lane; k < KP; k += 64) row[k] = 0;
   bool ok = i < n;
   float s = 0.f;
   if (ok) {
@@ -152,7 +165,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) k
   }
   const int64_t r0 = (int64_t)ty * kTile + (wv >> 1) * 64;
   const int64_t q0 = (int64_t)tx * kTile + (wv & 1) * 64;
-  const int KP = 3 * Dp;
+  const int KP = kp_of(Dp);
   const int h = lane >> 5, l32 = lane & 31;
   f32x16 acc[2][2];
 #pragma unroll
@@ -162,41 +175,58 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) k
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
   // K in chunks of KC = 32 (two MFMA k-steps): the workgroup's 128 A rows and 128 B rows of a
-  // chunk are staged in LDS (double buffer; rows padded to 80 B so the 32 rows a fragment read
+  // chunk are staged in LDS (double buffer; rows padded by 16 B so the 32 rows a fragment read
   // touches spread over the banks) and the next chunk's global loads are in flight while the
   // current one is multiplied -- every fragment is read from L2 once per workgroup instead of
   // once per wave.
-  constexpr int KC = 32, RS = KC + 8;
+  constexpr int KC = kKC, RS = KC + 8;
   __shared__ __attribute__((aligned(16))) uint16_t sa[2][kTile * RS];
   __shared__ __attribute__((aligned(16))) uint16_t sb[2][kTile * RS];
   const int tid = threadIdx.x;
   const int64_t ra0 = (int64_t)ty * kTile, qb0 = (int64_t)tx * kTile;
-  uint4 va0, va1, vb0, vb1;
-  // 128 rows x 64 B per operand = 512 16-B pieces: thread t moves pieces t and t + 256
-  const int row0 = tid >> 2, row1 = (tid + 256) >> 2, part = tid & 3;
-#define PFX_MATCH_GLOAD(k0)                                                                       \
-  va0 = *reinterpret_cast<const uint4*>(A.P + (ra0 + row0) * KP + (k0) + part * 8);               \
-  va1 = *reinterpret_cast<const uint4*>(A.P + (ra0 + row1) * KP + (k0) + part * 8);               \
-  vb0 = *reinterpret_cast<const uint4*>(B.P + (qb0 + row0) * KP + (k0) + part * 8);               \
-  vb1 = *reinterpret_cast<const uint4*>(B.P + (qb0 + row1) * KP + (k0) + part * 8)
-#define PFX_MATCH_SSTORE(buf)                                                                     \
-  *reinterpret_cast<uint4*>(&sa[buf][row0 * RS + part * 8]) = va0;                                \
-  *reinterpret_cast<uint4*>(&sa[buf][row1 * RS + part * 8]) = va1;                                \
-  *reinterpret_cast<uint4*>(&sb[buf][row0 * RS + part * 8]) = vb0;                                \
-  *reinterpret_cast<uint4*>(&sb[buf][row1 * RS + part * 8]) = vb1
+  // 128 rows x 2 KC B per operand = 16 KC 16-B pieces: thread t moves pieces t + 256 i
+  constexpr int PARTS = KC / 8, NP = PARTS / 2;
+  static_assert(NP == 2 || NP == 4, "KC 32 or 64");
+  uint4 va0, va1, va2, va3, vb0, vb1, vb2, vb3;  // (named: an array here went to scratch)
+  auto ld = [&](int i, int k0, uint4& x, uint4& y) {
+    const int pc = tid + 256 * i, rw = pc / PARTS, pt = pc % PARTS;
+    x = *reinterpret_cast<const uint4*>(A.P + (ra0 + rw) * KP + k0 + pt * 8);
+    y = *reinterpret_cast<const uint4*>(B.P + (qb0 + rw) * KP + k0 + pt * 8);
+  };
+  auto st = [&](int i, int buf, const uint4& x, const uint4& y) {
+    const int pc = tid + 256 * i, rw = pc / PARTS, pt = pc % PARTS;
+    *reinterpret_cast<uint4*>(&sa[buf][rw * RS + pt * 8]) = x;
+    *reinterpret_cast<uint4*>(&sb[buf][rw * RS + pt * 8]) = y;
+  };
+  auto gload = [&](int k0) {
+    ld(0, k0, va0, vb0);
+    ld(1, k0, va1, vb1);
+    if constexpr (NP == 4) {
+      ld(2, k0, va2, vb2);
+      ld(3, k0, va3, vb3);
+    }
+  };
+  auto sstore = [&](int buf) {
+    st(0, buf, va0, vb0);
+    st(1, buf, va1, vb1);
+    if constexpr (NP == 4) {
+      st(2, buf, va2, vb2);
+      st(3, buf, va3, vb3);
+    }
+  };
   const int nch = KP / KC;
   const int ar = (wv >> 1) * 64 + l32, br = (wv & 1) * 64 + l32;
-  PFX_MATCH_GLOAD(0);
-  PFX_MATCH_SSTORE(0);
+  gload(0);
+  sstore(0);
   __syncthreads();
   for (int c = 0; c < nch; ++c) {
     const int buf = c & 1;
     if (c + 1 < nch) {
-      PFX_MATCH_GLOAD((c + 1) * KC);
+      gload((c + 1) * KC);
     }
 #pragma unroll
-    for (int st = 0; st < 2; ++st) {
-      const int ko = 16 * st + 8 * h;
+    for (int ks = 0; ks < KC / 16; ++ks) {
+      const int ko = 16 * ks + 8 * h;
       const bf16x8 fa0 = *reinterpret_cast<const bf16x8*>(&sa[buf][ar * RS + ko]);
       const bf16x8 fa1 = *reinterpret_cast<const bf16x8*>(&sa[buf][(ar + 32) * RS + ko]);
       const bf16x8 fb0 = *reinterpret_cast<const bf16x8*>(&sb[buf][br * RS + ko]);
@@ -207,12 +237,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) k
       acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa1, fb1, acc[1][1], 0, 0, 0);
     }
     if (c + 1 < nch) {  // buf ^ 1 was last read before the previous barrier
-      PFX_MATCH_SSTORE(buf ^ 1);
+      sstore(buf ^ 1);
     }
     __syncthreads();
   }
-#undef PFX_MATCH_GLOAD
-#undef PFX_MATCH_SSTORE
   // epilogue: C/D map of 32x32 tiles: col = lane & 31, row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5)
   float cn2[2], cnr[2];
   bool cval[2];
@@ -448,7 +476,7 @@ Prepared prep(pfx_ctx* ctx, const char* tag, const float* X, int64_t n, int64_t 
               bool target) {
   const int64_t n_pad = std::max<int64_t>(ceil_div(n, kTile), 1) * kTile;
   const std::string t(tag);
-  uint16_t* P = ctx->buf((t + "_pk").c_str()).as<uint16_t>((size_t)n_pad * 3 * Dp);
+  uint16_t* P = ctx->buf((t + "_pk").c_str()).as<uint16_t>((size_t)n_pad * kp_of(Dp));
   float* n2 = ctx->buf((t + "_n2").c_str()).as<float>(n_pad);
   float* nr = ctx->buf((t + "_nr").c_str()).as<float>(n_pad);
   uint8_t* v = ctx->buf((t + "_v").c_str()).as<uint8_t>(n_pad);
