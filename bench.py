@@ -797,7 +797,8 @@ def bench_match(args, torch, dev, world, rank, local):
         tf, nf = ctx.kernel_time("match_filter")
         tsd, nsd = ctx.kernel_time("match_seed")
         gx, gy = pad(nt) // 128, pad(ns) // 128
-        seed_tiles = 4 * gx + 4 * (gy - 4) if (gx > 16 and gy > 16) else 0
+        sr, sc = min(gy, max(4, (gy + 19) // 20)), min(gx, max(4, (gx + 19) // 20))
+        seed_tiles = sr * gx + sc * (gy - sr) if (gx > 16 and gy > 16) else 0
         flops = ((1 + nf / max(nb, 1)) * pad(ns) * pad(nt) + (nsd / max(nb, 1)) * seed_tiles * 128 * 128) * 2.0 * 3 * 352
         tiles_s = (tb + tf + tsd) / max(nb, 1) / 1e3
         achieved = flops / tiles_s / 1e12 if tiles_s > 0 else 0.0

@@ -120,8 +120,8 @@ struct Side {
 // the tiles that lowered a bound) are emitted as (row, col, d^ - e) and tested against the final
 // bounds by k_match_exact_emit -- no second contraction.  PASS 1 (the fallback when the pair
 // list overflows): the contraction again, candidates against the final bounds.
-// EMIT = false (PASS 0 only): bounds alone, over the seeding cross (cross = 1: the first <= 4 row
-// tiles x every column tile and the first <= 4 column tiles x the other row tiles), so that the
+// EMIT = false (PASS 0 only): bounds alone, over the seeding cross (cross = 1: the first sr row
+// tiles x every column tile and the first sc column tiles x the other row tiles), so that the
 // emitting pass starts from bounds near final ones instead of from +inf.
 // Three waves per SIMD requested: the accumulators then live in VGPRs (no AGPR copies), 126 VGPRs,
 // four workgroups per CU -- 0.41 -> 0.34 ms for the 10k x 10k bound pass.
@@ -131,7 +131,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) k
                                                      int2* __restrict__ crow, int2* __restrict__ ccol,
                                                      unsigned* __restrict__ ncand, unsigned cap,
                                                      int4* __restrict__ emit, unsigned* __restrict__ nemit,
-                                                     unsigned ecap, int gx, int gy, int group, int cross) {
+                                                     unsigned ecap, int gx, int gy, int group, int cross,
+                                                     int sr, int sc) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   // XCD-aware tile order: workgroups are dealt round-robin over the 8 XCDs, so XCD x gets the
   // flat ids x, x + 8, ...; it is handed the x-th contiguous eighth of a grouped tile sequence
@@ -142,7 +143,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) k
     const int bid = blockIdx.x, T = gx * gy;
     int seq = bid;
     if (cross) {
-      const int sr = min(4, gy), sc = min(4, gx);
       if (seq < sr * gx) {
         ty = seq % sr;
         tx = seq / sr;
@@ -530,17 +530,21 @@ void match_nearest_dev(pfx_ctx* ctx, const float* src, int64_t ns, int64_t ss, c
   PFX_HIP(hipMemsetAsync(ncand, 0, 3 * sizeof(unsigned), st));
   PFX_HIP(hipMemsetAsync(bs, 0xff, sizeof(unsigned long long) * ns, st));
   PFX_HIP(hipMemsetAsync(bt, 0xff, sizeof(unsigned long long) * nt, st));
-  if (gx > 16 && gy > 16) {  // seed the bounds (a tenth of the tiles at 10k x 10k)
+  if (gx > 16 && gy > 16) {
+    // seed the bounds over the cross of the first sr row tiles and sc column tiles, a tenth of the
+    // tiles at any size (at least 4 each): a pair then passes a seeded bound with probability
+    // ~ 1 / (128 s), so the pair list stays at a few dozen pairs per row as the sets grow
     TimeScope ts0(ctx, "match_seed");
-    const unsigned ncross = (unsigned)(4 * gx + 4 * (gy - 4));
+    const int sr = std::min(gy, std::max(4, (gy + 19) / 20)), sc = std::min(gx, std::max(4, (gx + 19) / 20));
+    const unsigned ncross = (unsigned)(sr * gx + sc * (gy - sr));
     k_match_tiles<0, false><<<ncross, 256, 0, st>>>(a.side, b.side, D, Dp, c1, c2, Urow, Ucol, nullptr, nullptr,
-                                                    nullptr, 0, nullptr, nullptr, 0, gx, gy, 0, 1);
+                                                    nullptr, 0, nullptr, nullptr, 0, gx, gy, 0, 1, sr, sc);
     check_launch("k_match_tiles<0, false>");
   }
   {
     TimeScope ts1(ctx, "match_bound");
     k_match_tiles<0, true><<<grid, 256, 0, st>>>(a.side, b.side, D, Dp, c1, c2, Urow, Ucol, nullptr, nullptr, nullptr,
-                                                 0, emit, nemit, ecap, gx, gy, group, 0);
+                                                 0, emit, nemit, ecap, gx, gy, group, 0, 0, 0);
     check_launch("k_match_tiles<0, true>");
   }
   {
@@ -571,7 +575,7 @@ void match_nearest_dev(pfx_ctx* ctx, const float* src, int64_t ns, int64_t ss, c
     {
       TimeScope ts2(ctx, "match_filter");
       k_match_tiles<1, false><<<grid, 256, 0, st>>>(a.side, b.side, D, Dp, c1, c2, Urow, Ucol, crow, ccol, ncand,
-                                                    cap, nullptr, nullptr, 0, gx, gy, group, 0);
+                                                    cap, nullptr, nullptr, 0, gx, gy, group, 0, 0, 0);
       check_launch("k_match_tiles<1>");
     }
     {

@@ -6,6 +6,7 @@ cp gpurun_out/bench_$T.json profiles/${T}_bench_fpfh_line.json
 for w in shot match iss harris harris6d config1 fastnormals demand scans8 dense; do cp gpurun_out/bench_${w}_$T.json profiles/${T}_bench_${w}_line.json; done
 cp gpurun_out/prof_$T/run_kernel_stats.csv profiles/${T}_kernel_stats.csv
 cp gpurun_out/prof_iss_$T/run_kernel_stats.csv profiles/${T}_iss_kernel_stats.csv
+cp gpurun_out/prof_match_$T/run_kernel_stats.csv profiles/${T}_match_kernel_stats.csv
 cp gpurun_out/pmc_$T/summary.txt profiles/${T}_pmc_summary.txt
 cp gpurun_out/pmc_$T/pmc_normals_stage.json profiles/pmc_normals_stage.json
 cp gpurun_out/pmc_$T/pmc_normals_chain.json profiles/pmc_normals_chain.json

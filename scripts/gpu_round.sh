@@ -16,4 +16,5 @@ timeout -k 10 400 python bench.py --workload dense --steps 3 --warmup 1 > gpurun
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof_$TAG -o run -- python3 $R/bench.py --steps 5 --warmup 2 --no-cpu-baseline > $R/gpurun_out/prof_$TAG.log 2>&1 || { tail -20 $R/gpurun_out/prof_$TAG.log; exit 1; }
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof_iss_$TAG -o run -- python3 $R/bench.py --workload iss --steps 5 --warmup 2 --no-cpu-baseline > $R/gpurun_out/prof_iss_$TAG.log 2>&1 || { tail -20 $R/gpurun_out/prof_iss_$TAG.log; exit 1; }
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof_match_$TAG -o run -- python3 $R/bench.py --workload match --steps 20 --warmup 3 --no-cpu-baseline > $R/gpurun_out/prof_match_$TAG.log 2>&1 || { tail -20 $R/gpurun_out/prof_match_$TAG.log; exit 1; }
 cd $R && bash scripts/gpu_pmc.sh $TAG

@@ -55,10 +55,13 @@ def _check(ctx, src, tgt, stride=None):
 
 
 @pytest.mark.parametrize("kind,ns,nt", [("fpfh", 133, 151), ("fpfh", 1000, 777), ("shot", 300, 513),
-                                        ("shot", 2049, 1500)])
+                                        ("shot", 2049, 1500), ("shot", 2200, 2300)])
 def test_match_parity(ctx, kind, ns, nt):
+    """(2200 x 2300: over 16 tiles each way, so the seeding cross runs before the bound pass.)"""
     src, tgt = pair(kind, ns, nt, seed=ns + nt)
     assert _check(ctx, src, tgt) > 0
+    if ns > 2048 and nt > 2048:
+        assert 0 < ctx.stat("match_pairs_emitted") <= 64 * (ns + nt)
 
 
 def test_match_shot352_stride(ctx):
