@@ -320,8 +320,12 @@ void narf_release(pfx_ctx* ctx);
 pfx_status pcd_read_header(const char* path, pfx_pcd_header* out, std::string& err);
 int64_t pcd_load_xyz_dev(pfx_ctx* ctx, const char* path, float* d_x, float* d_y, float* d_z, int64_t cap,
                          pfx_pcd_header* hdr_out);
-void match_nearest_dev(pfx_ctx* ctx, const float* src, int64_t ns, int64_t ss, const float* tgt, int64_t nt,
-                       int64_t ts, int D, int32_t* s2t, float* ds2t, int32_t* t2s, float* dt2s);
+// mode 0: complete (one host round trip); 1: deferred -- returns true when the caller must, after
+// its own stream synchronisation, call match_pairs_overflowed and rerun with mode 2 if it says so;
+// 2: the two-contraction path (no pruned pair list)
+bool match_nearest_dev(pfx_ctx* ctx, const float* src, int64_t ns, int64_t ss, const float* tgt, int64_t nt,
+                       int64_t ts, int D, int32_t* s2t, float* ds2t, int32_t* t2s, float* dt2s, int mode = 0);
+bool match_pairs_overflowed(pfx_ctx* ctx);
 int64_t correspondences_dev(pfx_ctx* ctx, const float* src, int64_t ns, int64_t ss, const float* tgt, int64_t nt,
                             int64_t ts, int D, int32_t* query, int32_t* match, int64_t cap);
 

@@ -490,18 +490,26 @@ Prepared prep(pfx_ctx* ctx, const char* tag, const float* X, int64_t n, int64_t 
 
 // Both directions at once (the tiles serve rows and columns): s2t[i] = nearest target row of
 // source row i, t2s[j] = nearest source row of target row j (-1: no finite row / no target).
-void match_nearest_dev(pfx_ctx* ctx, const float* src, int64_t ns, int64_t ss, const float* tgt, int64_t nt,
-                       int64_t ts, int D, int32_t* s2t, float* ds2t, int32_t* t2s, float* dt2s) {
+bool match_pairs_overflowed(pfx_ctx* ctx) {
+  const unsigned* h = ctx->readback<unsigned>();  // (written by the deferred call's copy)
+  ctx->stats["match_pairs_emitted"] = h[2];
+  ctx->stats["match_candidates_rows"] = h[0];
+  ctx->stats["match_candidates_cols"] = h[1];
+  return (int64_t)h[2] > ctx->stats["match_pair_cap"];
+}
+
+bool match_nearest_dev(pfx_ctx* ctx, const float* src, int64_t ns, int64_t ss, const float* tgt, int64_t nt,
+                       int64_t ts, int D, int32_t* s2t, float* ds2t, int32_t* t2s, float* dt2s, int mode) {
   PFX_CHECK(D > 0 && ns >= 0 && nt >= 0 && ss >= D && ts >= D, "match: invalid dimensions");
   PFX_CHECK(ns < (int64_t(1) << 31) && nt < (int64_t(1) << 31), "match: too many rows");
   hipStream_t st = ctx->stream;
-  if (ns == 0 && nt == 0) return;
+  if (ns == 0 && nt == 0) return false;
   if (ns == 0 || nt == 0) {  // nothing to match against
     if (ns) PFX_HIP(hipMemsetAsync(s2t, 0xff, sizeof(int32_t) * ns, st));
     if (nt && t2s) PFX_HIP(hipMemsetAsync(t2s, 0xff, sizeof(int32_t) * nt, st));
     if (ns && ds2t) PFX_HIP(hipMemsetAsync(ds2t, 0xff, sizeof(float) * ns, st));
     if (nt && dt2s) PFX_HIP(hipMemsetAsync(dt2s, 0xff, sizeof(float) * nt, st));
-    return;
+    return false;
   }
   TimeScope total(ctx, "match", true);
   const int Dp = (D + 31) / 32 * 32;  // K = 3 Dp: whole 32-deep LDS chunks
@@ -524,7 +532,9 @@ void match_nearest_dev(pfx_ctx* ctx, const float* src, int64_t ns, int64_t ss, c
   // the pruned pair list: a few dozen pairs per row normally (PFX_MATCH_RECOMPUTE=1 forces the
   // two-contraction fallback)
   static const bool recompute = getenv("PFX_MATCH_RECOMPUTE") && *getenv("PFX_MATCH_RECOMPUTE") == '1';
-  const unsigned ecap = recompute ? 0u : (unsigned)std::min<int64_t>(64 * (ns + nt) + (1 << 16), int64_t(1) << 28);
+  const unsigned ecap =
+      (recompute || mode == 2) ? 0u : (unsigned)std::min<int64_t>(64 * (ns + nt) + (1 << 16), int64_t(1) << 28);
+  ctx->stats["match_pair_cap"] = ecap;
   int4* emit = ctx->buf("match_emit").as<int4>(std::max(ecap, 1u));
   unsigned* nemit = ncand + 2;
   PFX_HIP(hipMemsetAsync(ncand, 0, 3 * sizeof(unsigned), st));
@@ -557,11 +567,9 @@ void match_nearest_dev(pfx_ctx* ctx, const float* src, int64_t ns, int64_t ss, c
   if (t2s) k_match_finish<<<(unsigned)ceil_div(nt, 256), 256, 0, st>>>(bt, nt, t2s, dt2s);
   check_launch("k_match_finish");
   PFX_HIP(hipMemcpyAsync(h, ncand, 3 * sizeof(unsigned), hipMemcpyDeviceToHost, st));
+  if (mode == 1) return true;  // the caller synchronises once for everything it launched
   PFX_HIP(hipStreamSynchronize(st));  // the one host round trip of a normal call
-  ctx->stats["match_pairs_emitted"] = h[2];
-  ctx->stats["match_candidates_rows"] = h[0];
-  ctx->stats["match_candidates_cols"] = h[1];
-  if (h[2] <= ecap) return;
+  if (!match_pairs_overflowed(ctx)) return false;
   // fallback: the pair list overflowed (near-duplicate descriptors) -- the contraction again,
   // candidates against the final bounds, exact pass over the candidate lists
   DevBuf& cb = ctx->buf("match_cand");
@@ -598,6 +606,7 @@ void match_nearest_dev(pfx_ctx* ctx, const float* src, int64_t ns, int64_t ss, c
     }
     break;
   }
+  return false;
 }
 
 int64_t correspondences_dev(pfx_ctx* ctx, const float* src, int64_t ns, int64_t ss, const float* tgt, int64_t nt,
@@ -605,23 +614,31 @@ int64_t correspondences_dev(pfx_ctx* ctx, const float* src, int64_t ns, int64_t 
   hipStream_t st = ctx->stream;
   int32_t* s2t = ctx->buf("match_s2t").as<int32_t>(ns + 1);
   int32_t* t2s = ctx->buf("match_t2s").as<int32_t>(nt + 1);
-  match_nearest_dev(ctx, src, ns, ss, tgt, nt, ts, D, s2t, nullptr, t2s, nullptr);
-  if (ns == 0 || nt == 0) return 0;
+  if (ns == 0 || nt == 0) {
+    match_nearest_dev(ctx, src, ns, ss, tgt, nt, ts, D, s2t, nullptr, t2s, nullptr);
+    return 0;
+  }
   uint8_t* flags = ctx->buf("match_flags").as<uint8_t>(ns);
   int32_t* qsel = ctx->buf("match_qsel").as<int32_t>(ns);
   int64_t* nsel = ctx->buf("match_nsel").as<int64_t>(1);
-  k_match_mutual<<<(unsigned)ceil_div(ns, 256), 256, 0, st>>>(s2t, ns, t2s, flags);
-  check_launch("k_match_mutual");
-  size_t tb = 0;
-  PFX_HIP(rocprim::select(nullptr, tb, rocprim::counting_iterator<int32_t>(0), flags, qsel, nsel, (size_t)ns, st));
-  void* tmp = ctx->buf("match_tmp").get(tb + 16);
-  PFX_HIP(rocprim::select(tmp, tb, rocprim::counting_iterator<int32_t>(0), flags, qsel, nsel, (size_t)ns, st));
   int32_t* msel = ctx->buf("match_msel").as<int32_t>(ns);
-  k_match_gather<<<(unsigned)ceil_div(ns, 256), 256, 0, st>>>(qsel, nsel, s2t, msel);
-  check_launch("k_match_gather");
   int64_t n = 0;
-  PFX_HIP(hipMemcpyAsync(&n, nsel, sizeof(int64_t), hipMemcpyDeviceToHost, st));
-  PFX_HIP(hipStreamSynchronize(st));
+  // the nearest search deferred: one stream synchronisation for the whole chain; a pair-list
+  // overflow (seen after it) reruns the chain on the two-contraction path
+  for (int mode = 1; mode <= 2; ++mode) {
+    const bool check = match_nearest_dev(ctx, src, ns, ss, tgt, nt, ts, D, s2t, nullptr, t2s, nullptr, mode);
+    k_match_mutual<<<(unsigned)ceil_div(ns, 256), 256, 0, st>>>(s2t, ns, t2s, flags);
+    check_launch("k_match_mutual");
+    size_t tb = 0;
+    PFX_HIP(rocprim::select(nullptr, tb, rocprim::counting_iterator<int32_t>(0), flags, qsel, nsel, (size_t)ns, st));
+    void* tmp = ctx->buf("match_tmp").get(tb + 16);
+    PFX_HIP(rocprim::select(tmp, tb, rocprim::counting_iterator<int32_t>(0), flags, qsel, nsel, (size_t)ns, st));
+    k_match_gather<<<(unsigned)ceil_div(ns, 256), 256, 0, st>>>(qsel, nsel, s2t, msel);
+    check_launch("k_match_gather");
+    PFX_HIP(hipMemcpyAsync(&n, nsel, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+    PFX_HIP(hipStreamSynchronize(st));
+    if (!(check && match_pairs_overflowed(ctx))) break;
+  }
   if (n > 0 && n <= cap) {
     PFX_HIP(hipMemcpyAsync(query, qsel, sizeof(int32_t) * n, hipMemcpyDeviceToDevice, st));
     PFX_HIP(hipMemcpyAsync(match, msel, sizeof(int32_t) * n, hipMemcpyDeviceToDevice, st));
