@@ -80,17 +80,11 @@ def host_info():
     return {"cpu_model": model, "nproc": os.cpu_count() or 1, "affinity_cpus": affinity}
 
 
-def cpu_baseline(x, y, z, workload, sample=None, reps=5):
-    """The CPU restatement (oracle/, test infrastructure) on the same scan, threads as PCL:
-    NARF and FPFH single-threaded (PCL 1.7 defaults, non-OMP FPFHEstimation), normals and SHOT
-    OpenMP (NormalEstimationOMP / SHOTEstimationOMP) over OMP_NUM_THREADS -- the box's CPU share
-    for one GPU (16 there; its nproc reports the whole host).  SURVEY 8(d): one warm-up run (on a
-    1/10 subsample of the scan: pages the code and the allocator in) and the median of `reps`
-    full runs of the first scan of the timed cycle."""
+def _cpu_timed_runs(x, y, z, workload, sample, reps, threads):
+    """The timed CPU-restatement runs (in the pinned child process, see cpu_baseline)."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import numpy as np
     import oracle_lib as O
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
 
     def once(cx, cy, cz, samp):
         t0 = time.perf_counter()
@@ -113,6 +107,55 @@ def cpu_baseline(x, y, z, workload, sample=None, reps=5):
     for _ in range(reps):
         t, outputs, nrows = once(x, y, z, sample)
         times.append(t)
+    return times, outputs, nrows
+
+
+def cpu_child(path):
+    """`bench.py --cpu-child <npz>`: the timed runs in a process of their own (no torch, no GPU),
+    its OpenMP threads pinned one per core (OMP_PROC_BIND=close, OMP_PLACES=cores, set by the
+    parent before this process's OpenMP runtime starts) inside the first `threads` CPUs of the
+    parent's affinity mask; results back through the same npz path (+ .out.npz)."""
+    import numpy as np
+    f = np.load(path, allow_pickle=False)
+    threads = int(f["threads"])
+    try:
+        cpus = sorted(os.sched_getaffinity(0))[:threads]
+        os.sched_setaffinity(0, cpus)
+    except (AttributeError, OSError):
+        cpus = []
+    sample = f["sample"] if f["has_sample"] else None
+    times, (kp, nrm, desc), nrows = _cpu_timed_runs(f["x"], f["y"], f["z"], str(f["workload"]), sample,
+                                                    int(f["reps"]), threads)
+    if isinstance(desc, tuple):
+        desc = desc[0]
+    np.savez(path + ".out.npz", times=np.asarray(times), kp=np.asarray(kp), nx=nrm[0], ny=nrm[1], nz=nrm[2],
+             desc=np.asarray(desc), nrows=nrows, cpus=np.asarray(cpus, np.int64))
+
+
+def cpu_baseline(x, y, z, workload, sample=None, reps=5):
+    """The CPU restatement (oracle/, test infrastructure) on the same scan, threads as PCL:
+    NARF and FPFH single-threaded (PCL 1.7 defaults, non-OMP FPFHEstimation), normals and SHOT
+    OpenMP (NormalEstimationOMP / SHOTEstimationOMP) over OMP_NUM_THREADS -- the box's CPU share
+    for one GPU (16 there; its nproc reports the whole host).  SURVEY 8(d): one warm-up run (on a
+    1/10 subsample of the scan: pages the code and the allocator in) and the median of `reps`
+    full runs of the first scan of the timed cycle.  The runs happen in a child process whose
+    OpenMP threads are pinned one per core (unpinned threads spread 8.2-12.4 s over
+    five runs); the line reports every run and the spread beside the median."""
+    import subprocess
+    import tempfile
+    import numpy as np
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
+    with tempfile.TemporaryDirectory(prefix="pfx_cpu_") as td:
+        path = os.path.join(td, "scan.npz")
+        np.savez(path, x=x, y=y, z=z, workload=workload, reps=reps, threads=threads,
+                 sample=np.zeros(0, np.int64) if sample is None else np.asarray(sample), has_sample=sample is not None)
+        env = dict(os.environ, OMP_NUM_THREADS=str(threads), OMP_PROC_BIND="close", OMP_PLACES="cores")
+        subprocess.run([sys.executable, os.path.abspath(__file__), "--cpu-child", path], env=env, check=True)
+        r = np.load(path + ".out.npz", allow_pickle=False)
+        times = [tuple(float(v) for v in t) for t in r["times"]]
+        desc = r["desc"]
+        outputs = (r["kp"], (r["nx"], r["ny"], r["nz"]), (desc,) if workload != "fpfh" else desc)
+        nrows, cpus = int(r["nrows"]), [int(c) for c in r["cpus"]]
     tot = [sum(t) for t in times]
     order = sorted(range(len(tot)), key=lambda i: tot[i])
     mid = order[len(order) // 2]  # the median run (reps odd)
@@ -120,9 +163,11 @@ def cpu_baseline(x, y, z, workload, sample=None, reps=5):
     stage_med = list(times[mid])
     feat = "FPFH 1 thread" if workload == "fpfh" else f"SHOT {threads} threads"
     return dict(seconds=med, threads=threads, outputs=outputs, runs=[round(v, 3) for v in sorted(tot)],
+                spread=round((max(tot) - min(tot)) / med, 4),
+                pinning={"OMP_PROC_BIND": "close", "OMP_PLACES": "cores", "cpus": cpus},
                 sample=(f"the first 1M-point scan of the timed cycle through the CPU restatement (oracle/), 1 warm-up "
-                        f"(1/10 subsample) + median of {reps} full runs: NARF 1 thread {stage_med[0]:.2f}s, normals "
-                        f"{threads} threads "
+                        f"(1/10 subsample) + median of {reps} full runs in a child process with pinned OpenMP threads: "
+                        f"NARF 1 thread {stage_med[0]:.2f}s, normals {threads} threads "
                         f"{stage_med[1]:.2f}s, {feat} {stage_med[2]:.2f}s at {nrows} rows; real PCL is not available "
                         f"anywhere in this pipeline"))
 
@@ -150,10 +195,9 @@ def full_size_parity(outputs, kp, b, desc, rows, shot, normals_mask=None):
         odesc = odesc[0]
     sel = slice(None) if normals_mask is None else np.asarray(normals_mask) != 0
 
-    def same(a, c):
-        a, c = np.asarray(a, np.float32), np.asarray(c, np.float32)
-        return bool(a.shape == c.shape and np.array_equal(np.nan_to_num(a, nan=7).view(np.uint32),
-                                                          np.nan_to_num(c, nan=7).view(np.uint32)))
+    def same(a, c):  # raw bits, NaN rows included (PCL's quiet_NaN on both sides)
+        a, c = np.ascontiguousarray(np.asarray(a, np.float32)), np.ascontiguousarray(np.asarray(c, np.float32))
+        return bool(a.shape == c.shape and np.array_equal(a.view(np.uint32), c.view(np.uint32)))
     res = {"normals": all(same(t.cpu().numpy()[sel], o[sel]) for t, o in zip((b.nx, b.ny, b.nz), onorm)),
            "descriptors": same(desc[:rows].cpu().numpy(), odesc)}
     if kp is not None:
@@ -180,6 +224,9 @@ def load_pmc(name):
 
 
 def main():
+    if len(sys.argv) == 3 and sys.argv[1] == "--cpu-child":  # (cpu_baseline's pinned child: no torch)
+        cpu_child(sys.argv[2])
+        return
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
@@ -201,9 +248,6 @@ def main():
     from pcl_feature_extraction_amd import launch
     if launch.needs_spawn(args.gpus):
         sys.exit(launch.spawn(args.gpus, os.path.abspath(__file__), sys.argv[1:]))
-
-    if os.environ.get("PFX_BENCH_VERBOSE"):
-        os.environ["PFX_VERBOSE_STATS"] = "1"  # libpfx diagnostics (extra host syncs): verbose runs only
 
     import torch
     import torch.distributed as dist
@@ -520,6 +564,7 @@ def bench_scans(args, torch, dist, dev, world, rank, local):
             cb = cpu_baseline(x, y, z, "fpfh" if demand else args.workload, sample_np)
             cpu = {"value": round(npts / cb["seconds"] / 1e6, 6), "unit": "Mpoints/s",
                    "cores": cb["threads"], "kind": "port", "sample": cb["sample"], "runs_s": cb["runs"],
+                   "spread": cb["spread"], "pinning": cb["pinning"],
                    **host_info(),
                    "parity": full_size_parity(cb["outputs"], kp0, scans[0], sb.desc if shot else scans[0].desc, rows0,
                                               shot,

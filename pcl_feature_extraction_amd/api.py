@@ -488,10 +488,16 @@ def batch_plan(n_scans, n_devices, rows_per_scan=None):
     """pfx_batch_plan (host only, no device): (device_of_scan, slot_of_scan, row_offset[n_scans + 1])
     of the batch's round-robin deal and scan-order gather layout."""
     lib = N.lib()
+    n_scans = int(n_scans)
+    if n_scans < 0:  # (checked here: np.zeros(n_scans + 1) would raise a numpy error first)
+        raise N.PfxError(N.PFX_ERR_INVALID, f"pfx_batch_plan: n_scans = {n_scans} < 0")
+    rows = None if rows_per_scan is None else np.ascontiguousarray(rows_per_scan, np.int64).ravel()
+    if rows is not None and len(rows) != n_scans:  # the C side reads rows_per_scan[0..n_scans)
+        raise N.PfxError(N.PFX_ERR_INVALID,
+                         f"pfx_batch_plan: rows_per_scan has {len(rows)} entries for {n_scans} scans")
     dev = np.zeros(max(n_scans, 1), np.int32)
     slot = np.zeros(max(n_scans, 1), np.int32)
     off = np.zeros(n_scans + 1, np.int64)
-    rows = None if rows_per_scan is None else np.ascontiguousarray(rows_per_scan, np.int64)
     st = lib.pfx_batch_plan(int(n_scans), int(n_devices), None if rows is None else _ptr(rows), _ptr(dev), _ptr(slot),
                             _ptr(off))
     if st != 0:

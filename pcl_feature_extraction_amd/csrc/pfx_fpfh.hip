@@ -459,17 +459,6 @@ __global__ void __launch_bounds__(256, PFX_SPFH_WPE) k_fpfh_spfh(GridView g, con
       R.start[r] = __builtin_amdgcn_readfirstlane(R.start[r]);
       R.pref[r + 1] = __builtin_amdgcn_readfirstlane(R.pref[r + 1]);
     }
-#ifdef PFX_SPFH_RUNLOOP
-    // lane r < 9 keeps run r's (start, length); the run loop below is not unrolled (one copy of the
-    // candidate scan and the pair code: less code, fewer live scalar registers)
-    int32_t vstart = 0, vlen = 0;
-#pragma unroll
-    for (int r = 0; r < 9; ++r)
-      if (lane == r) {
-        vstart = R.start[r];
-        vlen = R.pref[r + 1] - R.pref[r];
-      }
-#endif
     const bool pn_fin = isfinite(pn.x) && isfinite(pn.y) && isfinite(pn.z);
     int k = 0, qn = 0;
     int* hc = hist[wv][lane & (kHistCopies - 1)];
@@ -529,15 +518,11 @@ __global__ void __launch_bounds__(256, PFX_SPFH_WPE) k_fpfh_spfh(GridView g, con
       __builtin_amdgcn_wave_barrier();
     };
     // candidates run by run (contiguous positions: no per-candidate run lookup)
-#ifdef PFX_SPFH_RUNLOOP
-#pragma unroll 1
-    for (int r = 0; r < 9; ++r) {
-      const int32_t rs = __builtin_amdgcn_readlane(vstart, r), rn = __builtin_amdgcn_readlane(vlen, r);
-#else
+    // (measured and rejected: the run loop not unrolled, runs read by readlane -- one copy of the
+    // candidate scan and the pair code, 1.23 -> 1.42 ms)
 #pragma unroll
     for (int r = 0; r < 9; ++r) {
       const int32_t rs = R.start[r], rn = R.pref[r + 1] - R.pref[r];
-#endif
       for (int32_t t0 = 0; t0 < rn; t0 += 64) {
         const int32_t t = t0 + lane;
         bool hit = false;

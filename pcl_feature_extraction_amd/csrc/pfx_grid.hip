@@ -207,8 +207,7 @@ void build_grid(pfx_ctx* ctx, Grid& g, const float* d_x, const float* d_y, const
   g.ux = d_x; g.uy = d_y; g.uz = d_z;
   double lo[3] = {0, 0, 0}, hi[3] = {0, 0, 0};
   g.oob = nullptr;
-  static const bool no_hint = getenv("PFX_GRID_NOHINT") != nullptr;  // A/B switch
-  if (use_hint && !no_hint && g.have_hint && n > 0) {
+  if (use_hint && g.have_hint && n > 0) {
     // speculative: the previous exact bounds, widened (no bounds pass, no host round trip)
     for (int d = 0; d < 3; ++d) {
       lo[d] = g.hint_lo[d];

@@ -114,6 +114,15 @@ struct Side {
   int64_t n;
 };
 
+// Slots [base, base + k) of the pair list.  Saturating: once the count has passed ecap (the list
+// overflowed; match_pairs_overflowed sees count > cap and reruns the second contraction) later
+// reservations do not add, so the 32-bit count cannot wrap back below the cap however many pairs
+// near-duplicate sets emit (up to ns x nt); it exceeds ecap by at most the in-flight reservations.
+__device__ __forceinline__ unsigned emit_reserve(unsigned* nemit, unsigned k, unsigned ecap) {
+  const unsigned cur = __hip_atomic_load(nemit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return cur > ecap ? cur : atomicAdd(nemit, k);
+}
+
 // PASS 0: row / column upper bounds, and the pruned pair list: after a tile's atomicMin the
 // running bound of a row (column) is >= its final U, so a pair with d^ - e above the running
 // bound of both its row and its column can never be a candidate; the rest (a few dozen per row:
@@ -336,7 +345,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) k
             } else {
               const int first = __ffsll((long long)m) - 1;
               unsigned base = 0;
-              if (lane == first) base = atomicAdd(nemit, k);
+              if (lane == first) base = emit_reserve(nemit, k, ecap);
               base = __shfl(base, first);
               if (em && base + pre < ecap) emit[base + pre] = pr;
             }
@@ -354,7 +363,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) k
     }
     if (staged) {
       unsigned base = 0;
-      if (lane == 0) base = atomicAdd(nemit, staged);
+      if (lane == 0) base = emit_reserve(nemit, staged, ecap);
       base = __shfl(base, 0);
       for (unsigned i = lane; i < staged; i += 64)
         if (base + i < ecap) emit[base + i] = stage[i];
@@ -526,14 +535,13 @@ bool match_nearest_dev(pfx_ctx* ctx, const float* src, int64_t ns, int64_t ss, c
   const float c1 = (2.0f * (float)D + 6.1f) * u, c2 = 12.2f * (float)D * u + 6.2f / 65536.0f;
   const int gx = (int)(b.n_pad / kTile), gy = (int)(a.n_pad / kTile);
   const unsigned grid = (unsigned)gx * (unsigned)gy;
-  static const int group = getenv("PFX_MATCH_GROUP") ? atoi(getenv("PFX_MATCH_GROUP")) : 8;
+  constexpr int group = 8;  // row tiles per XCD group of the tile order
   const bool vec = D % 4 == 0 && ss % 4 == 0 && ts % 4 == 0 && ((uintptr_t)src & 15) == 0 && ((uintptr_t)tgt & 15) == 0;
   unsigned* h = ctx->readback<unsigned>();
-  // the pruned pair list: a few dozen pairs per row normally (PFX_MATCH_RECOMPUTE=1 forces the
-  // two-contraction fallback)
-  static const bool recompute = getenv("PFX_MATCH_RECOMPUTE") && *getenv("PFX_MATCH_RECOMPUTE") == '1';
+  // the pruned pair list: a few dozen pairs per row normally (an overflow takes the two-contraction
+  // fallback: test_match_pair_list_overflow)
   const unsigned ecap =
-      (recompute || mode == 2) ? 0u : (unsigned)std::min<int64_t>(64 * (ns + nt) + (1 << 16), int64_t(1) << 28);
+      mode == 2 ? 0u : (unsigned)std::min<int64_t>(64 * (ns + nt) + (1 << 16), int64_t(1) << 28);
   ctx->stats["match_pair_cap"] = ecap;
   int4* emit = ctx->buf("match_emit").as<int4>(std::max(ecap, 1u));
   unsigned* nemit = ncand + 2;

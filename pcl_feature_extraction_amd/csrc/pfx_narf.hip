@@ -1394,9 +1394,7 @@ int64_t narf_dev(pfx_ctx* ctx, const float* x, const float* y, const float* z, i
     // waves per CU: 20 alone (interest 0.47 ms); 4 beside the normal estimation of the
     // overlapped step (sweep 20/12/8/4/3/2/1: 161.4/161.4/162.1/162.6/162.7/162.2/159.2 Mpoints/s),
     // where the latency-bound grid build and list set-up on the other stream need wave slots
-    // (PFX_FF_WAVES overrides, for sweeps)
-    static const char* ff_env = getenv("PFX_FF_WAVES");
-    const int ff_w = ff_env ? std::max(1, atoi(ff_env)) : (ctx->shared_device ? 4 : 20);
+    const int ff_w = ctx->shared_device ? 4 : 20;
     k_interest_ff<<<256 * ff_w, 64, 0, st>>>(I, P, pk, traits, scs, scd, sat, ip, grow_list, counters + 4, interest,
                                             fb1, counters + 3, counters + 1, work);
     check_launch("k_interest_ff");

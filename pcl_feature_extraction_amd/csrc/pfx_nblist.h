@@ -55,6 +55,9 @@ struct NormalsState {
   uint64_t grid_gen = 0;  // grid_a's build that indexes (x, y, z, n, r) (pfx_normals_prepare_dev)
   // normals_launch_dev: the lists check still owed by normals_finish_dev, and the outputs to redo
   bool pending = false;
+  // the chain plan of the unmasked lists of grid_a build `plan_gen`, launched on ctx->side right
+  // after that grid (ctx->fork_ev[3] marks its end); 0: none
+  uint64_t plan_gen = 0;
   float vp[3] = {0.f, 0.f, 0.f};
   float *nx = nullptr, *ny = nullptr, *nz = nullptr, *curv = nullptr;
 };

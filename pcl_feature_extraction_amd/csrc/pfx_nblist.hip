@@ -32,7 +32,9 @@ constexpr int kCapMid = 16384, kBucketsMid = 2048;  // 144 KB of LDS: one workgr
 #ifndef PFX_HUGE_BLOCKS
 #define PFX_HUGE_BLOCKS 1024
 #endif
-constexpr int kCapHuge = 1 << 18, kBucketsHuge = 4096, kHugeBlocks = PFX_HUGE_BLOCKS;  // 4 MB of scratch each (4 GB), allocated on demand; 1024 (was 256): dense 10M per-query tiers 449 -> 409 ms
+// the huge tier: up to kHugeBlocks workgroups with 4 MB of scratch each, allocated on demand for
+// as many workgroups as lists (>= 256); 1024 (was 256): dense 10M per-query tiers 449 -> 409 ms
+constexpr int kCapHuge = 1 << 18, kBucketsHuge = 4096, kHugeBlocks = PFX_HUGE_BLOCKS;
 constexpr int kNCounters = 20;
 
 // The lists of a wide tile are written unsorted to HBM by a test pass and ordered in place by the
@@ -822,7 +824,7 @@ __global__ void __launch_bounds__(256, TCAP <= kTcapSmall ? 4 : (STAGE ? 3 : 2))
 }
 
 // ---- wide tiles (round 4) ----------------------------------------------------------------
-// Every query of a tile whose 3x3x3 block has 8000 < T <= 65535 candidates (k_tile_class): one
+// Every query of a tile whose 3x3x3 block has T > 8000 candidates (k_tile_class): one
 // workgroup per tile (dynamic queue) streams the block through LDS in chunks shared by the
 // tile's (up to 16) queries -- the per-query kernel read the block once per query, with a run
 // search per candidate -- in a count pass and a pass writing the hits unsorted to their slots in
@@ -1303,7 +1305,7 @@ void build_lists(pfx_ctx* ctx, const Grid& G, const uint8_t* mask, double radius
   unsigned long long* cursor0 = B("cursor").as<unsigned long long>(4);
   // sort-only work (kListMode) of the lists the tile kernels write unsorted, by length; the
   // kernels read the queues from a device copy written by k_list_init
-  static const bool use_mid8 = !(getenv("PFX_LIST_MID8") && *getenv("PFX_LIST_MID8") == '0');  // A/B switch
+  constexpr bool use_mid8 = true;  // the 4k-8k tier (round 3; without it those lists take the 16k tier)
   const TierQ tq{{single, use_mid8 ? mid8 : mid, mid, huge},
                  {counters + 2, counters + (use_mid8 ? 14 : 12), counters + 12, counters + 3}};
   TierQ* tq_dev = static_cast<TierQ*>(B("tierq").get(sizeof(TierQ)));
@@ -1343,16 +1345,9 @@ void build_lists(pfx_ctx* ctx, const Grid& G, const uint8_t* mask, double radius
   // 4/2/1 166.6, 34.9, 229.6; 2/2/2 166.5, 33.5, 208.4 Mpoints/s), while the 10M-pt dense
   // variant, with ~10x the heavy tiles per workgroup, wants 4 again (P/D 2/1 8.83, 2/2 9.11,
   // 2/4 9.22, 4/4 9.25 Mpoints/s): the heavy classes take n / 2M tiles per fetch, clamped to
-  // [2, 4] / [1, 4].  PFX_TILE_CHUNK sets all three, PFX_TILE_CHUNK_S / _P / _D one class
-  auto env_or = [](const char* name, int dflt) {
-    const char* e = getenv(name);
-    return e ? std::max(1, atoi(e)) : dflt;
-  };
-  static const int chunk_all = env_or("PFX_TILE_CHUNK", 0);
+  // [2, 4] / [1, 4]
   const int heavy = (int)std::min<int64_t>(4, n >> 21);
-  const int ch_small = env_or("PFX_TILE_CHUNK_S", chunk_all ? chunk_all : 4),
-            ch_sparse = env_or("PFX_TILE_CHUNK_P", chunk_all ? chunk_all : std::max(2, heavy)),
-            ch_dense = env_or("PFX_TILE_CHUNK_D", chunk_all ? chunk_all : std::max(1, heavy));
+  const int ch_small = 4, ch_sparse = std::max(2, heavy), ch_dense = std::max(1, heavy);
   for (int attempt = 0; attempt < 3; ++attempt) {
     ListOut lo{off, cnt, lgs, static_cast<uint32_t*>(lb.ptr), cursor, lb.bytes / sizeof(uint32_t)};
     if (attempt) {  // (the first attempt's cursors were zeroed by k_list_init)
@@ -1390,8 +1385,16 @@ void build_lists(pfx_ctx* ctx, const Grid& G, const uint8_t* mask, double radius
                                         (mid_tier_wanted(ctx, tag, "_hint_mid") ? 2 : 0) | (use_mid8 ? 0 : 1) |
                                         (mid_tier_wanted(ctx, tag, "_hint_wide") ? 4 : 0));
     ctx->stats[std::string(tag) + "_ran_mid_tiers"] = ran_mids;
+    // one 4 MB scratch slice per workgroup of the persistent huge tier: as many workgroups as
+    // slices (sized from the queue length the first time it was seen, 256 to kHugeBlocks: a
+    // context holds 1-4 GB only when that many lists above 16k entries exist)
+    const size_t huge_slice = sizeof(uint32_t) * 4 * (size_t)kCapHuge;
+    auto huge_blocks = [&] { return (unsigned)std::min<size_t>(kHugeBlocks, hs.bytes / huge_slice); };
+    auto huge_alloc = [&](int count) {
+      hs.get(huge_slice * (size_t)std::min(kHugeBlocks, std::max(256, count)));
+    };
     auto launch_huge = [&] {
-      k_nb_query<kCapHuge, kBucketsHuge, true><<<kHugeBlocks, 256, 0, st>>>(
+      k_nb_query<kCapHuge, kBucketsHuge, true><<<huge_blocks(), 256, 0, st>>>(
           g, qpos, G.skeys, huge, counters + 3, rr, (float)kBucketsHuge / rr, isort, lo, nullptr, nullptr, counters + 4,
           static_cast<uint32_t*>(hs.ptr), counters + 9);
       check_launch("nblist huge lists");
@@ -1435,8 +1438,8 @@ void build_lists(pfx_ctx* ctx, const Grid& G, const uint8_t* mask, double radius
         if (use_mid8 && (ran_mids & 1)) launch_mid8();
         // lists of up to 16k entries, one 144 KB workgroup per CU
         if (ran_mids & 2) launch_mid();
-        // beyond 16k entries: once the 1 GB scratch exists the launch is unconditional (count on
-        // the device); the first time, the readback below decides
+        // beyond 16k entries: once the scratch exists the launch is unconditional (count on the
+        // device); the first time, the readback below decides
         if (hs.ptr) launch_huge();
       }
       check_launch("nblist lists");
@@ -1458,7 +1461,7 @@ void build_lists(pfx_ctx* ctx, const Grid& G, const uint8_t* mask, double radius
     read_back();
     if (!(ran_mids & 4) && rb->cnt[16] > 0) {  // skipped wide tiles had work: rerun with every tier
       note_mid_tiers(ctx, tag, rb->cnt);
-      ++ctx->stats[std::string(tag) + "_tier_catchups"];
+      ++ctx->stats[std::string(tag) + "_wide_reruns"];
       continue;
     }
     if ((!(ran_mids & 1) && rb->cnt[14] > 0) || (!(ran_mids & 2) && rb->cnt[12] > 0)) {
@@ -1476,9 +1479,14 @@ void build_lists(pfx_ctx* ctx, const Grid& G, const uint8_t* mask, double radius
     }
     note_mid_tiers(ctx, tag, rb->cnt);
     if (!hs.ptr && rb->cnt[3] > 0) {  // very long lists, first time: allocate the scratch and sort them
-      hs.get(sizeof(uint32_t) * (size_t)kHugeBlocks * 4 * kCapHuge);
+      huge_alloc(rb->cnt[3]);
       launch_huge();
       read_back();
+    } else if (hs.ptr && rb->cnt[3] > (int)huge_blocks() && huge_blocks() < (unsigned)kHugeBlocks) {
+      // more such lists than workgroups: more slices for the next build (this one has finished:
+      // the readback synchronised)
+      hs.release();
+      huge_alloc(rb->cnt[3]);
     }
     int* h_cnt = rb->cnt;
     unsigned long long* h_cur = rb->cur;

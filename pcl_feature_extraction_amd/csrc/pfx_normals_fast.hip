@@ -171,7 +171,7 @@ __global__ void __launch_bounds__(256, PFX_NF_WPE) k_normals_mfma(GridView g, fl
 
 __global__ void k_nan_fill4_fast(float* __restrict__ a, float* __restrict__ b, float* __restrict__ c,
                                  float* __restrict__ d, int64_t n) {
-  const float v = __uint_as_float(0xffffffffu);  // as the product path's fill
+  const float v = __builtin_nanf("");  // PCL's quiet_NaN (0x7FC00000), as the product path's fill
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     a[i] = v; b[i] = v; c[i] = v; d[i] = v;
   }

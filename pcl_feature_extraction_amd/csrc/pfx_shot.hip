@@ -699,16 +699,8 @@ void shot_dev(pfx_ctx* ctx, const float* sx, const float* sy, const float* sz, c
     PFX_HIP(hipFuncSetAttribute((const void*)k_shot<kCap>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     // lists <= kCapSmall: the split kernels in batches of kSplitBatch queries (sort + LRF
     // covariance per workgroup, the eigen solve one lane per query, frame + histogram per
-    // workgroup); PFX_SHOT_FUSED=1: every phase in one workgroup per query (k_shot<kCapSmall>)
-    static const bool fused = [] {
-      const char* e = getenv("PFX_SHOT_FUSED");
-      return e && *e && *e != '0';
-    }();
-    const unsigned blocks = (unsigned)std::min<int64_t>(nq, 256 * 10);
-    if (fused) {
-      k_shot<kCapSmall><<<blocks, 256, lds_s, st>>>(g, snx, sny, snz, qx, qy, qz, nq, nullptr, nullptr, over, n_over,
-                                                     r, desc, rf, err, nbr);
-    } else {
+    // workgroup; round 3: 1.93 -> 1.25 ms against every phase in one workgroup per query)
+    {
       constexpr int64_t kSplitBatch = 16384;
       const int64_t bq = std::min<int64_t>(nq, kSplitBatch);
       uint64_t* gkeys = ctx->buf("shot_keys").as<uint64_t>((size_t)bq * kCapSmall);

@@ -69,11 +69,10 @@ class OverlappedNarfFpfh:
         self.torch = torch
         self.ctx, self.ctx_side = ctx_main, ctx_side
         self.s_main = main_stream if main_stream is not None else torch.cuda.current_stream(device)
-        import os
         # the normal estimation is the step's critical path: its stream gets the higher priority,
         # so its short dependent launches (grid build, list set-up) are dispatched ahead of NARF's
-        # workgroups (A/B: 166.6 -> 167.8 Mpoints/s; PFX_SIDE_PRIO overrides)
-        self.s_side = torch.cuda.Stream(device, priority=int(os.environ.get("PFX_SIDE_PRIO", "-1")))
+        # workgroups (A/B: 166.6 -> 167.8 Mpoints/s)
+        self.s_side = torch.cuda.Stream(device, priority=-1)
         ctx_main.set_stream(self.s_main.cuda_stream)
         ctx_side.set_stream(self.s_side.cuda_stream)
         ctx_main.set_shared(True)  # NARF shares the device with the critical normal estimation
@@ -83,25 +82,27 @@ class OverlappedNarfFpfh:
         # FPFH's support first: normals of the points FPFH reads (pfx_fpfh_support_ball_dev), then
         # FPFH on the main stream while the side stream estimates the rest (same results)
         # (1: subset lists + chains, 2: every list, then the chains by workgroup partition)
-        self.support_first = int(os.environ.get("PFX_SUPPORT_FIRST", "0"))
+        # (schedule attributes: every value is pinned by a -m gpu parity test against the default,
+        # tests/test_gpu_pipeline.py)
+        self.support_first = 0
         # "support": with support_first = 1, estimate only the support's normals -- the step's
         # outputs (keypoints, descriptors) are unchanged, as the normals are an intermediate of
         # Features::compute (features.h:185-187); the other normal outputs are left unwritten
         self.normals_scope = "all"
         # the normal estimation's validation off the critical path (pfx_normals_launch_dev /
         # pfx_normals_finish_dev, FPFH queued in between; A/B 173.8 vs 172.1 Mpoints/s, 3 runs each;
-        # PFX_NORMALS_SPLIT=0: pfx_normals_dev, whose check precedes the chains)
-        self.split_check = os.environ.get("PFX_NORMALS_SPLIT", "1") == "1"
+        # False: pfx_normals_dev, whose check precedes the chains)
+        self.split_check = True
         # split form: the estimation's ~50 launches issued by the calling thread before NARF's (no
         # host round trip in them), the worker only waits for the check.  Two threads launching at
         # once contend inside the HIP runtime (~60 us per launch in the API trace instead of ~7),
         # which stretched the grid build at the head of the critical path.
-        self.launch_first = os.environ.get("PFX_NORMALS_LAUNCH_FIRST", "1") == "1"
+        self.launch_first = True
         # with launch_first: FPFH's surface grid (it needs only the cloud) queued before NARF, so
         # after NARF's host selection only the keypoint gather and the S marking remain before SPFH
         # (1: after the estimation's launch; 2: before it, with the estimation's list kernels gated
         # on it -- pfx_normals_gate_dev -- so it never queues behind them; 0: after NARF)
-        self.prep_first = int(os.environ.get("PFX_PREP_FIRST", "2"))
+        self.prep_first = 2
         self._support = None
 
     def __call__(self, b: ScanBuffers, normal_radius: float = 0.05, feat_radius: float = 0.08, params=None,
@@ -312,13 +313,11 @@ class BatchNarfFpfh:
     Results are those of narf_fpfh per scan (same kernels, same contexts per role)."""
 
     def __init__(self, torch, ctx_main: Context, ctx_side: Context, device, main_stream=None, side_stream=None):
-        import os
         self.torch = torch
         self.ctx, self.ctx_side = ctx_main, ctx_side
         self.s_main = main_stream if main_stream is not None else torch.cuda.current_stream(device)
         # side_stream: share an OverlappedNarfFpfh's stream when both drive the same contexts
-        self.s_side = side_stream if side_stream is not None else torch.cuda.Stream(
-            device, priority=int(os.environ.get("PFX_SIDE_PRIO", "-1")))
+        self.s_side = side_stream if side_stream is not None else torch.cuda.Stream(device, priority=-1)
         ctx_main.set_stream(self.s_main.cuda_stream)
         ctx_side.set_stream(self.s_side.cuda_stream)
         ctx_main.set_shared(True)

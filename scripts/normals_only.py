@@ -6,7 +6,6 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-os.environ.setdefault("PFX_VERBOSE_STATS", "1")
 
 import torch  # noqa: E402
 

@@ -33,8 +33,8 @@ def test_batch_driver_compiles_and_links():
     assert os.access(exe, os.X_OK)
 
 
-def _bits(a):
-    return np.nan_to_num(np.asarray(a, np.float32), nan=7.0).view(np.uint32)
+def _bits(a):  # raw bits, NaN rows included (PCL's quiet_NaN on every side)
+    return np.ascontiguousarray(np.asarray(a, np.float32)).view(np.uint32)
 
 
 @pytest.fixture(scope="module")

@@ -51,3 +51,16 @@ def test_plan_without_rows_and_invalid_counts():
         batch_plan(-1, 2)
     with pytest.raises(PfxError):
         batch_plan(2, 2, [3, -1])
+
+
+def test_plan_rejects_short_rows_and_negative_counts():
+    """rows_per_scan must hold n_scans entries (the C side reads that many), and any
+    n_scans < 0 is PfxError, not a numpy error."""
+    with pytest.raises(PfxError):
+        batch_plan(4, 2, [1, 2, 3])
+    with pytest.raises(PfxError):
+        batch_plan(2, 2, [1, 2, 3])
+    with pytest.raises(PfxError):
+        batch_plan(-5, 2)
+    dev, slot, off = batch_plan(3, 2, [1, 2, 3])
+    assert off.tolist() == [0, 1, 3, 6]

@@ -22,8 +22,8 @@ N_SCAN = 200_000
 SEEDS = [100 + i for i in range(8)]
 
 
-def _bits(a):
-    return np.nan_to_num(np.asarray(a, np.float32), nan=7.0).view(np.uint32)
+def _bits(a):  # raw bits, NaN rows included (PCL's quiet_NaN on every side)
+    return np.ascontiguousarray(np.asarray(a, np.float32)).view(np.uint32)
 
 
 def _free_port():

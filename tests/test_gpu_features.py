@@ -31,10 +31,10 @@ def _bits_equal(a, b):
 
 
 def _nan_aware_equal(a, b):
-    a = np.asarray(a, np.float32)
-    b = np.asarray(b, np.float32)
-    na, nb = np.isnan(a), np.isnan(b)
-    return np.array_equal(na, nb) and _bits_equal(a[~na], b[~nb])
+    # raw bits, NaN rows included: the product writes PCL's quiet_NaN (0x7FC00000) as the oracle does
+    a = np.ascontiguousarray(np.asarray(a, np.float32))
+    b = np.ascontiguousarray(np.asarray(b, np.float32))
+    return a.shape == b.shape and _bits_equal(a, b)
 
 
 @pytest.mark.parametrize("r", [0.05, 0.08])
@@ -130,18 +130,29 @@ def _xyz(*parts):
     return pts[:, 0].copy(), pts[:, 1].copy(), pts[:, 2].copy()
 
 
+def _wide_blob(rng):
+    """A uniform 0.15 m cube of 13k points: every tile inside has a 3x3x3 block of > 8000
+    candidates (a wide tile, k_nb_wide) while each list stays at <= ~2.5k entries (<= 4096: the
+    always-launched per-query tier), so it keeps the wide-tile hint alive and no 4k-16k hint."""
+    return rng.uniform(0, 0.15, (13000, 3)) + [10, 10, 1]
+
+
 def test_list_tier_hints_every_path_fresh_context():
-    """The 4k-8k / 8k-16k per-query list tiers launch only while a recent build of the (context,
-    tag) had work for them (pfx_nblist.hip mid_tier_wanted).  On a fresh context, once the hints
-    have decayed (17 builds without such lists), a cloud that needs the skipped tiers must still
-    come out exact on every path: the non-deferred catch-up with the global scratch already
-    allocated (the huge tier, which already ran on an empty queue, restarts at the count it drained --
-    ADVICE r03 high: the lists the catch-up appends were never fetched), with one or both tiers
-    skipped, and the deferred check's exact rebuild.  (Lists over 4k always pass through the 4k-8k
-    queue, so that hint cannot decay while the 8k-16k one is on.)"""
+    """The 4k-8k / 8k-16k per-query list tiers and the wide-tile kernel launch only while a recent
+    build of the (context, tag) had work for them (pfx_nblist.hip mid_tier_wanted).  On a fresh
+    context, once hints have decayed (17 builds without such lists), a cloud that needs the skipped
+    kernels must still come out exact on every path:
+      * the 8k-16k tier skipped while the wide tiles and the 4k-8k tier run: the non-deferred
+        catch-up proper (`_tier_catchups`) -- the lists over 8k come from wide tiles, which push
+        them straight to their tier, and the huge tier, which already ran on an empty queue, is
+        relaunched from the count it drained (the lists the catch-up appends were
+        never fetched);
+      * the wide tiles skipped too: the whole build reruns with every kernel (`_wide_reruns`);
+      * the deferred check's exact rebuild."""
     import torch
     from pcl_feature_extraction_amd import Context
     sparse, dense, mid8, mid, huge = _every_list_cloud()
+    wide = _wide_blob(np.random.default_rng(29))
     ex, ey, ez = _xyz(sparse, dense, mid8, mid, huge)
     ref = O.normals(ex, ey, ez, 0.05)
     dev = torch.device("cuda", 0)
@@ -166,26 +177,30 @@ def test_list_tier_hints_every_path_fresh_context():
             for a, b in zip(o, ref):
                 assert _nan_aware_equal(a.cpu().numpy(), b)
 
-        def catchups():
+        def stat(name):
             try:
-                return c.stat("normals_tier_catchups")
+                return c.stat("normals_" + name)
             except Exception:
                 return 0
 
         every_two_phase()                          # first build: every tier, scratch allocated
         assert c.stat("normals_huge") > 0 and c.stat("normals_mid") > 0 and c.stat("normals_mid8") > 0
-        sx, sy, sz = _xyz(sparse, mid8)
+        assert c.stat("normals_wide") > 0
+        wx, wy, wz = _xyz(sparse, mid8, wide)
+        lists_only(wx, wy, wz)
+        assert stat("wide") > 0 and stat("mid") == 0  # the warm-up cloud: wide tiles, no 8k-16k list
         for _ in range(17):
-            lists_only(sx, sy, sz)                 # the 8k-16k hint decays, the 4k-8k one stays
-        before = catchups()
-        every_two_phase()                          # 8k-16k skipped: catch-up of it, then huge again
-        assert catchups() == before + 1
+            lists_only(wx, wy, wz)                 # the 8k-16k hint decays, the 4k-8k and wide ones stay
+        assert stat("ran_mid_tiers") & 4 and not stat("ran_mid_tiers") & 2
+        cat, wre = stat("tier_catchups"), stat("wide_reruns")
+        every_two_phase()                          # 8k-16k skipped: the catch-up of it, then huge again
+        assert stat("tier_catchups") == cat + 1 and stat("wide_reruns") == wre
         px, py, pz = _xyz(sparse)
         for _ in range(17):
-            lists_only(px, py, pz)                 # both hints decay
-        before = catchups()
-        every_two_phase()                          # both skipped: catch-up of every per-query tier
-        assert catchups() == before + 1
+            lists_only(px, py, pz)                 # every hint decays
+        cat, wre = stat("tier_catchups"), stat("wide_reruns")
+        every_two_phase()                          # wide tiles skipped: the build reruns with everything
+        assert stat("wide_reruns") == wre + 1
         for _ in range(17):
             lists_only(px, py, pz)
         g = c.normals(ex, ey, ez, 0.05)            # deferred build (normals_dev): check + exact rebuild

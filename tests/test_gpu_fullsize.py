@@ -10,6 +10,7 @@ import numpy as np
 import pytest
 
 import oracle_lib as O
+from parity import bits_equal
 
 pytestmark = pytest.mark.gpu
 
@@ -18,9 +19,7 @@ THREADS = 16
 
 
 def _same(a, b):
-    a, b = np.asarray(a, np.float32), np.asarray(b, np.float32)
-    return a.shape == b.shape and np.array_equal(np.nan_to_num(a, nan=7).view(np.uint32),
-                                                 np.nan_to_num(b, nan=7).view(np.uint32))
+    return bits_equal(a, b)  # raw bits, NaN rows included
 
 
 def _scan(torch, dev, x, y, z, max_keypoints=1 << 16):

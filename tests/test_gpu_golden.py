@@ -4,14 +4,14 @@ import os
 import numpy as np
 import pytest
 
+from parity import bits_equal
+
 pytestmark = pytest.mark.gpu
 F = os.path.join(os.path.dirname(__file__), "golden", "oracle_small.npz")
 
 
 def _eq(a, b):
-    a, b = np.asarray(a, np.float32), np.asarray(b, np.float32)
-    na, nb = np.isnan(a), np.isnan(b)
-    return np.array_equal(na, nb) and np.array_equal(a[~na].view(np.uint32), b[~nb].view(np.uint32))
+    return bits_equal(a, b)  # raw bits, NaN rows included
 
 
 def test_gpu_matches_golden_fixtures(ctx):

@@ -4,6 +4,7 @@ import numpy as np
 import pytest
 
 import oracle_lib as O
+from parity import bits_equal
 
 pytestmark = pytest.mark.gpu
 
@@ -34,17 +35,17 @@ def test_overlapped_pass_matches_sequential_and_oracle():
         ctx.close(); ctx_n.close()
     (kp0, k0, n0, d0), (kp1, k1, n1, d1) = outs
     assert np.array_equal(kp0, kp1) and k0 == k1 and k0 > 0
-    assert np.array_equal(np.nan_to_num(n0, nan=7).view(np.uint32), np.nan_to_num(n1, nan=7).view(np.uint32))
-    assert np.array_equal(np.nan_to_num(d0, nan=7).view(np.uint32), np.nan_to_num(d1, nan=7).view(np.uint32))
+    assert bits_equal(n0, n1)
+    assert bits_equal(d0, d1)
     # against the CPU restatement
     okp = O.narf_keypoints(x, y, z)
     assert np.array_equal(kp1, okp)
     onx, ony, onz, oc = O.normals(x, y, z, 0.05)
     on = np.stack([onx, ony, onz, oc])
-    assert np.array_equal(np.nan_to_num(n1, nan=7).view(np.uint32), np.nan_to_num(on, nan=7).view(np.uint32))
+    assert bits_equal(n1, on)
     rows = okp[okp < n]
     od = O.fpfh(x, y, z, onx, ony, onz, x[rows], y[rows], z[rows], 0.08)
-    assert np.array_equal(np.nan_to_num(d1, nan=7).view(np.uint32), np.nan_to_num(od, nan=7).view(np.uint32))
+    assert bits_equal(d1, od)
 
 
 def test_two_phase_normals_and_support_mask():
@@ -73,7 +74,7 @@ def test_two_phase_normals_and_support_mask():
         a.synchronize(); b.synchronize()
     for r, o in zip(ref, out):
         r, o = r.cpu().numpy(), o.cpu().numpy()
-        assert np.array_equal(np.nan_to_num(r, nan=7).view(np.uint32), np.nan_to_num(o, nan=7).view(np.uint32))
+        assert bits_equal(r, o)
     cnt, idx, _ = O.radius_search(x, y, z, x[qi], y[qi], z[qi], 0.08, cap=4096)
     assert cnt.max() <= 4096
     S = np.unique(idx[idx >= 0])
@@ -141,7 +142,7 @@ def test_subset_normals_equal_full_estimation():
         a.synchronize(); b.synchronize()
     for r, o in zip(ref, out):
         r, o = r.cpu().numpy(), o.cpu().numpy()
-        assert np.array_equal(np.nan_to_num(r, nan=7).view(np.uint32), np.nan_to_num(o, nan=7).view(np.uint32))
+        assert bits_equal(r, o)
 
 
 @pytest.mark.parametrize("mode", [1, 2])
@@ -174,8 +175,8 @@ def test_support_first_pass_matches_default(mode):
         ctx.close(); ctx_n.close()
     (kp0, k0, n0, d0), (kp1, k1, n1, d1) = outs
     assert np.array_equal(kp0, kp1) and k0 == k1 and k0 > 0
-    assert np.array_equal(np.nan_to_num(n0, nan=7).view(np.uint32), np.nan_to_num(n1, nan=7).view(np.uint32))
-    assert np.array_equal(np.nan_to_num(d0, nan=7).view(np.uint32), np.nan_to_num(d1, nan=7).view(np.uint32))
+    assert bits_equal(n0, n1)
+    assert bits_equal(d0, d1)
 
 
 def test_split_check_pass_matches_default_with_reruns():
@@ -215,8 +216,8 @@ def test_split_check_pass_matches_default_with_reruns():
         res[split] = outs
     for (kp0, k0, n0, d0), (kp1, k1, n1, d1) in zip(res[False], res[True]):
         assert np.array_equal(kp0, kp1) and k0 == k1
-        assert np.array_equal(np.nan_to_num(n0, nan=7).view(np.uint32), np.nan_to_num(n1, nan=7).view(np.uint32))
-        assert np.array_equal(np.nan_to_num(d0, nan=7).view(np.uint32), np.nan_to_num(d1, nan=7).view(np.uint32))
+        assert bits_equal(n0, n1)
+        assert bits_equal(d0, d1)
 
 
 def test_overlapped_shot_matches_sequential():
@@ -248,5 +249,41 @@ def test_overlapped_shot_matches_sequential():
         ctx.close(); ctx_n.close()
     (r0, d0, f0), (r1, d1, f1) = outs
     assert r0 == r1 and r0 >= 500
-    assert np.array_equal(np.nan_to_num(d0, nan=7).view(np.uint32), np.nan_to_num(d1, nan=7).view(np.uint32))
-    assert np.array_equal(np.nan_to_num(f0, nan=7).view(np.uint32), np.nan_to_num(f1, nan=7).view(np.uint32))
+    assert bits_equal(d0, d1)
+    assert bits_equal(f0, f1)
+
+
+@pytest.mark.parametrize("launch_first,prep_first", [(False, 2), (True, 0), (True, 1)])
+def test_launch_order_variants_match_default(launch_first, prep_first):
+    """OverlappedNarfFpfh's launch-order attributes (every selectable schedule
+    pinned): the estimation issued by the worker thread instead of the caller (launch_first =
+    False) and FPFH's surface grid queued after NARF (prep_first 0) or after the estimation's
+    launch (1) give the default schedule's keypoints, normals and descriptors bit for bit."""
+    import torch
+    from pcl_feature_extraction_amd import Context
+    from pcl_feature_extraction_amd.pipeline import OverlappedNarfFpfh, alloc
+    from pcl_feature_extraction_amd.synth import synth_room
+    n = 150_000
+    x, y, z, _ = synth_room(n, 25)
+    dev = torch.device("cuda", 0)
+    outs = []
+    for variant in (None, (launch_first, prep_first)):
+        b = alloc(torch, n, dev, max_keypoints=4096)
+        b.x.copy_(torch.from_numpy(x)); b.y.copy_(torch.from_numpy(y)); b.z.copy_(torch.from_numpy(z))
+        ctx, ctx_n = Context(0), Context(0)
+        ctx.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+        run = OverlappedNarfFpfh(torch, ctx, ctx_n, dev)
+        if variant is not None:
+            run.launch_first, run.prep_first = variant
+        for _ in range(2):  # (the second pass reuses every buffer and the speculative grids)
+            kp, k = run(b)
+        run.check()
+        run.close()
+        torch.cuda.synchronize(dev)
+        outs.append((np.asarray(kp), k, np.stack([t.cpu().numpy() for t in (b.nx, b.ny, b.nz, b.curv)]),
+                     b.desc[:k].cpu().numpy()))
+        ctx.close(); ctx_n.close()
+    (kp0, k0, n0, d0), (kp1, k1, n1, d1) = outs
+    assert np.array_equal(kp0, kp1) and k0 == k1 and k0 > 0
+    assert bits_equal(n0, n1)
+    assert bits_equal(d0, d1)
