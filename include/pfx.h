@@ -69,7 +69,16 @@ typedef struct pfx_narf_params {
   float optimal_distance_to_high_surface_change; /* 0.25                    */
   float min_interest_value;                      /* 0.45                    */
   float min_surface_change_score;                /* 0.2                     */
-  int32_t do_non_maximum_suppression;            /* 1                       */
+  /* 1.  The greedy selection then orders the survivors with std::sort on strength, as PCL does:
+   * the order of EQUAL strengths is the sort implementation's (the libstdc++ this library is
+   * built with; PCL's was an Indigo-era GCC).  It decides the keypoints only when two tied
+   * survivors lie closer than min_distance_between_interest_points * support_size:
+   * scripts/narf_tie_report.py finds none on the reference's four clouds (their keypoints are
+   * independent of the toolchain: tests/test_oracle_narf_ties.py) and 6-11 such pairs on each
+   * configs[2] synthetic room, where 4-7 of ~85 keypoints move between the two extreme tie
+   * orders (profiles/r05_narf_tie_report.jsonl).  The GPU path and the oracle share this
+   * build's order. */
+  int32_t do_non_maximum_suppression;
   /* 1 (PCL's default).  Either value computes NarfKeypoint's COMPLETE interest formula
    * (calculateCompleteInterestImage); 1 only skips pixels that provably cannot reach
    * min_interest_value, so 0 and 1 give the same keypoints.  PCL 1.7's own sparse heuristics

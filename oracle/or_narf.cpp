@@ -44,6 +44,27 @@ enum {
 };
 inline uint32_t bit(int t) { return 1u << t; }
 
+// Alternative readings of the medium / low confidence statements of SURVEY A.5 / A.6, for the
+// sensitivity table of scripts/narf_alt_report.py (VERDICT r04 #2c: which statements the keypoint
+// set hinges on).  0 (always, outside that report) = the restatement as documented; each bit
+// swaps ONE statement for its most plausible other reading (orc_narf_set_alt).
+enum : int {
+  kAltPlaneFullWindow = 1 << 0,  // A.5.1 local plane: every pixel of the 5x5 window, 9 closest (not step 2, 4 closest)
+  kAltUpdateWithCentre = 1 << 1, // A.5.3 updatedScoreAccordingToNeighborValues: 3x3 mean incl. the centre
+  kAltUpdateNoEarlyOut = 1 << 2, // A.5.3 ... without the early return below minimum_border_probability
+  kAltShadowUnupdated = 1 << 3,  // A.5.4 shadow pass: every direction reads the un-updated scores
+  kAltCurvatureNoSqrt = 1 << 4,  // A.5.7 principal curvature magnitude = lambda_max (not its sqrt)
+  kAltBeamsNotCut = 1 << 5,      // A.5.7 curvature beams skip veil/shadow pixels instead of ending
+  kAltGrowOr = 1 << 6,           // A.6 region grow: accept only within 2 px AND within R (not OR)
+  kAltPosLessEq2 = 1 << 7,       // A.6 positive score: scs when pixel distance <= 2 (not < 2)
+  kAltNegNotSquared = 1 << 8,    // A.6 negative score not squared
+  kAltAngleAtan2 = 1 << 9,       // A.6 direction angle: 0.5 normAngle(2 atan2(v_y, v_x)) (not acos(v_x))
+  kAltCellRound = 1 << 10,       // A.6 histogram cell: lrint without floorf
+  kAltAcvNoSqrt = 1 << 11,       // A.6 interest = negative x max(h_i h_j nd) (no sqrt)
+};
+int g_alt = 0;
+inline bool alt(int b) { return (g_alt & b) != 0; }
+
 const float kInf = std::numeric_limits<float>::infinity();
 
 struct P4 { float x, y, z, range; };
@@ -318,6 +339,10 @@ struct Border {
     surf.assign((size_t)w * h, Surface());
     int step = (P.pixel_radius_plane_extraction / 2) + 1;
     int nn = (int)std::pow((double)(P.pixel_radius_plane_extraction / step + 1), 2.0);
+    if (alt(kAltPlaneFullWindow)) {
+      step = 1;
+      nn = (P.pixel_radius_plane_extraction + 1) * (P.pixel_radius_plane_extraction + 1);
+    }
 #pragma omp parallel for schedule(dynamic, 8)
     for (int y = 0; y < h; ++y)
       for (int x = 0; x < w; ++x) {
@@ -345,11 +370,11 @@ struct Border {
   float updatedScore(int x, int y, const std::vector<float>& s) const {
     const float bonus = 0.5f;
     float b = s[(size_t)y * w + x];
-    if (b + bonus * (1.0f - b) < P.minimum_border_probability) return b;
+    if (!alt(kAltUpdateNoEarlyOut) && b + bonus * (1.0f - b) < P.minimum_border_probability) return b;
     float avg = 0.0f, ws = 0.0f;
     for (int y2 = y - 1; y2 <= y + 1; ++y2)
       for (int x2 = x - 1; x2 <= x + 1; ++x2) {
-        if (!ri.inImage(x2, y2) || (x2 == x && y2 == y)) continue;
+        if (!ri.inImage(x2, y2) || (x2 == x && y2 == y && !alt(kAltUpdateWithCentre))) continue;
         avg += s[(size_t)y2 * w + x2];
         ws += 1.0f;
       }
@@ -392,14 +417,17 @@ struct Border {
     size_t n = (size_t)w * h;
     shL.assign(n, -1); shR.assign(n, -1); shT.assign(n, -1); shB.assign(n, -1);
     has_shadow.assign(n, 0);
+    // (alternative reading: the opposite-direction scores read before any update)
+    const std::vector<float> oL = sL, oR = sR, oT = sT, oB = sB;
+    const bool un = alt(kAltShadowUnupdated);
     for (int y = 0; y < h; ++y)
       for (int x = 0; x < w; ++x) {
         size_t i = (size_t)y * w + x;
         int s;
-        if (changeScoreShadow(x, y, -1, 0, sL, sR, s)) { has_shadow[i] = 1; shL[i] = s; }
-        if (changeScoreShadow(x, y, 1, 0, sR, sL, s)) { has_shadow[i] = 1; shR[i] = s; }
-        if (changeScoreShadow(x, y, 0, -1, sT, sB, s)) { has_shadow[i] = 1; shT[i] = s; }
-        if (changeScoreShadow(x, y, 0, 1, sB, sT, s)) { has_shadow[i] = 1; shB[i] = s; }
+        if (changeScoreShadow(x, y, -1, 0, sL, un ? oR : sR, s)) { has_shadow[i] = 1; shL[i] = s; }
+        if (changeScoreShadow(x, y, 1, 0, sR, un ? oL : sL, s)) { has_shadow[i] = 1; shR[i] = s; }
+        if (changeScoreShadow(x, y, 0, -1, sT, un ? oB : sB, s)) { has_shadow[i] = 1; shT[i] = s; }
+        if (changeScoreShadow(x, y, 0, 1, sB, un ? oT : sT, s)) { has_shadow[i] = 1; shB[i] = s; }
       }
   }
 
@@ -541,7 +569,10 @@ struct Border {
           }
           if (!ri.isValid(x2, y2)) continue;
           size_t i2 = (size_t)y2 * w + x2;
-          if (traits[i2] & (bit(VEIL_POINT) | bit(SHADOW_BORDER))) { bv = false; continue; }
+          if (traits[i2] & (bit(VEIL_POINT) | bit(SHADOW_BORDER))) {
+            if (!alt(kAltBeamsNotCut)) bv = false;
+            continue;
+          }
           if (!surf[i2].valid) continue;
           va.add(surf[i2].normal_no_jumps);
         }
@@ -551,7 +582,7 @@ struct Border {
     V3 evec[3];
     va.pca(ev, evec);
     main_dir = evec[2];
-    mag = std::sqrt(ev[2]);
+    mag = alt(kAltCurvatureNoSqrt) ? ev[2] : std::sqrt(ev[2]);
     if (!std::isfinite(mag)) return false;
     return true;
   }
@@ -643,7 +674,9 @@ void interestImage(const RangeImage& ri, const Border& B, const Params& P, std::
           const P4 point2 = ri.pts[(size_t)index2];
           const float pixelDistance = (float)std::max(std::abs(x2 - x), std::abs(y2 - y));
           const float distance_squared = sqDist(point, point2);
-          if (pixelDistance > 2.0f && distance_squared > radius_squared) continue;
+          if (alt(kAltGrowOr) ? (pixelDistance > 2.0f || distance_squared > radius_squared)
+                              : (pixelDistance > 2.0f && distance_squared > radius_squared))
+            continue;
           for (int y3 = std::max(0, y2 - 1); y3 <= std::min(h - 1, y2 + 1); ++y3)
             for (int x3 = std::max(0, x2 - 1); x3 <= std::min(w - 1, x2 + 1); ++x3) {
               int index3 = y3 * w + x3;
@@ -656,14 +689,17 @@ void interestImage(const RangeImage& ri, const Border& B, const Params& P, std::
           const float distance_factor = radius_reciprocal * distance;
           // nkdGetScores
           float neg = 1.0f - 0.5f * scs * std::max(1.0f - distance_factor / P.optimal_distance_to_high_surface_change, 0.0f);
-          neg = neg * neg;
-          const float pos = (pixelDistance < 2.0) ? scs : scs * (1.0f - distance_factor);
+          if (!alt(kAltNegNotSquared)) neg = neg * neg;
+          const bool near = alt(kAltPosLessEq2) ? pixelDistance <= 2.0 : pixelDistance < 2.0;
+          const float pos = near ? scs : scs * (1.0f - distance_factor);
           // nkdGetDirectionAngle: (rotation * direction).head<2> (), Affine3f * Vector3f (mv3 rows)
           V3 rot = v3(0.0f + mv3(tmp0, dir), 0.0f + mv3(tmp1, dir), 0.0f + mv3(tmp2, dir));
           float inv = std::sqrt(rot.x * rot.x + rot.y * rot.y);
           float dvx = rot.x * (1.0f / inv);  // Vector2f::normalize (): times the reciprocal
           float angle = 0.5f * normAngle(2.0f * acosf_glibc(dvx));
-          float cellf = std::floor((angle + d90) / d180 * hist_size);
+          if (alt(kAltAngleAtan2)) angle = 0.5f * normAngle(2.0f * std::atan2(rot.y * (1.0f / inv), dvx));
+          float cellf = alt(kAltCellRound) ? (angle + d90) / d180 * hist_size
+                                           : std::floor((angle + d90) / d180 * hist_size);
           int cell;
           if (!(cellf == cellf)) cell = 0;  // NaN -> lrint -> INT_MIN -> (int) 0
           else cell = std::min(hist_size - 1, (int)std::lrint(cellf));
@@ -682,7 +718,7 @@ void interestImage(const RangeImage& ri, const Border& B, const Params& P, std::
             acv = std::max(hist[c1] * hist[c2] * nd, acv);
           }
         }
-        acv = std::sqrt(acv);
+        if (!alt(kAltAcvNoSqrt)) acv = std::sqrt(acv);
         interest[(size_t)index] = negative_score * acv;
       }
   }
@@ -953,6 +989,9 @@ Camera makeCamera(int w, int h, float cx, float cy, float fx, float fy, const fl
 }  // namespace
 
 extern "C" {
+
+// the alternative-reading selector (test infrastructure: scripts/narf_alt_report.py only)
+void orc_narf_set_alt(int mask) { g_alt = mask; }
 
 // out: w*h*4 floats (x, y, z, range)
 int orc_range_image_planar(const float* x, const float* y, const float* z, i64 n, int w, int h, float cx, float cy,
