@@ -842,7 +842,7 @@ __global__ void __launch_bounds__(256) k_fpfh_weight_lists(GridView g, const int
     int pl = 1 << 20;
     for (int c0 = 0; c0 < k; c0 += 64) {
       const int m = min(64, k - c0);
-      const int32_t pos = lane < m ? entry_pos(list[off + ((int64_t)(c0 + lane) << lg)], rs) : qp;
+      const int32_t pos = lane < m ? entry_pos(list_entry(list, off, lg, c0 + lane), rs) : qp;
       const int32_t idx = g.perm[pos];
       const float4 p = g.sp[pos];
       const float d2 = flann_d2(q.x, q.y, q.z, p.x, p.y, p.z);
@@ -886,7 +886,7 @@ __global__ void __launch_bounds__(256) k_fpfh_weight_lists(GridView g, const int
         atomicAdd(err + 2, 1);
         sum = 0.0;
         for (int c = 0; c < k; ++c) {
-          const int32_t pos = entry_pos(list[off + ((int64_t)c << lg)], rs);
+          const int32_t pos = entry_pos(list_entry(list, off, lg, c), rs);
           const float4 p = g.sp[pos];
           const float d2 = flann_d2(q.x, q.y, q.z, p.x, p.y, p.z);
           if (d2 == 0.0f) continue;

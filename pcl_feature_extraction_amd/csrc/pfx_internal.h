@@ -156,10 +156,9 @@ struct pfx_ctx {
     if (!fpfh_rb_mem) PFX_HIP(hipHostMalloc(&fpfh_rb_mem, sizeof(pfx::FpfhReadback), hipHostMallocDefault));
     return static_cast<pfx::FpfhReadback*>(fpfh_rb_mem);
   }
-  // one side stream + fork/join events (normal estimation's long-list chains [0, 1], its chain
-  // plan made beside the list kernels [2, 3]), created on first use
+  // one side stream + fork/join events (normal estimation's long-list chains), created on first use
   hipStream_t side = nullptr;
-  hipEvent_t fork_ev[4] = {nullptr, nullptr, nullptr, nullptr};
+  hipEvent_t fork_ev[2] = {nullptr, nullptr};
   // host wait for a stream on the critical path of a call (a readback that sizes the next
   // launches): an event polled with hipEventQuery instead of hipStreamSynchronize's blocking
   // wait, whose wake-up left ~150 us idle on the stream per readback

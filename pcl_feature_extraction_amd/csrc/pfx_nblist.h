@@ -21,6 +21,24 @@ namespace pfx {
 constexpr uint32_t kEntryOffMask = 0x0fffffffu;
 __host__ __device__ __forceinline__ int entry_run(uint32_t e) { return (int)(e >> 28); }
 __host__ __device__ __forceinline__ uint32_t entry_off(uint32_t e) { return e & kEntryOffMask; }
+// Compact lists (round 5; builds with `compact`, the tile kernels' lists of blocks whose runs all
+// hold <= 4096 points): 16-bit run entries (r << 12) | off, flagged by bit 7 of lg[j]; off[j]
+// and the stride 2^(lg & 0x7f) then count 16-bit entries (entry m of query j at
+// ((const uint16_t*)list)[off[j] + (m << lg)]).  Read by the normal estimation's chains and by
+// FPFH's all-points weighting when it reuses those lists (list_entry); the other consumers build
+// without `compact`.  Per-query tiers write them too when k <= kLaneMaxCompact, so a wave of the
+// lane-per-query chains rarely mixes widths.
+constexpr uint8_t kLgCompact = 0x80;
+
+__host__ __device__ __forceinline__ uint32_t widen_entry16(uint32_t e16) {
+  return ((e16 >> 12) << 28) | (e16 & 0xfffu);
+}
+constexpr int kLaneMaxCompact = 2048;  // compact lists are at most this long (the lane-per-query chains' cap)
+// entry m of a list with offset `off` and lg byte `lgr`, either width, as a 32-bit run entry
+__device__ __forceinline__ uint32_t list_entry(const uint32_t* list, int64_t off, int lgr, int m) {
+  const int64_t i = off + ((int64_t)m << (lgr & 0x7f));
+  return (lgr & kLgCompact) ? widen_entry16(reinterpret_cast<const uint16_t*>(list)[i]) : list[i];
+}
 
 struct NbLists {
   int64_t nq = 0;            // number of queries
@@ -33,6 +51,8 @@ struct NbLists {
   const int32_t* cnt = nullptr;    // [nq]
   const uint8_t* lg = nullptr;     // [nq] log2 of the entry stride
   const uint32_t* list = nullptr;  // [slots] run entries
+  bool compact = false;            // lists may be 16-bit (kLgCompact)
+  int64_t list_cap = 0;            // entries the list buffer holds (every offset is below it)
   const uint32_t* skeys = nullptr; // cell key of each sorted position (the grid's)
   // deferred builds (build_lists with defer): nq is an upper bound and the query count lives on
   // the device until build_lists_check has run; kernels read it through nq_of()
@@ -55,9 +75,6 @@ struct NormalsState {
   uint64_t grid_gen = 0;  // grid_a's build that indexes (x, y, z, n, r) (pfx_normals_prepare_dev)
   // normals_launch_dev: the lists check still owed by normals_finish_dev, and the outputs to redo
   bool pending = false;
-  // the chain plan of the unmasked lists of grid_a build `plan_gen`, launched on ctx->side right
-  // after that grid (ctx->fork_ev[3] marks its end); 0: none
-  uint64_t plan_gen = 0;
   float vp[3] = {0.f, 0.f, 0.f};
   float *nx = nullptr, *ny = nullptr, *nz = nullptr, *curv = nullptr;
 };
@@ -68,7 +85,7 @@ struct NormalsState {
 // out.nq_dev = the device count); consumers may be launched behind them in stream order, and
 // build_lists_check must follow.
 void build_lists(pfx_ctx* ctx, const Grid& g, const uint8_t* mask, double radius, bool sorted, NbLists& out,
-                 const char* tag, bool defer = false, int want = 1);
+                 const char* tag, bool defer = false, int want = 1, bool compact = false);
 // The deferred build's readback: true and `out` completed (exact nq, statistics) when the lists are
 // valid; false when they must be rebuilt synchronously (list buffer too small, first very long
 // lists, or a speculative grid with points outside its bounds) -- their consumers rerun too.

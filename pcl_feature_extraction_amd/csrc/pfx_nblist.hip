@@ -182,6 +182,7 @@ struct ListOut {
   uint32_t* list;
   unsigned long long* cursor;  // [0] slots allocated, [1] neighbours, [2] neighbours in long lists, [3] long lists
   unsigned long long cap;
+  int compact;  // the tile kernels may write 16-bit entries (pfx_nblist.h kLgCompact)
 };
 
 // Candidate coordinates of a tile: staged in LDS, or read from the packed grid copy (L2).
@@ -730,6 +731,11 @@ __global__ void __launch_bounds__(256, TCAP <= kTcapSmall ? 4 : (STAGE ? 3 : 2))
     // [C] list slots, sort
     int lg = 0;
     while ((1 << lg) < qn) ++lg;
+    // 16-bit entries when every run of the block fits their 12-bit offset (the list bytes the
+    // chains stream from HBM halve)
+    bool c16 = out.compact != 0;
+#pragma unroll
+    for (int r = 0; r < 9; ++r) c16 = c16 && R.pref[r + 1] - R.pref[r] <= kCompactRun;
     int maxk = 0;
     for (int j = 0; j < qn; ++j) {
       const int k = s_k[j];
@@ -741,7 +747,7 @@ __global__ void __launch_bounds__(256, TCAP <= kTcapSmall ? 4 : (STAGE ? 3 : 2))
       const int k = s_k[tid];
       if (k <= LCAP) {
         out.cnt[start + tid] = k;
-        out.lg[start + tid] = (uint8_t)lg;
+        out.lg[start + tid] = (uint8_t)(lg | (c16 ? kLgCompact : 0));
       } else {
         // the per-query kernel (test + sort): measured against a second tile pass writing these
         // lists unsorted for a sort-only per-query pass, that pass cost more (room: dense tiles
@@ -787,7 +793,8 @@ __global__ void __launch_bounds__(256, TCAP <= kTcapSmall ? 4 : (STAGE ? 3 : 2))
       }
       // list slots come from a per-workgroup arena reserved kArena entries at a time (one
       // cursor atomic per arena, not per tile); unused arena tails are never read
-      const unsigned long long need = (unsigned long long)maxk << lg;
+      // (compact: two entries per 32-bit slot)
+      const unsigned long long need = c16 ? (((unsigned long long)maxk << lg) + 1) >> 1 : (unsigned long long)maxk << lg;
       if (need > arena_left) {
         const unsigned long long res = need > (unsigned long long)kArena ? need : (unsigned long long)kArena;
         arena_base = atomicAdd(out.cursor, res);
@@ -800,10 +807,27 @@ __global__ void __launch_bounds__(256, TCAP <= kTcapSmall ? 4 : (STAGE ? 3 : 2))
     if (ni < ntiles) sg.store(cxy, cz, s_qp, qn_n);
     __syncthreads();
     const int64_t base = (int64_t)s_base;
-    if (tid < qn && s_k[tid] <= LCAP) out.off[start + tid] = base + tid;
+    // (compact: offsets count 16-bit entries)
+    if (tid < qn && s_k[tid] <= LCAP) out.off[start + tid] = (c16 ? 2 * base : base) + tid;
     // coalesced write of the interleaved block (padding slots are left unwritten)
     const int total = maxk << lg;
-    if ((unsigned long long)(base + total) <= out.cap) {
+    if (c16) {
+      // two entries per 32-bit store (entries 2w, 2w + 1 of the block; padding halves are 0)
+      const int words = (total + 1) >> 1;
+      if ((unsigned long long)(base + words) <= out.cap) {
+        for (int w = tid; w < words; w += 256) {
+          uint32_t pair = 0;
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int e = 2 * w + h;
+            const int m = e >> lg, j = e & ((1 << lg) - 1);
+            const int k = j < qn ? s_k[j] : 0;
+            if (e < total && m < k && k <= LCAP) pair |= (uint32_t)run_entry16(R, lists[j][m]) << (16 * h);
+          }
+          out.list[base + w] = pair;
+        }
+      }
+    } else if ((unsigned long long)(base + total) <= out.cap) {
       for (int e = tid; e < total; e += 256) {
         const int m = e >> lg, j = e & ((1 << lg) - 1);
         if (j < qn) {
@@ -947,6 +971,11 @@ __device__ __forceinline__ uint32_t pos_entry(const Runs& R, int32_t p) {
   return e;
 }
 
+__device__ __forceinline__ uint32_t pos_entry16(const Runs& R, int32_t p) {
+  const uint32_t e = pos_entry(R, p);
+  return ((e >> 28) << 12) | (e & 0xfffu);
+}
+
 template <int CAP, int NB, bool GLOBAL>
 __global__ void __launch_bounds__(256) k_nb_query(GridView g, const int32_t* __restrict__ qpos,
                                                   const uint32_t* __restrict__ skeys,
@@ -1074,8 +1103,17 @@ __global__ void __launch_bounds__(256) k_nb_query(GridView g, const int32_t* __r
       __syncthreads();
       continue;
     }
+    // compact (16-bit) output: a compact build, runs of <= 4096 points, and a list the lane-per-query
+    // chains read (<= kLaneMaxCompact: k_normals_long reads 32-bit lists only)
+    bool c16 = out.compact != 0 && k <= kLaneMaxCompact;
+#pragma unroll
+    for (int r = 0; r < 9; ++r) c16 = c16 && R.pref[r + 1] - R.pref[r] <= kCompactRun;
+    if (tid == 0 && from_list && c16) {  // sorted in place: the same slots, as 16-bit entries
+      out.off[j] = 2 * (int64_t)s_base;
+      out.lg[j] = kLgCompact;
+    }
     if (tid == 0 && !from_list) {
-      const unsigned long long need = (unsigned long long)k;
+      const unsigned long long need = c16 ? ((unsigned long long)k + 1) >> 1 : (unsigned long long)k;
       if (need > arena_left) {
         const unsigned long long res = need > (unsigned long long)kArenaQuery ? need : (unsigned long long)kArenaQuery;
         arena_base = atomicAdd(out.cursor, res);
@@ -1089,9 +1127,9 @@ __global__ void __launch_bounds__(256) k_nb_query(GridView g, const int32_t* __r
         wg_long += need;
         ++wg_long_n;
       }
-      out.off[j] = (int64_t)s_base;
+      out.off[j] = c16 ? 2 * (int64_t)s_base : (int64_t)s_base;
       out.cnt[j] = k;
-      out.lg[j] = 0;
+      out.lg[j] = c16 ? kLgCompact : 0;
     }
     if (sorted && k > 1) {  // (the bucket counts were taken with the hits)
       if (tid < 64) {  // one wave scans the counts
@@ -1144,7 +1182,10 @@ __global__ void __launch_bounds__(256) k_nb_query(GridView g, const int32_t* __r
             if (dv < d) ++rank;
             else if (dv == d && v != s && g.perm[hits[v]] < g.perm[p]) ++rank;
           }
-          if (fits) out.list[off + st + rank] = pos_entry(R, (int32_t)p);
+          if (fits) {
+            if (c16) reinterpret_cast<uint16_t*>(out.list)[2 * off + st + rank] = (uint16_t)pos_entry16(R, (int32_t)p);
+            else out.list[off + st + rank] = pos_entry(R, (int32_t)p);
+          }
         }
         __syncthreads();
         TPROF_T(q2);
@@ -1177,8 +1218,13 @@ __global__ void __launch_bounds__(256) k_nb_query(GridView g, const int32_t* __r
     }
     __syncthreads();
     const int64_t off = (int64_t)s_base;
-    if ((unsigned long long)(off + k) <= out.cap)
-      for (int m = tid; m < k; m += 256) out.list[off + m] = pos_entry(R, (int32_t)hits[m]);
+    if ((unsigned long long)(off + k) <= out.cap) {
+      if (c16)
+        for (int m = tid; m < k; m += 256)
+          reinterpret_cast<uint16_t*>(out.list)[2 * off + m] = (uint16_t)pos_entry16(R, (int32_t)hits[m]);
+      else
+        for (int m = tid; m < k; m += 256) out.list[off + m] = pos_entry(R, (int32_t)hits[m]);
+    }
     __syncthreads();
   }
   if (tid == 0) {
@@ -1262,7 +1308,7 @@ bool build_lists_check(pfx_ctx* ctx, const Grid& G, NbLists& out, const char* ta
 }
 
 void build_lists(pfx_ctx* ctx, const Grid& G, const uint8_t* mask, double radius, bool sorted, NbLists& out,
-                 const char* tag, bool defer, int want) {
+                 const char* tag, bool defer, int want, bool compact) {
   hipStream_t st = ctx->stream;
   const int64_t n = G.n;
   GridView g = view(G);
@@ -1349,7 +1395,7 @@ void build_lists(pfx_ctx* ctx, const Grid& G, const uint8_t* mask, double radius
   const int heavy = (int)std::min<int64_t>(4, n >> 21);
   const int ch_small = 4, ch_sparse = std::max(2, heavy), ch_dense = std::max(1, heavy);
   for (int attempt = 0; attempt < 3; ++attempt) {
-    ListOut lo{off, cnt, lgs, static_cast<uint32_t*>(lb.ptr), cursor, lb.bytes / sizeof(uint32_t)};
+    ListOut lo{off, cnt, lgs, static_cast<uint32_t*>(lb.ptr), cursor, lb.bytes / sizeof(uint32_t), compact ? 1 : 0};
     if (attempt) {  // (the first attempt's cursors were zeroed by k_list_init)
       PFX_HIP(hipMemsetAsync(cursor, 0, 4 * sizeof(unsigned long long), st));
       PFX_HIP(hipMemsetAsync(counters + 2, 0, sizeof(int), st));  // per-query work
@@ -1455,6 +1501,8 @@ void build_lists(pfx_ctx* ctx, const Grid& G, const uint8_t* mask, double radius
       out.cnt = cnt;
       out.lg = lgs;
       out.list = lo.list;
+      out.compact = compact;
+      out.list_cap = (int64_t)lo.cap;
       out.skeys = G.skeys;
       return;
     }
@@ -1514,6 +1562,8 @@ void build_lists(pfx_ctx* ctx, const Grid& G, const uint8_t* mask, double radius
     out.cnt = cnt;
     out.lg = lgs;
     out.list = lo.list;
+    out.compact = compact;
+    out.list_cap = (int64_t)lo.cap;
     out.skeys = G.skeys;
     ctx->stats[std::string(tag) + "_tiles_sparse"] = h_cnt[0];
     ctx->stats[std::string(tag) + "_tiles_dense"] = h_cnt[1];

@@ -122,6 +122,15 @@ __device__ __forceinline__ uint32_t run_entry(const Runs& R, int32_t t) {
   return (uint32_t)t + d;
 }
 
+// compact (16-bit) run entry: (r << 12) | off, for blocks whose runs hold <= kCompactRun points
+constexpr int kCompactRun = 4096;
+__device__ __forceinline__ uint16_t run_entry16(const Runs& R, int32_t t) {
+  uint32_t d = 0u - (uint32_t)R.pref[0];
+#pragma unroll
+  for (int r = 1; r < 9; ++r) d = t >= R.pref[r] ? ((uint32_t)r << 12) - (uint32_t)R.pref[r] : d;
+  return (uint16_t)((uint32_t)t + d);
+}
+
 // Gather the neighbours of q into keys[0..min(k,cap)) (unsorted); returns k (may exceed cap).
 // Executed by every thread of the block (nthreads = blockDim.x, a multiple of 64); uses
 // `s_count` (LDS int) for the cross-wave compaction cursor.

@@ -25,6 +25,7 @@
 namespace pfx {
 namespace {
 
+constexpr int kBatch = 8;      // neighbour entries per half-batch (two in flight)
 #ifndef PFX_LANE_MAX
 #define PFX_LANE_MAX (2 * kLongList)
 #endif
@@ -33,7 +34,20 @@ namespace {
 // again).  Dense clouds (many long lists, the non-forked schedule): 4096 -- the dense 10M variant's
 // long-list chains 140 -> 91 ms against chain_big 17 -> 28 ms (14.0 -> 14.7 Mpoints/s).
 constexpr int kLaneMax = PFX_LANE_MAX;
+
 constexpr int kLaneMaxDense = 2 * kLaneMax;
+
+__device__ __forceinline__ void chain_add(float a[9], float x, float y, float z) {
+  a[0] = a[0] + x * x;
+  a[1] = a[1] + x * y;
+  a[2] = a[2] + x * z;
+  a[3] = a[3] + y * y;
+  a[4] = a[4] + y * z;
+  a[5] = a[5] + z * z;
+  a[6] = a[6] + x;
+  a[7] = a[7] + y;
+  a[8] = a[8] + z;
+}
 
 __device__ __forceinline__ void store_normal(const GridView& g, int32_t p, const float a[9], int k, float vpx,
                                              float vpy, float vpz, float* nx, float* ny, float* nz, float* curv) {
@@ -47,21 +61,17 @@ __device__ __forceinline__ void store_normal(const GridView& g, int32_t p, const
   curv[orig] = o[3];
 }
 
-// ---- the chain stage: one lane per query, candidate coordinates staged in LDS ----------------
+// ---- k_normals_chain: one lane per query, candidate coordinates staged in LDS ----------------
 //
-// A chain group is 256 consecutive queries (cell order: a few z-consecutive cells of one or a few
-// grid columns).  Their lists only reference the 3x3x3 blocks of their cells, i.e. runs of the
-// grid columns around the query columns.  k_chain_plan works out, per group, which columns and z
-// ranges those are (an LDS hash over the touched columns), the union's LDS layout (contiguous
-// position ranges of the cell-sorted packed copy, LDS bases by a block scan) and the per-(cell,
-// run) table that maps a list entry (r, off) to its LDS slot, and writes it as one plan record.
-// The chain kernels then start a group with one round of loads (the record + the queries' list
-// descriptors), one round of staging loads, and go: the seven dependent global rounds of the
-// planning no longer sit in front of every group's chains (round 4: ~30 % of a workgroup's life).
-// Modes: small (union <= kStageSmall: k_normals_chain, three workgroups per CU), big (<=
-// kStageBig: k_normals_chain_big, one 144 KB workgroup per CU, queued by the plan), table (larger
-// unions: the same table with global run starts, coordinates from L2), lane (> kMaxCells cells:
-// per-lane run starts).
+// A workgroup takes 256 consecutive queries (cell order: a few z-consecutive cells of one or a
+// few grid columns).  Their lists only reference the 3x3x3 blocks of their cells, i.e. runs of
+// the grid columns around the query columns.  The workgroup collects those columns (LDS hash),
+// takes per column the z range its queries need, and stages the union (contiguous position
+// ranges of the cell-sorted packed copy) in LDS once; a per-cell table maps a list entry's run
+// to its LDS base.  The nine chains then read neighbour coordinates from LDS (x, y as one ds_read_b64 over the 64 banks, z ds_read_b32) instead
+// of 64-address global gathers (the TA/L2 latency that bounded the previous version).
+// Fallbacks keep every list exact: union > kStageCap -> the same table with global bases;
+// > kMaxCells distinct cells -> per-lane run starts.
 constexpr int kMaxCells = 64;
 constexpr int kHash = 1024;
 constexpr int kStageSmall = 3584;  // SoA floats: 42 KB, three workgroups per CU
@@ -69,16 +79,25 @@ constexpr int kStageBig = 12288;   // 144 KB, one workgroup per CU: the dense re
 constexpr int kMaxCols = kMaxCells * 9;
 constexpr uint32_t kEmpty = 0xffffffffu;
 
-// plan record of one chain group, kPlanWords int32 words
-constexpr int kPlanCs = 4;                        // 64 words: cell slot (u8) of each query of the group
-constexpr int kPlanTbl = kPlanCs + 64;            // [cell slot * 9 + run]: LDS slot of the run's first point
-                                                  // (staged modes) or its sorted position (table mode)
-constexpr int kPlanOst = kPlanTbl + kMaxCols;     // union ranges: start position,
-constexpr int kPlanOlen = kPlanOst + kMaxCols;    //   length,
-constexpr int kPlanObase = kPlanOlen + kMaxCols;  //   LDS base
-constexpr int kPlanWords = kPlanObase + kMaxCols;
-enum : int { kModeSmall = 0, kModeTable = 1, kModeLane = 2, kModeBig = 3, kModeNone = 4 };
-
+template <int CAP>
+struct ChainLds {
+  static_assert(CAP * 3 >= 256 * 9, "lane-mode run tables live in the staging LDS");
+  union {
+    struct {  // x, y as one 8-byte word (one ds_read_b64 per neighbour over 64 banks) + z
+      float2 xy[CAP];
+      float z[CAP];
+    } c;
+    struct {
+      uint32_t key[kHash];
+      int32_t a[kHash];  // z low, then the run start
+      int32_t b[kHash];  // z high, then the LDS base
+    } h;
+  } u;
+  int32_t tbl[kMaxCells * 9];
+  int32_t ostart[kMaxCols], olen[kMaxCols], obase[kMaxCols];
+  uint32_t ckey[kMaxCells];
+  int32_t wsum[4], wocc[4];
+};
 __device__ __forceinline__ uint32_t col_hash(uint32_t c) { return (c * 2654435761u) >> 22; }  // 10 bits
 
 struct CellXYZ { int32_t x, y, z; };
@@ -114,44 +133,91 @@ __device__ __forceinline__ int block_scan(int v, int* wsum, int* total) {
   return off + inc - v;
 }
 
-struct PlanLds {
-  uint32_t key[kHash];
-  int32_t a[kHash];  // z low, then the run start
-  int32_t b[kHash];  // z high, then the LDS base
-  uint32_t ckey[kMaxCells];
-  int32_t wsum[4], wocc[4];
-};
+template <int KB, class At, class Fetch, int NBUF = 2>
+__device__ __forceinline__ void run_chain(At at_clamped, int k, Fetch fetch, float a[9]) {
+  // Branch-free batches: entry loads use a clamped index and padded terms are exact zeros
+  // (accumulators are never -0, so + 0.0f is the identity).  NBUF entry buffers rotate without
+  // register copies (a copy of a pending load forces a vmcnt wait), so NBUF - 1 batches of entry
+  // loads are always in flight behind the batch being summed.  (Measured and rejected in
+  // round 4: 32-bit element offsets, chains 0.50 -> 0.54-0.62 ms; an all-zero coordinate slot
+  // fetched by the padded steps instead of three coordinate selects, no change.  Round 5: deeper
+  // rotation in the three-workgroups-per-CU kernel and a software pipeline over the LDS rounds,
+  // both slower: 0.47 -> 0.50-0.75 ms.)
+  const int last = k - 1;
+  auto at = [&](int m) { return at_clamped(m < last ? m : last); };
+  auto half = [&](uint32_t (&eq)[KB], int m0) {
+    float4 c[KB];
+#pragma unroll
+    for (int b = 0; b < KB; ++b) c[b] = fetch(eq[b]);
+#pragma unroll
+    for (int b = 0; b < KB; ++b) eq[b] = at(m0 + NBUF * KB + b);
+#pragma unroll
+    for (int b = 0; b < KB; ++b) {
+      const bool in = m0 + b < k;
+      chain_add(a, in ? c[b].x : 0.f, in ? c[b].y : 0.f, in ? c[b].z : 0.f);
+    }
+  };
+  if constexpr (NBUF == 2) {  // (two named buffers: the round-4 form, kept as it compiles)
+    uint32_t eA[KB], eB[KB];
+#pragma unroll
+    for (int b = 0; b < KB; ++b) {
+      eA[b] = at(b);
+      eB[b] = at(KB + b);
+    }
+    for (int m0 = 0; m0 < k; m0 += 2 * KB) {
+      half(eA, m0);
+      half(eB, m0 + KB);  // unconditional (a branch here makes every wait conservative)
+    }
+  } else {
+    uint32_t e[NBUF][KB];
+#pragma unroll
+    for (int q = 0; q < NBUF; ++q)
+#pragma unroll
+      for (int b = 0; b < KB; ++b) e[q][b] = at(q * KB + b);
+    for (int m0 = 0; m0 < k; m0 += NBUF * KB) {
+#pragma unroll
+      for (int q = 0; q < NBUF; ++q) half(e[q], m0 + q * KB);
+    }
+  }
+}
 
-// one workgroup per chain group; cnt: [0] small, [1] table, [2] lane, [3] big groups (= bigq length)
-// The queries: qpos[j] (null: the unmasked build's j itself, every finite point in cell order),
-// their count *nq64, else *nq32 (the grid's cell_start[ncells]: the plan can be made straight
-// after the grid, before the lists exist), else nq (a list build with a host-known count).
-struct PlanQueries {
-  const int32_t* qpos;
-  const uint32_t* skeys;
-  const int64_t* nq64;
-  const int32_t* nq32;
-  int64_t nq;
-};
-__global__ void __launch_bounds__(256) k_chain_plan(GridView g, PlanQueries Q, int32_t* __restrict__ plan,
-                                                    int32_t* __restrict__ bigq, int* __restrict__ cnt) {
-  __shared__ PlanLds S;
+#ifdef PFX_SHOT_PROFILE
+__device__ unsigned long long g_chain_prof[16];  // [0|8] prologue cycles, [1|9] wave chain cycles,
+                                                 // [2|10] sum of wave max k, [3|11] waves, [4|12] WGs
+#endif
+
+template <int CAP, bool DEFER>
+__device__ __forceinline__ void chain_wg(ChainLds<CAP>& S, const GridView& g, const NbLists& L, int64_t j0,
+                                         float vpx, float vpy, float vpz, float* __restrict__ nx,
+                                         float* __restrict__ ny, float* __restrict__ nz, float* __restrict__ curv,
+                                         int32_t* __restrict__ longq, int* __restrict__ n_long,
+                                         int* __restrict__ modes, int64_t* __restrict__ deferq,
+                                         const uint8_t* __restrict__ mask, int want, int lane_max) {
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int64_t b = blockIdx.x;
-  const int64_t j = b * 256 + tid;
-  int32_t* __restrict__ rec = plan + b * kPlanWords;
-  const int64_t nq = Q.nq64 ? *Q.nq64 : (Q.nq32 ? (int64_t)*Q.nq32 : Q.nq);
-  const bool valid = j < nq;
+  const int64_t j = j0 + tid;
+#ifdef PFX_SHOT_PROFILE
+  constexpr int PO = CAP == kStageSmall ? 0 : 8;
+  const long long pt0 = clock64();
+#endif
+  const bool valid = j < nq_of(L);
+  int32_t p = 0;
   uint32_t key = 0, prev = kEmpty;
+  int k = 0;
+  bool active = false;  // this pass computes the query (masked passes: mask[caller] == want)
+  bool sel = false;     // mask[caller] != 0
   if (valid) {
-    key = Q.skeys[Q.qpos ? Q.qpos[j] : (int32_t)j];
-    if (tid > 0) prev = Q.skeys[Q.qpos ? Q.qpos[j - 1] : (int32_t)(j - 1)];
+    p = L.qpos[j];
+    key = L.skeys[p];
+    k = L.cnt[j];
+    if (tid > 0) prev = L.skeys[L.qpos[j - 1]];
+    sel = mask && mask[g.perm[p]] != 0;
+    active = !mask || want >= 2 || (sel == ((want & 1) != 0));
   }
-  if (!__syncthreads_or(valid)) {
-    if (tid == 0) rec[3] = kModeNone;
-    return;
+  if (want >= 2 && mask) {  // workgroup partition: all of a workgroup with any selected query
+    if ((__syncthreads_or(sel) != 0) != ((want & 1) != 0)) return;
   }
-  // cell slots: first query of each distinct cell in the group
+  if (!__syncthreads_or(active)) return;  // nothing of this pass in the workgroup
+  // cell slots: first query of each distinct cell in the workgroup
   const bool first = valid && key != prev;
   const uint64_t fm = __ballot(first);
   if (lane == 0) S.wsum[wv] = __popcll(fm);
@@ -163,310 +229,138 @@ __global__ void __launch_bounds__(256) k_chain_plan(GridView g, PlanQueries Q, i
     ncell += S.wsum[w];
   }
   const int cs = cbase + __popcll(fm & (lanemask_lt() | (1ull << lane))) - 1;
-  {  // cell slots as bytes, four queries per word
-    const uint32_t v = valid ? (uint32_t)(cs & 0xff) : 0u;
-    const uint32_t w = v | ((uint32_t)__shfl_down((int)v, 1) << 8) | ((uint32_t)__shfl_down((int)v, 2) << 16) |
-                       ((uint32_t)__shfl_down((int)v, 3) << 24);
-    if ((tid & 3) == 0) rec[kPlanCs + (tid >> 2)] = (int32_t)w;
-  }
   __syncthreads();
-  if (ncell > kMaxCells) {  // lane mode: every lane finds its own nine runs
-    if (tid == 0) {
-      rec[0] = ncell; rec[1] = 0; rec[2] = 0; rec[3] = kModeLane;
-      atomicAdd(&cnt[kModeLane], 1);
+  const bool indexed = ncell <= kMaxCells;
+  bool staged = false;
+  if (indexed) {
+    if (first) S.ckey[cs] = key;
+    for (int s = tid; s < kHash; s += 256) {
+      S.u.h.key[s] = kEmpty;
+      S.u.h.a[s] = 0x7fffffff;
+      S.u.h.b[s] = -1;
     }
-    return;
-  }
-  if (first) S.ckey[cs] = key;
-  for (int s = tid; s < kHash; s += 256) {
-    S.key[s] = kEmpty;
-    S.a[s] = 0x7fffffff;
-    S.b[s] = -1;
-  }
-  __syncthreads();
-  // touched columns and the z range each needs; each (cell, run)'s run start is loaded here already
-  constexpr int kIt = (kMaxCells * 9 + 255) / 256;
-  int32_t pre_sr[kIt];
+    __syncthreads();
+    // touched columns and the z range each needs; each (cell, run)'s run start is loaded here
+    // already (the run table below needs it: one global round less in the prologue)
+    constexpr int kIt = (kMaxCells * 9 + 255) / 256;
+    int32_t pre_sr[kIt];
 #pragma unroll
-  for (int it = 0; it < kIt; ++it) {
-    const int i = tid + 256 * it;
-    pre_sr[it] = 0;
-    if (i < ncell * 9) {
+    for (int it = 0; it < kIt; ++it) {
+      const int i = tid + 256 * it;
+      pre_sr[it] = 0;
+      if (i < ncell * 9) {
+        const CellXYZ c = cell_of(g, S.ckey[i / 9]);
+        const int r = i % 9, X = c.x + r / 3 - 1, Y = c.y + r % 3 - 1;
+        if (X >= 0 && X < g.nx && Y >= 0 && Y < g.ny) {
+          const uint32_t col = (uint32_t)X * (uint32_t)g.ny + (uint32_t)Y;
+          pre_sr[it] = g.cell_start[(int64_t)col * g.nz + (c.z > 0 ? c.z - 1 : 0)];
+          uint32_t h = col_hash(col);
+          for (;;) {
+            const uint32_t old = atomicCAS(&S.u.h.key[h], kEmpty, col);
+            if (old == kEmpty || old == col) break;
+            h = (h + 1) & (kHash - 1);
+          }
+          atomicMin(&S.u.h.a[h], c.z > 0 ? c.z - 1 : 0);
+          atomicMax(&S.u.h.b[h], c.z + 1 < g.nz ? c.z + 1 : g.nz - 1);
+        }
+      }
+    }
+    __syncthreads();
+    // position range of every touched column, LDS bases by a block scan
+    int st4[4], len4[4], lsum = 0, osum = 0;
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const int s = tid * 4 + v;
+      const uint32_t col = S.u.h.key[s];
+      st4[v] = len4[v] = 0;
+      if (col != kEmpty) {
+        const int64_t c0 = (int64_t)col * g.nz;
+        st4[v] = g.cell_start[c0 + S.u.h.a[s]];
+        len4[v] = g.cell_start[c0 + S.u.h.b[s] + 1] - st4[v];
+      }
+      lsum += len4[v];
+      osum += len4[v] > 0;
+    }
+    int total = 0, nocc = 0;
+    int lb = block_scan(lsum, S.wsum, &total);
+    int ob = block_scan(osum, S.wocc, &nocc);
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const int s = tid * 4 + v;
+      S.u.h.a[s] = st4[v];
+      S.u.h.b[s] = lb;
+      if (len4[v] > 0) {
+        S.ostart[ob] = st4[v];
+        S.olen[ob] = len4[v];
+        S.obase[ob] = lb;
+        ++ob;
+      }
+      lb += len4[v];
+    }
+    staged = total <= CAP;
+    if (DEFER && !staged) {  // the big-LDS pass takes this workgroup (every thread agrees)
+      if (tid == 0) deferq[atomicAdd(&modes[3], 1)] = j0;
+      __syncthreads();
+      return;
+    }
+    __syncthreads();
+    // run table: list entry (r, off) of a query of cell cs -> tbl[cs * 9 + r] + off
+#pragma unroll
+    for (int it = 0; it < kIt; ++it) {
+      const int i = tid + 256 * it;
+      if (i >= ncell * 9) continue;
       const CellXYZ c = cell_of(g, S.ckey[i / 9]);
       const int r = i % 9, X = c.x + r / 3 - 1, Y = c.y + r % 3 - 1;
+      int32_t t = 0;
       if (X >= 0 && X < g.nx && Y >= 0 && Y < g.ny) {
         const uint32_t col = (uint32_t)X * (uint32_t)g.ny + (uint32_t)Y;
-        pre_sr[it] = g.cell_start[(int64_t)col * g.nz + (c.z > 0 ? c.z - 1 : 0)];
-        uint32_t h = col_hash(col);
-        for (;;) {
-          const uint32_t old = atomicCAS(&S.key[h], kEmpty, col);
-          if (old == kEmpty || old == col) break;
-          h = (h + 1) & (kHash - 1);
+        const int32_t s_r = pre_sr[it];
+        t = s_r;
+        if (staged) {
+          uint32_t h = col_hash(col);
+          while (S.u.h.key[h] != col) h = (h + 1) & (kHash - 1);
+          t = S.u.h.b[h] + (s_r - S.u.h.a[h]);
         }
-        atomicMin(&S.a[h], c.z > 0 ? c.z - 1 : 0);
-        atomicMax(&S.b[h], c.z + 1 < g.nz ? c.z + 1 : g.nz - 1);
       }
+      S.tbl[i] = t;
     }
-  }
-  __syncthreads();
-  // position range of every touched column, LDS bases by a block scan
-  int st4[4], len4[4], lsum = 0, osum = 0;
+    __syncthreads();  // the hash is dead from here on: its LDS holds the staged candidates
+    if (staged) {
+      // flattened over the whole union (runs are short in sparse regions: a loop per run would
+      // serialise one global latency per run): element i -> run by binary search over the LDS
+      // bases, four elements per thread in flight
+      for (int i0 = 0; i0 < total; i0 += 4 * 256) {
+        int32_t src[4];
 #pragma unroll
-  for (int v = 0; v < 4; ++v) {
-    const int s = tid * 4 + v;
-    const uint32_t col = S.key[s];
-    st4[v] = len4[v] = 0;
-    if (col != kEmpty) {
-      const int64_t c0 = (int64_t)col * g.nz;
-      st4[v] = g.cell_start[c0 + S.a[s]];
-      len4[v] = g.cell_start[c0 + S.b[s] + 1] - st4[v];
-    }
-    lsum += len4[v];
-    osum += len4[v] > 0;
-  }
-  int total = 0, nocc = 0;
-  int lb = block_scan(lsum, S.wsum, &total);
-  int ob = block_scan(osum, S.wocc, &nocc);
-  const int mode = total <= kStageSmall ? kModeSmall : (total <= kStageBig ? kModeBig : kModeTable);
-  const bool staged = mode != kModeTable;
-#pragma unroll
-  for (int v = 0; v < 4; ++v) {
-    const int s = tid * 4 + v;
-    S.a[s] = st4[v];
-    S.b[s] = lb;
-    if (len4[v] > 0) {
-      if (staged) {
-        rec[kPlanOst + ob] = st4[v];
-        rec[kPlanOlen + ob] = len4[v];
-        rec[kPlanObase + ob] = lb;
-      }
-      ++ob;
-    }
-    lb += len4[v];
-  }
-  __syncthreads();
-  // run table: list entry (r, off) of a query of cell cs -> tbl[cs * 9 + r] + off
-#pragma unroll
-  for (int it = 0; it < kIt; ++it) {
-    const int i = tid + 256 * it;
-    if (i >= ncell * 9) continue;
-    const CellXYZ c = cell_of(g, S.ckey[i / 9]);
-    const int r = i % 9, X = c.x + r / 3 - 1, Y = c.y + r % 3 - 1;
-    int32_t t = 0;
-    if (X >= 0 && X < g.nx && Y >= 0 && Y < g.ny) {
-      const uint32_t col = (uint32_t)X * (uint32_t)g.ny + (uint32_t)Y;
-      const int32_t s_r = pre_sr[it];
-      t = s_r;
-      if (staged) {
-        uint32_t h = col_hash(col);
-        while (S.key[h] != col) h = (h + 1) & (kHash - 1);
-        t = S.b[h] + (s_r - S.a[h]);
-      }
-    }
-    rec[kPlanTbl + i] = t;
-  }
-  if (tid == 0) {
-    rec[0] = ncell; rec[1] = total; rec[2] = nocc; rec[3] = mode;
-    const int at = atomicAdd(&cnt[mode], 1);
-    if (mode == kModeBig) bigq[at] = (int32_t)b;
-  }
-}
-
-#ifndef PFX_CHAIN_NB
-#define PFX_CHAIN_NB 2
-#endif
-#ifndef PFX_CHAIN_KB
-#define PFX_CHAIN_KB 8
-#endif
-#ifndef PFX_CHAIN_NB_BIG
-#define PFX_CHAIN_NB_BIG 2
-#endif
-
-template <int CAP>
-struct ChainLds {
-  float2 xy[CAP + 1];  // x, y as one 8-byte word (one ds_read_b64 per neighbour over 64 banks) + z;
-  float z[CAP + 1];    // slot CAP: the zero point of the padded steps
-  int32_t tbl[kMaxCols];
-  int32_t ostart[kMaxCols], olen[kMaxCols], obase[kMaxCols];
-  int32_t nact;
-};
-static_assert(kStageSmall * 2 >= 256 * 9, "lane-mode run tables live in the staging LDS");
-
-// The nine ordered float chains of one query, packed two by two where the pairs fall out of the
-// (x, y) word: (xx, yy) and (xz, yz) on v_pk_mul_f32 / v_pk_add_f32 (each half rounds as the
-// scalar operation: the same bits as nine scalar chains), xy, zz and z scalar.
-typedef float cf2 __attribute__((ext_vector_type(2)));
-struct Chains {
-  cf2 xx_yy, xz_yz, x_y;
-  float xy, zz, z;
-  __device__ __forceinline__ void zero() {
-    xx_yy = xz_yz = x_y = cf2{0.f, 0.f};
-    xy = zz = z = 0.f;
-  }
-  __device__ __forceinline__ void add(float2 p, float pz) {
-    const cf2 v = cf2{p.x, p.y};
-    xx_yy = xx_yy + v * v;
-    xz_yz = xz_yz + v * cf2{pz, pz};
-    xy = xy + p.x * p.y;
-    zz = zz + pz * pz;
-    x_y = x_y + v;
-    z = z + pz;
-  }
-  __device__ __forceinline__ void out(float a[9]) const {
-    a[0] = xx_yy.x; a[1] = xy; a[2] = xz_yz.x; a[3] = xx_yy.y; a[4] = xz_yz.y; a[5] = zz;
-    a[6] = x_y.x; a[7] = x_y.y; a[8] = z;
-  }
-};
-
-// One query's chains over its list: branch-free batches (entry loads at a clamped index, padded
-// steps read the zero point: accumulators are never -0, so + 0.0f is the identity).  NB entry
-// buffers of KB entries rotate without register copies (a copy of a pending load forces a vmcnt
-// wait): NB - 1 batches of entry loads stay in flight behind the batch being summed (the list
-// loads come from HBM at several microseconds of latency under the chain stage's load).
-// slot(e) maps a list entry to its coordinate slot.
-template <int KB, int NB, class Slot, class Coord>
-__device__ __forceinline__ void run_chain(const uint32_t* lst, int lg, int k, Slot slot, int zslot, Coord coord,
-                                          Chains& A) {
-  const int last = k - 1;
-#ifdef PFX_DIAG_NOLOAD
-  auto at = [&](int m) { return lst[0] + (uint32_t)(m < last ? m : last); };
-#else
-  auto at = [&](int m) { return lst[(int64_t)(m < last ? m : last) << lg]; };
-#endif
-  uint32_t e[NB][KB];
-#pragma unroll
-  for (int q = 0; q < NB; ++q)
-#pragma unroll
-    for (int b = 0; b < KB; ++b) e[q][b] = at(q * KB + b);
-  auto step = [&](uint32_t (&eq)[KB], int m0) {
-    int32_t s[KB];
-#pragma unroll
-    for (int b = 0; b < KB; ++b) {
-      // slot of the (clamped) entry, always computed: the empty asm hides its LDS load from the
-      // select below (a select on a loaded value becomes a branch around the load, one LDS
-      // latency per step)
-      int32_t v = slot(eq[b]);
-      asm("" : "+v"(v));
-      s[b] = m0 + b < k ? v : zslot;
-    }
-    float2 p[KB];
-    float pz[KB];
-#pragma unroll
-    for (int b = 0; b < KB; ++b) coord(s[b], p[b], pz[b]);
-#pragma unroll
-    for (int b = 0; b < KB; ++b) eq[b] = at(m0 + NB * KB + b);
-#pragma unroll
-    for (int b = 0; b < KB; ++b) A.add(p[b], pz[b]);
-  };
-  for (int m0 = 0; m0 < k; m0 += NB * KB) {
-#pragma unroll
-    for (int q = 0; q < NB; ++q) step(e[q], m0 + q * KB);  // unconditional (a branch here makes every wait conservative)
-  }
-}
-
-#ifdef PFX_SHOT_PROFILE
-__device__ unsigned long long g_chain_prof[16];  // [0|8] prologue cycles, [1|9] wave chain cycles,
-                                                 // [2|10] sum of wave max k, [3|11] waves, [4|12] WGs
-#endif
-
-// Group b's chains.  CAP: the staging capacity of the calling kernel (small: the groups of mode
-// small, table and lane; big: the groups of mode big).  U: staging loads in flight per thread.
-template <int CAP, int U, int KB, int NB>
-__device__ __forceinline__ void chain_group(ChainLds<CAP>& S, const GridView& g, const NbLists& L,
-                                            const int32_t* __restrict__ plan, int64_t b, float vpx, float vpy,
-                                            float vpz, float* __restrict__ nx, float* __restrict__ ny,
-                                            float* __restrict__ nz, float* __restrict__ curv,
-                                            const uint8_t* __restrict__ mask, int want, int lane_max) {
-  constexpr bool BIG = CAP == kStageBig;
-  const int tid = threadIdx.x;
-  const int32_t* __restrict__ rec = plan + b * kPlanWords;
-  const int mode = __builtin_amdgcn_readfirstlane(rec[3]);
-  if (mode == kModeNone || (mode == kModeBig) != BIG) return;
-#ifdef PFX_SHOT_PROFILE
-  constexpr int PO = BIG ? 8 : 0;
-  const long long pt0 = clock64();
-#endif
-  const int ncell = __builtin_amdgcn_readfirstlane(rec[0]);
-  const int total = __builtin_amdgcn_readfirstlane(rec[1]);
-  const int nocc = __builtin_amdgcn_readfirstlane(rec[2]);
-  const int64_t j = b * 256 + tid;
-  const bool valid = j < nq_of(L);
-  int32_t p = 0;
-  int k = 0, lg = 0, cs = 0;
-  int64_t loff = 0;
-  bool active = false;  // this pass computes the query (masked passes: mask[caller] == want)
-  bool sel = false;     // mask[caller] != 0
-  if (valid) {
-    p = L.qpos[j];
-    k = L.cnt[j];
-    loff = L.off[j];
-    lg = L.lg[j];
-    cs = (rec[kPlanCs + (tid >> 2)] >> ((tid & 3) * 8)) & 0xff;
-    sel = mask && mask[g.perm[p]] != 0;
-    active = !mask || want >= 2 || (sel == ((want & 1) != 0));
-  }
-  if (want >= 2 && mask) {  // workgroup partition: all of a workgroup with any selected query
-    if ((__syncthreads_or(sel) != 0) != ((want & 1) != 0)) return;
-  }
-  if (!__syncthreads_or(active)) return;  // nothing of this pass in the group
-  const bool staged = mode == kModeSmall || mode == kModeBig;
-  if (mode != kModeLane) {
-    for (int s = tid; s < ncell * 9; s += 256) S.tbl[s] = rec[kPlanTbl + s];
-  }
-  if (staged) {
-    for (int s = tid; s < nocc; s += 256) {
-      S.ostart[s] = rec[kPlanOst + s];
-      S.olen[s] = rec[kPlanOlen + s];
-      S.obase[s] = rec[kPlanObase + s];
-    }
-    if (tid == 0) {
-      S.xy[CAP] = make_float2(0.f, 0.f);
-      S.z[CAP] = 0.f;
-    }
-  }
-  __syncthreads();
-  if (staged) {
-    // flattened over the whole union (runs are short in sparse regions: a loop per run would
-    // serialise one global latency per run): element i -> run by binary search over the LDS
-    // bases, U elements per thread in flight
-    for (int i0 = 0; i0 < total; i0 += U * 256) {
-      int32_t src[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int i = i0 + u * 256 + tid;
-        int lo = 0, hi = nocc - 1;
-        while (lo < hi) {
-          const int mid = (lo + hi + 1) >> 1;
-          if (S.obase[mid] <= i) lo = mid;
-          else hi = mid - 1;
+        for (int u = 0; u < 4; ++u) {
+          const int i = i0 + u * 256 + tid;
+          int lo = 0, hi = nocc - 1;
+          while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (S.obase[mid] <= i) lo = mid;
+            else hi = mid - 1;
+          }
+          src[u] = i < total ? S.ostart[lo] + (i - S.obase[lo]) : -1;
         }
-        src[u] = i < total ? S.ostart[lo] + (i - S.obase[lo]) : -1;
-      }
-      float4 v[U];  // (the packed copy: one load per point instead of three)
+        float4 v[4];  // (the packed copy: one load per point instead of three)
 #pragma unroll
-      for (int u = 0; u < U; ++u) v[u] = g.sp[src[u] < 0 ? 0 : src[u]];
+        for (int u = 0; u < 4; ++u) v[u] = g.sp[src[u] < 0 ? 0 : src[u]];
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int i = i0 + u * 256 + tid;
-        if (src[u] >= 0) {
-          S.xy[i] = make_float2(v[u].x, v[u].y);
-          S.z[i] = v[u].z;
+        for (int u = 0; u < 4; ++u) {
+          const int i = i0 + u * 256 + tid;
+          if (src[u] >= 0) {
+            S.u.c.xy[i] = make_float2(v[u].x, v[u].y);
+            S.u.c.z[i] = v[u].z;
+          }
         }
       }
     }
-  } else if (mode == kModeLane) {
-    // too many cells for the shared table: each lane keeps its own nine run starts in the
-    // (unused) staging LDS
-    int32_t* tb = reinterpret_cast<int32_t*>(S.xy) + tid * 9;
-    const uint32_t key = valid ? L.skeys[p] : 0u;
-#pragma unroll
-    for (int r = 0; r < 9; ++r) {
-      int32_t st, len;
-      block_run(g, key, r, st, len);
-      tb[r] = st;
-    }
+    __syncthreads();
+    if (tid == 0) atomicAdd(&modes[staged ? 0 : 1], 1);
+  } else if (tid == 0) {
+    atomicAdd(&modes[2], 1);
   }
-  __syncthreads();  // staged LDS complete
+  __syncthreads();  // LDS reuse: every thread has passed the shared phases
 #ifdef PFX_SHOT_PROFILE
   const long long pt1 = clock64();
   if (tid == 0) {
@@ -477,39 +371,64 @@ __device__ __forceinline__ void chain_group(ChainLds<CAP>& S, const GridView& g,
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) wk = max(wk, __shfl_xor(wk, o));
   const uint64_t wm = __ballot(active && k == wk);
-  const bool rec_lane = wm && (int)(tid & 63) == __builtin_ctzll(wm);
+  const bool rec = wm && lane == __builtin_ctzll(wm);
 #endif
   if (!active) return;
   if (k > lane_max) return;  // listed by k_long_lists, chained by k_normals_long
-  const uint32_t* lst = L.list + loff;
-  Chains A;
-  A.zero();
+  // the query's list: 32-bit run entries, or 16-bit ones (kLgCompact: the tile kernels' lists of
+  // blocks with runs of <= 4096 points).  The two widths take two loops behind a divergent branch:
+  // a wave of one width runs one of them (the same instructions per step either way), a mixed
+  // wave both in turn, exec-masked (a per-lane select of the width cost 32 spilled VGPRs).
+  const int lgr = L.lg[j];
+  const bool c16 = (lgr & kLgCompact) != 0;
+  const int lg = lgr & 0x7f;
+  const int64_t loff = L.off[j];
+  const uint32_t* l32 = L.list + loff;
+  const uint16_t* l16 = reinterpret_cast<const uint16_t*>(L.list) + loff;
+  auto at32 = [&](int m) { return l32[(int64_t)m << lg]; };
+  auto at16 = [&](int m) { return (uint32_t)l16[(int64_t)m << lg]; };
+  // run entry -> slot of run r's first point + offset (32-bit layout, or 16-bit: r << 12 | off)
+  auto slot32 = [](const int32_t* tb, uint32_t e) { return tb[entry_run(e)] + (int32_t)entry_off(e); };
+  auto slot16 = [](const int32_t* tb, uint32_t e) { return tb[e >> 12] + (int32_t)(e & 0xfffu); };
+  float a[9];
+#pragma unroll
+  for (int i = 0; i < 9; ++i) a[i] = 0.0f;
+  // run the chains with the loop of this wave's list width
+  // (round 5, measured: a per-lane width select in one loop for mixed waves of the big kernel,
+  // 0.217 -> 0.226 ms; four entry batches in flight there instead of two, no change)
+  auto chains = [&](auto fetch32, auto fetch16) {
+    if (c16) run_chain<kBatch>(at16, k, fetch16, a);
+    else run_chain<kBatch>(at32, k, fetch32, a);
+  };
   if (staged) {
     const int32_t* tb = S.tbl + cs * 9;
-    const float2* cxy = S.xy;
-    const float* czs = S.z;
-#ifdef PFX_DIAG_NOTBL
-    run_chain<KB, NB>(lst, lg, k, [&](uint32_t e) { return (int32_t)(entry_off(e) & 1023); }, CAP,
-#else
-    run_chain<KB, NB>(lst, lg, k, [&](uint32_t e) { return tb[entry_run(e)] + (int32_t)entry_off(e); }, CAP,
-#endif
-                  [&](int32_t i, float2& q, float& qz) { q = cxy[i]; qz = czs[i]; }, A);
-  } else {
-    // table / lane: positions of the packed global copy (slot -1: the zero point)
-    const int32_t* tb = mode == kModeTable ? S.tbl + cs * 9 : reinterpret_cast<const int32_t*>(S.xy) + tid * 9;
+    const float2* cxy = S.u.c.xy;
+    const float* czs = S.u.c.z;
+    auto lds = [&](int32_t i) {
+      const float2 v = cxy[i];
+      return make_float4(v.x, v.y, czs[i], 0.f);
+    };
+    chains([&](uint32_t e) { return lds(slot32(tb, e)); }, [&](uint32_t e) { return lds(slot16(tb, e)); });
+  } else if (indexed) {
+    const int32_t* tb = S.tbl + cs * 9;
     const float4* sp = g.sp;
-    run_chain<KB, NB>(lst, lg, k, [&](uint32_t e) { return tb[entry_run(e)] + (int32_t)entry_off(e); }, -1,
-                  [&](int32_t i, float2& q, float& qz) {
-                    const float4 c = sp[i < 0 ? 0 : i];
-                    q = i < 0 ? make_float2(0.f, 0.f) : make_float2(c.x, c.y);
-                    qz = i < 0 ? 0.f : c.z;
-                  }, A);
+    chains([&](uint32_t e) { return sp[slot32(tb, e)]; }, [&](uint32_t e) { return sp[slot16(tb, e)]; });
+  } else if constexpr (CAP != kStageBig) {  // (a deferred workgroup is indexed: never here)
+    // too many cells for the shared table: each lane keeps its own nine run starts in the
+    // (unused) staging LDS
+    int32_t* tb = reinterpret_cast<int32_t*>(S.u.c.xy) + tid * 9;
+#pragma unroll
+    for (int r = 0; r < 9; ++r) {
+      int32_t st, len;
+      block_run(g, key, r, st, len);
+      tb[r] = st;
+    }
+    const float4* sp = g.sp;
+    chains([&](uint32_t e) { return sp[slot32(tb, e)]; }, [&](uint32_t e) { return sp[slot16(tb, e)]; });
   }
-  float a[9];
-  A.out(a);
   store_normal(g, p, a, k, vpx, vpy, vpz, nx, ny, nz, curv);
 #ifdef PFX_SHOT_PROFILE
-  if (rec_lane) {
+  if (rec) {
     atomicAdd(&g_chain_prof[PO + 1], (unsigned long long)(clock64() - pt1));
     atomicAdd(&g_chain_prof[PO + 2], (unsigned long long)wk);
     atomicAdd(&g_chain_prof[PO + 3], 1ull);
@@ -517,31 +436,34 @@ __device__ __forceinline__ void chain_group(ChainLds<CAP>& S, const GridView& g,
 #endif
 }
 
-__global__ void __launch_bounds__(256, 3) k_normals_chain(GridView g, NbLists L, const int32_t* __restrict__ plan,
-                                                          float vpx, float vpy, float vpz, float* __restrict__ nx,
-                                                          float* __restrict__ ny, float* __restrict__ nz,
-                                                          float* __restrict__ curv, const uint8_t* __restrict__ mask,
-                                                          int want, int lane_max) {
+__global__ void __launch_bounds__(256, 3) k_normals_chain(GridView g, NbLists L, float vpx, float vpy, float vpz,
+                                                          float* __restrict__ nx, float* __restrict__ ny,
+                                                          float* __restrict__ nz, float* __restrict__ curv,
+                                                          int32_t* __restrict__ longq, int* __restrict__ n_long,
+                                                          int* __restrict__ modes, int64_t* __restrict__ deferq,
+                                                          const uint8_t* __restrict__ mask, int want,
+                                                          int lane_max) {
   __shared__ ChainLds<kStageSmall> S;
-  chain_group<kStageSmall, 14, PFX_CHAIN_KB, PFX_CHAIN_NB>(S, g, L, plan, blockIdx.x, vpx, vpy, vpz, nx, ny, nz, curv, mask, want, lane_max);
+  chain_wg<kStageSmall, true>(S, g, L, (int64_t)blockIdx.x * 256, vpx, vpy, vpz, nx, ny, nz, curv,
+                              longq, n_long, modes, deferq, mask, want, lane_max);
 }
 
-// the big groups: one 144 KB workgroup per CU, persistent over the plan's queue
-__global__ void __launch_bounds__(256, 1) k_normals_chain_big(GridView g, NbLists L,
-                                                              const int32_t* __restrict__ plan,
-                                                              const int32_t* __restrict__ bigq,
-                                                              const int* __restrict__ cnt, float vpx, float vpy,
+// the deferred (dense) workgroups: one 144 KB workgroup per CU, persistent over the queue
+__global__ void __launch_bounds__(256, 1) k_normals_chain_big(GridView g, NbLists L, float vpx, float vpy,
                                                               float vpz, float* __restrict__ nx,
                                                               float* __restrict__ ny, float* __restrict__ nz,
-                                                              float* __restrict__ curv,
+                                                              float* __restrict__ curv, int32_t* __restrict__ longq,
+                                                              int* __restrict__ n_long, int* __restrict__ modes,
+                                                              const int64_t* __restrict__ deferq,
                                                               const uint8_t* __restrict__ mask, int want,
                                                               int lane_max) {
   extern __shared__ __attribute__((aligned(16))) unsigned char dyn[];
   ChainLds<kStageBig>& S = *reinterpret_cast<ChainLds<kStageBig>*>(dyn);
-  const int count = cnt[kModeBig];
+  const int count = modes[3];
   for (int w = blockIdx.x; w < count; w += gridDim.x) {
-    __syncthreads();  // the previous group's chains have finished reading the LDS
-    chain_group<kStageBig, 16, 8, PFX_CHAIN_NB_BIG>(S, g, L, plan, bigq[w], vpx, vpy, vpz, nx, ny, nz, curv, mask, want, lane_max);
+    __syncthreads();  // the previous workgroup's chains have finished reading the LDS
+    chain_wg<kStageBig, false>(S, g, L, deferq[w], vpx, vpy, vpz, nx, ny, nz, curv, longq, n_long, modes, nullptr,
+                               mask, want, lane_max);
   }
 }
 
@@ -777,7 +699,6 @@ void normals_lists_dev(pfx_ctx* ctx, const float* x, const float* y, const float
   ns.z = z;
   ns.r = r;
   ns.L = NbLists();
-  ns.plan_gen = 0;
   if (n == 0) {
     ns.ready = true;
     return;
@@ -808,8 +729,9 @@ void normals_chains_dev(pfx_ctx* ctx, pfx_ctx* owner, const uint8_t* mask, int w
   hipStream_t st = ctx->stream;
   const Grid& G = owner->grid_a;
   int32_t* longq = ctx->buf("normals_longq").as<int32_t>(L.nq);
-  int* n_long = ctx->buf("normals_nlong").as<int>(1);  // long lists
-  PFX_HIP(hipMemsetAsync(n_long, 0, sizeof(int), st));
+  // [0] long lists, [1..3] chain modes (staged, table, lane), [4] deferred workgroups
+  int* n_long = ctx->buf("normals_nlong").as<int>(5);
+  PFX_HIP(hipMemsetAsync(n_long, 0, 5 * sizeof(int), st));
   const int64_t nb = ceil_div(L.nq, 256);
   // the long lists first: when they are few (their chains, bound by the longest list, leave the
   // device mostly idle) k_normals_long runs on a side stream concurrently with the short-list
@@ -833,32 +755,13 @@ void normals_chains_dev(pfx_ctx* ctx, pfx_ctx* owner, const uint8_t* mask, int w
     check_launch("k_normals_long");
   }
   {
-    // natural block order = round-robin over the 8 XCDs: the dense (heavy) groups cluster in
+    // natural block order = round-robin over the 8 XCDs: the dense (heavy) workgroups cluster in
     // space, so contiguous per-XCD slices would leave one XCD with ~1.4x the mean work
-    int32_t* plan;
-    int32_t* bigq;
-    int* pcnt;
-    NormalsState& ons = *owner->normals;
-    if (owner == ctx && ons.plan_gen != 0 && ons.plan_gen == G.gen) {
-      // made beside the list kernels (normals_plan_ahead)
-      plan = static_cast<int32_t*>(ctx->buf("normals_plan").ptr);
-      bigq = static_cast<int32_t*>(ctx->buf("normals_bigq").ptr);
-      pcnt = static_cast<int*>(ctx->buf("normals_plan_cnt").ptr);
-      PFX_HIP(hipStreamWaitEvent(st, ctx->fork_ev[3], 0));
-    } else {
-      plan = ctx->buf("normals_plan").as<int32_t>((size_t)nb * kPlanWords);
-      bigq = ctx->buf("normals_bigq").as<int32_t>(nb);
-      pcnt = ctx->buf("normals_plan_cnt").as<int>(4);
-      PFX_HIP(hipMemsetAsync(pcnt, 0, 4 * sizeof(int), st));
-      TimeScope ts(ctx, "normals_chain_plan");
-      k_chain_plan<<<(unsigned)nb, 256, 0, st>>>(view(G), PlanQueries{L.qpos, L.skeys, L.nq_dev, nullptr, L.nq}, plan, bigq,
-                                                 pcnt);
-      check_launch("k_chain_plan");
-    }
+    int64_t* deferq = ctx->buf("normals_deferq").as<int64_t>(nb);
     {
       TimeScope ts(ctx, "normals_chain");
-      k_normals_chain<<<(unsigned)nb, 256, 0, st>>>(view(G), L, plan, vp[0], vp[1], vp[2], nx, ny, nz, curv, mask,
-                                                    want, lane_max);
+      k_normals_chain<<<(unsigned)nb, 256, 0, st>>>(view(G), L, vp[0], vp[1], vp[2], nx, ny, nz, curv, longq, n_long,
+                                                    n_long + 1, deferq, mask, want, lane_max);
       check_launch("k_normals_chain");
     }
     static std::once_flag attr;  // contexts may run on several host threads
@@ -869,9 +772,9 @@ void normals_chains_dev(pfx_ctx* ctx, pfx_ctx* owner, const uint8_t* mask, int w
     });
     PFX_HIP(attr_err);
     TimeScope tb(ctx, "normals_chain_big");
-    k_normals_chain_big<<<256, 256, sizeof(ChainLds<kStageBig>), st>>>(view(G), L, plan, bigq, pcnt, vp[0],
-                                                                         vp[1], vp[2], nx, ny, nz, curv, mask, want,
-                                                                         lane_max);
+    k_normals_chain_big<<<256, 256, sizeof(ChainLds<kStageBig>), st>>>(view(G), L, vp[0], vp[1], vp[2], nx, ny, nz,
+                                                                         curv, longq, n_long, n_long + 1, deferq,
+                                                                         mask, want, lane_max);
     check_launch("k_normals_chain_big");
   }
   {
@@ -886,11 +789,10 @@ void normals_chains_dev(pfx_ctx* ctx, pfx_ctx* owner, const uint8_t* mask, int w
   }
   if (ctx->timer.enabled && !ctx->timer.stages_only) {  // per-kernel timing (diagnostics, host sync): the chain modes
     int h[5];
-    PFX_HIP(hipMemcpyAsync(h, n_long, sizeof(int), hipMemcpyDeviceToHost, st));
-    PFX_HIP(hipMemcpyAsync(h + 1, ctx->buf("normals_plan_cnt").ptr, 4 * sizeof(int), hipMemcpyDeviceToHost, st));
+    PFX_HIP(hipMemcpyAsync(h, n_long, sizeof(h), hipMemcpyDeviceToHost, st));
     PFX_HIP(hipStreamSynchronize(st));
     ctx->stats["normals_long_lists"] = h[0];
-    ctx->stats["normals_chain_wg_staged"] = h[1] + h[4];
+    ctx->stats["normals_chain_wg_staged"] = h[1];
     ctx->stats["normals_chain_wg_table"] = h[2];
     ctx->stats["normals_chain_wg_lane"] = h[3];
     ctx->stats["normals_chain_wg_deferred"] = h[4];
@@ -913,29 +815,6 @@ void normals_chains_dev(pfx_ctx* ctx, pfx_ctx* owner, const uint8_t* mask, int w
 
 namespace {
 
-// The chain plan of the unmasked lists of the grid just built, on the side stream beside the list
-// kernels: it needs only the grid (the queries are every finite point in cell order), and made
-// inline in front of the chains it cost ~90 us of dependent global rounds on the critical path.
-void normals_plan_ahead(pfx_ctx* ctx) {
-  NormalsState& ns = *ctx->normals;
-  const Grid& G = ctx->grid_a;
-  ns.plan_gen = 0;
-  if (G.n == 0) return;
-  const int64_t nb = ceil_div(G.n, 256);
-  int32_t* plan = ctx->buf("normals_plan").as<int32_t>((size_t)nb * kPlanWords);
-  int32_t* bigq = ctx->buf("normals_bigq").as<int32_t>(nb);
-  int* pcnt = ctx->buf("normals_plan_cnt").as<int>(4);
-  ctx->ensure_side();
-  PFX_HIP(hipEventRecord(ctx->fork_ev[2], ctx->stream));
-  PFX_HIP(hipStreamWaitEvent(ctx->side, ctx->fork_ev[2], 0));
-  PFX_HIP(hipMemsetAsync(pcnt, 0, 4 * sizeof(int), ctx->side));
-  k_chain_plan<<<(unsigned)nb, 256, 0, ctx->side>>>(view(G), PlanQueries{nullptr, G.skeys, nullptr, G.cell_start + G.ncells, 0},
-                                                    plan, bigq, pcnt);
-  check_launch("k_chain_plan");
-  PFX_HIP(hipEventRecord(ctx->fork_ev[3], ctx->side));
-  ns.plan_gen = G.gen;
-}
-
 // grid on the hint, NaN fill, list kernels launched without their readback (the lists check
 // follows in the caller); false when the speculative form does not apply
 bool normals_speculative_lists(pfx_ctx* ctx, const float* x, const float* y, const float* z, int64_t n, double r,
@@ -951,14 +830,12 @@ bool normals_speculative_lists(pfx_ctx* ctx, const float* x, const float* y, con
   ns.z = z;
   ns.r = r;
   ns.L = NbLists();
-  ns.plan_gen = 0;
   TimeScope phase(ctx, "normals_lists_phase", true);
   build_grid(ctx, ctx->grid_a, x, y, z, n, r, /*use_hint=*/true);
-  normals_plan_ahead(ctx);
   k_nan_fill4<<<(unsigned)std::min<int64_t>(ceil_div(n, 256), 4096), 256, 0, ctx->stream>>>(nx, ny, nz, curv, n);
   check_launch("k_nan_fill4");
   wait_lists_gate(ctx);
-  build_lists(ctx, ctx->grid_a, nullptr, r, true, ns.L, "normals", /*defer=*/true);
+  build_lists(ctx, ctx->grid_a, nullptr, r, true, ns.L, "normals", /*defer=*/true, /*want=*/1, /*compact=*/true);
   return true;
 }
 
@@ -1050,7 +927,6 @@ void normals_prepare_dev(pfx_ctx* ctx, const float* x, const float* y, const flo
   NormalsState& ns = *ctx->normals;
   ns.ready = false;
   ns.L = NbLists();
-  ns.plan_gen = 0;
   ns.n = n;
   ns.x = x;
   ns.y = y;
@@ -1082,7 +958,6 @@ void normals_subset_dev(pfx_ctx* ctx, const float* x, const float* y, const floa
                        ns.n == n && ns.r == r;
   if (!grid_ok) normals_prepare_dev(ctx, x, y, z, n, r);
   ns.ready = false;
-  ns.plan_gen = 0;  // (masked lists: their plan is made inline)
   hipStream_t st = ctx->stream;
   {
     TimeScope phase(ctx, "normals_lists_phase", true);

@@ -25,7 +25,7 @@ for name, gen, seed in (("room", synth_room, 2), ("seabed", synth_seabed, 3)):
         torch.cuda.synchronize()
         ctx.set_timing(True)
         ctx.reset_timing()
-        steps = 5
+        steps = int(os.environ.get("PFX_NO_STEPS", "20"))
         for _ in range(steps):
             ctx.normals_dev(b.x, b.y, b.z, 0.05, b.nx, b.ny, b.nz, b.curv)
         torch.cuda.synchronize()
