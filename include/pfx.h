@@ -196,10 +196,17 @@ pfx_status pfx_normals_finish_dev(pfx_ctx* ctx, int32_t* rerun);
 
 /* Scheduling hint (no reference counterpart): the next pfx_normals_launch_dev / pfx_normals_dev on
  * ctx makes its stream wait for hip_event (a hipEvent_t already recorded by the caller) after its
- * grid build and before its neighbour-list kernels, once.  The list kernels are persistent and
- * fill the device; a short stage on another stream that must not queue behind them (FPFH's
- * surface grid, which NARF's chain then follows) is kept ahead this way.  NULL clears it. */
+ * grid build and list set-up and before its neighbour-list kernels, once.  The list kernels are
+ * persistent and fill the device; a short stage on another stream that must not queue behind
+ * them (FPFH's surface grid, which NARF's chain then follows) is kept ahead this way.  NULL
+ * clears it. */
 pfx_status pfx_normals_gate_dev(pfx_ctx* ctx, void* hip_event);
+/* Scheduling aid: queue the (speculative) grid of the next pfx_normals_launch_dev /
+ * pfx_normals_dev on the same d_x, n and radius now, so the caller can issue it before another
+ * stream's work (and that work's gate, pfx_normals_gate_dev) and the estimation's lists after.
+ * Results are unchanged; any other call in between on ctx discards it. */
+pfx_status pfx_normals_grid_launch_dev(pfx_ctx* ctx, const float* d_x, const float* d_y, const float* d_z,
+                                       int64_t n, double radius);
 
 /* NormalEstimationOMP (tools.h:22-32) over a subset of the cloud: the points with
  * (d_mask[i] != 0) == want get PCL's normal and curvature bit for bit (their neighbours are

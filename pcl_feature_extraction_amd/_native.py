@@ -104,6 +104,7 @@ _SIGS = {
     "pfx_normals_launch_dev": (c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_dbl, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "pfx_normals_finish_dev": (c_int, [c_vp, c_vp]),
     "pfx_normals_gate_dev": (c_int, [c_vp, c_vp]),
+    "pfx_normals_grid_launch_dev": (c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_dbl]),
     "pfx_normals_subset_dev": (c_int, [c_vp, c_vp, c_vp, c_vp, c_i64, c_dbl, c_vp, ctypes.c_int32, c_vp, c_vp, c_vp,
                                        c_vp, c_vp]),
     "pfx_normals_chains_dev": (c_int, [c_vp, c_vp, c_vp, ctypes.c_int32, c_vp, c_vp, c_vp, c_vp, c_vp]),

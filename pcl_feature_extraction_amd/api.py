@@ -235,6 +235,12 @@ class Context:
         self._check(self._lib.pfx_normals_launch_dev(self.h, _ptr(x), _ptr(y), _ptr(z), x.numel(), float(r), vp,
                                                      _ptr(nx), _ptr(ny), _ptr(nz), _ptr(curv)))
 
+    def normals_grid_launch_dev(self, x, y, z, r):
+        """Queue the spatial grid of the next normals_launch_dev on this context's stream now
+        (pfx_normals_grid_launch_dev) so it runs ahead of work issued later on other streams;
+        the launch for the same cloud and radius then starts at its list kernels."""
+        self._check(self._lib.pfx_normals_grid_launch_dev(self.h, _ptr(x), _ptr(y), _ptr(z), x.numel(), float(r)))
+
     def normals_gate_dev(self, event):
         """The next normals launch on this context waits for `event` (a recorded torch.cuda.Event)
         between its grid build and its list kernels (pfx_normals_gate_dev); None clears it."""

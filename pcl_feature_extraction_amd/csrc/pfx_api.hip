@@ -332,6 +332,15 @@ pfx_status pfx_normals_launch_dev(pfx_ctx* ctx, const float* d_x, const float* d
   PFX_API_END(ctx)
 }
 
+pfx_status pfx_normals_grid_launch_dev(pfx_ctx* ctx, const float* d_x, const float* d_y, const float* d_z, int64_t n,
+                                       double radius) {
+  PFX_API_BEGIN
+  check_ctx(ctx);
+  if (n < 0 || (n && (!d_x || !d_y || !d_z))) throw Error(PFX_ERR_INVALID, "normals grid: invalid arguments");
+  pfx::normals_grid_launch_dev(ctx, d_x, d_y, d_z, n, radius);
+  PFX_API_END(ctx)
+}
+
 pfx_status pfx_normals_gate_dev(pfx_ctx* ctx, void* hip_event) {
   PFX_API_BEGIN
   check_ctx(ctx);

@@ -257,6 +257,7 @@ void normals_lists_dev(pfx_ctx* ctx, const float* x, const float* y, const float
 void normals_chains_dev(pfx_ctx* ctx, pfx_ctx* owner, const uint8_t* mask, int want, const float vp[3], float* nx,
                         float* ny, float* nz, float* curv);
 void normals_release(pfx_ctx* ctx);
+void normals_grid_launch_dev(pfx_ctx* ctx, const float* x, const float* y, const float* z, int64_t n, double r);
 void normals_launch_dev(pfx_ctx* ctx, const float* x, const float* y, const float* z, int64_t n, double r,
                         const float vp[3], float* nx, float* ny, float* nz, float* curv);
 bool normals_finish_dev(pfx_ctx* ctx);

@@ -75,6 +75,11 @@ struct NormalsState {
   uint64_t grid_gen = 0;  // grid_a's build that indexes (x, y, z, n, r) (pfx_normals_prepare_dev)
   // normals_launch_dev: the lists check still owed by normals_finish_dev, and the outputs to redo
   bool pending = false;
+  // normals_grid_launch_dev: grid_a build `grid_ahead_gen` queued for (x, n, r); 0: none
+  uint64_t grid_ahead_gen = 0;
+  const float* grid_ahead_x = nullptr;
+  int64_t grid_ahead_n = 0;
+  double grid_ahead_r = 0.0;
   float vp[3] = {0.f, 0.f, 0.f};
   float *nx = nullptr, *ny = nullptr, *nz = nullptr, *curv = nullptr;
 };

@@ -1445,6 +1445,11 @@ void build_lists(pfx_ctx* ctx, const Grid& G, const uint8_t* mask, double radius
           static_cast<uint32_t*>(hs.ptr), counters + 9);
       check_launch("nblist huge lists");
     };
+    if (ctx->lists_gate) {  // pfx_normals_gate_dev: the caller's event, once, right before the list kernels
+      // (after the list set-up above, which therefore overlaps the gated stage)
+      PFX_HIP(hipStreamWaitEvent(st, ctx->lists_gate, 0));
+      ctx->lists_gate = nullptr;
+    }
     {
       TimeScope ts(ctx, std::string(tag) + "_lists");
       {

@@ -660,13 +660,8 @@ __global__ void __launch_bounds__(256) k_normals_long(GridView g, NbLists L, con
 }  // namespace
 
 
-// pfx_normals_gate_dev: the caller's event, once, between the grid and the list kernels
-static void wait_lists_gate(pfx_ctx* ctx) {
-  if (!ctx->lists_gate) return;
-  hipEvent_t e = ctx->lists_gate;
-  ctx->lists_gate = nullptr;
-  PFX_HIP(hipStreamWaitEvent(ctx->stream, e, 0));
-}
+// pfx_normals_gate_dev: the caller's event is waited for inside build_lists, right before the
+// list kernels (after the list set-up)
 
 // The gate is borrowed for one normal-estimation call: whichever way the call ends (no points,
 // no list build, an error before the wait), the event is dropped with it, so no later call waits
@@ -708,7 +703,6 @@ void normals_lists_dev(pfx_ctx* ctx, const float* x, const float* y, const float
   build_grid(ctx, ctx->grid_a, x, y, z, n, r);
   k_nan_fill4<<<(unsigned)std::min<int64_t>(ceil_div(n, 256), 4096), 256, 0, st>>>(nx, ny, nz, curv, n);
   check_launch("k_nan_fill4");
-  wait_lists_gate(ctx);
   build_lists(ctx, ctx->grid_a, nullptr, r, true, ns.L, "normals");
   ctx->stats["normals_neighbors"] = ns.L.total;
   ctx->stats["normals_long_neighbors"] = ns.L.long_total;
@@ -831,10 +825,13 @@ bool normals_speculative_lists(pfx_ctx* ctx, const float* x, const float* y, con
   ns.r = r;
   ns.L = NbLists();
   TimeScope phase(ctx, "normals_lists_phase", true);
-  build_grid(ctx, ctx->grid_a, x, y, z, n, r, /*use_hint=*/true);
+  // (the grid queued ahead by normals_grid_launch_dev for this cloud and radius, else built here)
+  const bool ahead = ns.grid_ahead_gen != 0 && ns.grid_ahead_gen == ctx->grid_a.gen && ns.grid_ahead_x == x &&
+                     ns.grid_ahead_n == n && ns.grid_ahead_r == r;
+  ns.grid_ahead_gen = 0;
+  if (!ahead) build_grid(ctx, ctx->grid_a, x, y, z, n, r, /*use_hint=*/true);
   k_nan_fill4<<<(unsigned)std::min<int64_t>(ceil_div(n, 256), 4096), 256, 0, ctx->stream>>>(nx, ny, nz, curv, n);
   check_launch("k_nan_fill4");
-  wait_lists_gate(ctx);
   build_lists(ctx, ctx->grid_a, nullptr, r, true, ns.L, "normals", /*defer=*/true, /*want=*/1, /*compact=*/true);
   return true;
 }
@@ -916,6 +913,23 @@ bool normals_finish_dev(pfx_ctx* ctx) {
   ns->pending = false;
   const bool ok = build_lists_check(ctx, ctx->grid_a, ns->L, "normals");
   return normals_conclude(ctx, ok, ns->x, ns->y, ns->z, ns->n, ns->r, ns->vp, ns->nx, ns->ny, ns->nz, ns->curv);
+}
+
+// The speculative grid of the next normals_dev / normals_launch_dev of this cloud and radius,
+// queued now (no host wait once a previous build left its bounds hint): the caller can issue it
+// ahead of another stream's work and the estimation's list kernels after that work.
+void normals_grid_launch_dev(pfx_ctx* ctx, const float* x, const float* y, const float* z, int64_t n, double r) {
+  PFX_CHECK(r > 0.0, "normals: radius must be > 0");
+  PFX_CHECK(n >= 0, "normals: negative point count");
+  if (!ctx->normals) ctx->normals = new NormalsState();
+  NormalsState& ns = *ctx->normals;
+  ns.grid_ahead_gen = 0;
+  if (n == 0) return;
+  build_grid(ctx, ctx->grid_a, x, y, z, n, r, /*use_hint=*/true);
+  ns.grid_ahead_gen = ctx->grid_a.gen;
+  ns.grid_ahead_x = x;
+  ns.grid_ahead_n = n;
+  ns.grid_ahead_r = r;
 }
 
 // The grid of a subset estimation built ahead (it needs only the coordinates): the normal-estimation

@@ -253,12 +253,15 @@ def test_overlapped_shot_matches_sequential():
     assert bits_equal(f0, f1)
 
 
-@pytest.mark.parametrize("launch_first,prep_first", [(False, 2), (True, 0), (True, 1)])
-def test_launch_order_variants_match_default(launch_first, prep_first):
+@pytest.mark.parametrize("launch_first,prep_first,grid_first", [(False, 2, False), (True, 0, False), (True, 1, False),
+                                                                 (True, 2, True)])
+def test_launch_order_variants_match_default(launch_first, prep_first, grid_first):
     """OverlappedNarfFpfh's launch-order attributes (every selectable schedule
     pinned): the estimation issued by the worker thread instead of the caller (launch_first =
     False) and FPFH's surface grid queued after NARF (prep_first 0) or after the estimation's
-    launch (1) give the default schedule's keypoints, normals and descriptors bit for bit."""
+    launch (1), and the estimation's grid queued ahead of FPFH's rather than built inside its
+    launch (grid_first = True), give the default schedule's keypoints, normals and descriptors
+    bit for bit."""
     import torch
     from pcl_feature_extraction_amd import Context
     from pcl_feature_extraction_amd.pipeline import OverlappedNarfFpfh, alloc
@@ -267,14 +270,14 @@ def test_launch_order_variants_match_default(launch_first, prep_first):
     x, y, z, _ = synth_room(n, 25)
     dev = torch.device("cuda", 0)
     outs = []
-    for variant in (None, (launch_first, prep_first)):
+    for variant in (None, (launch_first, prep_first, grid_first)):
         b = alloc(torch, n, dev, max_keypoints=4096)
         b.x.copy_(torch.from_numpy(x)); b.y.copy_(torch.from_numpy(y)); b.z.copy_(torch.from_numpy(z))
         ctx, ctx_n = Context(0), Context(0)
         ctx.set_stream(torch.cuda.current_stream(dev).cuda_stream)
         run = OverlappedNarfFpfh(torch, ctx, ctx_n, dev)
         if variant is not None:
-            run.launch_first, run.prep_first = variant
+            run.launch_first, run.prep_first, run.grid_first = variant
         for _ in range(2):  # (the second pass reuses every buffer and the speculative grids)
             kp, k = run(b)
         run.check()
