@@ -1122,9 +1122,9 @@ __global__ void __launch_bounds__(256) k_nb_query(GridView g, const int32_t* __r
       s_base = arena_base;
       arena_base += need;
       arena_left -= need;
-      wg_total += need;
+      wg_total += (unsigned long long)k;  // (neighbours, not list words)
       if (k > kLongList) {
-        wg_long += need;
+        wg_long += (unsigned long long)k;
         ++wg_long_n;
       }
       out.off[j] = c16 ? 2 * (int64_t)s_base : (int64_t)s_base;

@@ -183,7 +183,8 @@ __device__ __forceinline__ void run_chain(At at_clamped, int k, Fetch fetch, flo
 
 #ifdef PFX_SHOT_PROFILE
 __device__ unsigned long long g_chain_prof[16];  // [0|8] prologue cycles, [1|9] wave chain cycles,
-                                                 // [2|10] sum of wave max k, [3|11] waves, [4|12] WGs
+                                                 // [2|10] sum of wave max k, [3|11] waves, [4|12] WGs,
+                                                 // [5|13] sum of the lanes' k
 #endif
 
 template <int CAP, bool DEFER>
@@ -367,9 +368,12 @@ __device__ __forceinline__ void chain_wg(ChainLds<CAP>& S, const GridView& g, co
     atomicAdd(&g_chain_prof[PO + 0], (unsigned long long)(pt1 - pt0));
     atomicAdd(&g_chain_prof[PO + 4], 1ull);
   }
-  int wk = (active && k <= lane_max) ? k : 0;
+  int wk = (active && k <= lane_max) ? k : 0, wsk = wk;
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) wk = max(wk, __shfl_xor(wk, o));
+  for (int o = 32; o > 0; o >>= 1) {
+    wk = max(wk, __shfl_xor(wk, o));
+    wsk += __shfl_xor(wsk, o);
+  }
   const uint64_t wm = __ballot(active && k == wk);
   const bool rec = wm && lane == __builtin_ctzll(wm);
 #endif
@@ -432,6 +436,7 @@ __device__ __forceinline__ void chain_wg(ChainLds<CAP>& S, const GridView& g, co
     atomicAdd(&g_chain_prof[PO + 1], (unsigned long long)(clock64() - pt1));
     atomicAdd(&g_chain_prof[PO + 2], (unsigned long long)wk);
     atomicAdd(&g_chain_prof[PO + 3], 1ull);
+    atomicAdd(&g_chain_prof[PO + 5], (unsigned long long)wsk);
   }
 #endif
 }
@@ -798,9 +803,9 @@ void normals_chains_dev(pfx_ctx* ctx, pfx_ctx* owner, const uint8_t* mask, int w
     PFX_HIP(hipMemcpyFromSymbol(pr, HIP_SYMBOL(g_chain_prof), sizeof(pr)));
     for (int b = 0; b < 16; b += 8)
       fprintf(stderr, "chain%s: WGs %llu prologue %.0f cyc/WG | waves %llu chain %.0f cyc/wave, max k %.1f/wave, "
-              "%.1f cyc/step\n", b ? "_big" : "", pr[b + 4], pr[b + 0] / (double)(pr[b + 4] + !pr[b + 4]), pr[b + 3],
+              "%.1f cyc/step, mean k %.1f/lane\n", b ? "_big" : "", pr[b + 4], pr[b + 0] / (double)(pr[b + 4] + !pr[b + 4]), pr[b + 3],
               pr[b + 1] / (double)(pr[b + 3] + !pr[b + 3]), pr[b + 2] / (double)(pr[b + 3] + !pr[b + 3]),
-              pr[b + 1] / (double)(pr[b + 2] + !pr[b + 2]));
+              pr[b + 1] / (double)(pr[b + 2] + !pr[b + 2]), pr[b + 5] / 64.0 / (double)(pr[b + 3] + !pr[b + 3]));
     const unsigned long long z[16] = {};
     PFX_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_chain_prof), z, sizeof(z)));
   }

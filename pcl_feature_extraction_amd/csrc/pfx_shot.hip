@@ -18,6 +18,19 @@
 namespace pfx {
 namespace {
 
+#ifdef PFX_SHOT_PROFILE
+// phase cycles of k_shot_hist (thread 0 of each workgroup): [0] frame, [1] updates + masks,
+// [2] offsets, [3] scatter, [4] bin sums, [5] normalisation + output, [6] queries
+// [7] sequential normalisations, [8] normalisation cycles, [9] set-up before the first chunk
+// k_shot_lrf: [10] search + sort, [11] records, [12] LRF chains, [13] queries
+__device__ unsigned long long g_shot_prof[16];
+#define SPROF_T(v) long long v = (threadIdx.x == 0) ? clock64() : 0
+#define SPROF_ADD(i, a, b) if (threadIdx.x == 0) atomicAdd(&g_shot_prof[i], (unsigned long long)((b) - (a)))
+#else
+#define SPROF_T(v)
+#define SPROF_ADD(i, a, b)
+#endif
+
 constexpr int kCapSmall = 2048;  // sorted-neighbour capacity of the first pass (LDS keys, 5 WG/CU)
 constexpr int kCap = 16384;      // second pass for the longer lists (1 WG/CU)
 constexpr int kChunk = 256;   // neighbours staged per chunk
@@ -132,7 +145,7 @@ struct ShotLds {
       float val[5 * kChunk];            // the chunk's update values bucketed by bin, neighbour order
     } upd;
   };
-  float hist[kLen];
+  alignas(16) float hist[kLen];
   double cov[10];
   double axes[6];  // v1 (x axis), v3 (z axis)
   int lrf_l[4];    // normalisation: per-wave smallest lsb exponent and largest square
@@ -143,63 +156,84 @@ struct ShotLds {
 
 // ---- the phases of one query, shared by the fused and the split kernels ----
 
-// A neighbour key's point: by caller index (the fused kernel) or, POS, by cell-sorted position --
-// the split kernels convert their keys once (ipos), after which every coordinate and normal of a
-// neighbourhood comes from a few contiguous runs (one float4 each) instead of six caller-order
-// gathers.
-template <bool POS>
-__device__ __forceinline__ float3 key_xyz(const GridView& g, int32_t p) {
-  if (POS) {
-    const float4 c = g.sp[p];
-    return make_float3(c.x, c.y, c.z);
+// A query's neighbour j for the frame and the histogram: its offset from the query (the float
+// subtraction PCL's `delta` is) with its d2, and its normal.  NbKeys: from the FLANN keys and the
+// caller-order arrays (the fused kernel); NbRecs: from the records k_shot_lrf writes (one float4
+// of offset + d2 and one of normal per neighbour, two planes of kCapSmall per query), so the
+// split kernels read a neighbour with one coalesced load instead of a key, then its point.
+struct NbKeys {
+  const uint64_t* keys;
+  const float *ux, *uy, *uz, *nx, *ny, *nz;
+  float cx, cy, cz;
+  __device__ __forceinline__ float4 pt(int j) const {
+    const uint64_t key = keys[j];
+    const int32_t p = key_idx(key);
+    return make_float4(ux[p] - cx, uy[p] - cy, uz[p] - cz, key_d2(key));
   }
-  return make_float3(g.ux[p], g.uy[p], g.uz[p]);
-}
+  __device__ __forceinline__ float3 nrm(int j) const {
+    const int32_t p = key_idx(keys[j]);
+    return make_float3(nx[p], ny[p], nz[p]);
+  }
+};
+struct NbRecs {
+  const float4* __restrict__ pts;   // {dx, dy, dz, d2}
+  const float4* __restrict__ nrms;  // {nx, ny, nz, 0}
+  __device__ __forceinline__ float4 pt(int j) const { return pts[j]; }
+  __device__ __forceinline__ float3 nrm(int j) const {
+    const float4 v = nrms[j];
+    return make_float3(v.x, v.y, v.z);
+  }
+};
+// (a copy of the query: a zero offset -- a difference of finite floats is zero only when they are
+// equal)
+__device__ __forceinline__ bool nb_self(const float4& c) { return c.x == 0.0f && c.y == 0.0f && c.z == 0.0f; }
 
 // SHOTLocalReferenceFrameEstimation's weighted double covariance over keys[0..k): S.cov (3x3
 // row-major + the weight sum at [9]), S.n_invalid (copies of the query), S.zero_prefix.
 // Every thread forms its neighbour's chain terms dist * (v_a * v_b) and dist exactly as the
 // reference loop does; lanes 0..6 then add them in neighbour order (the only sequential part).
 // An invalid neighbour (a copy of the query) contributes +0.0, which leaves a chain unchanged.
-template <bool POS, class Lds>
-__device__ __forceinline__ void shot_lrf(Lds& S, const GridView& g, const uint64_t* keys, int k, float cx,
-                                         float cy, float cz, double radius) {
+template <class Lds, class Src>
+__device__ __forceinline__ void shot_lrf(Lds& S, double (*lrf)[kChunk], const Src& src, int k, double radius) {
   const int tid = threadIdx.x;
   if (tid == 0) {
     S.n_invalid = 0; S.zero_prefix = 0; S.plusT = 0; S.plusN = 0;
   }
   double acc = 0.0;
+  // the next chunk's neighbour is loaded while lanes 0..6 sum the current one
+  float4 c_n = tid < k ? src.pt(tid) : make_float4(0.f, 0.f, 0.f, 0.f);
   for (int c0 = 0; c0 < k; c0 += kChunk) {
     const int m = min(kChunk, k - c0);
+    const float4 c = c_n;
+    if (c0 + kChunk + tid < k) c_n = src.pt(c0 + kChunk + tid);
     __syncthreads();
     if (tid < m) {
-      const uint64_t key = keys[c0 + tid];
-      const float3 c3 = key_xyz<POS>(g, key_idx(key));
-      const float px = c3.x, py = c3.y, pz = c3.z;
-      const bool valid = !(px == cx && py == cy && pz == cz);
-      const double vx = (double)(px - cx), vy = (double)(py - cy), vz = (double)(pz - cz);
-      const double dist = radius - sqrt((double)key_d2(key));
-      S.lrf[0][tid] = valid ? dist * (vx * vx) : 0.0;
-      S.lrf[1][tid] = valid ? dist * (vx * vy) : 0.0;
-      S.lrf[2][tid] = valid ? dist * (vx * vz) : 0.0;
-      S.lrf[3][tid] = valid ? dist * (vy * vy) : 0.0;
-      S.lrf[4][tid] = valid ? dist * (vy * vz) : 0.0;
-      S.lrf[5][tid] = valid ? dist * (vz * vz) : 0.0;
-      S.lrf[6][tid] = valid ? dist : 0.0;
+      const bool valid = !nb_self(c);
+      const double vx = (double)c.x, vy = (double)c.y, vz = (double)c.z;
+      const double dist = radius - sqrt((double)c.w);
+      lrf[0][tid] = valid ? dist * (vx * vx) : 0.0;
+      lrf[1][tid] = valid ? dist * (vx * vy) : 0.0;
+      lrf[2][tid] = valid ? dist * (vx * vz) : 0.0;
+      lrf[3][tid] = valid ? dist * (vy * vy) : 0.0;
+      lrf[4][tid] = valid ? dist * (vy * vz) : 0.0;
+      lrf[5][tid] = valid ? dist * (vz * vz) : 0.0;
+      lrf[6][tid] = valid ? dist : 0.0;
       if (!valid) atomicAdd(&S.n_invalid, 1);
-      if (key_d2(key) == 0.0f) atomicAdd(&S.zero_prefix, 1);
+      if (c.w == 0.0f) atomicAdd(&S.zero_prefix, 1);
     }
     __syncthreads();
-    if (tid < kChains) {
-      const double* row = S.lrf[tid];
+    if (tid < kChains) {  // (32 terms loaded per round: one LDS latency per 32 dependent adds)
+      const double* row = lrf[tid];
       int t = 0;
-      for (; t + 8 <= m; t += 8) {
-        const double2 a = *reinterpret_cast<const double2*>(row + t);
-        const double2 b = *reinterpret_cast<const double2*>(row + t + 2);
-        const double2 c = *reinterpret_cast<const double2*>(row + t + 4);
-        const double2 e = *reinterpret_cast<const double2*>(row + t + 6);
-        acc = acc + a.x; acc = acc + a.y; acc = acc + b.x; acc = acc + b.y;
-        acc = acc + c.x; acc = acc + c.y; acc = acc + e.x; acc = acc + e.y;
+      for (; t + 32 <= m; t += 32) {
+        double2 v[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) v[u] = *reinterpret_cast<const double2*>(row + t + 2 * u);
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+          acc = acc + v[u].x;
+          acc = acc + v[u].y;
+        }
       }
       for (; t < m; ++t) acc = acc + row[t];
     }
@@ -227,21 +261,27 @@ __device__ __forceinline__ bool shot_eigen(const double cov[10], int valid, doub
 }
 
 // sign disambiguation of S.axes over the valid neighbours, then S.rf (x, y = z cross x, z)
-template <bool POS>
-__device__ __forceinline__ void shot_frame(ShotLds& S, const GridView& g, const uint64_t* keys, int k, int valid,
-                                           float cx, float cy, float cz) {
+template <class Src>
+__device__ __forceinline__ void shot_frame(ShotLds& S, const Src& src, int k, int valid) {
   const int tid = threadIdx.x, lane = tid & 63;
   {
     const double v1x = S.axes[0], v1y = S.axes[1], v1z = S.axes[2];
     const double v3x = S.axes[3], v3y = S.axes[4], v3z = S.axes[5];
     int cT = 0, cN = 0;
-    for (int j = tid; j < k; j += 256) {
-      const float3 c3 = key_xyz<POS>(g, key_idx(keys[j]));
-      const float px = c3.x, py = c3.y, pz = c3.z;
-      if (px == cx && py == cy && pz == cz) continue;
-      const double vx = (double)(px - cx), vy = (double)(py - cy), vz = (double)(pz - cz);
-      if (((vx * v1x + vy * v1y) + vz * v1z) + 0.0 >= 0) ++cT;
-      if (((vx * v3x + vy * v3y) + vz * v3z) + 0.0 >= 0) ++cN;
+    for (int j0 = tid; j0 < k; j0 += 4 * 256) {  // (four neighbours per thread in flight)
+      float4 c[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int j = j0 + 256 * u;
+        c[u] = src.pt(j < k ? j : j0);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if (j0 + 256 * u >= k || nb_self(c[u])) continue;
+        const double vx = (double)c[u].x, vy = (double)c[u].y, vz = (double)c[u].z;
+        if (((vx * v1x + vy * v1y) + vz * v1z) + 0.0 >= 0) ++cT;
+        if (((vx * v3x + vy * v3y) + vz * v3z) + 0.0 >= 0) ++cN;
+      }
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) { cT += __shfl_xor(cT, o); cN += __shfl_xor(cN, o); }
@@ -254,10 +294,8 @@ __device__ __forceinline__ void shot_frame(ShotLds& S, const GridView& g, const 
     // the valid neighbours in order: the d2 == 0 prefix holds every invalid one
     const int zp = S.zero_prefix;
     int valid_in_prefix = 0;
-    for (int j = 0; j < zp; ++j) {
-      const float3 c3 = key_xyz<POS>(g, key_idx(keys[j]));
-      if (!(c3.x == cx && c3.y == cy && c3.z == cz)) ++valid_in_prefix;
-    }
+    for (int j = 0; j < zp; ++j)
+      if (!nb_self(src.pt(j))) ++valid_in_prefix;
     for (int w = 0; w < 2; ++w) {
       int plus = 2 * counts[w] - valid;
       if (plus == 0) {
@@ -267,15 +305,13 @@ __device__ __forceinline__ void shot_frame(ShotLds& S, const GridView& g, const 
           int j;
           if (ne < valid_in_prefix) {
             int seen = -1;
-            for (j = 0; j < zp; ++j) {
-              const float3 c3 = key_xyz<POS>(g, key_idx(keys[j]));
-              if (!(c3.x == cx && c3.y == cy && c3.z == cz) && ++seen == ne) break;
-            }
+            for (j = 0; j < zp; ++j)
+              if (!nb_self(src.pt(j)) && ++seen == ne) break;
           } else {
             j = zp + (ne - valid_in_prefix);
           }
-          const float3 c3 = key_xyz<POS>(g, key_idx(keys[j]));
-          const double vx = (double)(c3.x - cx), vy = (double)(c3.y - cy), vz = (double)(c3.z - cz);
+          const float4 c = src.pt(j);
+          const double vx = (double)c.x, vy = (double)c.y, vz = (double)c.z;
           if (((vx * ax[w][0] + vy * ax[w][1]) + vz * ax[w][2]) + 0.0 > 0) ++plus;
         }
         if (plus < 3)
@@ -303,12 +339,8 @@ __device__ __forceinline__ int lsb_exp_f(float v) {
 }
 
 // the SHOT histogram from S.rf, normalizeHistogram, outputs
-// (POS: the normals come from snp, the cell-sorted float4 copy; else nx/ny/nz by caller index)
-template <bool POS>
-__device__ __forceinline__ void shot_hist(ShotLds& S, const GridView& g, const uint64_t* keys, int k, float cx,
-                                          float cy, float cz, const float* __restrict__ nx,
-                                          const float* __restrict__ ny, const float* __restrict__ nz,
-                                          const float4* __restrict__ snp, double radius, float* __restrict__ d,
+template <class Src>
+__device__ __forceinline__ void shot_hist(ShotLds& S, const Src& src, int k, double radius, float* __restrict__ d,
                                           float* __restrict__ rfo) {
   const int tid = threadIdx.x, lane = tid & 63;
   // Bin ownership for the histogram: thread j accumulates bins j and j + 256 in registers.
@@ -323,30 +355,44 @@ __device__ __forceinline__ void shot_hist(ShotLds& S, const GridView& g, const u
   // so PCL's sequential order restricted to one bin is neighbour order.  Per chunk: hit masks
   // per bin -> counts -> offsets -> every update written to its bin's bucket at its rank among
   // the bin's hits (a stable counting sort) -> each bin's owner adds its bucket in order.
+  // a neighbour's offset + d2 and normal: the next chunk's are loaded while this one's updates
+  // are binned
+  SPROF_T(ps0);
+  float4 c_n = make_float4(0.f, 0.f, 0.f, 0.f);
+  float3 nv_n = make_float3(0.f, 0.f, 0.f);
+  if (tid < k) {
+    c_n = src.pt(tid);
+    nv_n = src.nrm(tid);
+  }
+#ifdef PFX_SHOT_PROFILE
+  bool first_chunk = true;
+#endif
   for (int c0 = 0; c0 < k; c0 += kChunk) {
     const int m = min(kChunk, k - c0);
     int bins[5];
     float vals[5];
 #pragma unroll
     for (int s = 0; s < 5; ++s) bins[s] = -1;
+    const float4 c = c_n;
+    const float3 nv = nv_n;
+    if (c0 + kChunk + tid < k) {
+      c_n = src.pt(c0 + kChunk + tid);
+      nv_n = src.nrm(c0 + kChunk + tid);
+    }
+    SPROF_T(ph0);
+#ifdef PFX_SHOT_PROFILE
+    if (first_chunk) SPROF_ADD(9, ps0, ph0);
+    first_chunk = false;
+#endif
     if (tid < m) {
-      const uint64_t key = keys[c0 + tid];
-      const int32_t p = key_idx(key);
-      float pnx, pny, pnz;
-      if (POS) {
-        const float4 nv = snp[p];
-        pnx = nv.x; pny = nv.y; pnz = nv.z;
-      } else {
-        pnx = nx[p]; pny = ny[p]; pnz = nz[p];
-      }
-      const double distance = sqrt((double)key_d2(key));
+      const float pnx = nv.x, pny = nv.y, pnz = nv.z;
+      const double distance = sqrt((double)c.w);
       if (isfinite(pnx) && isfinite(pny) && isfinite(pnz) && !(fabs(distance - 0.0) < 1E-15)) {
         double cosd = dot4(mk3(pnx, pny, pnz), fz);
         if (cosd > 1.0) cosd = 1.0;
         if (cosd < -1.0) cosd = -1.0;
         const double binDist = ((1.0 + cosd) * kBins) / 2;
-        const float3 c3 = key_xyz<POS>(g, p);
-        const f3 delta = mk3(c3.x - cx, c3.y - cy, c3.z - cz);
+        const f3 delta = mk3(c.x, c.y, c.z);
         shot_updates(delta, distance, binDist, fx, fy, fz, radius, bins, vals);
       }
       const uint64_t bit = 1ull << (tid & 63);
@@ -355,6 +401,8 @@ __device__ __forceinline__ void shot_hist(ShotLds& S, const GridView& g, const u
         if (bins[s] >= 0) atomicOr(reinterpret_cast<unsigned long long*>(&S.upd.mask[bins[s]][tid >> 6]), bit);
     }
     __syncthreads();
+    SPROF_T(ph1);
+    SPROF_ADD(1, ph0, ph1);
     // hit counts -> exclusive offsets (wave 0: 6 bins per lane, then a wave scan)
     if (tid < 64) {
       int c[6], tot = 0;
@@ -381,6 +429,8 @@ __device__ __forceinline__ void shot_hist(ShotLds& S, const GridView& g, const u
       }
     }
     __syncthreads();
+    SPROF_T(ph2);
+    SPROF_ADD(2, ph1, ph2);
     if (tid < m) {  // scatter: rank = hits of the bin from lower neighbours of the chunk
       const int wq = tid >> 6;
       const uint64_t below = lanemask_lt();
@@ -394,6 +444,8 @@ __device__ __forceinline__ void shot_hist(ShotLds& S, const GridView& g, const u
       }
     }
     __syncthreads();
+    SPROF_T(ph3);
+    SPROF_ADD(3, ph2, ph3);
 #pragma unroll
     for (int o = 0; o < 2; ++o) {
       const int b = o ? b1 : b0;
@@ -415,7 +467,10 @@ __device__ __forceinline__ void shot_hist(ShotLds& S, const GridView& g, const u
       }
     }
     __syncthreads();
+    SPROF_T(ph4);
+    SPROF_ADD(4, ph3, ph4);
   }
+  SPROF_T(pe0);
   S.hist[b0] = h0;
   if (b1 < kLen) S.hist[b1] = h1;
   __syncthreads();
@@ -455,12 +510,29 @@ __device__ __forceinline__ void shot_hist(ShotLds& S, const GridView& g, const u
         acc_norm = tot;
       } else {
         acc_norm = 0;
-        for (int j = 0; j < kLen; ++j) acc_norm += S.hist[j] * S.hist[j];
+        // (PCL's order; the squares read 16 at a time, so only the additions are sequential)
+        for (int j = 0; j < kLen; j += 16) {
+          float4 v[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const float4*>(S.hist + j + 4 * u);
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            acc_norm += v[u].x * v[u].x;
+            acc_norm += v[u].y * v[u].y;
+            acc_norm += v[u].z * v[u].z;
+            acc_norm += v[u].w * v[u].w;
+          }
+        }
+#ifdef PFX_SHOT_PROFILE
+        atomicAdd(&g_shot_prof[7], 1ull);
+#endif
       }
       S.cov[0] = sqrt(acc_norm);
     }
     __syncthreads();
   }
+  SPROF_T(pe1);
+  SPROF_ADD(8, pe0, pe1);
   const float nrm = (float)S.cov[0];
   for (int i = tid; i < kLen; i += 256) d[i] = S.hist[i] / nrm;
   if (tid < 9) rfo[tid] = S.rf[tid];
@@ -511,7 +583,8 @@ __global__ void __launch_bounds__(256) k_shot(GridView g, const float* __restric
       continue;
     }
     if (tid == 0) atomicAdd(nbr, (unsigned long long)k);
-    shot_lrf<false>(S, g, keys, k, cx, cy, cz, radius);
+    const NbKeys src{keys, g.ux, g.uy, g.uz, nx, ny, nz, cx, cy, cz};
+    shot_lrf(S, S.lrf, src, k, radius);
     const int valid = k - S.n_invalid;
     if (tid == 0) {
       double cov[10], axes[6];
@@ -524,8 +597,8 @@ __global__ void __launch_bounds__(256) k_shot(GridView g, const float* __restric
       shot_nan(d, rfo);
       continue;
     }
-    shot_frame<false>(S, g, keys, k, valid, cx, cy, cz);
-    shot_hist<false>(S, g, keys, k, cx, cy, cz, nx, ny, nz, nullptr, radius, d, rfo);
+    shot_frame(S, src, k, valid);
+    shot_hist(S, src, k, radius, d, rfo);
   }
 }
 
@@ -550,21 +623,22 @@ struct ShotQuery {
   int k, n_invalid, zero_prefix, status;
 };
 
-// the LDS of the LRF phase alone (kernel A: three workgroups per CU beside the sort's keys)
+// the LDS of the LRF phase alone (kernel A; its chain terms live in the sort's scratch half of
+// the keys, free once the keys are sorted: 34 KB a workgroup, four per CU)
 struct LrfLds {
-  double lrf[kChains][kChunk];
   double cov[10];
   int n_invalid, zero_prefix, plusT, plusN;
 };
 
-// A: sort + LRF covariance, keys kept in global memory (stride kCapSmall)
+// A: sort + LRF covariance; the neighbour records (NbRecs: offset + d2, normal) kept in global
+// memory for C (two planes of kCapSmall float4 per query)
 __global__ void __launch_bounds__(256) k_shot_lrf(GridView g, const float* __restrict__ qx,
                                                   const float* __restrict__ qy, const float* __restrict__ qz,
                                                   int64_t base, int64_t nq, int32_t* __restrict__ over,
                                                   int* __restrict__ n_over,
                                                   double radius, float* __restrict__ desc, float* __restrict__ rf_out,
-                                                  uint64_t* __restrict__ gkeys, ShotQuery* __restrict__ sq,
-                                                  const int32_t* __restrict__ ipos,
+                                                  float4* __restrict__ grec, ShotQuery* __restrict__ sq,
+                                                  const int32_t* __restrict__ ipos, const float4* __restrict__ snp,
                                                   unsigned long long* __restrict__ nbr) {
   extern __shared__ __attribute__((aligned(16))) uint64_t keys[];  // kCapSmall + kCapSmall scratch
   __shared__ LrfLds S;
@@ -580,6 +654,7 @@ __global__ void __launch_bounds__(256) k_shot_lrf(GridView g, const float* __res
       if (tid == 0) sq[l].status = 1;
       continue;
     }
+    SPROF_T(l0);
     const int k = sorted_neighbors_bucketed(g, cx, cy, cz, rr, keys, keys + kCapSmall, kCapSmall, &s_count, SB);
     if (k > kCapSmall) {
       if (tid == 0) {
@@ -589,16 +664,43 @@ __global__ void __launch_bounds__(256) k_shot_lrf(GridView g, const float* __res
       continue;
     }
     if (tid == 0) atomicAdd(nbr, (unsigned long long)k);
-    // keys (d2, caller index) in FLANN order -> (d2, cell-sorted position), same order
-    uint64_t* gk = gkeys + l * kCapSmall;
-    for (int i = tid; i < k; i += 256) {
-      const uint64_t key = keys[i];
-      const uint64_t pk = (key & 0xffffffff00000000ull) | (uint32_t)ipos[key_idx(key)];
-      keys[i] = pk;
-      gk[i] = pk;
+    SPROF_T(l1);
+    SPROF_ADD(10, l0, l1);
+    SPROF_ADD(13, 0, 1);
+    // the keys (d2, caller index) in FLANN order -> the neighbour records, same order (read back
+    // by this thread in shot_lrf, and by the frame and histogram kernel)
+    // (four neighbours per thread in flight: two dependent global rounds for the whole list)
+    float4* rp = grec + l * 2 * kCapSmall;
+    for (int i0 = tid; i0 < k; i0 += 4 * 256) {
+      uint64_t key[4];
+      int32_t pos[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        key[u] = keys[min(i0 + 256 * u, k - 1)];
+        pos[u] = ipos[key_idx(key[u])];
+      }
+      float4 c[4], nv[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        c[u] = g.sp[pos[u]];
+        nv[u] = snp[pos[u]];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int i = i0 + 256 * u;
+        if (i < k) {
+          rp[i] = make_float4(c[u].x - cx, c[u].y - cy, c[u].z - cz, key_d2(key[u]));
+          rp[kCapSmall + i] = make_float4(nv[u].x, nv[u].y, nv[u].z, 0.0f);
+        }
+      }
     }
     __syncthreads();
-    shot_lrf<true>(S, g, keys, k, cx, cy, cz, radius);
+    SPROF_T(l2);
+    SPROF_ADD(11, l1, l2);
+    static_assert(sizeof(double) * kChains * kChunk <= sizeof(uint64_t) * kCapSmall, "chain terms fit the sort scratch");
+    shot_lrf(S, reinterpret_cast<double(*)[kChunk]>(keys + kCapSmall), NbRecs{rp, rp + kCapSmall}, k, radius);
+    SPROF_T(l3);
+    SPROF_ADD(12, l2, l3);
     if (tid < 10) sq[l].cov[tid] = S.cov[tid];
     if (tid == 0) {
       sq[l].k = k;
@@ -629,15 +731,12 @@ __global__ void __launch_bounds__(64) k_shot_eigen(ShotQuery* __restrict__ sq, i
 #ifndef PFX_SHOT_HIST_WG
 #define PFX_SHOT_HIST_WG 3
 #endif
-__global__ void __launch_bounds__(256, PFX_SHOT_HIST_WG) k_shot_hist(GridView g, const float* __restrict__ nx,
-                                                   const float* __restrict__ ny, const float* __restrict__ nz,
-                                                   const float* __restrict__ qx, const float* __restrict__ qy,
-                                                   const float* __restrict__ qz, int64_t base, int64_t nq,
-                                                   double radius, float* __restrict__ desc,
-                                                   float* __restrict__ rf_out, const uint64_t* __restrict__ gkeys,
-                                                   const ShotQuery* __restrict__ sq,
-                                                   const float4* __restrict__ snp) {
-  __shared__ ShotLds S;  // (the keys are read from global memory: eight workgroups per CU)
+__global__ void __launch_bounds__(256, PFX_SHOT_HIST_WG) k_shot_hist(int64_t base, int64_t nq, double radius,
+                                                                      float* __restrict__ desc,
+                                                                      float* __restrict__ rf_out,
+                                                                      const float4* __restrict__ grec,
+                                                                      const ShotQuery* __restrict__ sq) {
+  __shared__ ShotLds S;  // (the neighbour records are read from global memory)
   const int tid = threadIdx.x;
   for (int64_t l = blockIdx.x; l < nq; l += gridDim.x) {
     const int64_t q = base + l;
@@ -650,7 +749,7 @@ __global__ void __launch_bounds__(256, PFX_SHOT_HIST_WG) k_shot_hist(GridView g,
       continue;
     }
     const int k = sq[l].k;
-    const uint64_t* keys = gkeys + l * kCapSmall;
+    const NbRecs src{grec + l * 2 * kCapSmall, grec + l * 2 * kCapSmall + kCapSmall};
     if (tid < 6) S.axes[tid] = sq[l].axes[tid];
     if (tid == 0) {
       S.zero_prefix = sq[l].zero_prefix;
@@ -658,8 +757,14 @@ __global__ void __launch_bounds__(256, PFX_SHOT_HIST_WG) k_shot_hist(GridView g,
       S.plusN = 0;
     }
     __syncthreads();
-    shot_frame<true>(S, g, keys, k, k - sq[l].n_invalid, qx[q], qy[q], qz[q]);
-    shot_hist<true>(S, g, keys, k, qx[q], qy[q], qz[q], nx, ny, nz, snp, radius, d, rfo);
+    SPROF_T(f0);
+    shot_frame(S, src, k, k - sq[l].n_invalid);
+    SPROF_T(f1);
+    SPROF_ADD(0, f0, f1);
+    shot_hist(S, src, k, radius, d, rfo);
+    SPROF_T(f2);
+    SPROF_ADD(5, f1, f2);
+    SPROF_ADD(6, 0, 1);
   }
 }
 
@@ -703,7 +808,7 @@ void shot_dev(pfx_ctx* ctx, const float* sx, const float* sy, const float* sz, c
     {
       constexpr int64_t kSplitBatch = 16384;
       const int64_t bq = std::min<int64_t>(nq, kSplitBatch);
-      uint64_t* gkeys = ctx->buf("shot_keys").as<uint64_t>((size_t)bq * kCapSmall);
+      float4* grec = ctx->buf("shot_recs").as<float4>((size_t)bq * 2 * kCapSmall);
       ShotQuery* sq = ctx->buf("shot_q").as<ShotQuery>((size_t)bq);
       int32_t* ipos = ctx->buf("shot_ipos").as<int32_t>(ns);
       float4* snp = ctx->buf("shot_snp").as<float4>(ns);
@@ -711,10 +816,9 @@ void shot_dev(pfx_ctx* ctx, const float* sx, const float* sy, const float* sz, c
       for (int64_t q0 = 0; q0 < nq; q0 += kSplitBatch) {
         const int64_t m = std::min<int64_t>(kSplitBatch, nq - q0);
         const unsigned bl = (unsigned)std::min<int64_t>(m, 256 * 10);
-        k_shot_lrf<<<bl, 256, lds_s, st>>>(g, qx, qy, qz, q0, m, over, n_over, r, desc, rf, gkeys, sq, ipos, nbr);
+        k_shot_lrf<<<bl, 256, lds_s, st>>>(g, qx, qy, qz, q0, m, over, n_over, r, desc, rf, grec, sq, ipos, snp, nbr);
         k_shot_eigen<<<(unsigned)ceil_div(m, 64), 64, 0, st>>>(sq, m);
-        k_shot_hist<<<(unsigned)std::min<int64_t>(m, 256 * 16), 256, 0, st>>>(g, snx, sny, snz, qx, qy, qz, q0, m, r,
-                                                                           desc, rf, gkeys, sq, snp);
+        k_shot_hist<<<(unsigned)std::min<int64_t>(m, 256 * 16), 256, 0, st>>>(q0, m, r, desc, rf, grec, sq);
       }
     }
     // longer lists: grid sized for the worst case, the count stays on the device
@@ -728,6 +832,19 @@ void shot_dev(pfx_ctx* ctx, const float* sx, const float* sy, const float* sz, c
   PFX_HIP(hipMemcpyAsync(&h_nbr, nbr, sizeof(h_nbr), hipMemcpyDeviceToHost, st));
   PFX_HIP(hipStreamSynchronize(st));
   ctx->stats["shot_neighbors"] = (int64_t)h_nbr;
+#ifdef PFX_SHOT_PROFILE
+  {
+    unsigned long long pr[16];
+    PFX_HIP(hipMemcpyFromSymbol(pr, HIP_SYMBOL(g_shot_prof), sizeof(pr)));
+    const double nq_ = (double)(pr[6] + !pr[6]);
+    fprintf(stderr, "shot_hist cycles/query: frame %.0f setup %.0f updates %.0f offsets %.0f scatter %.0f sums %.0f norm %.0f | hist total %.0f (%llu queries, %llu sequential norms)\n",
+            pr[0] / nq_, pr[9] / nq_, pr[1] / nq_, pr[2] / nq_, pr[3] / nq_, pr[4] / nq_, pr[8] / nq_, pr[5] / nq_, pr[6], pr[7]);
+    fprintf(stderr, "shot_lrf cycles/query: search+sort %.0f records %.0f chains %.0f\n", pr[10] / (double)(pr[13] + !pr[13]),
+            pr[11] / (double)(pr[13] + !pr[13]), pr[12] / (double)(pr[13] + !pr[13]));
+    const unsigned long long z[16] = {};
+    PFX_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_shot_prof), z, sizeof(z)));
+  }
+#endif
   if (h > 0)
     throw Error(PFX_ERR_CAPACITY, "shot: a query has " + std::to_string(h) + " neighbours (> " +
                                       std::to_string(kCap) + " supported)");

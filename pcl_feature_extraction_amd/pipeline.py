@@ -109,6 +109,11 @@ class OverlappedNarfFpfh:
         # the normal stage gains 0.08 ms, the step loses 0.15 ms to NARF and FPFH's grid queued
         # behind it), so off; pinned by tests/test_gpu_pipeline.py
         self.grid_first = False
+        # shot(): the SHOT surface grid queued before the normal estimation, whose list kernels then
+        # wait for it (pfx_normals_gate_dev), instead of after NARF (where its radix sort runs beside
+        # the persistent list kernels, ~0.85 ms instead of ~0.03).  Measured (r05, 2 runs each):
+        # 197.0 / 198.2 vs 198.2 / 199.5 Mpoints/s, so off; pinned by tests/test_gpu_pipeline.py
+        self.shot_prep_first = False
         self._support = None
 
     def __call__(self, b: ScanBuffers, normal_radius: float = 0.05, feat_radius: float = 0.08, params=None,
@@ -273,6 +278,11 @@ class OverlappedNarfFpfh:
                 launched.set()
             return self.ctx_side.normals_finish_dev()
 
+        if self.shot_prep_first:
+            self.ctx.fpfh_prepare_dev(b.x, b.y, b.z, feat_radius)
+            gate = torch.cuda.Event()
+            gate.record(self.s_main)
+            self.ctx_side.normals_gate_dev(gate)
         fut = self.pool.submit(est, b.x, b.y, b.z, normal_radius, b.nx, b.ny, b.nz, b.curv)
 
         def run_shot():
@@ -289,7 +299,8 @@ class OverlappedNarfFpfh:
                 torch.index_select(b.x, 0, sample, out=s.qx[k:k + m])
                 torch.index_select(b.y, 0, sample, out=s.qy[k:k + m])
                 torch.index_select(b.z, 0, sample, out=s.qz[k:k + m])
-            self.ctx.fpfh_prepare_dev(b.x, b.y, b.z, feat_radius)
+            if not self.shot_prep_first:
+                self.ctx.fpfh_prepare_dev(b.x, b.y, b.z, feat_radius)
             rows = k + m
             launched.wait()
             self.s_main.wait_event(ev)

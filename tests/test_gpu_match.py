@@ -116,5 +116,10 @@ def test_match_pair_list_overflow(ctx):
     base = shot_like(rng, 2)
     src = base[rng.integers(0, 2, 2000)]
     tgt = base[rng.integers(0, 2, 2000)]
+    _gpu_nearest(ctx, src, tgt)
+    # (the emission count saturates just past the cap once the list has overflowed)
+    assert ctx.stat("match_pair_cap") == 64 * (len(src) + len(tgt)) + 65536
+    assert ctx.stat("match_pairs_emitted") > ctx.stat("match_pair_cap")
     _check(ctx, src, tgt)
-    assert ctx.stat("match_pairs_emitted") > 64 * (len(src) + len(tgt)) + 65536
+    # (the correspondences' second call goes straight to the two-contraction path: cap 0)
+    assert ctx.stat("match_pairs_emitted") > ctx.stat("match_pair_cap")

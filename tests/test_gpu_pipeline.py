@@ -220,9 +220,11 @@ def test_split_check_pass_matches_default_with_reruns():
         assert bits_equal(d0, d1)
 
 
-def test_overlapped_shot_matches_sequential():
+@pytest.mark.parametrize("shot_prep_first", [True, False])
+def test_overlapped_shot_matches_sequential(shot_prep_first):
     """OverlappedNarfFpfh.shot (normals on the side stream beside NARF, SHOT's surface grid
-    prepared ahead) == pipeline.narf_shot on one stream, descriptors and frames bit for bit."""
+    prepared ahead: before the estimation, its list kernels gated on it, or after NARF) ==
+    pipeline.narf_shot on one stream, descriptors and frames bit for bit."""
     import torch
     from pcl_feature_extraction_amd import Context
     from pcl_feature_extraction_amd.pipeline import OverlappedNarfFpfh, alloc, alloc_shot, narf_shot
@@ -240,6 +242,7 @@ def test_overlapped_shot_matches_sequential():
         ctx.set_stream(torch.cuda.current_stream(dev).cuda_stream)
         if overlapped:
             run = OverlappedNarfFpfh(torch, ctx, ctx_n, dev)
+            run.shot_prep_first = shot_prep_first
             rows = run.shot(b, s, sample)
             run.close()
         else:
