@@ -78,6 +78,33 @@ __device__ __forceinline__ void rec_unpack(int v, Runs& R, int32_t& q0, int& qn)
   qn = __builtin_amdgcn_readlane(v, kRecQn);
 }
 
+// Query record (one per query the per-query tiers take, indexed by its query index j, written by
+// the tile / wide-tile kernel that queues it): the 9 run starts and 10 prefixes of its block, its
+// cell-sorted position and coordinates.  A per-query workgroup then starts with one record load
+// (one lane per word, unpacked with readlane) instead of the chain qpos -> skeys -> cell_start
+// (three dependent global rounds) plus the coordinate load.
+constexpr int kQRecQp = 19, kQRecX = 20;
+__device__ __forceinline__ void qrec_write(int32_t* __restrict__ qrec, int64_t j, const Runs& R, int32_t qp, float x,
+                                           float y, float z) {
+  int4* o = reinterpret_cast<int4*>(qrec + j * kRecInts);
+  o[0] = make_int4(R.start[0], R.start[1], R.start[2], R.start[3]);
+  o[1] = make_int4(R.start[4], R.start[5], R.start[6], R.start[7]);
+  o[2] = make_int4(R.start[8], R.pref[0], R.pref[1], R.pref[2]);
+  o[3] = make_int4(R.pref[3], R.pref[4], R.pref[5], R.pref[6]);
+  o[4] = make_int4(R.pref[7], R.pref[8], R.pref[9], qp);
+  o[5] = make_int4(__float_as_int(x), __float_as_int(y), __float_as_int(z), 0);
+}
+__device__ __forceinline__ void qrec_unpack(int v, Runs& R, int32_t& qp, float4& q) {
+#pragma unroll
+  for (int r = 0; r < 9; ++r) R.start[r] = __builtin_amdgcn_readlane(v, r);
+#pragma unroll
+  for (int r = 0; r < 10; ++r) R.pref[r] = __builtin_amdgcn_readlane(v, 9 + r);
+  qp = __builtin_amdgcn_readlane(v, kQRecQp);
+  q = make_float4(__int_as_float(__builtin_amdgcn_readlane(v, kQRecX)),
+                  __int_as_float(__builtin_amdgcn_readlane(v, kQRecX + 1)),
+                  __int_as_float(__builtin_amdgcn_readlane(v, kQRecX + 2)), 0.0f);
+}
+
 __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   __builtin_amdgcn_wave_barrier();
@@ -183,6 +210,7 @@ struct ListOut {
   unsigned long long* cursor;  // [0] slots allocated, [1] neighbours, [2] neighbours in long lists, [3] long lists
   unsigned long long cap;
   int compact;  // the tile kernels may write 16-bit entries (pfx_nblist.h kLgCompact)
+  int32_t* qrec;  // query records of the lists queued to the per-query tiers (kRecInts per query)
 };
 
 // Candidate coordinates of a tile: staged in LDS, or read from the packed grid copy (L2).
@@ -723,7 +751,12 @@ __global__ void __launch_bounds__(256, TCAP <= kTcapSmall ? 4 : (STAGE ? 3 : 2))
     if (lane == 0) {
 #pragma unroll
       for (int u = 0; u < QW; ++u)
-        if (wv + 4 * u < qn) s_k[wv + 4 * u] = ok ? cursor[u] : LCAP + 1;
+        if (wv + 4 * u < qn) {
+          const int kq = ok ? cursor[u] : LCAP + 1;
+          s_k[wv + 4 * u] = kq;
+          // an overflowing list goes to the per-query kernel: its record, from the owner wave
+          if (kq > LCAP) qrec_write(out.qrec, start + wv + 4 * u, R, s_qp[wv + 4 * u], qxy[u].x, qxy[u].y, qz[u]);
+        }
     }
     __syncthreads();
     TPROF_T(p1);
@@ -905,7 +938,10 @@ __global__ void __launch_bounds__(256) k_nb_wide(GridView g, const int32_t* __re
     if (lane == 0) {
 #pragma unroll
       for (int u = 0; u < QW; ++u)
-        if (act[u]) s_k[wv + 4 * u] = cursor[u];
+        if (act[u]) {
+          s_k[wv + 4 * u] = cursor[u];
+          qrec_write(out.qrec, start + wv + 4 * u, R, s_qp[wv + 4 * u], qxy[u].x, qxy[u].y, qz[u]);
+        }
     }
     __syncthreads();
     int need = 0;
@@ -977,9 +1013,8 @@ __device__ __forceinline__ uint32_t pos_entry16(const Runs& R, int32_t p) {
 }
 
 template <int CAP, int NB, bool GLOBAL>
-__global__ void __launch_bounds__(256) k_nb_query(GridView g, const int32_t* __restrict__ qpos,
-                                                  const uint32_t* __restrict__ skeys,
-                                                  const int32_t* __restrict__ work, const int* __restrict__ n_ptr,
+__global__ void __launch_bounds__(256) k_nb_query(GridView g, const int32_t* __restrict__ work,
+                                                  const int* __restrict__ n_ptr,
                                                   float rr, float bscale, int sorted, ListOut out,
                                                   int32_t* __restrict__ over, int* __restrict__ n_over,
                                                   int* __restrict__ err, uint32_t* __restrict__ scratch,
@@ -1009,10 +1044,11 @@ __global__ void __launch_bounds__(256) k_nb_query(GridView g, const int32_t* __r
     const int32_t jw = work[w];
     const bool from_list = (jw & kListMode) != 0;  // the list is in place, unsorted: sort only
     const int32_t j = jw & (kListMode - 1);
-    const int32_t qp = qpos[j];
-    const float4 q = g.sp[qp];
+    // the query's record (its block: the runs its list entries refer to)
     Runs R;
-    block_runs(g, skeys[qp], R);  // the query's own cell: the runs its list entries refer to
+    int32_t qp;
+    float4 q;
+    qrec_unpack((tid & 63) < kRecInts ? out.qrec[(int64_t)j * kRecInts + (tid & 63)] : 0, R, qp, q);
     if (tid == 0) s_count = 0;
     for (int b = tid; b < NB; b += 256) bcount[b] = 0;
     __syncthreads();
@@ -1340,6 +1376,7 @@ void build_lists(pfx_ctx* ctx, const Grid& G, const uint8_t* mask, double radius
   int32_t* wq = B("wide").as<int32_t>((size_t)n);  // wide-tile work: record indices
   int32_t* mid = B("mid").as<int32_t>(n);
   int32_t* mid8 = B("mid8").as<int32_t>(n);
+  int32_t* qrec = B("qrec").as<int32_t>((size_t)n * kRecInts);
   unsigned long long* cursor = B("cursor").as<unsigned long long>(4);
   size_t t1 = 0, t2 = 0, t3 = 0;
   PFX_HIP(rocprim::select(nullptr, t1, rocprim::counting_iterator<int32_t>(0), flags, qpos, d_nq, (size_t)n, st));
@@ -1395,7 +1432,7 @@ void build_lists(pfx_ctx* ctx, const Grid& G, const uint8_t* mask, double radius
   const int heavy = (int)std::min<int64_t>(4, n >> 21);
   const int ch_small = 4, ch_sparse = std::max(2, heavy), ch_dense = std::max(1, heavy);
   for (int attempt = 0; attempt < 3; ++attempt) {
-    ListOut lo{off, cnt, lgs, static_cast<uint32_t*>(lb.ptr), cursor, lb.bytes / sizeof(uint32_t), compact ? 1 : 0};
+    ListOut lo{off, cnt, lgs, static_cast<uint32_t*>(lb.ptr), cursor, lb.bytes / sizeof(uint32_t), compact ? 1 : 0, qrec};
     if (attempt) {  // (the first attempt's cursors were zeroed by k_list_init)
       PFX_HIP(hipMemsetAsync(cursor, 0, 4 * sizeof(unsigned long long), st));
       PFX_HIP(hipMemsetAsync(counters + 2, 0, sizeof(int), st));  // per-query work
@@ -1415,13 +1452,13 @@ void build_lists(pfx_ctx* ctx, const Grid& G, const uint8_t* mask, double radius
     DevBuf& hs = B("scratch");
     auto launch_mid8 = [&] {
       k_nb_query<kCapMid8, kBucketsMid8, false><<<256 * 2, 256, lds_m8, st>>>(
-          g, qpos, G.skeys, mid8, counters + 14, rr, (float)kBucketsMid8 / rr, isort, lo, mid, counters + 12,
+          g, mid8, counters + 14, rr, (float)kBucketsMid8 / rr, isort, lo, mid, counters + 12,
           counters + 4, nullptr, counters + 15);
       check_launch("nblist 8k lists");
     };
     auto launch_mid = [&] {
       k_nb_query<kCapMid, kBucketsMid, false><<<256, 256, lds_m, st>>>(
-          g, qpos, G.skeys, mid, counters + 12, rr, (float)kBucketsMid / rr, isort, lo, huge, counters + 3,
+          g, mid, counters + 12, rr, (float)kBucketsMid / rr, isort, lo, huge, counters + 3,
           counters + 4, nullptr, counters + 13);
       check_launch("nblist 16k lists");
     };
@@ -1441,7 +1478,7 @@ void build_lists(pfx_ctx* ctx, const Grid& G, const uint8_t* mask, double radius
     };
     auto launch_huge = [&] {
       k_nb_query<kCapHuge, kBucketsHuge, true><<<huge_blocks(), 256, 0, st>>>(
-          g, qpos, G.skeys, huge, counters + 3, rr, (float)kBucketsHuge / rr, isort, lo, nullptr, nullptr, counters + 4,
+          g, huge, counters + 3, rr, (float)kBucketsHuge / rr, isort, lo, nullptr, nullptr, counters + 4,
           static_cast<uint32_t*>(hs.ptr), counters + 9);
       check_launch("nblist huge lists");
     };
@@ -1480,7 +1517,7 @@ void build_lists(pfx_ctx* ctx, const Grid& G, const uint8_t* mask, double radius
       {
         TimeScope t3(ctx, std::string(tag) + "_lists_query");
         k_nb_query<kCapQuery, kBucketsQuery, false><<<256 * 4, 256, lds_q, st>>>(
-            g, qpos, G.skeys, single, counters + 2, rr, (float)kBucketsQuery / rr, isort, lo,
+            g, single, counters + 2, rr, (float)kBucketsQuery / rr, isort, lo,
             use_mid8 ? mid8 : mid, counters + (use_mid8 ? 14 : 12), counters + 4, nullptr, counters + 8);
         // lists of 4k-8k entries (dense clouds: ~14 % of the 10M-pt room's queries, 31 % of its
         // entries) in two 72 KB workgroups per CU instead of the 16k tier's one (10M-pt dense

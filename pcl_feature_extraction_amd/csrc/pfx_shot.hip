@@ -19,10 +19,8 @@ namespace pfx {
 namespace {
 
 #ifdef PFX_SHOT_PROFILE
-// phase cycles of k_shot_hist (thread 0 of each workgroup): [0] frame, [1] updates + masks,
-// [2] offsets, [3] scatter, [4] bin sums, [5] normalisation + output, [6] queries
-// [7] sequential normalisations, [8] normalisation cycles, [9] set-up before the first chunk
-// k_shot_lrf: [10] search + sort, [11] records, [12] LRF chains, [13] queries
+// phase cycles (thread 0 of each workgroup): [7] sequential normalisations, [8] normalisation
+// cycles; k_shot_lrf: [10] search + sort, [11] records, [12] LRF chains, [13] queries
 __device__ unsigned long long g_shot_prof[16];
 #define SPROF_T(v) long long v = (threadIdx.x == 0) ? clock64() : 0
 #define SPROF_ADD(i, a, b) if (threadIdx.x == 0) atomicAdd(&g_shot_prof[i], (unsigned long long)((b) - (a)))
@@ -261,8 +259,8 @@ __device__ __forceinline__ bool shot_eigen(const double cov[10], int valid, doub
 }
 
 // sign disambiguation of S.axes over the valid neighbours, then S.rf (x, y = z cross x, z)
-template <class Src>
-__device__ __forceinline__ void shot_frame(ShotLds& S, const Src& src, int k, int valid) {
+template <class Lds, class Src>
+__device__ __forceinline__ void shot_frame(Lds& S, const Src& src, int k, int valid) {
   const int tid = threadIdx.x, lane = tid & 63;
   {
     const double v1x = S.axes[0], v1y = S.axes[1], v1z = S.axes[2];
@@ -338,138 +336,96 @@ __device__ __forceinline__ int lsb_exp_f(float v) {
   return (e ? e : 1) - 150 + __builtin_ctz(full);
 }
 
-// the SHOT histogram from S.rf, normalizeHistogram, outputs
-template <class Src>
-__device__ __forceinline__ void shot_hist(ShotLds& S, const Src& src, int k, double radius, float* __restrict__ d,
-                                          float* __restrict__ rfo) {
+// The histogram's per-chunk binning.  Each neighbour adds to at most one bin per update statement
+// (its <= 5 bins are distinct), so PCL's sequential order restricted to one bin is neighbour
+// order.  Per chunk of m neighbours (one per thread): hit masks per bin -> counts -> offsets ->
+// every update written to its bin's bucket at its rank among the bin's hits (a stable counting
+// sort) -> each bin's owner (thread j: bins j and j + 256) adds its bucket in order.  The masks
+// must be zero on entry (they are left zero).
+__device__ __forceinline__ void hist_chunk(ShotLds& S, int m, const int bins[5], const float vals[5], float& h0,
+                                           float& h1) {
   const int tid = threadIdx.x, lane = tid & 63;
-  // Bin ownership for the histogram: thread j accumulates bins j and j + 256 in registers.
   const int b0 = tid, b1 = tid + 256;
-  float h0 = 0.0f, h1 = 0.0f;
-  for (int i = tid; i < kLen; i += 256)
+  if (tid < m) {
+    const uint64_t bit = 1ull << (tid & 63);
+#pragma unroll
+    for (int s = 0; s < 5; ++s)
+      if (bins[s] >= 0) atomicOr(reinterpret_cast<unsigned long long*>(&S.upd.mask[bins[s]][tid >> 6]), bit);
+  }
+  __syncthreads();
+  // hit counts -> exclusive offsets (wave 0: 6 bins per lane, then a wave scan)
+  if (tid < 64) {
+    int c[6], tot = 0;
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+      const int bb = tid * 6 + i;
+      c[i] = 0;
+      if (bb < kLen)
+        for (int w = 0; w < kMaskWords; ++w) c[i] += __popcll(S.upd.mask[bb][w]);
+      tot += c[i];
+    }
+    int incl = tot;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int y = __shfl_up(incl, o);
+      if (lane >= o) incl += y;
+    }
+    int run = incl - tot;
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+      const int bb = tid * 6 + i;
+      if (bb < kLen) S.upd.off[bb] = run;
+      run += c[i];
+    }
+  }
+  __syncthreads();
+  if (tid < m) {  // scatter: rank = hits of the bin from lower neighbours of the chunk
+    const int wq = tid >> 6;
+    const uint64_t below = lanemask_lt();
+#pragma unroll
+    for (int s = 0; s < 5; ++s) {
+      const int bb = bins[s];
+      if (bb < 0) continue;
+      int r = __popcll(S.upd.mask[bb][wq] & below);
+      for (int w = 0; w < wq; ++w) r += __popcll(S.upd.mask[bb][w]);
+      S.upd.val[S.upd.off[bb] + r] = vals[s];
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int o = 0; o < 2; ++o) {
+    const int b = o ? b1 : b0;
+    if (b < kLen) {
+      int cnt = 0;
+      for (int w = 0; w < kMaskWords; ++w) {
+        cnt += __popcll(S.upd.mask[b][w]);
+        S.upd.mask[b][w] = 0;  // ready for the next chunk
+      }
+      const float* v = S.upd.val + S.upd.off[b];
+      float h = o ? h1 : h0;
+      int i = 0;
+      for (; i + 4 <= cnt; i += 4) {
+        const float a0 = v[i], a1 = v[i + 1], a2 = v[i + 2], a3 = v[i + 3];
+        h = h + a0; h = h + a1; h = h + a2; h = h + a3;
+      }
+      for (; i < cnt; ++i) h = h + v[i];
+      if (o) h1 = h; else h0 = h;
+    }
+  }
+  __syncthreads();
+}
+
+__device__ __forceinline__ void hist_clear(ShotLds& S) {
+  for (int i = threadIdx.x; i < kLen; i += 256)
     for (int w = 0; w < kMaskWords; ++w) S.upd.mask[i][w] = 0;
   __syncthreads();
-  const f3 fx = mk3(S.rf[0], S.rf[1], S.rf[2]), fy = mk3(S.rf[3], S.rf[4], S.rf[5]),
-           fz = mk3(S.rf[6], S.rf[7], S.rf[8]);
-  // Each neighbour adds to at most one bin per update statement (its <= 5 bins are distinct),
-  // so PCL's sequential order restricted to one bin is neighbour order.  Per chunk: hit masks
-  // per bin -> counts -> offsets -> every update written to its bin's bucket at its rank among
-  // the bin's hits (a stable counting sort) -> each bin's owner adds its bucket in order.
-  // a neighbour's offset + d2 and normal: the next chunk's are loaded while this one's updates
-  // are binned
-  SPROF_T(ps0);
-  float4 c_n = make_float4(0.f, 0.f, 0.f, 0.f);
-  float3 nv_n = make_float3(0.f, 0.f, 0.f);
-  if (tid < k) {
-    c_n = src.pt(tid);
-    nv_n = src.nrm(tid);
-  }
-#ifdef PFX_SHOT_PROFILE
-  bool first_chunk = true;
-#endif
-  for (int c0 = 0; c0 < k; c0 += kChunk) {
-    const int m = min(kChunk, k - c0);
-    int bins[5];
-    float vals[5];
-#pragma unroll
-    for (int s = 0; s < 5; ++s) bins[s] = -1;
-    const float4 c = c_n;
-    const float3 nv = nv_n;
-    if (c0 + kChunk + tid < k) {
-      c_n = src.pt(c0 + kChunk + tid);
-      nv_n = src.nrm(c0 + kChunk + tid);
-    }
-    SPROF_T(ph0);
-#ifdef PFX_SHOT_PROFILE
-    if (first_chunk) SPROF_ADD(9, ps0, ph0);
-    first_chunk = false;
-#endif
-    if (tid < m) {
-      const float pnx = nv.x, pny = nv.y, pnz = nv.z;
-      const double distance = sqrt((double)c.w);
-      if (isfinite(pnx) && isfinite(pny) && isfinite(pnz) && !(fabs(distance - 0.0) < 1E-15)) {
-        double cosd = dot4(mk3(pnx, pny, pnz), fz);
-        if (cosd > 1.0) cosd = 1.0;
-        if (cosd < -1.0) cosd = -1.0;
-        const double binDist = ((1.0 + cosd) * kBins) / 2;
-        const f3 delta = mk3(c.x, c.y, c.z);
-        shot_updates(delta, distance, binDist, fx, fy, fz, radius, bins, vals);
-      }
-      const uint64_t bit = 1ull << (tid & 63);
-#pragma unroll
-      for (int s = 0; s < 5; ++s)
-        if (bins[s] >= 0) atomicOr(reinterpret_cast<unsigned long long*>(&S.upd.mask[bins[s]][tid >> 6]), bit);
-    }
-    __syncthreads();
-    SPROF_T(ph1);
-    SPROF_ADD(1, ph0, ph1);
-    // hit counts -> exclusive offsets (wave 0: 6 bins per lane, then a wave scan)
-    if (tid < 64) {
-      int c[6], tot = 0;
-#pragma unroll
-      for (int i = 0; i < 6; ++i) {
-        const int bb = tid * 6 + i;
-        c[i] = 0;
-        if (bb < kLen)
-          for (int w = 0; w < kMaskWords; ++w) c[i] += __popcll(S.upd.mask[bb][w]);
-        tot += c[i];
-      }
-      int incl = tot;
-#pragma unroll
-      for (int o = 1; o < 64; o <<= 1) {
-        const int y = __shfl_up(incl, o);
-        if (lane >= o) incl += y;
-      }
-      int run = incl - tot;
-#pragma unroll
-      for (int i = 0; i < 6; ++i) {
-        const int bb = tid * 6 + i;
-        if (bb < kLen) S.upd.off[bb] = run;
-        run += c[i];
-      }
-    }
-    __syncthreads();
-    SPROF_T(ph2);
-    SPROF_ADD(2, ph1, ph2);
-    if (tid < m) {  // scatter: rank = hits of the bin from lower neighbours of the chunk
-      const int wq = tid >> 6;
-      const uint64_t below = lanemask_lt();
-#pragma unroll
-      for (int s = 0; s < 5; ++s) {
-        const int bb = bins[s];
-        if (bb < 0) continue;
-        int r = __popcll(S.upd.mask[bb][wq] & below);
-        for (int w = 0; w < wq; ++w) r += __popcll(S.upd.mask[bb][w]);
-        S.upd.val[S.upd.off[bb] + r] = vals[s];
-      }
-    }
-    __syncthreads();
-    SPROF_T(ph3);
-    SPROF_ADD(3, ph2, ph3);
-#pragma unroll
-    for (int o = 0; o < 2; ++o) {
-      const int b = o ? b1 : b0;
-      if (b < kLen) {
-        int cnt = 0;
-        for (int w = 0; w < kMaskWords; ++w) {
-          cnt += __popcll(S.upd.mask[b][w]);
-          S.upd.mask[b][w] = 0;  // ready for the next chunk
-        }
-        const float* v = S.upd.val + S.upd.off[b];
-        float h = o ? h1 : h0;
-        int i = 0;
-        for (; i + 4 <= cnt; i += 4) {
-          const float a0 = v[i], a1 = v[i + 1], a2 = v[i + 2], a3 = v[i + 3];
-          h = h + a0; h = h + a1; h = h + a2; h = h + a3;
-        }
-        for (; i < cnt; ++i) h = h + v[i];
-        if (o) h1 = h; else h0 = h;
-      }
-    }
-    __syncthreads();
-    SPROF_T(ph4);
-    SPROF_ADD(4, ph3, ph4);
-  }
+}
+
+// normalizeHistogram and the outputs (rfo: the frame rows, nullable)
+__device__ __forceinline__ void hist_finish(ShotLds& S, float h0, float h1, float* __restrict__ d,
+                                            float* __restrict__ rfo) {
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int b0 = tid, b1 = tid + 256;
   SPROF_T(pe0);
   S.hist[b0] = h0;
   if (b1 < kLen) S.hist[b1] = h1;
@@ -535,8 +491,59 @@ __device__ __forceinline__ void shot_hist(ShotLds& S, const Src& src, int k, dou
   SPROF_ADD(8, pe0, pe1);
   const float nrm = (float)S.cov[0];
   for (int i = tid; i < kLen; i += 256) d[i] = S.hist[i] / nrm;
-  if (tid < 9) rfo[tid] = S.rf[tid];
+  if (rfo && tid < 9) rfo[tid] = S.rf[tid];
   __syncthreads();
+}
+
+// a neighbour's (<= 5) histogram updates from the frame S.rf (fx, fy, fz)
+__device__ __forceinline__ void nb_updates(const float4& c, const float3& nv, const f3& fx, const f3& fy,
+                                           const f3& fz, double radius, int bins[5], float vals[5]) {
+#pragma unroll
+  for (int s = 0; s < 5; ++s) bins[s] = -1;
+  const double distance = sqrt((double)c.w);
+  if (isfinite(nv.x) && isfinite(nv.y) && isfinite(nv.z) && !(fabs(distance - 0.0) < 1E-15)) {
+    double cosd = dot4(mk3(nv.x, nv.y, nv.z), fz);
+    if (cosd > 1.0) cosd = 1.0;
+    if (cosd < -1.0) cosd = -1.0;
+    const double binDist = ((1.0 + cosd) * kBins) / 2;
+    shot_updates(mk3(c.x, c.y, c.z), distance, binDist, fx, fy, fz, radius, bins, vals);
+  }
+}
+
+// the SHOT histogram from S.rf, normalizeHistogram, outputs (the fused kernel: updates computed
+// chunk by chunk)
+template <class Src>
+__device__ __forceinline__ void shot_hist(ShotLds& S, const Src& src, int k, double radius, float* __restrict__ d,
+                                          float* __restrict__ rfo) {
+  const int tid = threadIdx.x;
+  float h0 = 0.0f, h1 = 0.0f;
+  hist_clear(S);
+  const f3 fx = mk3(S.rf[0], S.rf[1], S.rf[2]), fy = mk3(S.rf[3], S.rf[4], S.rf[5]),
+           fz = mk3(S.rf[6], S.rf[7], S.rf[8]);
+  for (int c0 = 0; c0 < k; c0 += kChunk) {
+    const int m = min(kChunk, k - c0);
+    int bins[5];
+    float vals[5];
+#pragma unroll
+    for (int s = 0; s < 5; ++s) bins[s] = -1;
+    if (tid < m) nb_updates(src.pt(c0 + tid), src.nrm(c0 + tid), fx, fy, fz, radius, bins, vals);
+    hist_chunk(S, m, bins, vals, h0, h1);
+  }
+  hist_finish(S, h0, h1, d, rfo);
+}
+
+// the split kernels' update records: one 32-B record per neighbour, {bin0 | bin1 << 16,
+// bin2 | bin3 << 16, bin4 (low half), val0} + {val1, val2, val3, val4} (bins as int16, -1: none)
+__device__ __forceinline__ void upd_pack(const int bins[5], const float vals[5], uint4& a, float4& b) {
+  auto h = [](int v) { return (uint32_t)(uint16_t)(int16_t)v; };
+  a = make_uint4(h(bins[0]) | (h(bins[1]) << 16), h(bins[2]) | (h(bins[3]) << 16), h(bins[4]),
+                 __float_as_uint(vals[0]));
+  b = make_float4(vals[1], vals[2], vals[3], vals[4]);
+}
+__device__ __forceinline__ void upd_unpack(const uint4& a, const float4& b, int bins[5], float vals[5]) {
+  auto s = [](uint32_t v) { return (int)(int16_t)(uint16_t)v; };
+  bins[0] = s(a.x); bins[1] = s(a.x >> 16); bins[2] = s(a.y); bins[3] = s(a.y >> 16); bins[4] = s(a.z);
+  vals[0] = __uint_as_float(a.w); vals[1] = b.x; vals[2] = b.y; vals[3] = b.z; vals[4] = b.w;
 }
 
 __device__ __forceinline__ void shot_nan(float* __restrict__ d, float* __restrict__ rfo) {
@@ -725,27 +732,32 @@ __global__ void __launch_bounds__(64) k_shot_eigen(ShotQuery* __restrict__ sq, i
   }
 }
 
-// C: sign disambiguation, histogram, normalisation (workgroups per CU: the double-precision
-// interpolation of shot_updates wants ~195 VGPRs, i.e. two; held to three (168): SHOT stage 1.455
-// -> 1.247 ms on configs[3], four (128, with spills) 1.32)
+// C: sign disambiguation and the histogram updates of every neighbour, written as records (the
+// double-precision interpolation of shot_updates, ~170 VGPRs: three workgroups per CU, with no
+// barrier between a workgroup's neighbours)
+struct FrameLds {
+  double axes[6];
+  float rf[9];
+  int zero_prefix, plusT, plusN;
+};
 #ifndef PFX_SHOT_HIST_WG
 #define PFX_SHOT_HIST_WG 3
 #endif
-__global__ void __launch_bounds__(256, PFX_SHOT_HIST_WG) k_shot_hist(int64_t base, int64_t nq, double radius,
-                                                                      float* __restrict__ desc,
-                                                                      float* __restrict__ rf_out,
-                                                                      const float4* __restrict__ grec,
-                                                                      const ShotQuery* __restrict__ sq) {
-  __shared__ ShotLds S;  // (the neighbour records are read from global memory)
+__global__ void __launch_bounds__(256, PFX_SHOT_HIST_WG) k_shot_frame(int64_t base, int64_t nq, double radius,
+                                                                       float* __restrict__ desc,
+                                                                       float* __restrict__ rf_out,
+                                                                       const float4* __restrict__ grec,
+                                                                       const ShotQuery* __restrict__ sq,
+                                                                       uint4* __restrict__ upd) {
+  __shared__ FrameLds S;
   const int tid = threadIdx.x;
   for (int64_t l = blockIdx.x; l < nq; l += gridDim.x) {
     const int64_t q = base + l;
     const int status = sq[l].status;
     if (status == 1 || status == 2) continue;
-    float* d = desc + q * kLen;
     float* rfo = rf_out + q * 9;
     if (status == 3) {
-      shot_nan(d, rfo);
+      shot_nan(desc + q * kLen, rfo);
       continue;
     }
     const int k = sq[l].k;
@@ -757,14 +769,64 @@ __global__ void __launch_bounds__(256, PFX_SHOT_HIST_WG) k_shot_hist(int64_t bas
       S.plusN = 0;
     }
     __syncthreads();
-    SPROF_T(f0);
     shot_frame(S, src, k, k - sq[l].n_invalid);
-    SPROF_T(f1);
-    SPROF_ADD(0, f0, f1);
-    shot_hist(S, src, k, radius, d, rfo);
-    SPROF_T(f2);
-    SPROF_ADD(5, f1, f2);
-    SPROF_ADD(6, 0, 1);
+    __syncthreads();
+    if (tid < 9) rfo[tid] = S.rf[tid];
+    const f3 fx = mk3(S.rf[0], S.rf[1], S.rf[2]), fy = mk3(S.rf[3], S.rf[4], S.rf[5]),
+             fz = mk3(S.rf[6], S.rf[7], S.rf[8]);
+    uint4* u = upd + l * 2 * kCapSmall;
+    for (int j = tid; j < k; j += 256) {
+      int bins[5];
+      float vals[5];
+      nb_updates(src.pt(j), src.nrm(j), fx, fy, fz, radius, bins, vals);
+      uint4 a;
+      float4 b;
+      upd_pack(bins, vals, a, b);
+      u[2 * j] = a;
+      reinterpret_cast<float4*>(u)[2 * j + 1] = b;
+    }
+    __syncthreads();  // S is rewritten by the next query
+  }
+}
+
+// D: the histogram from the update records, normalisation, descriptor (no double-precision
+// interpolation here: a light kernel, many workgroups per CU)
+__global__ void __launch_bounds__(256) k_shot_accum(int64_t base, int64_t nq, float* __restrict__ desc,
+                                                    const uint4* __restrict__ upd,
+                                                    const ShotQuery* __restrict__ sq) {
+  __shared__ ShotLds S;
+  const int tid = threadIdx.x;
+  for (int64_t l = blockIdx.x; l < nq; l += gridDim.x) {
+    if (sq[l].status != 0) continue;
+    const int k = sq[l].k;
+    const uint4* u = upd + l * 2 * kCapSmall;
+    float h0 = 0.0f, h1 = 0.0f;
+    hist_clear(S);
+    // the next chunk's records are loaded while this one is binned
+    uint4 a_n = make_uint4(0, 0, 0, 0);
+    float4 b_n = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (tid < k) {
+      a_n = u[2 * tid];
+      b_n = reinterpret_cast<const float4*>(u)[2 * tid + 1];
+    }
+    for (int c0 = 0; c0 < k; c0 += kChunk) {
+      const int m = min(kChunk, k - c0);
+      const uint4 a = a_n;
+      const float4 b = b_n;
+      if (c0 + kChunk + tid < k) {
+        a_n = u[2 * (c0 + kChunk + tid)];
+        b_n = reinterpret_cast<const float4*>(u)[2 * (c0 + kChunk + tid) + 1];
+      }
+      int bins[5];
+      float vals[5];
+      upd_unpack(a, b, bins, vals);
+      if (tid >= m) {
+#pragma unroll
+        for (int s = 0; s < 5; ++s) bins[s] = -1;
+      }
+      hist_chunk(S, m, bins, vals, h0, h1);
+    }
+    hist_finish(S, h0, h1, desc + (base + l) * kLen, nullptr);
   }
 }
 
@@ -810,6 +872,7 @@ void shot_dev(pfx_ctx* ctx, const float* sx, const float* sy, const float* sz, c
       const int64_t bq = std::min<int64_t>(nq, kSplitBatch);
       float4* grec = ctx->buf("shot_recs").as<float4>((size_t)bq * 2 * kCapSmall);
       ShotQuery* sq = ctx->buf("shot_q").as<ShotQuery>((size_t)bq);
+      uint4* upd = ctx->buf("shot_upd").as<uint4>((size_t)bq * 2 * kCapSmall);
       int32_t* ipos = ctx->buf("shot_ipos").as<int32_t>(ns);
       float4* snp = ctx->buf("shot_snp").as<float4>(ns);
       k_shot_prep<<<(unsigned)ceil_div(ns, 256), 256, 0, st>>>(ctx->grid_b.perm, ns, snx, sny, snz, ipos, snp);
@@ -818,7 +881,8 @@ void shot_dev(pfx_ctx* ctx, const float* sx, const float* sy, const float* sz, c
         const unsigned bl = (unsigned)std::min<int64_t>(m, 256 * 10);
         k_shot_lrf<<<bl, 256, lds_s, st>>>(g, qx, qy, qz, q0, m, over, n_over, r, desc, rf, grec, sq, ipos, snp, nbr);
         k_shot_eigen<<<(unsigned)ceil_div(m, 64), 64, 0, st>>>(sq, m);
-        k_shot_hist<<<(unsigned)std::min<int64_t>(m, 256 * 16), 256, 0, st>>>(q0, m, r, desc, rf, grec, sq);
+        k_shot_frame<<<(unsigned)std::min<int64_t>(m, 256 * 16), 256, 0, st>>>(q0, m, r, desc, rf, grec, sq, upd);
+        k_shot_accum<<<(unsigned)std::min<int64_t>(m, 256 * 16), 256, 0, st>>>(q0, m, desc, upd, sq);
       }
     }
     // longer lists: grid sized for the worst case, the count stays on the device
@@ -836,9 +900,8 @@ void shot_dev(pfx_ctx* ctx, const float* sx, const float* sy, const float* sz, c
   {
     unsigned long long pr[16];
     PFX_HIP(hipMemcpyFromSymbol(pr, HIP_SYMBOL(g_shot_prof), sizeof(pr)));
-    const double nq_ = (double)(pr[6] + !pr[6]);
-    fprintf(stderr, "shot_hist cycles/query: frame %.0f setup %.0f updates %.0f offsets %.0f scatter %.0f sums %.0f norm %.0f | hist total %.0f (%llu queries, %llu sequential norms)\n",
-            pr[0] / nq_, pr[9] / nq_, pr[1] / nq_, pr[2] / nq_, pr[3] / nq_, pr[4] / nq_, pr[8] / nq_, pr[5] / nq_, pr[6], pr[7]);
+    const double nq_ = (double)(pr[13] + !pr[13]);
+    fprintf(stderr, "shot_accum normalisation %.0f cycles/query (%llu sequential)\n", pr[8] / nq_, pr[7]);
     fprintf(stderr, "shot_lrf cycles/query: search+sort %.0f records %.0f chains %.0f\n", pr[10] / (double)(pr[13] + !pr[13]),
             pr[11] / (double)(pr[13] + !pr[13]), pr[12] / (double)(pr[13] + !pr[13]));
     const unsigned long long z[16] = {};
