@@ -114,13 +114,13 @@ struct Side {
   int64_t n;
 };
 
-// Slots [base, base + k) of the pair list.  Saturating: once the count has passed ecap (the list
-// overflowed; match_pairs_overflowed sees count > cap and reruns the second contraction) later
-// reservations do not add, so the 32-bit count cannot wrap back below the cap however many pairs
-// near-duplicate sets emit (up to ns x nt); it exceeds ecap by at most the in-flight reservations.
-__device__ __forceinline__ unsigned emit_reserve(unsigned* nemit, unsigned k, unsigned ecap) {
-  const unsigned cur = __hip_atomic_load(nemit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  return cur > ecap ? cur : atomicAdd(nemit, k);
+// Slots [base, base + k) of the pair list.  The count is 64-bit, so it cannot wrap back below the
+// cap however many pairs near-duplicate sets emit (up to ns x nt; match_pairs_overflowed sees
+// count > cap and reruns the second contraction).  (Round 5: a saturating 32-bit count -- an
+// atomic load before each add -- slowed the bound pass 0.41 -> 1.0 ms: every wave's reservation
+// then made two accesses to the one contended address.)
+__device__ __forceinline__ unsigned long long emit_reserve(unsigned long long* nemit, unsigned k) {
+  return atomicAdd(nemit, (unsigned long long)k);
 }
 
 // PASS 0: row / column upper bounds, and the pruned pair list: after a tile's atomicMin the
@@ -139,7 +139,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) k
                                                      uint32_t* __restrict__ Urow, uint32_t* __restrict__ Ucol,
                                                      int2* __restrict__ crow, int2* __restrict__ ccol,
                                                      unsigned* __restrict__ ncand, unsigned cap,
-                                                     int4* __restrict__ emit, unsigned* __restrict__ nemit,
+                                                     int4* __restrict__ emit, unsigned long long* __restrict__ nemit,
                                                      unsigned ecap, int gx, int gy, int group, int cross,
                                                      int sr, int sc) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -344,8 +344,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) k
               staged += k;
             } else {
               const int first = __ffsll((long long)m) - 1;
-              unsigned base = 0;
-              if (lane == first) base = emit_reserve(nemit, k, ecap);
+              unsigned long long base = 0;
+              if (lane == first) base = emit_reserve(nemit, k);
               base = __shfl(base, first);
               if (em && base + pre < ecap) emit[base + pre] = pr;
             }
@@ -362,8 +362,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) k
       if (h == 0 && v < __uint_as_float(kInfBits) && q < B.n) atomicMin(&Ucol[q], __float_as_uint(v));
     }
     if (staged) {
-      unsigned base = 0;
-      if (lane == 0) base = emit_reserve(nemit, staged, ecap);
+      unsigned long long base = 0;
+      if (lane == 0) base = emit_reserve(nemit, staged);
       base = __shfl(base, 0);
       for (unsigned i = lane; i < staged; i += 64)
         if (base + i < ecap) emit[base + i] = stage[i];
@@ -401,13 +401,13 @@ template <bool VEC>
 __global__ void __launch_bounds__(256) k_match_exact_emit(const float* __restrict__ A, int64_t sa,
                                                           const float* __restrict__ B, int64_t sb, int D,
                                                           const int4* __restrict__ emit,
-                                                          const unsigned* __restrict__ nemit, unsigned ecap,
+                                                          const unsigned long long* __restrict__ nemit, unsigned ecap,
                                                           const uint32_t* __restrict__ Urow,
                                                           const uint32_t* __restrict__ Ucol,
                                                           unsigned* __restrict__ ncand,
                                                           unsigned long long* __restrict__ bs,
                                                           unsigned long long* __restrict__ bt) {
-  const unsigned n = min(*nemit, ecap);
+  const unsigned n = (unsigned)min(*nemit, (unsigned long long)ecap);
   unsigned nr = 0, nc = 0;
   for (unsigned t = blockIdx.x * 256 + threadIdx.x; t < n; t += gridDim.x * 256) {
     const int4 p = emit[t];
@@ -501,10 +501,11 @@ Prepared prep(pfx_ctx* ctx, const char* tag, const float* X, int64_t n, int64_t 
 // source row i, t2s[j] = nearest source row of target row j (-1: no finite row / no target).
 bool match_pairs_overflowed(pfx_ctx* ctx) {
   const unsigned* h = ctx->readback<unsigned>();  // (written by the deferred call's copy)
-  ctx->stats["match_pairs_emitted"] = h[2];
+  const unsigned long long emitted = (unsigned long long)h[2] | ((unsigned long long)h[3] << 32);
+  ctx->stats["match_pairs_emitted"] = (int64_t)emitted;
   ctx->stats["match_candidates_rows"] = h[0];
   ctx->stats["match_candidates_cols"] = h[1];
-  return (int64_t)h[2] > ctx->stats["match_pair_cap"];
+  return (int64_t)emitted > ctx->stats["match_pair_cap"];
 }
 
 bool match_nearest_dev(pfx_ctx* ctx, const float* src, int64_t ns, int64_t ss, const float* tgt, int64_t nt,
@@ -528,7 +529,8 @@ bool match_nearest_dev(pfx_ctx* ctx, const float* src, int64_t ns, int64_t ss, c
   uint32_t* Ucol = ctx->buf("match_ucol").as<uint32_t>(b.n_pad);
   unsigned long long* bs = ctx->buf("match_bs").as<unsigned long long>(ns);
   unsigned long long* bt = ctx->buf("match_bt").as<unsigned long long>(nt);
-  unsigned* ncand = ctx->buf("match_ncand").as<unsigned>(3);
+  // [0] row candidates, [1] column candidates, [2..3] the 64-bit pair count
+  unsigned* ncand = ctx->buf("match_ncand").as<unsigned>(4);
   PFX_HIP(hipMemsetAsync(Urow, 0x7f, sizeof(uint32_t) * a.n_pad, st));  // 0x7f7f7f7f: above any bound
   PFX_HIP(hipMemsetAsync(Ucol, 0x7f, sizeof(uint32_t) * b.n_pad, st));
   const float u = 5.9604645e-8f;  // 2^-24
@@ -544,8 +546,8 @@ bool match_nearest_dev(pfx_ctx* ctx, const float* src, int64_t ns, int64_t ss, c
       mode == 2 ? 0u : (unsigned)std::min<int64_t>(64 * (ns + nt) + (1 << 16), int64_t(1) << 28);
   ctx->stats["match_pair_cap"] = ecap;
   int4* emit = ctx->buf("match_emit").as<int4>(std::max(ecap, 1u));
-  unsigned* nemit = ncand + 2;
-  PFX_HIP(hipMemsetAsync(ncand, 0, 3 * sizeof(unsigned), st));
+  unsigned long long* nemit = reinterpret_cast<unsigned long long*>(ncand + 2);
+  PFX_HIP(hipMemsetAsync(ncand, 0, 4 * sizeof(unsigned), st));
   PFX_HIP(hipMemsetAsync(bs, 0xff, sizeof(unsigned long long) * ns, st));
   PFX_HIP(hipMemsetAsync(bt, 0xff, sizeof(unsigned long long) * nt, st));
   if (gx > 16 && gy > 16) {
@@ -574,7 +576,7 @@ bool match_nearest_dev(pfx_ctx* ctx, const float* src, int64_t ns, int64_t ss, c
   k_match_finish<<<(unsigned)ceil_div(ns, 256), 256, 0, st>>>(bs, ns, s2t, ds2t);
   if (t2s) k_match_finish<<<(unsigned)ceil_div(nt, 256), 256, 0, st>>>(bt, nt, t2s, dt2s);
   check_launch("k_match_finish");
-  PFX_HIP(hipMemcpyAsync(h, ncand, 3 * sizeof(unsigned), hipMemcpyDeviceToHost, st));
+  PFX_HIP(hipMemcpyAsync(h, ncand, 4 * sizeof(unsigned), hipMemcpyDeviceToHost, st));
   if (mode == 1) return true;  // the caller synchronises once for everything it launched
   PFX_HIP(hipStreamSynchronize(st));  // the one host round trip of a normal call
   if (!match_pairs_overflowed(ctx)) return false;
