@@ -138,8 +138,10 @@ struct ShotLds {
   union {
     double lrf[kChains][kChunk];  // per-neighbour chain terms of one chunk (0 for invalid ones)
     struct {
-      uint64_t mask[kLen][kMaskWords];  // which neighbours of the chunk hit each bin
+      uint64_t mask[kMaskWords][kLen];  // which neighbours of the chunk hit each bin (word-major:
+                                        // the bin owners' reads are lane-consecutive)
       int off[kLen + 1];                // bucket offsets (exclusive scan of the hit counts)
+      int seg[8];                       // the counts' scan: totals of the 64-bin segments
       float val[5 * kChunk];            // the chunk's update values bucketed by bin, neighbour order
     } upd;
   };
@@ -346,39 +348,47 @@ __device__ __forceinline__ void hist_chunk(ShotLds& S, int m, const int bins[5],
                                            float& h1) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int b0 = tid, b1 = tid + 256;
+  SPROF_T(h0t);
   if (tid < m) {
     const uint64_t bit = 1ull << (tid & 63);
 #pragma unroll
     for (int s = 0; s < 5; ++s)
-      if (bins[s] >= 0) atomicOr(reinterpret_cast<unsigned long long*>(&S.upd.mask[bins[s]][tid >> 6]), bit);
+      if (bins[s] >= 0) atomicOr(reinterpret_cast<unsigned long long*>(&S.upd.mask[tid >> 6][bins[s]]), bit);
   }
   __syncthreads();
-  // hit counts -> exclusive offsets (wave 0: 6 bins per lane, then a wave scan)
-  if (tid < 64) {
-    int c[6], tot = 0;
+  SPROF_T(h1t);
+  SPROF_ADD(0, h0t, h1t);
+  // hit counts -> exclusive offsets: thread t counts its bins t and t + 256 (the bins it sums
+  // below), wave scans, the eight segment totals through LDS
+  int c0 = 0, c1 = 0;
 #pragma unroll
-    for (int i = 0; i < 6; ++i) {
-      const int bb = tid * 6 + i;
-      c[i] = 0;
-      if (bb < kLen)
-        for (int w = 0; w < kMaskWords; ++w) c[i] += __popcll(S.upd.mask[bb][w]);
-      tot += c[i];
-    }
-    int incl = tot;
+  for (int w = 0; w < kMaskWords; ++w) c0 += __popcll(S.upd.mask[w][b0]);
+  if (b1 < kLen)
 #pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const int y = __shfl_up(incl, o);
-      if (lane >= o) incl += y;
-    }
-    int run = incl - tot;
+    for (int w = 0; w < kMaskWords; ++w) c1 += __popcll(S.upd.mask[w][b1]);
+  int i0 = c0, i1 = c1;
 #pragma unroll
-    for (int i = 0; i < 6; ++i) {
-      const int bb = tid * 6 + i;
-      if (bb < kLen) S.upd.off[bb] = run;
-      run += c[i];
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y0 = __shfl_up(i0, o), y1 = __shfl_up(i1, o);
+    if (lane >= o) { i0 += y0; i1 += y1; }
+  }
+  const int wv = tid >> 6;
+  if (lane == 63) { S.upd.seg[wv] = i0; S.upd.seg[4 + wv] = i1; }
+  __syncthreads();
+  {
+    int p0 = 0, p1 = 0;
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const int s0 = S.upd.seg[v], s1 = S.upd.seg[4 + v];
+      p1 += s0;
+      if (v < wv) { p0 += s0; p1 += s1; }
     }
+    S.upd.off[b0] = p0 + i0 - c0;
+    if (b1 < kLen) S.upd.off[b1] = p1 + i1 - c1;
   }
   __syncthreads();
+  SPROF_T(h2t);
+  SPROF_ADD(1, h1t, h2t);
   if (tid < m) {  // scatter: rank = hits of the bin from lower neighbours of the chunk
     const int wq = tid >> 6;
     const uint64_t below = lanemask_lt();
@@ -386,21 +396,21 @@ __device__ __forceinline__ void hist_chunk(ShotLds& S, int m, const int bins[5],
     for (int s = 0; s < 5; ++s) {
       const int bb = bins[s];
       if (bb < 0) continue;
-      int r = __popcll(S.upd.mask[bb][wq] & below);
-      for (int w = 0; w < wq; ++w) r += __popcll(S.upd.mask[bb][w]);
+      int r = __popcll(S.upd.mask[wq][bb] & below);
+      for (int w = 0; w < wq; ++w) r += __popcll(S.upd.mask[w][bb]);
       S.upd.val[S.upd.off[bb] + r] = vals[s];
     }
   }
   __syncthreads();
+  SPROF_T(h3t);
+  SPROF_ADD(2, h2t, h3t);
 #pragma unroll
   for (int o = 0; o < 2; ++o) {
     const int b = o ? b1 : b0;
     if (b < kLen) {
-      int cnt = 0;
-      for (int w = 0; w < kMaskWords; ++w) {
-        cnt += __popcll(S.upd.mask[b][w]);
-        S.upd.mask[b][w] = 0;  // ready for the next chunk
-      }
+      const int cnt = o ? c1 : c0;
+#pragma unroll
+      for (int w = 0; w < kMaskWords; ++w) S.upd.mask[w][b] = 0;  // ready for the next chunk
       const float* v = S.upd.val + S.upd.off[b];
       float h = o ? h1 : h0;
       int i = 0;
@@ -413,11 +423,13 @@ __device__ __forceinline__ void hist_chunk(ShotLds& S, int m, const int bins[5],
     }
   }
   __syncthreads();
+  SPROF_T(h4t);
+  SPROF_ADD(3, h3t, h4t);
 }
 
 __device__ __forceinline__ void hist_clear(ShotLds& S) {
   for (int i = threadIdx.x; i < kLen; i += 256)
-    for (int w = 0; w < kMaskWords; ++w) S.upd.mask[i][w] = 0;
+    for (int w = 0; w < kMaskWords; ++w) S.upd.mask[w][i] = 0;
   __syncthreads();
 }
 
@@ -610,7 +622,8 @@ __global__ void __launch_bounds__(256) k_shot(GridView g, const float* __restric
 }
 
 // the split kernels' views of the surface: caller index -> cell-sorted position, and the normals
-// in cell order
+// in cell order (round 5: the records gathered from caller-order packed copies instead -- one
+// global round, not two -- measured 0.92 -> 0.97 ms: the cell-sorted gathers' locality wins)
 __global__ void k_shot_prep(const int32_t* __restrict__ perm, int64_t n, const float* __restrict__ nx,
                             const float* __restrict__ ny, const float* __restrict__ nz, int32_t* __restrict__ ipos,
                             float4* __restrict__ snp) {
@@ -769,8 +782,11 @@ __global__ void __launch_bounds__(256, PFX_SHOT_HIST_WG) k_shot_frame(int64_t ba
       S.plusN = 0;
     }
     __syncthreads();
+    SPROF_T(f0t);
     shot_frame(S, src, k, k - sq[l].n_invalid);
     __syncthreads();
+    SPROF_T(f1t);
+    SPROF_ADD(6, f0t, f1t);
     if (tid < 9) rfo[tid] = S.rf[tid];
     const f3 fx = mk3(S.rf[0], S.rf[1], S.rf[2]), fy = mk3(S.rf[3], S.rf[4], S.rf[5]),
              fz = mk3(S.rf[6], S.rf[7], S.rf[8]);
@@ -786,12 +802,18 @@ __global__ void __launch_bounds__(256, PFX_SHOT_HIST_WG) k_shot_frame(int64_t ba
       reinterpret_cast<float4*>(u)[2 * j + 1] = b;
     }
     __syncthreads();  // S is rewritten by the next query
+    SPROF_T(f2t);
+    SPROF_ADD(9, f1t, f2t);
+    SPROF_ADD(14, 0, 1);
   }
 }
 
 // D: the histogram from the update records, normalisation, descriptor (no double-precision
 // interpolation here: a light kernel, many workgroups per CU)
-__global__ void __launch_bounds__(256) k_shot_accum(int64_t base, int64_t nq, float* __restrict__ desc,
+#ifndef PFX_SHOT_ACCUM_WG
+#define PFX_SHOT_ACCUM_WG 8
+#endif
+__global__ void __launch_bounds__(256, PFX_SHOT_ACCUM_WG) k_shot_accum(int64_t base, int64_t nq, float* __restrict__ desc,
                                                     const uint4* __restrict__ upd,
                                                     const ShotQuery* __restrict__ sq) {
   __shared__ ShotLds S;
@@ -799,6 +821,7 @@ __global__ void __launch_bounds__(256) k_shot_accum(int64_t base, int64_t nq, fl
   for (int64_t l = blockIdx.x; l < nq; l += gridDim.x) {
     if (sq[l].status != 0) continue;
     const int k = sq[l].k;
+    SPROF_T(a0t);
     const uint4* u = upd + l * 2 * kCapSmall;
     float h0 = 0.0f, h1 = 0.0f;
     hist_clear(S);
@@ -827,6 +850,9 @@ __global__ void __launch_bounds__(256) k_shot_accum(int64_t base, int64_t nq, fl
       hist_chunk(S, m, bins, vals, h0, h1);
     }
     hist_finish(S, h0, h1, desc + (base + l) * kLen, nullptr);
+    SPROF_T(a1t);
+    SPROF_ADD(4, a0t, a1t);
+    SPROF_ADD(5, 0, 1);
   }
 }
 
@@ -902,6 +928,10 @@ void shot_dev(pfx_ctx* ctx, const float* sx, const float* sy, const float* sz, c
     PFX_HIP(hipMemcpyFromSymbol(pr, HIP_SYMBOL(g_shot_prof), sizeof(pr)));
     const double nq_ = (double)(pr[13] + !pr[13]);
     fprintf(stderr, "shot_accum normalisation %.0f cycles/query (%llu sequential)\n", pr[8] / nq_, pr[7]);
+    const double na = (double)(pr[5] + !pr[5]), nf = (double)(pr[14] + !pr[14]);
+    fprintf(stderr, "shot_accum cycles/query %.0f: masks %.0f counts %.0f scatter %.0f sums %.0f (%llu queries)\n",
+            pr[4] / na, pr[0] / na, pr[1] / na, pr[2] / na, pr[3] / na, pr[5]);
+    fprintf(stderr, "shot_frame cycles/query: frame %.0f updates %.0f\n", pr[6] / nf, pr[9] / nf);
     fprintf(stderr, "shot_lrf cycles/query: search+sort %.0f records %.0f chains %.0f\n", pr[10] / (double)(pr[13] + !pr[13]),
             pr[11] / (double)(pr[13] + !pr[13]), pr[12] / (double)(pr[13] + !pr[13]));
     const unsigned long long z[16] = {};
