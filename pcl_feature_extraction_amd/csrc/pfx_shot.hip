@@ -142,10 +142,11 @@ struct ShotLds {
                                         // the bin owners' reads are lane-consecutive)
       int off[kLen + 1];                // bucket offsets (exclusive scan of the hit counts)
       int seg[8];                       // the counts' scan: totals of the 64-bin segments
+      uint32_t pw[kLen];                // per bin: hits from waves < 1, < 2, < 3 (a byte each)
       float val[5 * kChunk];            // the chunk's update values bucketed by bin, neighbour order
     } upd;
+    alignas(16) float hist[kLen];  // the finished histogram (written once the chunks are binned)
   };
-  alignas(16) float hist[kLen];
   double cov[10];
   double axes[6];  // v1 (x axis), v3 (z axis)
   int lrf_l[4];    // normalisation: per-wave smallest lsb exponent and largest square
@@ -360,12 +361,26 @@ __device__ __forceinline__ void hist_chunk(ShotLds& S, int m, const int bins[5],
   SPROF_ADD(0, h0t, h1t);
   // hit counts -> exclusive offsets: thread t counts its bins t and t + 256 (the bins it sums
   // below), wave scans, the eight segment totals through LDS
+  static_assert(kMaskWords == 4, "one byte per lower wave");
   int c0 = 0, c1 = 0;
+  {
+    uint32_t pw = 0;
 #pragma unroll
-  for (int w = 0; w < kMaskWords; ++w) c0 += __popcll(S.upd.mask[w][b0]);
-  if (b1 < kLen)
+    for (int w = 0; w < kMaskWords; ++w) {
+      c0 += __popcll(S.upd.mask[w][b0]);
+      if (w < kMaskWords - 1) pw |= (uint32_t)c0 << (8 * w);
+    }
+    S.upd.pw[b0] = pw;
+  }
+  if (b1 < kLen) {
+    uint32_t pw = 0;
 #pragma unroll
-    for (int w = 0; w < kMaskWords; ++w) c1 += __popcll(S.upd.mask[w][b1]);
+    for (int w = 0; w < kMaskWords; ++w) {
+      c1 += __popcll(S.upd.mask[w][b1]);
+      if (w < kMaskWords - 1) pw |= (uint32_t)c1 << (8 * w);
+    }
+    S.upd.pw[b1] = pw;
+  }
   int i0 = c0, i1 = c1;
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) {
@@ -397,7 +412,7 @@ __device__ __forceinline__ void hist_chunk(ShotLds& S, int m, const int bins[5],
       const int bb = bins[s];
       if (bb < 0) continue;
       int r = __popcll(S.upd.mask[wq][bb] & below);
-      for (int w = 0; w < wq; ++w) r += __popcll(S.upd.mask[w][bb]);
+      if (wq) r += (int)((S.upd.pw[bb] >> (8 * (wq - 1))) & 0xffu);
       S.upd.val[S.upd.off[bb] + r] = vals[s];
     }
   }
