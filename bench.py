@@ -736,8 +736,8 @@ def scans_line(args, world, n_scans, scans_here, shot, elapsed, timers, iso, nb_
         shot_gbs = sbytes / shot_s / 1e9 if shot_s > 0 else 0.0
         stage = roofline
         stage.pop("bound")
-        roofline = {"bound": "hbm", "kernel": "SHOT stage: k_shot_prep + k_shot_lrf + k_shot_eigen + k_shot_hist "
-                                              "(+ k_shot<16384> for lists over 2,048)",
+        roofline = {"bound": "hbm", "kernel": "SHOT stage: k_shot_ipos + k_shot_prep + k_shot_lrf + k_shot_eigen + "
+                                              "k_shot_frame + k_shot_accum (+ k_shot<16384> for lists over 2,048)",
                     "achieved": round(shot_gbs, 2), "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": round(shot_gbs / HBM_PEAK_GBS, 5), "traffic": None,
                     "algorithmic_bytes_per_launch": int(sbytes), "avg_ms": round(shot_s * 1e3, 4),
