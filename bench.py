@@ -49,7 +49,7 @@ DENSE_POINTS = 10_000_000  # SURVEY 8(d) dense variant: configs[2]'s scene at 10
 SHOT_SAMPLE = 10_000
 CYCLE_SEEDS = [2, 100, 101, 102]  # the headline's distinct scans: configs[2]'s seed first
 
-VERBOSE_TIMERS = ["grid_bbox", "grid_build", "normals", "normals_fast", "normals_mfma", "normals_lists_phase", "normals_tiles", "normals_lists",
+VERBOSE_TIMERS = ["narf", "grid_bbox", "grid_build", "normals", "normals_fast", "normals_mfma", "normals_lists_phase", "normals_tiles", "normals_lists",
                   "normals_lists_small", "normals_lists_sparse",
                   "normals_lists_dense", "normals_lists_wide", "normals_lists_query", "normals_chain", "normals_chain_big", "normals_long", "range_image",
                   "narf_border", "narf_interest", "narf_nms", "narf_gather", "fpfh_mark", "fpfh_spfh",
@@ -107,7 +107,14 @@ def _cpu_timed_runs(x, y, z, workload, sample, reps, threads):
     for _ in range(reps):
         t, outputs, nrows = once(x, y, z, sample)
         times.append(t)
-    return times, outputs, nrows
+    # BASELINE.md's all-single-threaded figure: the normal estimation once more on one thread
+    # (NARF and FPFH already run on one); one run, not a median (~35-60 s)
+    single_normals = -1.0
+    if workload == "fpfh" and os.environ.get("PFX_CPU_SINGLE", "1") != "0":
+        t0 = time.perf_counter()
+        O.normals(x, y, z, 0.05, threads=1)
+        single_normals = time.perf_counter() - t0
+    return times, outputs, nrows, single_normals
 
 
 def cpu_child(path):
@@ -124,12 +131,12 @@ def cpu_child(path):
     except (AttributeError, OSError):
         cpus = []
     sample = f["sample"] if f["has_sample"] else None
-    times, (kp, nrm, desc), nrows = _cpu_timed_runs(f["x"], f["y"], f["z"], str(f["workload"]), sample,
-                                                    int(f["reps"]), threads)
+    times, (kp, nrm, desc), nrows, single_normals = _cpu_timed_runs(f["x"], f["y"], f["z"], str(f["workload"]),
+                                                                    sample, int(f["reps"]), threads)
     if isinstance(desc, tuple):
         desc = desc[0]
     np.savez(path + ".out.npz", times=np.asarray(times), kp=np.asarray(kp), nx=nrm[0], ny=nrm[1], nz=nrm[2],
-             desc=np.asarray(desc), nrows=nrows, cpus=np.asarray(cpus, np.int64))
+             desc=np.asarray(desc), nrows=nrows, cpus=np.asarray(cpus, np.int64), single_normals=single_normals)
 
 
 def cpu_baseline(x, y, z, workload, sample=None, reps=5):
@@ -156,13 +163,23 @@ def cpu_baseline(x, y, z, workload, sample=None, reps=5):
         desc = r["desc"]
         outputs = (r["kp"], (r["nx"], r["ny"], r["nz"]), (desc,) if workload != "fpfh" else desc)
         nrows, cpus = int(r["nrows"]), [int(c) for c in r["cpus"]]
+        single_normals = float(r["single_normals"]) if "single_normals" in r.files else -1.0
     tot = [sum(t) for t in times]
     order = sorted(range(len(tot)), key=lambda i: tot[i])
     mid = order[len(order) // 2]  # the median run (reps odd)
     med = tot[mid]
     stage_med = list(times[mid])
     feat = "FPFH 1 thread" if workload == "fpfh" else f"SHOT {threads} threads"
-    return dict(seconds=med, threads=threads, outputs=outputs, runs=[round(v, 3) for v in sorted(tot)],
+    single = None
+    if single_normals > 0:  # NARF and FPFH of the median run (one thread each) + normals on one thread
+        secs = stage_med[0] + single_normals + stage_med[2]
+        single = {"value": round(len(x) / secs / 1e6, 6), "unit": "Mpoints/s", "cores": 1, "seconds": round(secs, 3),
+                  "normals_1_thread_s": round(single_normals, 3),
+                  "note": "BASELINE.md's all-single-threaded figure: NARF + FPFH of the median run (one thread each) "
+                          "+ one single-threaded run of the normal estimation on the same scan"}
+    return dict(seconds=med, threads=threads, outputs=outputs, runs=[round(v, 3) for v in sorted(tot)], single=single,
+                stages_s={"narf": round(stage_med[0], 3), "normals": round(stage_med[1], 3),
+                          "features": round(stage_med[2], 3)},
                 spread=round((max(tot) - min(tot)) / med, 4),
                 pinning={"OMP_PROC_BIND": "close", "OMP_PLACES": "cores", "cpus": cpus},
                 sample=(f"the first 1M-point scan of the timed cycle through the CPU restatement (oracle/), 1 warm-up "
@@ -564,6 +581,10 @@ def bench_scans(args, torch, dist, dev, world, rank, local):
             cb = cpu_baseline(x, y, z, "fpfh" if demand else args.workload, sample_np)
             cpu = {"value": round(npts / cb["seconds"] / 1e6, 6), "unit": "Mpoints/s",
                    "cores": cb["threads"], "kind": "port", "sample": cb["sample"], "runs_s": cb["runs"],
+                   "stages_s": cb["stages_s"], "all_single_threaded": cb["single"],
+                   "cores_note": ("OMP_NUM_THREADS = the box's CPU share for one GPU (16; nproc reports the whole "
+                                  "host, shared by its eight GPUs' jobs): BASELINE.md's 'all host cores' for the OpenMP "
+                                  "legs of a one-GPU job"),
                    "spread": cb["spread"], "pinning": cb["pinning"],
                    **host_info(),
                    "parity": full_size_parity(cb["outputs"], kp0, scans[0], sb.desc if shot else scans[0].desc, rows0,
@@ -577,6 +598,13 @@ def bench_scans(args, torch, dist, dev, world, rank, local):
                         oracle_outputs(hx_, hy_, hz_), resident[j][0], scans[j], scans[j].desc, resident[j][1], False)})
                 line["parity_all_scans"] = all(all(v for k, v in d.items() if k != "seed")
                                                for d in [cpu["parity"]] + cpu["parity_cycle"])
+                line["parity_all_scans_note"] = (
+                    "bit-exact against the CPU restatement (oracle/), itself unpinned against real PCL (absent). "
+                    "The keypoints of these four rooms depend on std::sort's tie order in NarfKeypoint's greedy "
+                    "selection: 6/6/11/9 tied NMS survivor pairs closer than 0.05 m, and 4/7/4/6 of their 83-89 "
+                    "keypoints move between the two extreme tie orders (profiles/r05_narf_tie_report.jsonl). The GPU "
+                    "path and the oracle sort with this build's libstdc++ and agree; a PCL built with another "
+                    "standard library may order those ties differently. The reference's own four clouds have no ties.")
             if demand:
                 cpu["note"] = ("the reference's CPU path (every normal, as PCL computes them): the descriptors and "
                                "keypoints are the outputs compared; normals compared on the support only")
@@ -774,12 +802,25 @@ def scans_line(args, world, n_scans, scans_here, shot, elapsed, timers, iso, nb_
             workload = (f"SURVEY 8(d) dense variant: configs[2]'s room scene (same scale) at {npts // 1_000_000}M "
                         f"points, NARF(support 0.2) + normals(r 0.05) + FPFH(r 0.08) at the keypoints")
             data = f"synthetic (synth_room at 10x density: {npts} points, k(0.05)~{int(nb / npts)}; see synth.py)"
+    # the critical path: every stage's HIP-event time on its own stream inside the
+    # timed region, per scan -- NARF on the main stream beside the normal estimation on the side
+    # stream, then FPFH's SPFH and weighting on the main stream behind the normals
+    stages = {}
+    for nm, key in (("narf", "narf"), ("normals", "normals_fast" if fast else "normals"), ("fpfh_spfh", "fpfh_spfh"),
+                    ("fpfh_weight", "fpfh_weight"), ("shot", "shot")):
+        ms, calls = timers.get(key, (0.0, 0))
+        if calls:
+            stages[nm] = round(ms / max(per_scan_calls, 1), 4)
+    stages_note = ("HIP events around each stage on its stream, inside the timed region, per scan; NARF (range image, "
+                   "borders, interest, NMS + the host greedy selection, keypoint gather) runs on the main stream while "
+                   "the normal estimation runs on the side stream, then SPFH and the weighting follow the normals")
     return {
         "metric": metric, "value": round(value, 4), "unit": "Mpoints/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
         "higher_is_better": True, "scaling": scaling, "vs_baseline": None, "dtype": "f32", "data": data,
         "config": {"workload": workload, "points_per_scan": npts, "scans_per_step": n_scans,
                    "image": "640x480", "parallelism": f"scan-per-gpu x{world}"},
+        "stages_ms_per_scan": stages, "stages_note": stages_note,
         "roofline": roofline,
     }
 

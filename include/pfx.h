@@ -202,7 +202,7 @@ pfx_status pfx_normals_finish_dev(pfx_ctx* ctx, int32_t* rerun);
  * clears it. */
 pfx_status pfx_normals_gate_dev(pfx_ctx* ctx, void* hip_event);
 /* Scheduling aid: queue the (speculative) grid of the next pfx_normals_launch_dev /
- * pfx_normals_dev on the same d_x, n and radius now, so the caller can issue it before another
+ * pfx_normals_dev on the same d_x, d_y, d_z, n and radius now, so the caller can issue it before another
  * stream's work (and that work's gate, pfx_normals_gate_dev) and the estimation's lists after.
  * Results are unchanged; any other call in between on ctx discards it. */
 pfx_status pfx_normals_grid_launch_dev(pfx_ctx* ctx, const float* d_x, const float* d_y, const float* d_z,

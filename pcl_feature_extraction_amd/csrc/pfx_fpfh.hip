@@ -604,6 +604,16 @@ __device__ __forceinline__ int lsb_exp(float v) {
   return (e ? e : 1) - 150 + __builtin_ctz(m);
 }
 
+// lsb_exp without branches (v != 0; a select instead of the early return), for the per-neighbour
+// step of k_fpfh_weight_lists
+__device__ __forceinline__ int lsb_exp_select(float v) {
+  const uint32_t b = __float_as_uint(v);
+  const int e = (int)((b >> 23) & 0xff);
+  const uint32_t m = (b & 0x7fffffu) | (e ? 0x800000u : 0u);
+  const int r = (e ? e : 1) - 150 + __builtin_ctz(m);
+  return e == 255 ? 1000 : r;
+}
+
 // Weighting: one 1024-thread workgroup per query.  The 33 float chains (strict FLANN order)
 // run one per lane over SPFH rows staged in LDS.  The three double block sums are formed in
 // parallel: every value is a non-negative float, so when all of them are multiples of 2^L and
@@ -804,6 +814,9 @@ __global__ void __launch_bounds__(kWT) k_fpfh_weight(GridView g, const float* __
 // neighbours' SPFH rows 8 at a time (loads in flight together).  Block sums: each lane's double
 // partial sum + smallest binade, combined in any order when exact (as k_fpfh_weight), else PCL's
 // sequential loop by one lane per block.
+#ifndef PFX_WL_PIPE
+#define PFX_WL_PIPE 2
+#endif
 __device__ __forceinline__ int32_t entry_pos(uint32_t e, const int32_t (&rs)[9]) {
   const int r = entry_run(e);
   int32_t s = rs[0];
@@ -812,6 +825,7 @@ __device__ __forceinline__ int32_t entry_pos(uint32_t e, const int32_t (&rs)[9])
   return s + (int32_t)entry_off(e);
 }
 
+template <bool BUF>  // BUF: ns * 132 B < 2^31, the SPFH rows read through a buffer descriptor
 __global__ void __launch_bounds__(256) k_fpfh_weight_lists(GridView g, const int32_t* __restrict__ qpos,
                                                            const int64_t* __restrict__ loff,
                                                            const int32_t* __restrict__ lcnt,
@@ -825,11 +839,19 @@ __global__ void __launch_bounds__(256) k_fpfh_weight_lists(GridView g, const int
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int64_t nw = (int64_t)gridDim.x * 4;
   int kmax = 0;  // added to err[1] once per wave (same-address atomics serialise)
+#if PFX_WL_PIPE == 2
+  // the SPFH rows through a buffer descriptor (32-bit offsets; the caller keeps ns * 132 B below
+  // 2^31): lanes >= 33 read bin 0 of the row (in range; their values are never stored)
+  const __amdgpu_buffer_rsrc_t srsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(spfh), 0, 0x7fffffff,
+                                                                          0x00020000);
+  const int vlane = (lane < kDesc ? lane : 0) * 4;
+#endif
   for (int64_t j = (int64_t)blockIdx.x * 4 + wv; j < nq; j += nw) {
-    const int32_t qp = qpos[j];
-    const int k = lcnt[j];
+    // (wave-uniform: scalar registers, so the per-neighbour bounds stay scalar)
+    const int32_t qp = __builtin_amdgcn_readfirstlane(qpos[j]);
+    const int k = __builtin_amdgcn_readfirstlane(lcnt[j]);
     const int64_t off = loff[j];
-    const int lg = llg[j];
+    const int lg = __builtin_amdgcn_readfirstlane(llg[j]);
     Runs R;
     block_runs(g, skeys[qp], R);
     int32_t rs[9];
@@ -840,6 +862,96 @@ __global__ void __launch_bounds__(256) k_fpfh_weight_lists(GridView g, const int
     float fh = 0.0f;
     double ps = 0.0;
     int pl = 1 << 20;
+#if PFX_WL_PIPE == 2
+    // Round 6: the per-neighbour step without branches or 64-bit address arithmetic.  The SPFH
+    // row load is a buffer load (descriptor built once, the row offset id * 132 B in an SGPR, the
+    // lane's bin offset in a VGPR); the double block partial sum adds every value (all are
+    // non-negative floats -- SPFH percentages times 1/d2 -- and a skipped neighbour's is +0, which
+    // leaves a non-negative double sum unchanged), and only the smallest set-bit exponent is
+    // selected per value.  The branchy form spent ~16 scalar instructions per neighbour on the exec
+    // mask (k_fpfh_weight_lists: 24 VALU + 16 SALU per neighbour step).
+    for (int c0 = 0; c0 < k; c0 += 64) {
+      const int m = min(64, k - c0);
+      const int32_t pos = lane < m ? entry_pos(list_entry(list, off, lg, c0 + lane), rs) : qp;
+      const int32_t idx = g.perm[pos];
+      const float4 p = g.sp[pos];
+      const float d2 = flann_d2(q.x, q.y, q.z, p.x, p.y, p.z);
+      const float w = (d2 == 0.0f || lane >= m) ? 0.0f : 1.0f / d2;  // 0: the query itself, or past m
+      for (int j0 = 0; j0 < m; j0 += 8) {
+        float v[8], wu[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int jj = j0 + u < m ? j0 + u : m - 1;
+          const int id = __builtin_amdgcn_readfirstlane(__builtin_amdgcn_readlane(idx, jj));
+          wu[u] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(w), j0 + u < 64 ? j0 + u : 63));
+          if constexpr (BUF) v[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(srsrc, vlane, id * (kDesc * 4), 0));
+          else v[u] = spfh[(int64_t)id * kDesc + (vlane >> 2)];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          // w = 0 adds +0 (rows finite, fh >= +0): PCL's `continue`, bit for bit
+          const float val = v[u] * wu[u];
+          fh = fh + val;
+          ps += (double)val;
+          pl = val != 0.0f ? min(pl, lsb_exp_select(val)) : pl;
+        }
+      }
+    }
+#elif PFX_WL_PIPE
+    // Software-pipelined over batches of 8 neighbours (round 6): the SPFH rows of batch b + 1 are
+    // loaded while batch b is summed, and each 64-entry chunk's entries are resolved (position,
+    // caller index, 1/d2) one chunk ahead -- the loop used to wait one L2 latency per batch.
+    auto resolve = [&](int c0, int32_t& idx, float& w) {
+      const int m = min(64, k - c0);
+      const int32_t pos = lane < m ? entry_pos(list_entry(list, off, lg, c0 + lane), rs) : qp;
+      idx = g.perm[pos];
+      const float4 p = g.sp[pos];
+      const float d2 = flann_d2(q.x, q.y, q.z, p.x, p.y, p.z);
+      w = d2 == 0.0f ? 0.0f : 1.0f / d2;  // 0 marks a skipped neighbour (the query itself)
+    };
+    const int nbat = (k + 7) >> 3;
+    int32_t idxA = qi, idxB = qi;  // the chunk of the batch being loaded, and the chunk after it
+    float wA = 0.0f, wB = 0.0f;
+    if (k > 0) resolve(0, idxA, wA);
+    if (k > 64) resolve(64, idxB, wB);
+    auto load_batch = [&](int b, int32_t idx, float w, float (&v)[8], float (&wu)[8]) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int e = 8 * b + u;  // neighbour index in the list
+        const int jj = e < k ? (e & 63) : ((k - 1) & 63);
+        const int id = __builtin_amdgcn_readlane(idx, jj);
+        wu[u] = e < k ? __int_as_float(__builtin_amdgcn_readlane(__float_as_int(w), jj)) : 0.0f;
+        v[u] = lane < kDesc ? spfh[(int64_t)id * kDesc + lane] : 0.0f;
+      }
+    };
+    float v[8], wu[8];
+    if (nbat > 0) load_batch(0, idxA, wA, v, wu);
+    for (int b = 0; b < nbat; ++b) {
+      float vn[8], wn[8];
+      const int b1 = b + 1;
+      if ((b1 & 7) == 0 && b1 < nbat) {  // batch b + 1 opens the next chunk: rotate, resolve one more
+        idxA = idxB;
+        wA = wB;
+        if (64 * (b1 / 8 + 1) < k) resolve(64 * (b1 / 8 + 1), idxB, wB);
+      }
+      if (b1 < nbat) load_batch(b1, idxA, wA, vn, wn);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        // w = 0 adds +0 (rows finite, fh >= +0): PCL's `continue`, bit for bit
+        const float val = v[u] * wu[u];
+        fh = fh + val;
+        if (wu[u] != 0.0f && val != 0.0f) {
+          ps += (double)val;
+          pl = min(pl, lsb_exp(val));
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        v[u] = vn[u];
+        wu[u] = wn[u];
+      }
+    }
+#else
     for (int c0 = 0; c0 < k; c0 += 64) {
       const int m = min(64, k - c0);
       const int32_t pos = lane < m ? entry_pos(list_entry(list, off, lg, c0 + lane), rs) : qp;
@@ -868,6 +980,7 @@ __global__ void __launch_bounds__(256) k_fpfh_weight_lists(GridView g, const int
         }
       }
     }
+#endif
     if (lane < kDesc) {
       s_ps[wv][lane] = ps;
       s_pl[wv][lane] = pl;
@@ -1112,7 +1225,7 @@ void fpfh_dev(pfx_ctx* ctx, const float* sx, const float* sy, const float* sz, c
   int2* slowq = ctx->buf("fpfh_slowq").as<int2>(slow_cap);
   {
     // the S count stays on the device: grid-stride launches sized for the worst case
-    TimeScope ts(ctx, "fpfh_spfh");
+    TimeScope ts(ctx, "fpfh_spfh", true);
     // 16 waves per CU (measured, 1M-point room: 8 -> 1.06 ms, 12 -> 1.13, 16 -> 0.94, 20 -> 0.99,
     // 32 -> 1.24, 128 -> 2.45)
     const int64_t waves = std::min<int64_t>(ns, 256 * 4 * 16);
@@ -1124,7 +1237,7 @@ void fpfh_dev(pfx_ctx* ctx, const float* sx, const float* sy, const float* sz, c
     check_launch("k_fpfh_spfh");
   }
   if (same) {  // input == surface: FLANN-ordered lists of every grid point, a wave per query
-    TimeScope ts(ctx, "fpfh_weight");
+    TimeScope ts(ctx, "fpfh_weight", true);
     // Features::compute estimates the normals of the same cloud first (features.h:187-195):
     // when that search had this radius, its lists are this one's (grid_a indexes the same
     // points); otherwise they are built on the FPFH grid
@@ -1140,11 +1253,18 @@ void fpfh_dev(pfx_ctx* ctx, const float* sx, const float* sy, const float* sz, c
     ctx->stats["fpfh_weight_lists_reused"] = reuse ? 1 : 0;
     k_nan_rows_nonfinite<<<(unsigned)ceil_div(ns * kDesc, 256), 256, 0, st>>>(sx, sy, sz, ns, out);
     if (L.nq > 0)
-      k_fpfh_weight_lists<<<(unsigned)std::min<int64_t>(ceil_div(L.nq, 4), 256 * 8), 256, 0, st>>>(
-          reuse ? view(ctx->grid_a) : g, L.qpos, L.off, L.cnt, L.lg, L.list, L.skeys, L.nq, spfh, out, err);
+    {
+      const unsigned bl = (unsigned)std::min<int64_t>(ceil_div(L.nq, 4), 256 * 8);
+      const GridView gv = reuse ? view(ctx->grid_a) : g;
+      if (ns * kDesc * 4 < ((int64_t)1 << 31))
+        k_fpfh_weight_lists<true><<<bl, 256, 0, st>>>(gv, L.qpos, L.off, L.cnt, L.lg, L.list, L.skeys, L.nq, spfh, out, err);
+      else
+        k_fpfh_weight_lists<false><<<bl, 256, 0, st>>>(gv, L.qpos, L.off, L.cnt, L.lg, L.list, L.skeys, L.nq, spfh, out,
+                                                       err);
+    }
     check_launch("k_fpfh_weight_lists");
   } else {
-    TimeScope ts(ctx, "fpfh_weight");
+    TimeScope ts(ctx, "fpfh_weight", true);
     const size_t lds = sizeof(uint64_t) * 2 * kCapW;
     PFX_HIP(hipFuncSetAttribute((const void*)k_fpfh_weight<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     const unsigned blocks = (unsigned)std::min<int64_t>(nq, 256 * 2);

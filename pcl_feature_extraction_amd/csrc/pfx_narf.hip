@@ -1305,6 +1305,8 @@ int64_t narf_dev(pfx_ctx* ctx, const float* x, const float* y, const float* z, i
             "narf: pixel_radius_plane_extraction must be in [0, 4]");
   NarfState& S = state(ctx);
   hipStream_t st = ctx->stream;
+  // the whole keypoint call on its stream (host round trips included): a stage timer
+  TimeScope total(ctx, "narf", true);
   Img I = make_img(cam);
   S.w = I.w;
   S.h = I.h;

@@ -77,7 +77,7 @@ struct NormalsState {
   bool pending = false;
   // normals_grid_launch_dev: grid_a build `grid_ahead_gen` queued for (x, n, r); 0: none
   uint64_t grid_ahead_gen = 0;
-  const float* grid_ahead_x = nullptr;
+  const float *grid_ahead_x = nullptr, *grid_ahead_y = nullptr, *grid_ahead_z = nullptr;
   int64_t grid_ahead_n = 0;
   double grid_ahead_r = 0.0;
   float vp[3] = {0.f, 0.f, 0.f};
@@ -89,8 +89,11 @@ struct NormalsState {
 // defer: launch the list kernels and return without the host readback (out.nq = an upper bound,
 // out.nq_dev = the device count); consumers may be launched behind them in stream order, and
 // build_lists_check must follow.
+// gate: the normal estimation's builds only -- wait for (and clear) the event of
+// pfx_normals_gate_dev right before the list kernels; other builds leave it for the next
+// normal estimation (the pfx.h contract).
 void build_lists(pfx_ctx* ctx, const Grid& g, const uint8_t* mask, double radius, bool sorted, NbLists& out,
-                 const char* tag, bool defer = false, int want = 1, bool compact = false);
+                 const char* tag, bool defer = false, int want = 1, bool compact = false, bool gate = false);
 // The deferred build's readback: true and `out` completed (exact nq, statistics) when the lists are
 // valid; false when they must be rebuilt synchronously (list buffer too small, first very long
 // lists, or a speculative grid with points outside its bounds) -- their consumers rerun too.

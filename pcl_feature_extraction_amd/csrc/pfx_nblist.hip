@@ -22,6 +22,9 @@ namespace pfx {
 namespace {
 
 constexpr int kQ = 16;  // tile: consecutive queries of one cell
+#ifndef PFX_SORT_PAIR
+#define PFX_SORT_PAIR 0
+#endif
 typedef float pf2 __attribute__((ext_vector_type(2)));  // packed f32 pair (v_pk_add_f32 / v_pk_mul_f32)
 constexpr int kArena = 16384;   // list entries per arena reservation of a tile workgroup (> a typical tile)
 constexpr int kArenaQuery = 16384;  // ... of a per-query workgroup (lists of 1k-4k entries)
@@ -232,12 +235,35 @@ struct CandGlobal {
 };
 
 #ifdef PFX_SHOT_PROFILE
+// phase probes, accumulated in registers and added to the globals once per workgroup / wave at
+// the kernel's end (an atomic per probe left global atomics outstanding that the kernel's own
+// vmcnt waits then waited for, inflating the very phases they measured)
 __device__ unsigned long long g_tile_prof[24];
+// per-wave probes (lane 0 of every wave): [class * 4 + i], class 0 small / 1 sparse / 2 dense;
+// i = 0 the wave's own sort work, 1 its wait at the barrier after the sort, 2 the staging round
+// (sort barrier -> staged registers stored), 3 the list-write loop
+__device__ unsigned long long g_tile_prof2[12];
+#define TPROF_DECL unsigned long long tacc_[24] = {}, wacc_[12] = {}
 #define TPROF_T(v) long long v = (threadIdx.x == 0) ? clock64() : 0
-#define TPROF_ADD(i, a, b) if (threadIdx.x == 0) atomicAdd(&g_tile_prof[i], (unsigned long long)((b) - (a)))
+#define TPROF_ADD(i, a, b) tacc_[i] += (unsigned long long)((b) - (a))
+#define WPROF_T(v) long long v = ((threadIdx.x & 63) == 0) ? clock64() : 0
+#define WPROF_ADD(i, a, b) wacc_[i] += (unsigned long long)((b) - (a))
+#define TPROF_FLUSH                                                                      \
+  do {                                                                                   \
+    if (threadIdx.x == 0)                                                                \
+      _Pragma("unroll") for (int i_ = 0; i_ < 24; ++i_)                                  \
+        if (tacc_[i_]) atomicAdd(&g_tile_prof[i_], tacc_[i_]);                           \
+    if ((threadIdx.x & 63) == 0)                                                         \
+      _Pragma("unroll") for (int i_ = 0; i_ < 12; ++i_)                                  \
+        if (wacc_[i_]) atomicAdd(&g_tile_prof2[i_], wacc_[i_]);                          \
+  } while (0)
 #else
+#define TPROF_DECL
 #define TPROF_T(v)
 #define TPROF_ADD(i, a, b)
+#define WPROF_T(v)
+#define WPROF_ADD(i, a, b)
+#define TPROF_FLUSH
 #endif
 
 // wave_sort for k <= 64 * E with every element's (t, d2, bucket, slot) kept in registers
@@ -269,12 +295,7 @@ __device__ __forceinline__ void wave_sort_regs(uint16_t* L, int k, float qx, flo
     int c[PER], sum = 0;
 #pragma unroll
     for (int v = 0; v < PER; ++v) { c[v] = bcount[lane * PER + v]; sum += c[v]; }
-    int inc = sum;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const int x = __shfl_up(inc, o);
-      if (lane >= o) inc += x;
-    }
+    const int inc = wave_incl_scan(sum);
     int ex = inc - sum;
 #pragma unroll
     for (int v = 0; v < PER; ++v) { bpos[lane * PER + v] = ex; ex += c[v]; }
@@ -340,7 +361,6 @@ template <int NB, class Cand>
 __device__ __forceinline__ void wave_sort(uint16_t* L, int k, float qx, float qy, float qz, const Cand& cand,
                                           float bscale, uint32_t* Sd, uint16_t* St, int* bcount, int* bpos,
                                           const GridView& g, const Runs& R, int lane) {
-  TPROF_T(w0);
   for (int b = lane; b < NB; b += 64) bcount[b] = 0;
   wave_sync();
   for (int e = lane; e < k; e += 64) {
@@ -351,26 +371,17 @@ __device__ __forceinline__ void wave_sort(uint16_t* L, int k, float qx, float qy
     atomicAdd(&bcount[b < NB ? b : NB - 1], 1);
   }
   wave_sync();
-  TPROF_T(w1);
-  TPROF_ADD(8, w0, w1);
   {
     constexpr int PER = NB / 64;
     int c[PER], s = 0;
 #pragma unroll
     for (int v = 0; v < PER; ++v) { c[v] = bcount[lane * PER + v]; s += c[v]; }
-    int inc = s;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const int x = __shfl_up(inc, o);
-      if (lane >= o) inc += x;
-    }
+    const int inc = wave_incl_scan(s);
     int ex = inc - s;
 #pragma unroll
     for (int v = 0; v < PER; ++v) { bpos[lane * PER + v] = ex; ex += c[v]; }
   }
   wave_sync();
-  TPROF_T(w2);
-  TPROF_ADD(9, w1, w2);
   for (int e = lane; e < k; e += 64) {
     const int t = L[e];
     float px, py, pz;
@@ -383,8 +394,6 @@ __device__ __forceinline__ void wave_sort(uint16_t* L, int k, float qx, float qy
     St[slot] = (uint16_t)t;
   }
   wave_sync();
-  TPROF_T(w3);
-  TPROF_ADD(10, w2, w3);
   // rank inside the bucket; two elements per lane per round and the first four bucket entries
   // read at once, so the LDS round trips of a round overlap
   auto bucket_rank = [&](int s, uint32_t d, int t, int st, int en) {
@@ -423,8 +432,6 @@ __device__ __forceinline__ void wave_sort(uint16_t* L, int k, float qx, float qy
     if (h1) L[st1 + r1] = (uint16_t)t1;
   }
   wave_sync();
-  TPROF_T(w4);
-  TPROF_ADD(11, w3, w4);
 }
 
 // k <= 64: one entry per lane, rank = entries with a smaller d2, counted over v_readlane (no
@@ -456,6 +463,193 @@ __device__ __forceinline__ void wave_rank_sort(uint16_t* L, int k, float qx, flo
   wave_sync();
   if (in) L[rank] = (uint16_t)t;
   wave_sync();
+}
+
+// Two lists of one wave sorted as one (round 6, the small tiles): elements 0..kA-1 are list A's,
+// kA..k-1 list B's, and B's buckets follow A's, so one pass of the bucket sort orders both and
+// every dependent LDS round serves two lists (a wave sorted its four lists one after another:
+// a chain of ~8 LDS round trips each).  Bucket words pack the count (low 16 bits) and, after the
+// scan, the running position (high 16 bits), so both lists' 2 NB buckets take the LDS of one
+// list's count and position arrays; the elements go to their lists' rows in bucket order (no
+// separate index scratch), so only their d2 bits need scratch (Sd, 2 LCAP entries).
+template <int NB, int E, class Cand>
+__device__ __forceinline__ void wave_sort_pair(uint16_t* LA, int kA, float ax, float ay, float az, uint16_t* LB,
+                                               int kB, float bx, float by, float bz, const Cand& cand, float bscale,
+                                               uint32_t* Sd, uint32_t* bw, const GridView& g, const Runs& R,
+                                               int lane) {
+  constexpr int NBT = 2 * NB, PER = NBT / 64;
+  static_assert(PER % 4 == 0, "bucket words are cleared and scanned four per 16-byte access");
+  const int k = kA + kB;
+#pragma unroll
+  for (int v = 0; v < PER; v += 4) reinterpret_cast<uint4*>(bw + lane * PER + v)[0] = make_uint4(0, 0, 0, 0);
+  int t[E], b[E];
+  uint32_t d[E];
+#pragma unroll
+  for (int i = 0; i < E; ++i) {
+    const int e = lane + 64 * i;
+    t[i] = e < kA ? LA[e] : (e < k ? LB[e - kA] : 0);
+  }
+  wave_sync();
+#pragma unroll
+  for (int i = 0; i < E; ++i) {
+    const int e = lane + 64 * i;
+    const bool inB = e >= kA;
+    float px, py, pz;
+    cand.get(t[i], px, py, pz);
+    const float d2 = flann_d2(inB ? bx : ax, inB ? by : ay, inB ? bz : az, px, py, pz);
+    d[i] = __float_as_uint(d2);  // d2 >= +0: bit order == value order
+    const int bb = (int)(d2 * bscale);
+    b[i] = (bb < NB ? bb : NB - 1) + (inB ? NB : 0);
+    if (e < k) atomicAdd(&bw[b[i]], 1u);
+  }
+  wave_sync();
+  {
+    uint32_t c[PER];
+    int sum = 0;
+#pragma unroll
+    for (int v = 0; v < PER; v += 4) {
+      const uint4 w4 = reinterpret_cast<const uint4*>(bw + lane * PER + v)[0];
+      c[v] = w4.x;
+      c[v + 1] = w4.y;
+      c[v + 2] = w4.z;
+      c[v + 3] = w4.w;
+    }
+#pragma unroll
+    for (int v = 0; v < PER; ++v) sum += (int)c[v];
+    uint32_t ex = (uint32_t)(wave_incl_scan(sum) - sum);
+#pragma unroll
+    for (int v = 0; v < PER; ++v) {
+      const uint32_t cnt = c[v];
+      c[v] = (ex << 16) | cnt;
+      ex += cnt;
+    }
+#pragma unroll
+    for (int v = 0; v < PER; v += 4)
+      reinterpret_cast<uint4*>(bw + lane * PER + v)[0] = make_uint4(c[v], c[v + 1], c[v + 2], c[v + 3]);
+  }
+  wave_sync();
+  int slot[E];
+#pragma unroll
+  for (int i = 0; i < E; ++i) slot[i] = lane + 64 * i < k ? (int)(atomicAdd(&bw[b[i]], 1u << 16) >> 16) : 0;
+#pragma unroll
+  for (int i = 0; i < E; ++i)
+    if (lane + 64 * i < k) {
+      Sd[slot[i]] = d[i];
+      if (slot[i] < kA) LA[slot[i]] = (uint16_t)t[i];
+      else LB[slot[i] - kA] = (uint16_t)t[i];
+    }
+  wave_sync();
+  // bucket [st, en): en = its position after the scatter; rank = keys of the bucket below mine
+  int st[E], rank[E];
+  bool tie = false;
+#pragma unroll
+  for (int i = 0; i < E; ++i) {
+    const uint32_t w = bw[b[i]];
+    const int en = (int)(w >> 16);
+    st[i] = en - (int)(w & 0xffffu);
+    uint32_t dv[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) dv[j] = st[i] + j < en ? Sd[st[i] + j] : 0xffffffffu;
+    int r = 0, eq = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      r += dv[j] < d[i];
+      eq += dv[j] == d[i];
+    }
+    for (int v = st[i] + 4; v < en; ++v) {
+      const uint32_t x = Sd[v];
+      r += x < d[i];
+      eq += x == d[i];
+    }
+    rank[i] = r;
+    tie |= lane + 64 * i < k && eq > 1;
+  }
+  if (__builtin_amdgcn_ballot_w64(tie)) {  // equal d2: the caller index decides (FLANN); rare
+#pragma unroll
+    for (int i = 0; i < E; ++i) {
+      if (lane + 64 * i >= k) continue;
+      const int en = (int)(bw[b[i]] >> 16);
+      const int32_t mine = g.perm[run_pos(R, t[i])];
+      for (int v = st[i]; v < en; ++v) {
+        if (v == slot[i] || Sd[v] != d[i]) continue;
+        const int tv = v < kA ? LA[v] : LB[v - kA];
+        if (g.perm[run_pos(R, tv)] < mine) ++rank[i];
+      }
+    }
+  }
+  wave_sync();  // every bucket-order entry read before the final positions overwrite them
+#pragma unroll
+  for (int i = 0; i < E; ++i)
+    if (lane + 64 * i < k) {
+      const int pos = st[i] + rank[i];
+      if (pos < kA) LA[pos] = (uint16_t)t[i];
+      else LB[pos - kA] = (uint16_t)t[i];
+    }
+  wave_sync();
+}
+
+// kA + kB <= 64: one entry per lane, ranked among the entries of its own list (v_readlane, no LDS)
+template <class Cand>
+__device__ __forceinline__ void wave_rank_sort_pair(uint16_t* LA, int kA, float ax, float ay, float az, uint16_t* LB,
+                                                    int kB, float bx, float by, float bz, const Cand& cand,
+                                                    const GridView& g, const Runs& R, int lane) {
+  const int k = kA + kB;
+  const bool in = lane < k, inB = lane >= kA;
+  const int t = lane < kA ? LA[lane] : (in ? LB[lane - kA] : 0);
+  float px, py, pz;
+  cand.get(t, px, py, pz);
+  const uint32_t d = in ? __float_as_uint(flann_d2(inB ? bx : ax, inB ? by : ay, inB ? bz : az, px, py, pz))
+                        : 0xffffffffu;
+  const int lo = inB ? kA : 0, hi = inB ? k : kA;  // the lanes of my list
+  int rank = 0, eq = 0;
+  for (int m = 0; m < k; ++m) {
+    const uint32_t dm = (uint32_t)__builtin_amdgcn_readlane((int)d, m);
+    const bool mine = m >= lo && m < hi;
+    rank += (mine && dm < d) ? 1 : 0;
+    eq += (mine && dm == d) ? 1 : 0;
+  }
+  if (__builtin_amdgcn_ballot_w64(in && eq > 1)) {
+    const int32_t id = in ? g.perm[run_pos(R, t)] : 0x7fffffff;
+    rank = 0;
+    for (int m = 0; m < k; ++m) {
+      const uint32_t dm = (uint32_t)__builtin_amdgcn_readlane((int)d, m);
+      const int32_t im = __builtin_amdgcn_readlane(id, m);
+      const bool mine = m >= lo && m < hi;
+      rank += (mine && (dm < d || (dm == d && im < id))) ? 1 : 0;
+    }
+  }
+  wave_sync();
+  if (in) {
+    if (inB) LB[rank] = (uint16_t)t;
+    else LA[rank] = (uint16_t)t;
+  }
+  wave_sync();
+}
+
+// the pair by the smallest register tier that holds kA + kB (<= 384, E <= 6: the register tiers
+// of the one-list sort in these kernels); a longer pair is sorted as two one-list passes
+template <int NB, class Cand>
+__device__ __forceinline__ void sort_pair_tiers(uint16_t* LA, int kA, float ax, float ay, float az, uint16_t* LB,
+                                                int kB, float bx, float by, float bz, const Cand& cand, float bscale,
+                                                uint32_t* Sd, uint32_t* bw, const GridView& g, const Runs& R, int lane) {
+  const int k = kA + kB;
+  if (k <= 64) wave_rank_sort_pair(LA, kA, ax, ay, az, LB, kB, bx, by, bz, cand, g, R, lane);
+  else if (k <= 128) wave_sort_pair<NB, 2>(LA, kA, ax, ay, az, LB, kB, bx, by, bz, cand, bscale, Sd, bw, g, R, lane);
+  else if (k <= 192) wave_sort_pair<NB, 3>(LA, kA, ax, ay, az, LB, kB, bx, by, bz, cand, bscale, Sd, bw, g, R, lane);
+  else if (k <= 256) wave_sort_pair<NB, 4>(LA, kA, ax, ay, az, LB, kB, bx, by, bz, cand, bscale, Sd, bw, g, R, lane);
+  else if (k <= 320) wave_sort_pair<NB, 5>(LA, kA, ax, ay, az, LB, kB, bx, by, bz, cand, bscale, Sd, bw, g, R, lane);
+  else wave_sort_pair<NB, 6>(LA, kA, ax, ay, az, LB, kB, bx, by, bz, cand, bscale, Sd, bw, g, R, lane);
+}
+template <int NB, class Cand>
+__device__ __forceinline__ void sort_pair(uint16_t* LA, int kA, float ax, float ay, float az, uint16_t* LB, int kB,
+                                          float bx, float by, float bz, const Cand& cand, float bscale, uint32_t* Sd,
+                                          uint32_t* bw, const GridView& g, const Runs& R, int lane) {
+  if (kA + kB <= 384) {
+    sort_pair_tiers<NB>(LA, kA, ax, ay, az, LB, kB, bx, by, bz, cand, bscale, Sd, bw, g, R, lane);
+  } else {
+    sort_pair_tiers<NB>(LA, kA, ax, ay, az, LA, 0, ax, ay, az, cand, bscale, Sd, bw, g, R, lane);
+    sort_pair_tiers<NB>(LB, kB, bx, by, bz, LB, 0, bx, by, bz, cand, bscale, Sd, bw, g, R, lane);
+  }
 }
 
 template <int NB, class Cand, bool SMALL = false>
@@ -615,9 +809,13 @@ __global__ void __launch_bounds__(256, TCAP <= kTcapSmall ? 4 : (STAGE ? 3 : 2))
   // (a miss stores its candidate to its lane's slot: the test loop has no branch)
   __shared__ uint16_t lists_flat[Q * (LCAP + 2) + 4 * 64];
   uint16_t(*lists)[LCAP + 2] = reinterpret_cast<uint16_t(*)[LCAP + 2]>(lists_flat);
-  __shared__ uint32_t sd[4][LCAP];
-  __shared__ uint16_t stt[4][LCAP];
-  __shared__ int bcount[4][NB], bpos[4][NB];
+  // the small tiles sort their lists in pairs (sort_pair: d2 scratch for two lists, packed
+  // bucket words for both, no index scratch); the other classes one list at a time
+  constexpr bool PAIR = TCAP <= kTcapSmall && PFX_SORT_PAIR;
+  __shared__ uint32_t sd[4][PAIR ? 2 * LCAP : LCAP];
+  __shared__ uint16_t stt[4][PAIR ? 2 : LCAP];
+  __shared__ int bcount[4][PAIR ? 1 : NB], bpos[4][PAIR ? 1 : NB];
+  __shared__ __attribute__((aligned(16))) uint32_t bw[4][PAIR ? 2 * NB : 4];
   __shared__ int s_k[Q];
   __shared__ int32_t s_qp[Q];
   __shared__ unsigned long long s_base;
@@ -627,6 +825,7 @@ __global__ void __launch_bounds__(256, TCAP <= kTcapSmall ? 4 : (STAGE ? 3 : 2))
   const uint32_t trash_at = (uint32_t)(Q * (LCAP + 2) + 64 * wv + lane);
   const uint32_t wrow = (uint32_t)(wv * (LCAP + 2));  // the wave's first list row (its queries: wv + 4 u)
   const int ntiles = *ntiles_ptr;
+  TPROF_DECL;
   unsigned long long wg_total = 0, arena_base = 0, arena_left = 0;  // thread 0's
   int next_chunk = 0;                                                // thread 0's
   if (tid == 0) {
@@ -762,6 +961,8 @@ __global__ void __launch_bounds__(256, TCAP <= kTcapSmall ? 4 : (STAGE ? 3 : 2))
     TPROF_T(p1);
     TPROF_ADD(TCAP <= kTcapSmall ? 17 : (STAGE ? 1 : 5), p0, p1);
     // [C] list slots, sort
+    WPROF_T(ws0);
+    [[maybe_unused]] constexpr int kWp0 = TCAP <= kTcapSmall ? 0 : (STAGE ? 4 : 8);
     int lg = 0;
     while ((1 << lg) < qn) ++lg;
     // 16-bit entries when every run of the block fits their 12-bit offset (the list bytes the
@@ -776,6 +977,18 @@ __global__ void __launch_bounds__(256, TCAP <= kTcapSmall ? 4 : (STAGE ? 3 : 2))
     }
     if (tid == 0)
       for (int j = 0; j < qn; ++j) wg_total += s_k[j] <= LCAP ? (unsigned long long)s_k[j] : 0ull;
+    // list slots come from a per-workgroup arena reserved kArena entries at a time (one cursor
+    // atomic per arena, not per tile); unused arena tails are never read (compact: two entries per
+    // 32-bit slot).  The reservation is issued here and its result read in [D], after the sort:
+    // the atomic's round trip (same-address, every workgroup) used to stall the whole workgroup
+    // at [D]'s barrier (round 6; the file is built without the atomic optimizer, which reads an
+    // atomic's result at once to spread it over the lanes)
+    const unsigned long long need = c16 ? (((unsigned long long)maxk << lg) + 1) >> 1 : (unsigned long long)maxk << lg;
+    unsigned long long arena_new = 0, arena_res = 0;  // thread 0's
+    if (tid == 0 && need > arena_left) {
+      arena_res = need > (unsigned long long)kArena ? need : (unsigned long long)kArena;
+      arena_new = atomicAdd(out.cursor, arena_res);
+    }
     if (tid < qn) {
       const int k = s_k[tid];
       if (k <= LCAP) {
@@ -788,7 +1001,20 @@ __global__ void __launch_bounds__(256, TCAP <= kTcapSmall ? 4 : (STAGE ? 3 : 2))
         tq->q[0][wave_push_slot(tq->n[0])] = start + tid;
       }
     }
-    if (sorted) {
+    if (sorted && PAIR) {
+      // lists u = 0, 1 together and u = 2, 3 together (a list that is absent, empty, single or
+      // overflowing takes part with k = 0)
+      const CandLds cand{cxy, cz};
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int uA = 2 * h, uB = 2 * h + 1, jA = wv + 4 * uA, jB = wv + 4 * uB;
+        const int kA = (ok && jA < qn && cursor[uA] <= LCAP && cursor[uA] > 1) ? cursor[uA] : 0;
+        const int kB = (ok && jB < qn && cursor[uB] <= LCAP && cursor[uB] > 1) ? cursor[uB] : 0;
+        if (kA + kB > 1)  // wave-uniform
+          sort_pair<NB>(lists[jA], kA, qxy[uA].x, qxy[uA].y, qz[uA], lists[jB], kB, qxy[uB].x, qxy[uB].y, qz[uB], cand,
+                        bscale, sd[wv], bw[wv], g, R, lane);
+      }
+    } else if (sorted) {
 #pragma unroll
       for (int u = 0; u < QW; ++u) {
         const int j = wv + 4 * u;
@@ -806,9 +1032,14 @@ __global__ void __launch_bounds__(256, TCAP <= kTcapSmall ? 4 : (STAGE ? 3 : 2))
         }
       }
     }
+    WPROF_T(ws1);
+    WPROF_ADD(kWp0 + 0, ws0, ws1);
     __syncthreads();
     TPROF_T(p2);
     TPROF_ADD(TCAP <= kTcapSmall ? 18 : (STAGE ? 2 : 6), p1, p2);
+    WPROF_T(ws2);
+    [[maybe_unused]] constexpr int kWp = TCAP <= kTcapSmall ? 0 : (STAGE ? 4 : 8);
+    WPROF_ADD(kWp + 1, ws1, ws2);
     // [D] one latency round: the next tile's staging loads, the list-slot reservation and the
     // queue fetch; their results land in LDS, then this tile's lists are written (stores in
     // flight until the next tile's round)
@@ -822,23 +1053,21 @@ __global__ void __launch_bounds__(256, TCAP <= kTcapSmall ? 4 : (STAGE ? 3 : 2))
     if (tid == 0) {
       if (ni + 1 == i_end) {  // publish the next chunk (fetched one chunk ago), fetch the one after
         s_chunk = next_chunk;
-        next_chunk = atomicAdd(next_tile, chunk);
+        next_chunk = atomicAdd(next_tile, chunk);  // (read a chunk later)
       }
-      // list slots come from a per-workgroup arena reserved kArena entries at a time (one
-      // cursor atomic per arena, not per tile); unused arena tails are never read
-      // (compact: two entries per 32-bit slot)
-      const unsigned long long need = c16 ? (((unsigned long long)maxk << lg) + 1) >> 1 : (unsigned long long)maxk << lg;
-      if (need > arena_left) {
-        const unsigned long long res = need > (unsigned long long)kArena ? need : (unsigned long long)kArena;
-        arena_base = atomicAdd(out.cursor, res);
-        arena_left = res;
+      if (arena_res) {  // the reservation issued in [C]
+        arena_base = arena_new;
+        arena_left = arena_res;
       }
       s_base = arena_base;
       arena_base += need;
       arena_left -= need;
     }
     if (ni < ntiles) sg.store(cxy, cz, s_qp, qn_n);
+    WPROF_T(ws3);
+    WPROF_ADD(kWp + 2, ws2, ws3);
     __syncthreads();
+    WPROF_T(ws4);
     const int64_t base = (int64_t)s_base;
     // (compact: offsets count 16-bit entries)
     if (tid < qn && s_k[tid] <= LCAP) out.off[start + tid] = (c16 ? 2 * base : base) + tid;
@@ -869,6 +1098,8 @@ __global__ void __launch_bounds__(256, TCAP <= kTcapSmall ? 4 : (STAGE ? 3 : 2))
         }
       }
     }
+    WPROF_T(ws5);
+    WPROF_ADD(kWp + 3, ws4, ws5);
     __syncthreads();  // lists and s_k read before the next tile's test overwrites them
     TPROF_T(p3);
     TPROF_ADD(TCAP <= kTcapSmall ? 19 : (STAGE ? 3 : 7), p2, p3);
@@ -878,6 +1109,7 @@ __global__ void __launch_bounds__(256, TCAP <= kTcapSmall ? 4 : (STAGE ? 3 : 2))
     qn = qn_n;
   }
   if (tid == 0 && wg_total) atomicAdd(out.cursor + 1, wg_total);
+  TPROF_FLUSH;
 }
 
 // ---- wide tiles (round 4) ----------------------------------------------------------------
@@ -1035,8 +1267,16 @@ __global__ void __launch_bounds__(256) k_nb_query(GridView g, const int32_t* __r
   // thread 0's: list slots from a per-workgroup arena and the totals added once per workgroup
   // (one same-address atomic per query made the cursors the bottleneck of this kernel)
   unsigned long long wg_total = 0, wg_long = 0, wg_long_n = 0, arena_base = 0, arena_left = 0;
+  TPROF_DECL;
+  // thread 0 holds the next work item, fetched one item ahead (its round trip overlaps the current
+  // item instead of stalling the workgroup at the top of every item; round 6)
+  int w_next = 0;
+  if (tid == 0) w_next = atomicAdd(next_work, 1);
   for (;;) {  // dynamic queue: list lengths (and costs) differ by orders of magnitude
-    if (tid == 0) s_w = atomicAdd(next_work, 1);
+    if (tid == 0) {
+      s_w = w_next;
+      if (w_next < count) w_next = atomicAdd(next_work, 1);
+    }
     __syncthreads();
     const int w = s_w;
     __syncthreads();
@@ -1148,36 +1388,39 @@ __global__ void __launch_bounds__(256) k_nb_query(GridView g, const int32_t* __r
       out.off[j] = 2 * (int64_t)s_base;
       out.lg[j] = kLgCompact;
     }
-    if (tid == 0 && !from_list) {
-      const unsigned long long need = c16 ? ((unsigned long long)k + 1) >> 1 : (unsigned long long)k;
-      if (need > arena_left) {
-        const unsigned long long res = need > (unsigned long long)kArenaQuery ? need : (unsigned long long)kArenaQuery;
-        arena_base = atomicAdd(out.cursor, res);
-        arena_left = res;
-      }
-      s_base = arena_base;
-      arena_base += need;
-      arena_left -= need;
-      wg_total += (unsigned long long)k;  // (neighbours, not list words)
-      if (k > kLongList) {
-        wg_long += (unsigned long long)k;
-        ++wg_long_n;
-      }
-      out.off[j] = c16 ? 2 * (int64_t)s_base : (int64_t)s_base;
-      out.cnt[j] = k;
-      out.lg[j] = c16 ? kLgCompact : 0;
+    // list slots from the workgroup's arena: a refill's atomic is issued here and its result read
+    // by commit() after the sort's scatter (its round trip overlaps the scan and the scatter)
+    const unsigned long long need = c16 ? ((unsigned long long)k + 1) >> 1 : (unsigned long long)k;
+    unsigned long long arena_new = 0, arena_res = 0;  // thread 0's
+    if (tid == 0 && !from_list && need > arena_left) {
+      arena_res = need > (unsigned long long)kArenaQuery ? need : (unsigned long long)kArenaQuery;
+      arena_new = atomicAdd(out.cursor, arena_res);
     }
+    auto commit = [&]() {  // thread 0, before the barrier that precedes the list write
+      if (tid == 0 && !from_list) {
+        if (arena_res) {
+          arena_base = arena_new;
+          arena_left = arena_res;
+        }
+        s_base = arena_base;
+        arena_base += need;
+        arena_left -= need;
+        wg_total += (unsigned long long)k;  // (neighbours, not list words)
+        if (k > kLongList) {
+          wg_long += (unsigned long long)k;
+          ++wg_long_n;
+        }
+        out.off[j] = c16 ? 2 * (int64_t)s_base : (int64_t)s_base;
+        out.cnt[j] = k;
+        out.lg[j] = c16 ? kLgCompact : 0;
+      }
+    };
     if (sorted && k > 1) {  // (the bucket counts were taken with the hits)
       if (tid < 64) {  // one wave scans the counts
         constexpr int PER = NB / 64;
         int s = 0;
         for (int v = 0; v < PER; ++v) s += bcount[tid * PER + v];
-        int inc = s;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-          const int x = __shfl_up(inc, o);
-          if (tid >= o) inc += x;
-        }
+        const int inc = wave_incl_scan(s);
         int ex = inc - s;
         for (int v = 0; v < PER; ++v) { bpos[tid * PER + v] = ex; ex += bcount[tid * PER + v]; }
       }
@@ -1203,9 +1446,11 @@ __global__ void __launch_bounds__(256) k_nb_query(GridView g, const int32_t* __r
             hits[slot] = rp[u];
           }
         }
+        commit();
         __syncthreads();
         const int64_t off = (int64_t)s_base;
-        const bool fits = (unsigned long long)(off + k) <= out.cap;
+        // (a compact list occupies (k + 1) / 2 words: the words its slot reservation counted)
+        const bool fits = (unsigned long long)(off + (c16 ? (k + 1) / 2 : k)) <= out.cap;
         // exact (d2, caller index) rank inside the bucket, written straight to the list
         for (int s = tid; s < k; s += 256) {
           const uint32_t d = hd[s], p = hits[s];
@@ -1252,9 +1497,10 @@ __global__ void __launch_bounds__(256) k_nb_query(GridView g, const int32_t* __r
         }
       }
     }
+    commit();
     __syncthreads();
     const int64_t off = (int64_t)s_base;
-    if ((unsigned long long)(off + k) <= out.cap) {
+    if ((unsigned long long)(off + (c16 ? (k + 1) / 2 : k)) <= out.cap) {
       if (c16)
         for (int m = tid; m < k; m += 256)
           reinterpret_cast<uint16_t*>(out.list)[2 * off + m] = (uint16_t)pos_entry16(R, (int32_t)hits[m]);
@@ -1270,6 +1516,7 @@ __global__ void __launch_bounds__(256) k_nb_query(GridView g, const int32_t* __r
       atomicAdd(out.cursor + 3, wg_long_n);
     }
   }
+  TPROF_FLUSH;
 }
 
 std::string bname(const char* tag, const char* what) { return std::string(tag) + "_" + what; }
@@ -1344,7 +1591,7 @@ bool build_lists_check(pfx_ctx* ctx, const Grid& G, NbLists& out, const char* ta
 }
 
 void build_lists(pfx_ctx* ctx, const Grid& G, const uint8_t* mask, double radius, bool sorted, NbLists& out,
-                 const char* tag, bool defer, int want, bool compact) {
+                 const char* tag, bool defer, int want, bool compact, bool gate) {
   hipStream_t st = ctx->stream;
   const int64_t n = G.n;
   GridView g = view(G);
@@ -1482,7 +1729,7 @@ void build_lists(pfx_ctx* ctx, const Grid& G, const uint8_t* mask, double radius
           static_cast<uint32_t*>(hs.ptr), counters + 9);
       check_launch("nblist huge lists");
     };
-    if (ctx->lists_gate) {  // pfx_normals_gate_dev: the caller's event, once, right before the list kernels
+    if (gate && ctx->lists_gate) {  // pfx_normals_gate_dev: the caller's event, once, right before the list kernels
       // (after the list set-up above, which therefore overlaps the gated stage)
       PFX_HIP(hipStreamWaitEvent(st, ctx->lists_gate, 0));
       ctx->lists_gate = nullptr;
@@ -1625,6 +1872,13 @@ void build_lists(pfx_ctx* ctx, const Grid& G, const uint8_t* mask, double radius
               pr[3], pr[4], pr[5], pr[6], pr[7], pr[16], pr[17], pr[18], pr[19]);
       fprintf(stderr, "%s query cycles: test %llu sort+write %llu | entries %llu candidates %llu\n", tag, pr[20],
               pr[21], pr[22], pr[23]);
+      unsigned long long pw[12];
+      PFX_HIP(hipMemcpyFromSymbol(pw, HIP_SYMBOL(g_tile_prof2), sizeof(pw)));
+      fprintf(stderr, "%s wave cycles (sum over waves): small sort %llu sortwait %llu staging %llu listwrite %llu | "
+              "sparse %llu %llu %llu %llu | dense %llu %llu %llu %llu\n", tag, pw[0], pw[1], pw[2], pw[3], pw[4], pw[5],
+              pw[6], pw[7], pw[8], pw[9], pw[10], pw[11]);
+      static const unsigned long long zw[12] = {};
+      PFX_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_tile_prof2), zw, sizeof(zw)));
       static const unsigned long long zero[24] = {};
       PFX_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_tile_prof), zero, sizeof(zero)));
     }

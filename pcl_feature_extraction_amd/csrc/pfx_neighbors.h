@@ -24,6 +24,19 @@ __device__ __forceinline__ uint64_t lanemask_lt() {
   return lane == 0 ? 0ull : (~0ull >> (64 - lane));
 }
 
+// Inclusive prefix sum over the 64 lanes of a wave on DPP row shifts and row broadcasts (round 6):
+// no LDS traffic -- __shfl_up is a ds_bpermute, so the six steps of a shuffle scan were six
+// dependent LDS-pipe latencies in the middle of every list sort.  Every lane must be active.
+__device__ __forceinline__ int wave_incl_scan(int v) {
+  v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, true);   // row_shr:1
+  v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, true);   // row_shr:2
+  v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, true);   // row_shr:4
+  v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, true);   // row_shr:8 (rows of 16 scanned)
+  v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false);  // row_bcast:15 -> rows 1, 3
+  v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false);  // row_bcast:31 -> rows 2, 3
+  return v;
+}
+
 // slot for each calling lane in an array filled through `counter`: one atomic per wave, not per
 // lane (same-address atomics serialise at the L2)
 __device__ __forceinline__ int wave_push_slot(int* counter) {

@@ -34,6 +34,8 @@ constexpr int kBatch = 8;      // neighbour entries per half-batch (two in fligh
 // again).  Dense clouds (many long lists, the non-forked schedule): 4096 -- the dense 10M variant's
 // long-list chains 140 -> 91 ms against chain_big 17 -> 28 ms (14.0 -> 14.7 Mpoints/s).
 constexpr int kLaneMax = PFX_LANE_MAX;
+// compact (16-bit) lists reach kLaneMaxCompact entries and k_normals_long reads 32-bit lists only
+static_assert(kLaneMax >= kLaneMaxCompact, "lists up to kLaneMaxCompact must take the lane-per-query chains");
 
 constexpr int kLaneMaxDense = 2 * kLaneMax;
 
@@ -113,12 +115,7 @@ __device__ __forceinline__ CellXYZ cell_of(const GridView& g, uint32_t key) {
 // block-wide exclusive scan of v (256 threads); returns the prefix, *total = sum
 __device__ __forceinline__ int block_scan(int v, int* wsum, int* total) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  int inc = v;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const int x = __shfl_up(inc, o);
-    if (lane >= o) inc += x;
-  }
+  const int inc = wave_incl_scan(v);
   if (lane == 63) wsum[wv] = inc;
   __syncthreads();
   int off = 0, tot = 0;
@@ -708,7 +705,7 @@ void normals_lists_dev(pfx_ctx* ctx, const float* x, const float* y, const float
   build_grid(ctx, ctx->grid_a, x, y, z, n, r);
   k_nan_fill4<<<(unsigned)std::min<int64_t>(ceil_div(n, 256), 4096), 256, 0, st>>>(nx, ny, nz, curv, n);
   check_launch("k_nan_fill4");
-  build_lists(ctx, ctx->grid_a, nullptr, r, true, ns.L, "normals");
+  build_lists(ctx, ctx->grid_a, nullptr, r, true, ns.L, "normals", false, 1, false, /*gate=*/true);
   ctx->stats["normals_neighbors"] = ns.L.total;
   ctx->stats["normals_long_neighbors"] = ns.L.long_total;
   ctx->stats["normals_long_queries"] = ns.L.long_nq;
@@ -832,12 +829,13 @@ bool normals_speculative_lists(pfx_ctx* ctx, const float* x, const float* y, con
   TimeScope phase(ctx, "normals_lists_phase", true);
   // (the grid queued ahead by normals_grid_launch_dev for this cloud and radius, else built here)
   const bool ahead = ns.grid_ahead_gen != 0 && ns.grid_ahead_gen == ctx->grid_a.gen && ns.grid_ahead_x == x &&
-                     ns.grid_ahead_n == n && ns.grid_ahead_r == r;
+                     ns.grid_ahead_y == y && ns.grid_ahead_z == z && ns.grid_ahead_n == n && ns.grid_ahead_r == r;
   ns.grid_ahead_gen = 0;
   if (!ahead) build_grid(ctx, ctx->grid_a, x, y, z, n, r, /*use_hint=*/true);
   k_nan_fill4<<<(unsigned)std::min<int64_t>(ceil_div(n, 256), 4096), 256, 0, ctx->stream>>>(nx, ny, nz, curv, n);
   check_launch("k_nan_fill4");
-  build_lists(ctx, ctx->grid_a, nullptr, r, true, ns.L, "normals", /*defer=*/true, /*want=*/1, /*compact=*/true);
+  build_lists(ctx, ctx->grid_a, nullptr, r, true, ns.L, "normals", /*defer=*/true, /*want=*/1, /*compact=*/true,
+              /*gate=*/true);
   return true;
 }
 
@@ -933,6 +931,8 @@ void normals_grid_launch_dev(pfx_ctx* ctx, const float* x, const float* y, const
   build_grid(ctx, ctx->grid_a, x, y, z, n, r, /*use_hint=*/true);
   ns.grid_ahead_gen = ctx->grid_a.gen;
   ns.grid_ahead_x = x;
+  ns.grid_ahead_y = y;
+  ns.grid_ahead_z = z;
   ns.grid_ahead_n = n;
   ns.grid_ahead_r = r;
 }
@@ -983,7 +983,8 @@ void normals_subset_dev(pfx_ctx* ctx, const float* x, const float* y, const floa
     k_nan_fill4_masked<<<(unsigned)std::min<int64_t>(ceil_div(n, 256), 4096), 256, 0, st>>>(nx, ny, nz, curv, n, mask,
                                                                                            want);
     check_launch("k_nan_fill4_masked");
-    build_lists(ctx, ctx->grid_a, mask, r, true, ns.L, "normals", /*defer=*/false, want);
+    build_lists(ctx, ctx->grid_a, mask, r, true, ns.L, "normals", /*defer=*/false, want, /*compact=*/false,
+                /*gate=*/true);
   }
   ns.ready = true;
   if (ns.L.nq > 0) normals_chains_dev(ctx, ctx, nullptr, 0, vp, nx, ny, nz, curv);

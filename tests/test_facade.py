@@ -31,6 +31,7 @@ def test_facade_compiles_and_links():
 
 @pytest.mark.gpu
 def test_facade_matches_c_abi(ctx, tmp_path):
+    from parity import bits_equal
     from pcl_feature_extraction_amd.pcd import read_pcd
     exe = build_driver()
     r = subprocess.run([exe, PCD, str(tmp_path), PCD_T], capture_output=True, text=True, timeout=300)
@@ -42,18 +43,17 @@ def test_facade_matches_c_abi(ctx, tmp_path):
     nrm = np.fromfile(tmp_path / "normals.f32", np.float32).reshape(-1, 8)
     want = np.stack(ctx.normals(x, y, z, 0.05))
     got = nrm[:, [0, 1, 2, 4]].T
-    assert np.array_equal(np.isnan(got), np.isnan(want))
-    ok = ~np.isnan(want)
-    assert np.array_equal(got[ok].view(np.uint32), want[ok].view(np.uint32))
+    # raw bits, NaN rows included (PCL's quiet_NaN for points without a normal)
+    assert bits_equal(got, want)
     rows = kp[kp < len(x)]
     fp = np.fromfile(tmp_path / "fpfh.f32", np.float32).reshape(-1, 33)
     wf = ctx.fpfh(x, y, z, want[0], want[1], want[2], x[rows], y[rows], z[rows], 0.08)
     assert fp.shape == wf.shape
-    assert np.array_equal(np.nan_to_num(fp, nan=-1.0).view(np.uint32), np.nan_to_num(wf, nan=-1.0).view(np.uint32))
+    assert bits_equal(fp, wf)
     sd = np.fromfile(tmp_path / "shot.f32", np.float32).reshape(-1, 352)
     wd, _ = ctx.shot(x, y, z, want[0], want[1], want[2], x[rows], y[rows], z[rows], 0.08)
     assert sd.shape == wd.shape
-    assert np.array_equal(np.nan_to_num(sd, nan=-1.0).view(np.uint32), np.nan_to_num(wd, nan=-1.0).view(np.uint32))
+    assert bits_equal(sd, wd)
 
     # features.h:224-273 run verbatim against the facade (two threads, KdTreeFLANN<FPFHSignature33>)
     tf = np.fromfile(tmp_path / "fpfh_target.f32", np.float32).reshape(-1, 33)

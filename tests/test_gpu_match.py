@@ -117,7 +117,8 @@ def test_match_pair_list_overflow(ctx):
     src = base[rng.integers(0, 2, 2000)]
     tgt = base[rng.integers(0, 2, 2000)]
     _gpu_nearest(ctx, src, tgt)
-    # (the emission count saturates just past the cap once the list has overflowed)
+    # (the emission count is a 64-bit counter of every emitted pair: past the cap once the list
+    # has overflowed)
     assert ctx.stat("match_pair_cap") == 64 * (len(src) + len(tgt)) + 65536
     assert ctx.stat("match_pairs_emitted") > ctx.stat("match_pair_cap")
     _check(ctx, src, tgt)

@@ -10,6 +10,7 @@ import numpy as np
 import pytest
 
 import oracle_lib as O
+from parity import bits, bits_equal
 from pcl_feature_extraction_amd.pcd import read_pcd
 
 pytestmark = pytest.mark.gpu
@@ -23,12 +24,8 @@ def _cloud(name):
 
 
 def _same(a, b):
-    a = np.asarray(a, np.float32).ravel()
-    b = np.asarray(b, np.float32).ravel()
-    na, nb = np.isnan(a), np.isnan(b)
-    if not np.array_equal(na, nb):
-        return False
-    return np.array_equal(a[~na].view(np.uint32), b[~nb].view(np.uint32))
+    """Raw 32-bit patterns, NaN pixels included (a NaN with another payload is a mismatch)."""
+    return bits_equal(np.asarray(a, np.float32).ravel(), np.asarray(b, np.float32).ravel())
 
 
 @pytest.mark.parametrize("name", CLOUDS)
@@ -60,7 +57,7 @@ def test_narf_keypoints_bit_exact(ctx, name):
     dense = np.asarray(dbg["interest"], np.float32).ravel()
     hi = dense >= 0.45
     assert np.array_equal(sparse[hi].view(np.uint32), dense[hi].view(np.uint32))
-    assert np.all((sparse[~hi] == 0) | (sparse[~hi] == dense[~hi]) | (np.isnan(sparse[~hi]) & np.isnan(dense[~hi])))
+    assert np.all((sparse[~hi] == 0) | (bits(sparse[~hi]) == bits(dense[~hi])))
     assert np.array_equal(kp, okp)
     assert len(kp) > 0
     assert np.all(np.diff(kp) > 0)  # ascending pixel indices
