@@ -1133,8 +1133,10 @@ def bench_config1(args, torch, dev, world, rank, local):
     NormalEstimationOMP (r 0.05) + FPFHEstimation (r 0.05) at every point, input == surface
     (PCL's all-points SPFH branch, features.h:188-195 with the cloud as both).  One step =
     pfx_normals_dev + pfx_fpfh_dev(same_as_surface) on the device-resident cloud.  roofline: the
-    SPFH stage (k_fpfh_spfh + exact + finalize), the dominant cost here: sum_{p in S} |N(p)| x
-    24 B, S = every point."""
+    dominant FPFH kernel of the step -- the all-points weighting over the FLANN
+    lists (sum_q |N(q)| x 136 B: the 33-float SPFH row + the list entry per neighbour) or SPFH
+    (sum_{p in S} |N(p)| x 24 B, S = every point), whichever took longer; both beside it.  The
+    timed region carries the stage timers only; the per-kernel breakdown comes from extra steps."""
     import numpy as np
 
     from pcl_feature_extraction_amd import Context
@@ -1157,22 +1159,37 @@ def bench_config1(args, torch, dev, world, rank, local):
     for _ in range(max(args.warmup, 1)):
         step()
     torch.cuda.synchronize(dev)
-    ctx.set_timing(True)
+    ctx.set_timing(True, stages_only=True)
     ctx.reset_timing()
     elapsed = timed(torch, torch.distributed, dev, world, args.steps, step)
+    live = {nm: round(ctx.kernel_time(nm)[0] / args.steps, 4) for nm in ("normals", "fpfh_spfh", "fpfh_weight")}
+    detail_steps = max(3, args.steps // 4)
+    ctx.set_timing(True)
+    ctx.reset_timing()
+    timed(torch, torch.distributed, dev, world, detail_steps, step)
     if rank != 0:
         ctx.close()
         return
     names = ("normals", "fpfh_mark", "fpfh_spfh", "fpfh_weight", "grid_build", "normals_lists_small",
              "normals_lists_sparse", "normals_lists_dense", "normals_lists_wide", "normals_lists_query", "normals_chain",
              "normals_chain_big", "normals_long")
-    stages = {nm: round(ctx.kernel_time(nm)[0] / args.steps, 4) for nm in names}
+    stages = {nm: round(ctx.kernel_time(nm)[0] / detail_steps, 4) for nm in names}
     ctx.set_timing(False)
     pairs = ctx.stat("fpfh_spfh_pairs")
     nb = ctx.stat("normals_neighbors")
-    spfh_ms = stages["fpfh_spfh"]
-    algo = pairs * 24
-    achieved = algo / (spfh_ms / 1e3) / 1e9 if spfh_ms > 0 else 0.0
+    spfh_ms, weight_ms = live["fpfh_spfh"], live["fpfh_weight"]
+    kern = {"fpfh_spfh": {"kernel": "k_fpfh_spfh + k_fpfh_exact + k_fpfh_finalize", "ms": spfh_ms,
+                          "algorithmic_bytes_per_launch": int(pairs * 24),
+                          "note": "sum_{p in S} |N(p)| x 24 B (xyz + normal per pair, SURVEY 8(d)); S = all 100k points"},
+            "fpfh_weight": {"kernel": "k_fpfh_weight_lists / k_fpfh_weight_units (input == surface)", "ms": weight_ms,
+                            "algorithmic_bytes_per_launch": int(nb * 136),
+                            "note": "sum_q |N(q)| x 136 B (the neighbour's 33-float SPFH row + its list entry)"}}
+    for v in kern.values():
+        v["achieved"] = round(v["algorithmic_bytes_per_launch"] / (v["ms"] / 1e3) / 1e9, 2) if v["ms"] > 0 else None
+        v["frac"] = round(v["achieved"] / HBM_PEAK_GBS, 5) if v["achieved"] else None
+    dom = max(kern, key=lambda nm: kern[nm]["ms"])
+    algo = kern[dom]["algorithmic_bytes_per_launch"]
+    achieved = kern[dom]["achieved"] or 0.0
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
         sys.path.insert(0, os.path.join(ROOT, "tests"))
@@ -1194,10 +1211,9 @@ def bench_config1(args, torch, dev, world, rank, local):
         med = tot[len(tot) // 2]
         st = [sorted(t[i] for t in runs)[len(runs) // 2] for i in range(2)]
 
-        def same(a, c):
-            a, c = np.asarray(a, np.float32), np.asarray(c, np.float32)
-            return bool(a.shape == c.shape and np.array_equal(np.nan_to_num(a, nan=7).view(np.uint32),
-                                                              np.nan_to_num(c, nan=7).view(np.uint32)))
+        def same(a, c):  # raw bits, NaN rows included (PCL's quiet_NaN on both sides)
+            a, c = np.ascontiguousarray(np.asarray(a, np.float32)), np.ascontiguousarray(np.asarray(c, np.float32))
+            return bool(a.shape == c.shape and np.array_equal(a.view(np.uint32), c.view(np.uint32)))
         parity = {"normals": all(same(t.cpu().numpy(), o) for t, o in zip((b.nx, b.ny, b.nz, b.curv), out[0])),
                   "descriptors": same(b.desc[:n].cpu().numpy(), out[1])}
         cpu = {"value": round(n / med / 1e6, 6), "unit": "Mpoints/s", "cores": threads, "kind": "port",
@@ -1214,11 +1230,13 @@ def bench_config1(args, torch, dev, world, rank, local):
         "config": {"workload": "configs[1] 100k-pt synthetic room, NormalEstimation(r 0.05) + FPFH(r 0.05) at all "
                                "points (input == surface)", "points_per_scan": n,
                    "parallelism": f"scan-per-gpu x{world}"},
-        "roofline": {"bound": "hbm", "kernel": "k_fpfh_spfh + k_fpfh_exact + k_fpfh_finalize", "achieved": round(achieved, 2),
+        "stages_ms_per_scan": live,
+        "roofline": {"bound": "hbm", "kernel": kern[dom]["kernel"], "achieved": round(achieved, 2),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
-                     "algorithmic_bytes_per_launch": int(algo), "avg_ms": spfh_ms, "pairs_per_launch": int(pairs),
-                     "note": "sum_{p in S} |N(p)| x 24 B (xyz + normal per pair, SURVEY 8(d)); S = all 100k points",
-                     "normals_neighbors": int(nb), "stages_ms_per_step": stages},
+                     "algorithmic_bytes_per_launch": int(algo), "avg_ms": kern[dom]["ms"], "pairs_per_launch": int(pairs),
+                     "note": kern[dom]["note"] + "; the dominant FPFH kernel of the step (live stage timers)",
+                     "kernels": kern, "normals_neighbors": int(nb), "stages_ms_per_step": stages,
+                     "stages_basis": f"per-kernel HIP events over {detail_steps} extra steps after the timed region"},
         "cpu_baseline": cpu,
     }
     print(json.dumps(line), flush=True)

@@ -604,14 +604,14 @@ __device__ __forceinline__ int lsb_exp(float v) {
   return (e ? e : 1) - 150 + __builtin_ctz(m);
 }
 
-// lsb_exp without branches (v != 0; a select instead of the early return), for the per-neighbour
-// step of k_fpfh_weight_lists
-__device__ __forceinline__ int lsb_exp_select(float v) {
-  const uint32_t b = __float_as_uint(v);
-  const int e = (int)((b >> 23) & 0xff);
-  const uint32_t m = (b & 0x7fffffu) | (e ? 0x800000u : 0u);
-  const int r = (e ? e : 1) - 150 + __builtin_ctz(m);
-  return e == 255 ? 1000 : r;
+// A lower bound of lsb_exp for the per-neighbour step of k_fpfh_weight_lists: a float of biased
+// exponent e is a multiple of 2^(max(e, 1) - 150), so the block-sum test stays sufficient (every
+// addend a multiple of 2^L, total below 2^(L + 52)) with the exponent alone -- two instructions
+// instead of the trailing-zero count; only its margin shrinks, by the addends' trailing zeros
+// (1000 for a non-finite value, as lsb_exp)
+__device__ __forceinline__ int lsb_exp_bound(float v) {
+  const int e = (int)((__float_as_uint(v) >> 23) & 0xff);
+  return e == 255 ? 1000 : (e ? e : 1) - 150;
 }
 
 // Weighting: one 1024-thread workgroup per query.  The 33 float chains (strict FLANN order)
@@ -882,7 +882,7 @@ __global__ void __launch_bounds__(256) k_fpfh_weight_lists(GridView g, const int
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
           const int jj = j0 + u < m ? j0 + u : m - 1;
-          const int id = __builtin_amdgcn_readfirstlane(__builtin_amdgcn_readlane(idx, jj));
+          const int id = __builtin_amdgcn_readlane(idx, jj);
           wu[u] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(w), j0 + u < 64 ? j0 + u : 63));
           if constexpr (BUF) v[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(srsrc, vlane, id * (kDesc * 4), 0));
           else v[u] = spfh[(int64_t)id * kDesc + (vlane >> 2)];
@@ -893,7 +893,7 @@ __global__ void __launch_bounds__(256) k_fpfh_weight_lists(GridView g, const int
           const float val = v[u] * wu[u];
           fh = fh + val;
           ps += (double)val;
-          pl = val != 0.0f ? min(pl, lsb_exp_select(val)) : pl;
+          pl = val != 0.0f ? min(pl, lsb_exp_bound(val)) : pl;
         }
       }
     }
@@ -1256,7 +1256,8 @@ void fpfh_dev(pfx_ctx* ctx, const float* sx, const float* sy, const float* sz, c
     {
       const unsigned bl = (unsigned)std::min<int64_t>(ceil_div(L.nq, 4), 256 * 8);
       const GridView gv = reuse ? view(ctx->grid_a) : g;
-      if (ns * kDesc * 4 < ((int64_t)1 << 31))
+      const bool buf = ns * kDesc * 4 < ((int64_t)1 << 31);
+      if (buf)
         k_fpfh_weight_lists<true><<<bl, 256, 0, st>>>(gv, L.qpos, L.off, L.cnt, L.lg, L.list, L.skeys, L.nq, spfh, out, err);
       else
         k_fpfh_weight_lists<false><<<bl, 256, 0, st>>>(gv, L.qpos, L.off, L.cnt, L.lg, L.list, L.skeys, L.nq, spfh, out,

@@ -22,8 +22,8 @@ namespace pfx {
 namespace {
 
 constexpr int kQ = 16;  // tile: consecutive queries of one cell
-#ifndef PFX_SORT_PAIR
-#define PFX_SORT_PAIR 0
+#ifndef PFX_TIERS_COARSE
+#define PFX_TIERS_COARSE 0
 #endif
 typedef float pf2 __attribute__((ext_vector_type(2)));  // packed f32 pair (v_pk_add_f32 / v_pk_mul_f32)
 constexpr int kArena = 16384;   // list entries per arena reservation of a tile workgroup (> a typical tile)
@@ -465,199 +465,22 @@ __device__ __forceinline__ void wave_rank_sort(uint16_t* L, int k, float qx, flo
   wave_sync();
 }
 
-// Two lists of one wave sorted as one (round 6, the small tiles): elements 0..kA-1 are list A's,
-// kA..k-1 list B's, and B's buckets follow A's, so one pass of the bucket sort orders both and
-// every dependent LDS round serves two lists (a wave sorted its four lists one after another:
-// a chain of ~8 LDS round trips each).  Bucket words pack the count (low 16 bits) and, after the
-// scan, the running position (high 16 bits), so both lists' 2 NB buckets take the LDS of one
-// list's count and position arrays; the elements go to their lists' rows in bucket order (no
-// separate index scratch), so only their d2 bits need scratch (Sd, 2 LCAP entries).
-template <int NB, int E, class Cand>
-__device__ __forceinline__ void wave_sort_pair(uint16_t* LA, int kA, float ax, float ay, float az, uint16_t* LB,
-                                               int kB, float bx, float by, float bz, const Cand& cand, float bscale,
-                                               uint32_t* Sd, uint32_t* bw, const GridView& g, const Runs& R,
-                                               int lane) {
-  constexpr int NBT = 2 * NB, PER = NBT / 64;
-  static_assert(PER % 4 == 0, "bucket words are cleared and scanned four per 16-byte access");
-  const int k = kA + kB;
-#pragma unroll
-  for (int v = 0; v < PER; v += 4) reinterpret_cast<uint4*>(bw + lane * PER + v)[0] = make_uint4(0, 0, 0, 0);
-  int t[E], b[E];
-  uint32_t d[E];
-#pragma unroll
-  for (int i = 0; i < E; ++i) {
-    const int e = lane + 64 * i;
-    t[i] = e < kA ? LA[e] : (e < k ? LB[e - kA] : 0);
-  }
-  wave_sync();
-#pragma unroll
-  for (int i = 0; i < E; ++i) {
-    const int e = lane + 64 * i;
-    const bool inB = e >= kA;
-    float px, py, pz;
-    cand.get(t[i], px, py, pz);
-    const float d2 = flann_d2(inB ? bx : ax, inB ? by : ay, inB ? bz : az, px, py, pz);
-    d[i] = __float_as_uint(d2);  // d2 >= +0: bit order == value order
-    const int bb = (int)(d2 * bscale);
-    b[i] = (bb < NB ? bb : NB - 1) + (inB ? NB : 0);
-    if (e < k) atomicAdd(&bw[b[i]], 1u);
-  }
-  wave_sync();
-  {
-    uint32_t c[PER];
-    int sum = 0;
-#pragma unroll
-    for (int v = 0; v < PER; v += 4) {
-      const uint4 w4 = reinterpret_cast<const uint4*>(bw + lane * PER + v)[0];
-      c[v] = w4.x;
-      c[v + 1] = w4.y;
-      c[v + 2] = w4.z;
-      c[v + 3] = w4.w;
-    }
-#pragma unroll
-    for (int v = 0; v < PER; ++v) sum += (int)c[v];
-    uint32_t ex = (uint32_t)(wave_incl_scan(sum) - sum);
-#pragma unroll
-    for (int v = 0; v < PER; ++v) {
-      const uint32_t cnt = c[v];
-      c[v] = (ex << 16) | cnt;
-      ex += cnt;
-    }
-#pragma unroll
-    for (int v = 0; v < PER; v += 4)
-      reinterpret_cast<uint4*>(bw + lane * PER + v)[0] = make_uint4(c[v], c[v + 1], c[v + 2], c[v + 3]);
-  }
-  wave_sync();
-  int slot[E];
-#pragma unroll
-  for (int i = 0; i < E; ++i) slot[i] = lane + 64 * i < k ? (int)(atomicAdd(&bw[b[i]], 1u << 16) >> 16) : 0;
-#pragma unroll
-  for (int i = 0; i < E; ++i)
-    if (lane + 64 * i < k) {
-      Sd[slot[i]] = d[i];
-      if (slot[i] < kA) LA[slot[i]] = (uint16_t)t[i];
-      else LB[slot[i] - kA] = (uint16_t)t[i];
-    }
-  wave_sync();
-  // bucket [st, en): en = its position after the scatter; rank = keys of the bucket below mine
-  int st[E], rank[E];
-  bool tie = false;
-#pragma unroll
-  for (int i = 0; i < E; ++i) {
-    const uint32_t w = bw[b[i]];
-    const int en = (int)(w >> 16);
-    st[i] = en - (int)(w & 0xffffu);
-    uint32_t dv[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) dv[j] = st[i] + j < en ? Sd[st[i] + j] : 0xffffffffu;
-    int r = 0, eq = 0;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      r += dv[j] < d[i];
-      eq += dv[j] == d[i];
-    }
-    for (int v = st[i] + 4; v < en; ++v) {
-      const uint32_t x = Sd[v];
-      r += x < d[i];
-      eq += x == d[i];
-    }
-    rank[i] = r;
-    tie |= lane + 64 * i < k && eq > 1;
-  }
-  if (__builtin_amdgcn_ballot_w64(tie)) {  // equal d2: the caller index decides (FLANN); rare
-#pragma unroll
-    for (int i = 0; i < E; ++i) {
-      if (lane + 64 * i >= k) continue;
-      const int en = (int)(bw[b[i]] >> 16);
-      const int32_t mine = g.perm[run_pos(R, t[i])];
-      for (int v = st[i]; v < en; ++v) {
-        if (v == slot[i] || Sd[v] != d[i]) continue;
-        const int tv = v < kA ? LA[v] : LB[v - kA];
-        if (g.perm[run_pos(R, tv)] < mine) ++rank[i];
-      }
-    }
-  }
-  wave_sync();  // every bucket-order entry read before the final positions overwrite them
-#pragma unroll
-  for (int i = 0; i < E; ++i)
-    if (lane + 64 * i < k) {
-      const int pos = st[i] + rank[i];
-      if (pos < kA) LA[pos] = (uint16_t)t[i];
-      else LB[pos - kA] = (uint16_t)t[i];
-    }
-  wave_sync();
-}
-
-// kA + kB <= 64: one entry per lane, ranked among the entries of its own list (v_readlane, no LDS)
-template <class Cand>
-__device__ __forceinline__ void wave_rank_sort_pair(uint16_t* LA, int kA, float ax, float ay, float az, uint16_t* LB,
-                                                    int kB, float bx, float by, float bz, const Cand& cand,
-                                                    const GridView& g, const Runs& R, int lane) {
-  const int k = kA + kB;
-  const bool in = lane < k, inB = lane >= kA;
-  const int t = lane < kA ? LA[lane] : (in ? LB[lane - kA] : 0);
-  float px, py, pz;
-  cand.get(t, px, py, pz);
-  const uint32_t d = in ? __float_as_uint(flann_d2(inB ? bx : ax, inB ? by : ay, inB ? bz : az, px, py, pz))
-                        : 0xffffffffu;
-  const int lo = inB ? kA : 0, hi = inB ? k : kA;  // the lanes of my list
-  int rank = 0, eq = 0;
-  for (int m = 0; m < k; ++m) {
-    const uint32_t dm = (uint32_t)__builtin_amdgcn_readlane((int)d, m);
-    const bool mine = m >= lo && m < hi;
-    rank += (mine && dm < d) ? 1 : 0;
-    eq += (mine && dm == d) ? 1 : 0;
-  }
-  if (__builtin_amdgcn_ballot_w64(in && eq > 1)) {
-    const int32_t id = in ? g.perm[run_pos(R, t)] : 0x7fffffff;
-    rank = 0;
-    for (int m = 0; m < k; ++m) {
-      const uint32_t dm = (uint32_t)__builtin_amdgcn_readlane((int)d, m);
-      const int32_t im = __builtin_amdgcn_readlane(id, m);
-      const bool mine = m >= lo && m < hi;
-      rank += (mine && (dm < d || (dm == d && im < id))) ? 1 : 0;
-    }
-  }
-  wave_sync();
-  if (in) {
-    if (inB) LB[rank] = (uint16_t)t;
-    else LA[rank] = (uint16_t)t;
-  }
-  wave_sync();
-}
-
-// the pair by the smallest register tier that holds kA + kB (<= 384, E <= 6: the register tiers
-// of the one-list sort in these kernels); a longer pair is sorted as two one-list passes
-template <int NB, class Cand>
-__device__ __forceinline__ void sort_pair_tiers(uint16_t* LA, int kA, float ax, float ay, float az, uint16_t* LB,
-                                                int kB, float bx, float by, float bz, const Cand& cand, float bscale,
-                                                uint32_t* Sd, uint32_t* bw, const GridView& g, const Runs& R, int lane) {
-  const int k = kA + kB;
-  if (k <= 64) wave_rank_sort_pair(LA, kA, ax, ay, az, LB, kB, bx, by, bz, cand, g, R, lane);
-  else if (k <= 128) wave_sort_pair<NB, 2>(LA, kA, ax, ay, az, LB, kB, bx, by, bz, cand, bscale, Sd, bw, g, R, lane);
-  else if (k <= 192) wave_sort_pair<NB, 3>(LA, kA, ax, ay, az, LB, kB, bx, by, bz, cand, bscale, Sd, bw, g, R, lane);
-  else if (k <= 256) wave_sort_pair<NB, 4>(LA, kA, ax, ay, az, LB, kB, bx, by, bz, cand, bscale, Sd, bw, g, R, lane);
-  else if (k <= 320) wave_sort_pair<NB, 5>(LA, kA, ax, ay, az, LB, kB, bx, by, bz, cand, bscale, Sd, bw, g, R, lane);
-  else wave_sort_pair<NB, 6>(LA, kA, ax, ay, az, LB, kB, bx, by, bz, cand, bscale, Sd, bw, g, R, lane);
-}
-template <int NB, class Cand>
-__device__ __forceinline__ void sort_pair(uint16_t* LA, int kA, float ax, float ay, float az, uint16_t* LB, int kB,
-                                          float bx, float by, float bz, const Cand& cand, float bscale, uint32_t* Sd,
-                                          uint32_t* bw, const GridView& g, const Runs& R, int lane) {
-  if (kA + kB <= 384) {
-    sort_pair_tiers<NB>(LA, kA, ax, ay, az, LB, kB, bx, by, bz, cand, bscale, Sd, bw, g, R, lane);
-  } else {
-    sort_pair_tiers<NB>(LA, kA, ax, ay, az, LA, 0, ax, ay, az, cand, bscale, Sd, bw, g, R, lane);
-    sort_pair_tiers<NB>(LB, kB, bx, by, bz, LB, 0, bx, by, bz, cand, bscale, Sd, bw, g, R, lane);
-  }
-}
-
 template <int NB, class Cand, bool SMALL = false>
 __device__ __forceinline__ void sort_list(uint16_t* L, int k, float qx, float qy, float qz, const Cand& cand,
                                           float bscale, uint32_t* Sd, uint16_t* St, int* bcount, int* bpos,
                                           const GridView& g, const Runs& R, int lane) {
   // register tiers in steps of 64-128 elements: the unrolled per-element work of a tier runs for
   // every slot, so a list is sorted by the smallest tier that holds it
+#if PFX_TIERS_COARSE  // (A/B: fewer tiers, a third of the code -- the instruction-cache footprint)
+  if (k <= 64) wave_rank_sort(L, k, qx, qy, qz, cand, g, R, lane);
+  else if (k <= 128) wave_sort_regs<NB, 2>(L, k, qx, qy, qz, cand, bscale, Sd, St, bcount, bpos, g, R, lane);
+  else if (k <= 256) wave_sort_regs<NB, 4>(L, k, qx, qy, qz, cand, bscale, Sd, St, bcount, bpos, g, R, lane);
+  else if (SMALL) wave_sort_regs<NB, 6>(L, k, qx, qy, qz, cand, bscale, Sd, St, bcount, bpos, g, R, lane);
+  else if (k <= 512) wave_sort_regs<NB, 8>(L, k, qx, qy, qz, cand, bscale, Sd, St, bcount, bpos, g, R, lane);
+  else if (k <= 1024) wave_sort_regs<NB, 16>(L, k, qx, qy, qz, cand, bscale, Sd, St, bcount, bpos, g, R, lane);
+  else wave_sort<NB>(L, k, qx, qy, qz, cand, bscale, Sd, St, bcount, bpos, g, R, lane);
+  return;
+#endif
   if (k <= 64) wave_rank_sort(L, k, qx, qy, qz, cand, g, R, lane);
   else if (k <= 128) wave_sort_regs<NB, 2>(L, k, qx, qy, qz, cand, bscale, Sd, St, bcount, bpos, g, R, lane);
   else if (k <= 192) wave_sort_regs<NB, 3>(L, k, qx, qy, qz, cand, bscale, Sd, St, bcount, bpos, g, R, lane);
@@ -809,13 +632,9 @@ __global__ void __launch_bounds__(256, TCAP <= kTcapSmall ? 4 : (STAGE ? 3 : 2))
   // (a miss stores its candidate to its lane's slot: the test loop has no branch)
   __shared__ uint16_t lists_flat[Q * (LCAP + 2) + 4 * 64];
   uint16_t(*lists)[LCAP + 2] = reinterpret_cast<uint16_t(*)[LCAP + 2]>(lists_flat);
-  // the small tiles sort their lists in pairs (sort_pair: d2 scratch for two lists, packed
-  // bucket words for both, no index scratch); the other classes one list at a time
-  constexpr bool PAIR = TCAP <= kTcapSmall && PFX_SORT_PAIR;
-  __shared__ uint32_t sd[4][PAIR ? 2 * LCAP : LCAP];
-  __shared__ uint16_t stt[4][PAIR ? 2 : LCAP];
-  __shared__ int bcount[4][PAIR ? 1 : NB], bpos[4][PAIR ? 1 : NB];
-  __shared__ __attribute__((aligned(16))) uint32_t bw[4][PAIR ? 2 * NB : 4];
+  __shared__ uint32_t sd[4][LCAP];
+  __shared__ uint16_t stt[4][LCAP];
+  __shared__ int bcount[4][NB], bpos[4][NB];
   __shared__ int s_k[Q];
   __shared__ int32_t s_qp[Q];
   __shared__ unsigned long long s_base;
@@ -1001,20 +820,7 @@ __global__ void __launch_bounds__(256, TCAP <= kTcapSmall ? 4 : (STAGE ? 3 : 2))
         tq->q[0][wave_push_slot(tq->n[0])] = start + tid;
       }
     }
-    if (sorted && PAIR) {
-      // lists u = 0, 1 together and u = 2, 3 together (a list that is absent, empty, single or
-      // overflowing takes part with k = 0)
-      const CandLds cand{cxy, cz};
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int uA = 2 * h, uB = 2 * h + 1, jA = wv + 4 * uA, jB = wv + 4 * uB;
-        const int kA = (ok && jA < qn && cursor[uA] <= LCAP && cursor[uA] > 1) ? cursor[uA] : 0;
-        const int kB = (ok && jB < qn && cursor[uB] <= LCAP && cursor[uB] > 1) ? cursor[uB] : 0;
-        if (kA + kB > 1)  // wave-uniform
-          sort_pair<NB>(lists[jA], kA, qxy[uA].x, qxy[uA].y, qz[uA], lists[jB], kB, qxy[uB].x, qxy[uB].y, qz[uB], cand,
-                        bscale, sd[wv], bw[wv], g, R, lane);
-      }
-    } else if (sorted) {
+    if (sorted) {
 #pragma unroll
       for (int u = 0; u < QW; ++u) {
         const int j = wv + 4 * u;

@@ -8,8 +8,11 @@ cd "$(dirname "$0")/../pcl_feature_extraction_amd/csrc"
 D=build_var/$OUT
 mkdir -p $D
 for f in *.hip; do
+  EXTRA=""
+  # (the Makefile's per-file flags: pfx_nblist.hip without the atomic optimizer)
+  [ "$f" = pfx_nblist.hip ] && EXTRA="-mllvm -amdgpu-atomic-optimizer-strategy=None"
   /opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -ffp-contract=off -fPIC -Wall -Wno-unused-function \
-    -Wno-unused-result -munsafe-fp-atomics "$@" -c $f -o $D/${f%.hip}.o &
+    -Wno-unused-result -munsafe-fp-atomics $EXTRA "$@" -c $f -o $D/${f%.hip}.o &
   while [ $(jobs -r | wc -l) -ge 8 ]; do sleep 0.2; done
 done
 wait
