@@ -22,9 +22,6 @@ namespace pfx {
 namespace {
 
 constexpr int kQ = 16;  // tile: consecutive queries of one cell
-#ifndef PFX_TIERS_COARSE
-#define PFX_TIERS_COARSE 0
-#endif
 typedef float pf2 __attribute__((ext_vector_type(2)));  // packed f32 pair (v_pk_add_f32 / v_pk_mul_f32)
 constexpr int kArena = 16384;   // list entries per arena reservation of a tile workgroup (> a typical tile)
 constexpr int kArenaQuery = 16384;  // ... of a per-query workgroup (lists of 1k-4k entries)
@@ -471,16 +468,6 @@ __device__ __forceinline__ void sort_list(uint16_t* L, int k, float qx, float qy
                                           const GridView& g, const Runs& R, int lane) {
   // register tiers in steps of 64-128 elements: the unrolled per-element work of a tier runs for
   // every slot, so a list is sorted by the smallest tier that holds it
-#if PFX_TIERS_COARSE  // (A/B: fewer tiers, a third of the code -- the instruction-cache footprint)
-  if (k <= 64) wave_rank_sort(L, k, qx, qy, qz, cand, g, R, lane);
-  else if (k <= 128) wave_sort_regs<NB, 2>(L, k, qx, qy, qz, cand, bscale, Sd, St, bcount, bpos, g, R, lane);
-  else if (k <= 256) wave_sort_regs<NB, 4>(L, k, qx, qy, qz, cand, bscale, Sd, St, bcount, bpos, g, R, lane);
-  else if (SMALL) wave_sort_regs<NB, 6>(L, k, qx, qy, qz, cand, bscale, Sd, St, bcount, bpos, g, R, lane);
-  else if (k <= 512) wave_sort_regs<NB, 8>(L, k, qx, qy, qz, cand, bscale, Sd, St, bcount, bpos, g, R, lane);
-  else if (k <= 1024) wave_sort_regs<NB, 16>(L, k, qx, qy, qz, cand, bscale, Sd, St, bcount, bpos, g, R, lane);
-  else wave_sort<NB>(L, k, qx, qy, qz, cand, bscale, Sd, St, bcount, bpos, g, R, lane);
-  return;
-#endif
   if (k <= 64) wave_rank_sort(L, k, qx, qy, qz, cand, g, R, lane);
   else if (k <= 128) wave_sort_regs<NB, 2>(L, k, qx, qy, qz, cand, bscale, Sd, St, bcount, bpos, g, R, lane);
   else if (k <= 192) wave_sort_regs<NB, 3>(L, k, qx, qy, qz, cand, bscale, Sd, St, bcount, bpos, g, R, lane);

@@ -11,10 +11,16 @@ import torch  # noqa: E402
 
 from pcl_feature_extraction_amd import Context  # noqa: E402
 from pcl_feature_extraction_amd.pipeline import alloc  # noqa: E402
-from pcl_feature_extraction_amd.synth import synth_room, synth_seabed  # noqa: E402
+from pcl_feature_extraction_amd.synth import ROOM_SCALE, synth_room, synth_seabed  # noqa: E402
 
-for name, gen, seed in (("room", synth_room, 2), ("seabed", synth_seabed, 3)):
-    x, y, z, _ = gen(1_000_000, seed)
+SCENES = {
+    "room": lambda: synth_room(1_000_000, 2),
+    "seabed": lambda: synth_seabed(1_000_000, 3),
+    # bench --workload dense: the room scene at 10x the density (same scale)
+    "dense": lambda: synth_room(10_000_000, 2, scale=ROOM_SCALE * 0.1 ** 0.5),
+}
+for name in os.environ.get("PFX_NO_SCENES", "room,seabed").split(","):
+    x, y, z, _ = SCENES[name]()
     dev = torch.device("cuda", 0)
     b = alloc(torch, len(x), dev)
     b.x.copy_(torch.from_numpy(x)); b.y.copy_(torch.from_numpy(y)); b.z.copy_(torch.from_numpy(z))
@@ -40,5 +46,6 @@ for name, gen, seed in (("room", synth_room, 2), ("seabed", synth_seabed, 3)):
                 return ctx.stat("normals_" + k)
             except Exception:  # (a library build without that statistic)
                 return None
-        st = {k: stat(k) for k in ("wide", "single", "mid", "huge")}
+        st = {k: stat(k) for k in ("wide", "single", "mid", "huge", "long_lists", "queries", "tiles_sparse", "tiles_dense",
+                                   "chain_wg_staged", "chain_wg_table", "chain_wg_lane", "chain_wg_deferred")}
         print(name, json.dumps(t), json.dumps(st), "chain GB/s %.0f frac %.3f" % (gbs, gbs / 8000.0), flush=True)
