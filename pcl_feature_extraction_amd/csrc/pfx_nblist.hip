@@ -35,6 +35,14 @@ constexpr int kCapMid = 16384, kBucketsMid = 2048;  // 144 KB of LDS: one workgr
 // the huge tier: up to kHugeBlocks workgroups with 4 MB of scratch each, allocated on demand for
 // as many workgroups as lists (>= 256); 1024 (was 256): dense 10M per-query tiers 449 -> 409 ms
 constexpr int kCapHuge = 1 << 18, kBucketsHuge = 4096, kHugeBlocks = PFX_HUGE_BLOCKS;
+// threads per workgroup of the per-query tiers (see k_nb_query)
+#ifndef PFX_NT_QUERY
+#define PFX_NT_QUERY 512
+#endif
+#ifndef PFX_NT_MID
+#define PFX_NT_MID 1024
+#endif
+constexpr int kNtQuery = PFX_NT_QUERY, kNtMid8 = PFX_NT_QUERY, kNtMid = PFX_NT_MID, kNtHuge = 256;
 constexpr int kNCounters = 20;
 
 // The lists of a wide tile are written unsorted to HBM by a test pass and ordered in place by the
@@ -45,6 +53,10 @@ struct TierQ {
   int32_t* q[4];
   int* n[4];
 };
+// the per-query tier of a list of k entries (<= 4096, <= 8192, <= 16384, beyond)
+__device__ __forceinline__ int query_tier(int k) {
+  return k <= kCapQuery ? 0 : (k <= kCapMid8 ? 1 : (k <= kCapMid ? 2 : 3));
+}
 
 // Tile record (written by k_tile_class, one per tile, in class order): the 9 candidate runs of
 // the tile's 3x3x3 block, its first query (index into qpos) and query count.  A workgroup loads
@@ -497,7 +509,7 @@ __device__ __forceinline__ void sort_list(uint16_t* L, int k, float qx, float qy
 // (the kernels get the queues through one pointer to a device copy: eight pointers as kernel
 // arguments pushed the tile kernels into spilling scalar registers)
 __device__ __forceinline__ void push_sort(const TierQ* tq, int32_t j, int k) {
-  const int t = k <= kCapQuery ? 0 : (k <= kCapMid8 ? 1 : (k <= kCapMid ? 2 : 3));
+  const int t = query_tier(k);
   tq->q[t][atomicAdd(tq->n[t], 1)] = j | kListMode;
 }
 
@@ -804,7 +816,11 @@ __global__ void __launch_bounds__(256, TCAP <= kTcapSmall ? 4 : (STAGE ? 3 : 2))
         // the per-query kernel (test + sort): measured against a second tile pass writing these
         // lists unsorted for a sort-only per-query pass, that pass cost more (room: dense tiles
         // +0.22 ms against 0.07 saved; dense variant: no change)
-        tq->q[0][wave_push_slot(tq->n[0])] = start + tid;
+        // (the tier that holds k: a dense tile's 4k-8k lists no longer pass through the 4k tier's
+        // test first)
+        const int t = ok ? query_tier(k) : 0;
+        if (t == 0) tq->q[0][wave_push_slot(tq->n[0])] = start + tid;
+        else tq->q[t][atomicAdd(tq->n[t], 1)] = start + tid;
       }
     }
     if (sorted) {
@@ -1020,9 +1036,10 @@ __global__ void __launch_bounds__(256) k_nb_wide(GridView g, const int32_t* __re
   }
 }
 
-// One 256-thread workgroup per query: candidates streamed from L2/HBM, the list bucket-sorted
+// One workgroup of NT threads per query: candidates streamed from L2/HBM, the list bucket-sorted
 // in LDS (GLOBAL = false) or in a per-workgroup global scratch slice (GLOBAL = true).
-// Lists longer than CAP go to `over` (or raise err when over == nullptr).
+// A test-mode list longer than CAP goes straight to the tier that holds it (`tq`: its length is
+// known once it has been counted), or raises err when tq == nullptr.
 // list entry of grid position p: (run << 28) | offset in the run
 __device__ __forceinline__ uint32_t pos_entry(const Runs& R, int32_t p) {
   uint32_t e = 0;
@@ -1037,15 +1054,54 @@ __device__ __forceinline__ uint32_t pos_entry16(const Runs& R, int32_t p) {
   return ((e >> 28) << 12) | (e & 0xfffu);
 }
 
-template <int CAP, int NB, bool GLOBAL>
-__global__ void __launch_bounds__(256) k_nb_query(GridView g, const int32_t* __restrict__ work,
-                                                  const int* __restrict__ n_ptr,
-                                                  float rr, float bscale, int sorted, ListOut out,
-                                                  int32_t* __restrict__ over, int* __restrict__ n_over,
-                                                  int* __restrict__ err, uint32_t* __restrict__ scratch,
-                                                  int* __restrict__ next_work) {
+// exclusive scan of NB bucket counts into bpos by all NT threads (NB / NT consecutive buckets
+// each: a one-wave scan of 16-64 buckets per lane read them at a lane stride of 16-64 words,
+// 16-64-way LDS bank conflicts)
+template <int NB, int NT>
+__device__ __forceinline__ void bucket_scan(const int* bcount, int* bpos, int* wsum) {
+  constexpr int PER = NB >= NT ? NB / NT : 1;
+  const int tid = threadIdx.x;
+  const bool in = tid * PER < NB;
+  int c[PER];
+  int s = 0;
+#pragma unroll
+  for (int v = 0; v < PER; ++v) {
+    c[v] = in ? bcount[tid * PER + v] : 0;
+    s += c[v];
+  }
+  const int inc = wave_incl_scan(s);
+  if ((tid & 63) == 63) wsum[tid >> 6] = inc;
+  __syncthreads();
+  int ex = inc - s;
+  for (int w = 0; w < (tid >> 6); ++w) ex += wsum[w];
+  if (in) {
+#pragma unroll
+    for (int v = 0; v < PER; ++v) {
+      bpos[tid * PER + v] = ex;
+      ex += c[v];
+    }
+  }
+}
+
+// the GLOBAL tier's rank pass reads the bucket-ordered d2 bits through LDS windows of this many
+constexpr int kRankWindow = 1024;  // (4 KB: the tier keeps four workgroups per CU)
+
+// NT (round 6): 512 threads for the 4k / 8k tiers, 1024 for the 16k tier -- their LDS, not their
+// registers, caps the workgroups per CU (4 / 2 / 1), so a wider workgroup halves each list's
+// chain of dependent latency rounds at the same LDS (the 16k tier ran one wave per SIMD)
+// WPE: the waves per SIMD the tier's LDS allows (the register budget the compiler is held to)
+template <int CAP, int NB, bool GLOBAL, int NT, int WPE>
+__global__ void __launch_bounds__(NT, WPE) k_nb_query(GridView g, const int32_t* __restrict__ work,
+                                                 const int* __restrict__ n_ptr,
+                                                 float rr, float bscale, int sorted, ListOut out,
+                                                 const TierQ* __restrict__ tq,
+                                                 int* __restrict__ err, uint32_t* __restrict__ scratch,
+                                                 int* __restrict__ next_work) {
+  static_assert(NT % 256 == 0 && CAP % NT == 0, "whole rounds of NT entries");
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
   __shared__ int bcount[NB], bpos[NB];
+  __shared__ uint32_t wd[GLOBAL ? kRankWindow : 1];  // GLOBAL: the rank pass's window of d2 bits
+  __shared__ int wsum[NT / 64];
   __shared__ int s_count;
   __shared__ unsigned long long s_base;
   uint32_t* base_arr = GLOBAL ? scratch + (size_t)blockIdx.x * 4 * CAP : smem;
@@ -1053,37 +1109,57 @@ __global__ void __launch_bounds__(256) k_nb_query(GridView g, const int32_t* __r
   uint32_t* hd = base_arr + CAP;    // d2 bits of hits
   uint32_t* sdv = base_arr + 2 * CAP;  // (GLOBAL: bucket-ordered copies)
   uint32_t* spv = base_arr + 3 * CAP;
-  const int tid = threadIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63;
   const int count = *n_ptr;
   if (count == 0) return;  // an empty tier costs only its dispatch (the queue head stays 0)
-  __shared__ int s_w;
+  __shared__ int s_w, s_wn;
   // thread 0's: list slots from a per-workgroup arena and the totals added once per workgroup
   // (one same-address atomic per query made the cursors the bottleneck of this kernel)
   unsigned long long wg_total = 0, wg_long = 0, wg_long_n = 0, arena_base = 0, arena_left = 0;
   TPROF_DECL;
-  // thread 0 holds the next work item, fetched one item ahead (its round trip overlaps the current
-  // item instead of stalling the workgroup at the top of every item; round 6)
-  int w_next = 0;
-  if (tid == 0) w_next = atomicAdd(next_work, 1);
+  // Work items are fetched two ahead by thread 0 (w1: the next item, w2: the one after), so each
+  // item's work index is loaded at the top of the item before it and its record after that item's
+  // first phase: an item starts with its record in registers (round 6: it used to start with the
+  // chain queue atomic -> work[] -> record, three dependent round trips)
+  int w1 = 0, w2 = 0;
+  if (tid == 0) {
+    w1 = atomicAdd(next_work, 1);
+    w2 = w1 < count ? atomicAdd(next_work, 1) : count;
+  }
+  int32_t jw_pf = 0;   // the next item's work entry
+  int rec_pf = 0;      // and its record word (lane l < kRecInts of each wave: word l)
+  bool have_pf = false;
   for (;;) {  // dynamic queue: list lengths (and costs) differ by orders of magnitude
     if (tid == 0) {
-      s_w = w_next;
-      if (w_next < count) w_next = atomicAdd(next_work, 1);
+      s_w = w1;
+      s_wn = w2;
+      w1 = w2;
+      if (w2 < count) w2 = atomicAdd(next_work, 1);
     }
     __syncthreads();
-    const int w = s_w;
+    const int w = s_w, wn = s_wn;
     __syncthreads();
     if (w >= count) break;
-    const int32_t jw = work[w];
+    int32_t jw;
+    int recv;
+    if (have_pf) {
+      jw = jw_pf;
+      recv = rec_pf;
+    } else {
+      jw = work[w];
+      recv = lane < kRecInts ? out.qrec[(int64_t)(jw & (kListMode - 1)) * kRecInts + lane] : 0;
+    }
+    const bool pf = wn < count;
+    const int32_t jn = pf ? work[wn] : 0;  // (its record load is issued after the first phase)
     const bool from_list = (jw & kListMode) != 0;  // the list is in place, unsorted: sort only
     const int32_t j = jw & (kListMode - 1);
     // the query's record (its block: the runs its list entries refer to)
     Runs R;
     int32_t qp;
     float4 q;
-    qrec_unpack((tid & 63) < kRecInts ? out.qrec[(int64_t)j * kRecInts + (tid & 63)] : 0, R, qp, q);
+    qrec_unpack(recv, R, qp, q);
     if (tid == 0) s_count = 0;
-    for (int b = tid; b < NB; b += 256) bcount[b] = 0;
+    for (int b = tid; b < NB; b += NT) bcount[b] = 0;
     __syncthreads();
     TPROF_T(q0);
     if (from_list) {
@@ -1097,12 +1173,12 @@ __global__ void __launch_bounds__(256) k_nb_query(GridView g, const int32_t* __r
         s_base = (unsigned long long)lo;
         if (kl > CAP) atomicMax(err, kl);
       }
-      for (int e0 = tid; e0 < kk; e0 += 4 * 256) {
+      for (int e0 = tid; e0 < kk; e0 += 4 * NT) {
         int32_t pos[4];
         float4 c[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-          const uint32_t en = out.list[lo + min(e0 + 256 * u, kk - 1)];
+          const uint32_t en = out.list[lo + min(e0 + NT * u, kk - 1)];
           const int r = entry_run(en);
           int32_t st = R.start[0];
 #pragma unroll
@@ -1112,7 +1188,7 @@ __global__ void __launch_bounds__(256) k_nb_query(GridView g, const int32_t* __r
         }
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-          const int e = e0 + 256 * u;
+          const int e = e0 + NT * u;
           if (e < kk) {
             const float d2 = flann_d2(q.x, q.y, q.z, c[u].x, c[u].y, c[u].z);
             hits[e] = (uint32_t)pos[u];
@@ -1123,12 +1199,12 @@ __global__ void __launch_bounds__(256) k_nb_query(GridView g, const int32_t* __r
         }
       }
     }
-    for (int t0 = 0; !from_list && t0 < R.pref[9]; t0 += 4 * 256) {  // 4 candidates per thread in flight
+    for (int t0 = 0; !from_list && t0 < R.pref[9]; t0 += 4 * NT) {  // 4 candidates per thread in flight
       float4 c[4];
       int32_t pos[4];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        const int t = t0 + u * 256 + tid;
+        const int t = t0 + u * NT + tid;
         pos[u] = t < R.pref[9] ? run_pos(R, t) : -1;
         c[u] = g.sp[pos[u] < 0 ? 0 : pos[u]];
       }
@@ -1144,11 +1220,11 @@ __global__ void __launch_bounds__(256) k_nb_query(GridView g, const int32_t* __r
         tot += __popcll(m[u]);
       }
       int base = 0;
-      if ((tid & 63) == 0 && tot) base = atomicAdd(&s_count, tot);
+      if (lane == 0 && tot) base = atomicAdd(&s_count, tot);
       base = __shfl(base, 0);
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        if ((m[u] >> (tid & 63)) & 1) {
+        if ((m[u] >> lane) & 1) {
           const int slot = base + __popcll(m[u] & lanemask_lt());
           if (slot < CAP) {
             hits[slot] = (uint32_t)pos[u];
@@ -1161,13 +1237,21 @@ __global__ void __launch_bounds__(256) k_nb_query(GridView g, const int32_t* __r
       }
     }
     __syncthreads();
+    // the next item's record (its work entry has arrived with this item's loads)
+    rec_pf = pf && lane < kRecInts ? out.qrec[(int64_t)(jn & (kListMode - 1)) * kRecInts + lane] : 0;
+    jw_pf = jn;
+    have_pf = pf;
     TPROF_T(q1);
     if (!GLOBAL && CAP == kCapQuery) { TPROF_ADD(20, q0, q1); }
     const int k = s_count;
     if (k > CAP) {
       if (tid == 0) {
-        if (over) over[atomicAdd(n_over, 1)] = j;
-        else atomicMax(err, k);
+        if (tq) {
+          const int t = query_tier(k);
+          tq->q[t][atomicAdd(tq->n[t], 1)] = j;
+        } else {
+          atomicMax(err, k);
+        }
       }
       __syncthreads();
       continue;
@@ -1208,33 +1292,33 @@ __global__ void __launch_bounds__(256) k_nb_query(GridView g, const int32_t* __r
         out.lg[j] = c16 ? kLgCompact : 0;
       }
     };
+    // the entry at bucket-order slot s of position p goes to list slot st + rank
+    auto put = [&](int64_t off, int slot, uint32_t p) {
+      if (c16) reinterpret_cast<uint16_t*>(out.list)[2 * off + slot] = (uint16_t)pos_entry16(R, (int32_t)p);
+      else out.list[off + slot] = pos_entry(R, (int32_t)p);
+    };
+    auto bucket_of = [&](uint32_t d) {
+      const int b = (int)(__uint_as_float(d) * bscale);
+      return b < NB ? b : NB - 1;
+    };
     if (sorted && k > 1) {  // (the bucket counts were taken with the hits)
-      if (tid < 64) {  // one wave scans the counts
-        constexpr int PER = NB / 64;
-        int s = 0;
-        for (int v = 0; v < PER; ++v) s += bcount[tid * PER + v];
-        const int inc = wave_incl_scan(s);
-        int ex = inc - s;
-        for (int v = 0; v < PER; ++v) { bpos[tid * PER + v] = ex; ex += bcount[tid * PER + v]; }
-      }
+      bucket_scan<NB, NT>(bcount, bpos, wsum);
       __syncthreads();
       if constexpr (!GLOBAL) {
-        // bucket scatter in place through registers (8 B of LDS per entry: 4 workgroups per CU)
-        constexpr int PT = CAP / 256;
+        // bucket scatter in place through registers (8 B of LDS per entry)
+        constexpr int PT = CAP / NT;
         uint32_t rp[PT], rd[PT];
 #pragma unroll
         for (int u = 0; u < PT; ++u) {
-          const int e = tid + u * 256;
+          const int e = tid + u * NT;
           rp[u] = e < k ? hits[e] : 0u;
           rd[u] = e < k ? hd[e] : 0u;
         }
         __syncthreads();
 #pragma unroll
         for (int u = 0; u < PT; ++u) {
-          if (tid + u * 256 < k) {
-            int b = (int)(__uint_as_float(rd[u]) * bscale);
-            b = b < NB ? b : NB - 1;
-            const int slot = atomicAdd(&bpos[b], 1);
+          if (tid + u * NT < k) {
+            const int slot = atomicAdd(&bpos[bucket_of(rd[u])], 1);
             hd[slot] = rd[u];
             hits[slot] = rp[u];
           }
@@ -1245,10 +1329,9 @@ __global__ void __launch_bounds__(256) k_nb_query(GridView g, const int32_t* __r
         // (a compact list occupies (k + 1) / 2 words: the words its slot reservation counted)
         const bool fits = (unsigned long long)(off + (c16 ? (k + 1) / 2 : k)) <= out.cap;
         // exact (d2, caller index) rank inside the bucket, written straight to the list
-        for (int s = tid; s < k; s += 256) {
+        for (int s = tid; s < k; s += NT) {
           const uint32_t d = hd[s], p = hits[s];
-          int b = (int)(__uint_as_float(d) * bscale);
-          b = b < NB ? b : NB - 1;
+          const int b = bucket_of(d);
           const int en = bpos[b], st = en - bcount[b];
           int rank = 0;
           for (int v = st; v < en; ++v) {
@@ -1256,50 +1339,84 @@ __global__ void __launch_bounds__(256) k_nb_query(GridView g, const int32_t* __r
             if (dv < d) ++rank;
             else if (dv == d && v != s && g.perm[hits[v]] < g.perm[p]) ++rank;
           }
-          if (fits) {
-            if (c16) reinterpret_cast<uint16_t*>(out.list)[2 * off + st + rank] = (uint16_t)pos_entry16(R, (int32_t)p);
-            else out.list[off + st + rank] = pos_entry(R, (int32_t)p);
-          }
+          if (fits) put(off, st + rank, p);
         }
         __syncthreads();
         TPROF_T(q2);
         if (CAP == kCapQuery) { TPROF_ADD(21, q1, q2); TPROF_ADD(22, 0, (long long)k); TPROF_ADD(23, 0, (long long)R.pref[9]); }
         continue;
       } else {
-        for (int e = tid; e < k; e += 256) {
-          const uint32_t d = hd[e];
-          int b = (int)(__uint_as_float(d) * bscale);
-          b = b < NB ? b : NB - 1;
-          const int slot = atomicAdd(&bpos[b], 1);
-          sdv[slot] = d;
-          spv[slot] = hits[e];
-        }
-        __syncthreads();
-        for (int s = tid; s < k; s += 256) {
-          const uint32_t d = sdv[s], p = spv[s];
-          int b = (int)(__uint_as_float(d) * bscale);
-          b = b < NB ? b : NB - 1;
-          const int en = bpos[b], st = en - bcount[b];
-          int rank = 0;
-          for (int v = st; v < en; ++v) {
-            const uint32_t dv = sdv[v];
-            if (dv < d) ++rank;
-            else if (dv == d && v != s && g.perm[spv[v]] < g.perm[p]) ++rank;
+        // scatter to bucket order (scratch), four entries per thread in flight
+        for (int e0 = tid; e0 < k; e0 += 4 * NT) {
+          uint32_t dd[4], pp[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const int e = min(e0 + u * NT, k - 1);
+            dd[u] = hd[e];
+            pp[u] = hits[e];
           }
-          hits[st + rank] = p;
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            if (e0 + u * NT < k) {
+              const int slot = atomicAdd(&bpos[bucket_of(dd[u])], 1);
+              sdv[slot] = dd[u];
+              spv[slot] = pp[u];
+            }
+          }
         }
+        commit();
+        __syncthreads();
+        const int64_t off = (int64_t)s_base;
+        const bool fits = (unsigned long long)(off + (c16 ? (k + 1) / 2 : k)) <= out.cap;
+        // rank pass in windows of kRankWindow bucket-order entries staged in LDS (it read every
+        // bucket mate from the scratch: one dependent L2 round trip per mate); a bucket that
+        // straddles the window reads its mates from the scratch
+        for (int w0 = 0; w0 < k; w0 += kRankWindow) {
+          const int wn = min(kRankWindow, k - w0);
+          constexpr int WPT = kRankWindow / NT;
+          uint32_t wv_[WPT];
+#pragma unroll
+          for (int u = 0; u < WPT; ++u) wv_[u] = sdv[w0 + min(tid + u * NT, wn - 1)];
+#pragma unroll
+          for (int u = 0; u < WPT; ++u) wd[tid + u * NT] = wv_[u];
+          __syncthreads();
+          for (int s = w0 + tid; s < w0 + wn; s += NT) {
+            const uint32_t p = spv[s];
+            const uint32_t d = wd[s - w0];
+            const int b = bucket_of(d);
+            const int en = bpos[b], st = en - bcount[b];
+            int rank = 0;
+            bool tie = false;
+            if (st >= w0 && en <= w0 + wn) {
+              for (int v = st; v < en; ++v) {
+                const uint32_t dv = wd[v - w0];
+                rank += dv < d ? 1 : 0;
+                tie |= dv == d && v != s;
+              }
+            } else {
+              for (int v = st; v < en; ++v) {
+                const uint32_t dv = sdv[v];
+                rank += dv < d ? 1 : 0;
+                tie |= dv == d && v != s;
+              }
+            }
+            if (tie) {  // equal d2: the caller index decides (FLANN); rare
+              const int32_t mine = g.perm[p];
+              for (int v = st; v < en; ++v)
+                if (v != s && sdv[v] == d && g.perm[spv[v]] < mine) ++rank;
+            }
+            if (fits) put(off, st + rank, p);
+          }
+          __syncthreads();  // the window is rewritten by the next one
+        }
+        continue;
       }
     }
     commit();
     __syncthreads();
     const int64_t off = (int64_t)s_base;
-    if ((unsigned long long)(off + (c16 ? (k + 1) / 2 : k)) <= out.cap) {
-      if (c16)
-        for (int m = tid; m < k; m += 256)
-          reinterpret_cast<uint16_t*>(out.list)[2 * off + m] = (uint16_t)pos_entry16(R, (int32_t)hits[m]);
-      else
-        for (int m = tid; m < k; m += 256) out.list[off + m] = pos_entry(R, (int32_t)hits[m]);
-    }
+    if ((unsigned long long)(off + (c16 ? (k + 1) / 2 : k)) <= out.cap)
+      for (int m = tid; m < k; m += NT) put(off, m, hits[m]);
     __syncthreads();
   }
   if (tid == 0) {
@@ -1451,13 +1568,13 @@ void build_lists(pfx_ctx* ctx, const Grid& G, const uint8_t* mask, double radius
     check_launch("nblist tiles");
   }
   const size_t lds_q = sizeof(uint32_t) * 2 * kCapQuery;
-  PFX_HIP(hipFuncSetAttribute((const void*)k_nb_query<kCapQuery, kBucketsQuery, false>,
+  PFX_HIP(hipFuncSetAttribute((const void*)k_nb_query<kCapQuery, kBucketsQuery, false, kNtQuery, kNtQuery / 64>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_q));
   const size_t lds_m8 = sizeof(uint32_t) * 2 * kCapMid8;
-  PFX_HIP(hipFuncSetAttribute((const void*)k_nb_query<kCapMid8, kBucketsMid8, false>,
+  PFX_HIP(hipFuncSetAttribute((const void*)k_nb_query<kCapMid8, kBucketsMid8, false, kNtMid8, kNtMid8 / 128>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_m8));
   const size_t lds_m = sizeof(uint32_t) * 2 * kCapMid;
-  PFX_HIP(hipFuncSetAttribute((const void*)k_nb_query<kCapMid, kBucketsMid, false>,
+  PFX_HIP(hipFuncSetAttribute((const void*)k_nb_query<kCapMid, kBucketsMid, false, kNtMid, kNtMid / 256>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_m));
   DevBuf& lb = B("list");
   if (!lb.ptr) lb.get(sizeof(uint32_t) * 64 * (size_t)(n + 1));
@@ -1491,15 +1608,15 @@ void build_lists(pfx_ctx* ctx, const Grid& G, const uint8_t* mask, double radius
     };
     DevBuf& hs = B("scratch");
     auto launch_mid8 = [&] {
-      k_nb_query<kCapMid8, kBucketsMid8, false><<<256 * 2, 256, lds_m8, st>>>(
-          g, mid8, counters + 14, rr, (float)kBucketsMid8 / rr, isort, lo, mid, counters + 12,
-          counters + 4, nullptr, counters + 15);
+      k_nb_query<kCapMid8, kBucketsMid8, false, kNtMid8, kNtMid8 / 128><<<256 * 2, kNtMid8, lds_m8, st>>>(
+          g, mid8, counters + 14, rr, (float)kBucketsMid8 / rr, isort, lo, tq_dev, counters + 4, nullptr,
+          counters + 15);
       check_launch("nblist 8k lists");
     };
     auto launch_mid = [&] {
-      k_nb_query<kCapMid, kBucketsMid, false><<<256, 256, lds_m, st>>>(
-          g, mid, counters + 12, rr, (float)kBucketsMid / rr, isort, lo, huge, counters + 3,
-          counters + 4, nullptr, counters + 13);
+      k_nb_query<kCapMid, kBucketsMid, false, kNtMid, kNtMid / 256><<<256, kNtMid, lds_m, st>>>(
+          g, mid, counters + 12, rr, (float)kBucketsMid / rr, isort, lo, tq_dev, counters + 4, nullptr,
+          counters + 13);
       check_launch("nblist 16k lists");
     };
     // (see mid_tier_wanted; a rerun launches every tier)
@@ -1517,8 +1634,8 @@ void build_lists(pfx_ctx* ctx, const Grid& G, const uint8_t* mask, double radius
       hs.get(huge_slice * (size_t)std::min(kHugeBlocks, std::max(256, count)));
     };
     auto launch_huge = [&] {
-      k_nb_query<kCapHuge, kBucketsHuge, true><<<huge_blocks(), 256, 0, st>>>(
-          g, huge, counters + 3, rr, (float)kBucketsHuge / rr, isort, lo, nullptr, nullptr, counters + 4,
+      k_nb_query<kCapHuge, kBucketsHuge, true, kNtHuge, 4><<<huge_blocks(), kNtHuge, 0, st>>>(
+          g, huge, counters + 3, rr, (float)kBucketsHuge / rr, isort, lo, nullptr, counters + 4,
           static_cast<uint32_t*>(hs.ptr), counters + 9);
       check_launch("nblist huge lists");
     };
@@ -1556,9 +1673,9 @@ void build_lists(pfx_ctx* ctx, const Grid& G, const uint8_t* mask, double radius
       }
       {
         TimeScope t3(ctx, std::string(tag) + "_lists_query");
-        k_nb_query<kCapQuery, kBucketsQuery, false><<<256 * 4, 256, lds_q, st>>>(
-            g, single, counters + 2, rr, (float)kBucketsQuery / rr, isort, lo,
-            use_mid8 ? mid8 : mid, counters + (use_mid8 ? 14 : 12), counters + 4, nullptr, counters + 8);
+        k_nb_query<kCapQuery, kBucketsQuery, false, kNtQuery, kNtQuery / 64><<<256 * 4, kNtQuery, lds_q, st>>>(
+            g, single, counters + 2, rr, (float)kBucketsQuery / rr, isort, lo, tq_dev, counters + 4, nullptr,
+            counters + 8);
         // lists of 4k-8k entries (dense clouds: ~14 % of the 10M-pt room's queries, 31 % of its
         // entries) in two 72 KB workgroups per CU instead of the 16k tier's one (10M-pt dense
         // variant: per-query lists 750 -> 650 ms, 1066 -> 968 ms per step; PFX_LIST_MID8=0 turns

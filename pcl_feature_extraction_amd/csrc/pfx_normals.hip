@@ -37,7 +37,10 @@ constexpr int kLaneMax = PFX_LANE_MAX;
 // compact (16-bit) lists reach kLaneMaxCompact entries and k_normals_long reads 32-bit lists only
 static_assert(kLaneMax >= kLaneMaxCompact, "lists up to kLaneMaxCompact must take the lane-per-query chains");
 
-constexpr int kLaneMaxDense = 2 * kLaneMax;
+#ifndef PFX_LANE_DENSE_MUL
+#define PFX_LANE_DENSE_MUL 2
+#endif
+constexpr int kLaneMaxDense = PFX_LANE_DENSE_MUL * kLaneMax;
 
 __device__ __forceinline__ void chain_add(float a[9], float x, float y, float z) {
   a[0] = a[0] + x * x;
