@@ -42,7 +42,16 @@ constexpr int kCapHuge = 1 << 18, kBucketsHuge = 4096, kHugeBlocks = PFX_HUGE_BL
 #ifndef PFX_NT_MID
 #define PFX_NT_MID 1024
 #endif
-constexpr int kNtQuery = PFX_NT_QUERY, kNtMid8 = PFX_NT_QUERY, kNtMid = PFX_NT_MID, kNtHuge = 256;
+#ifndef PFX_NT_MID8
+#define PFX_NT_MID8 1024
+#endif
+#ifndef PFX_Q_PF  // the per-query tiers' record prefetch (A/B)
+#define PFX_Q_PF 1
+#endif
+#ifndef PFX_Q_WPE  // waves per SIMD the 4k tier's registers are held to
+#define PFX_Q_WPE 8
+#endif
+constexpr int kNtQuery = PFX_NT_QUERY, kNtMid8 = PFX_NT_MID8, kNtMid = PFX_NT_MID, kNtHuge = 256;
 constexpr int kNCounters = 20;
 
 // The lists of a wide tile are written unsorted to HBM by a test pass and ordered in place by the
@@ -247,12 +256,12 @@ struct CandGlobal {
 // phase probes, accumulated in registers and added to the globals once per workgroup / wave at
 // the kernel's end (an atomic per probe left global atomics outstanding that the kernel's own
 // vmcnt waits then waited for, inflating the very phases they measured)
-__device__ unsigned long long g_tile_prof[24];
+__device__ unsigned long long g_tile_prof[28];
 // per-wave probes (lane 0 of every wave): [class * 4 + i], class 0 small / 1 sparse / 2 dense;
 // i = 0 the wave's own sort work, 1 its wait at the barrier after the sort, 2 the staging round
 // (sort barrier -> staged registers stored), 3 the list-write loop
 __device__ unsigned long long g_tile_prof2[12];
-#define TPROF_DECL unsigned long long tacc_[24] = {}, wacc_[12] = {}
+#define TPROF_DECL unsigned long long tacc_[28] = {}, wacc_[12] = {}
 #define TPROF_T(v) long long v = (threadIdx.x == 0) ? clock64() : 0
 #define TPROF_ADD(i, a, b) tacc_[i] += (unsigned long long)((b) - (a))
 #define WPROF_T(v) long long v = ((threadIdx.x & 63) == 0) ? clock64() : 0
@@ -260,7 +269,7 @@ __device__ unsigned long long g_tile_prof2[12];
 #define TPROF_FLUSH                                                                      \
   do {                                                                                   \
     if (threadIdx.x == 0)                                                                \
-      _Pragma("unroll") for (int i_ = 0; i_ < 24; ++i_)                                  \
+      _Pragma("unroll") for (int i_ = 0; i_ < 28; ++i_)                                  \
         if (tacc_[i_]) atomicAdd(&g_tile_prof[i_], tacc_[i_]);                           \
     if ((threadIdx.x & 63) == 0)                                                         \
       _Pragma("unroll") for (int i_ = 0; i_ < 12; ++i_)                                  \
@@ -526,12 +535,15 @@ __device__ __forceinline__ void tile_pass(const GridView& g, const Runs& R, int 
   const int tid = threadIdx.x, lane = tid & 63;
 #pragma unroll
   for (int u = 0; u < QW; ++u) cursor[u] = 0;
+  // streamed chunks: chunk c + 1's loads are issued right after chunk c is in LDS and land during
+  // chunk c's test (round 6: each chunk waited a full L2 round trip before its test)
+  float4 cc[STAGE ? 1 : CH / 256];
+  if (!STAGE)
+#pragma unroll
+    for (int u = 0; u < CH / 256; ++u) cc[u] = g.sp[run_pos(R, min(tid + 256 * u, T - 1))];
   for (int c0 = 0; c0 < T; c0 += (STAGE ? T : CH)) {
     const int cend = STAGE ? T : min(T, c0 + CH);
     if (!STAGE) {
-      float4 cc[CH / 256];
-#pragma unroll
-      for (int u = 0; u < CH / 256; ++u) cc[u] = g.sp[run_pos(R, min(c0 + tid + 256 * u, T - 1))];
       __syncthreads();  // the previous chunk's readers are done
 #pragma unroll
       for (int u = 0; u < CH / 256; ++u) {
@@ -539,6 +551,9 @@ __device__ __forceinline__ void tile_pass(const GridView& g, const Runs& R, int 
         hz[tid + 256 * u] = cc[u].z;
       }
       __syncthreads();
+      if (c0 + CH < T)
+#pragma unroll
+        for (int u = 0; u < CH / 256; ++u) cc[u] = g.sp[run_pos(R, min(c0 + CH + tid + 256 * u, T - 1))];
     }
     const float2* XYs = STAGE ? cxy : hxy - c0;
     const float* Zs = STAGE ? cz : hz - c0;
@@ -1084,11 +1099,15 @@ __device__ __forceinline__ void bucket_scan(const int* bcount, int* bpos, int* w
 }
 
 // the GLOBAL tier's rank pass reads the bucket-ordered d2 bits through LDS windows of this many
-constexpr int kRankWindow = 1024;  // (4 KB: the tier keeps four workgroups per CU)
+// (16 KB: with its one bucket array, 16 KB, the tier keeps four workgroups per CU)
+constexpr int kRankWindow = 4096;
 
-// NT (round 6): 512 threads for the 4k / 8k tiers, 1024 for the 16k tier -- their LDS, not their
-// registers, caps the workgroups per CU (4 / 2 / 1), so a wider workgroup halves each list's
-// chain of dependent latency rounds at the same LDS (the 16k tier ran one wave per SIMD)
+// NT (round 6): 512 threads for the 4k tier, 1024 for the 8k and 16k tiers -- their LDS, not their
+// registers, caps the workgroups per CU (4 / 2 / 1), so a wider workgroup shortens each list's
+// chain of dependent latency rounds at the same LDS (the 16k tier ran one wave per SIMD).
+// GLOBAL (the > 16k tier): one bucket array (counts, scanned in place to starts, advanced by the
+// scatter to ends: a bucket is [end of b - 1, end of b)), eight entries per thread in flight in
+// the passes over the scratch, the rank pass through LDS windows
 // WPE: the waves per SIMD the tier's LDS allows (the register budget the compiler is held to)
 template <int CAP, int NB, bool GLOBAL, int NT, int WPE>
 __global__ void __launch_bounds__(NT, WPE) k_nb_query(GridView g, const int32_t* __restrict__ work,
@@ -1099,8 +1118,9 @@ __global__ void __launch_bounds__(NT, WPE) k_nb_query(GridView g, const int32_t*
                                                  int* __restrict__ next_work) {
   static_assert(NT % 256 == 0 && CAP % NT == 0, "whole rounds of NT entries");
   extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
-  __shared__ int bcount[NB], bpos[NB];
+  __shared__ int bcount[NB], bpos[GLOBAL ? 1 : NB];
   __shared__ uint32_t wd[GLOBAL ? kRankWindow : 1];  // GLOBAL: the rank pass's window of d2 bits
+  constexpr int UL = GLOBAL ? 8 : 4;  // entries / candidates per thread in flight
   __shared__ int wsum[NT / 64];
   __shared__ int s_count;
   __shared__ unsigned long long s_base;
@@ -1142,14 +1162,14 @@ __global__ void __launch_bounds__(NT, WPE) k_nb_query(GridView g, const int32_t*
     if (w >= count) break;
     int32_t jw;
     int recv;
-    if (have_pf) {
+    if (PFX_Q_PF && have_pf) {
       jw = jw_pf;
       recv = rec_pf;
     } else {
       jw = work[w];
       recv = lane < kRecInts ? out.qrec[(int64_t)(jw & (kListMode - 1)) * kRecInts + lane] : 0;
     }
-    const bool pf = wn < count;
+    const bool pf = PFX_Q_PF && wn < count;
     const int32_t jn = pf ? work[wn] : 0;  // (its record load is issued after the first phase)
     const bool from_list = (jw & kListMode) != 0;  // the list is in place, unsorted: sort only
     const int32_t j = jw & (kListMode - 1);
@@ -1173,11 +1193,11 @@ __global__ void __launch_bounds__(NT, WPE) k_nb_query(GridView g, const int32_t*
         s_base = (unsigned long long)lo;
         if (kl > CAP) atomicMax(err, kl);
       }
-      for (int e0 = tid; e0 < kk; e0 += 4 * NT) {
-        int32_t pos[4];
-        float4 c[4];
+      for (int e0 = tid; e0 < kk; e0 += UL * NT) {
+        int32_t pos[UL];
+        float4 c[UL];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
+        for (int u = 0; u < UL; ++u) {
           const uint32_t en = out.list[lo + min(e0 + NT * u, kk - 1)];
           const int r = entry_run(en);
           int32_t st = R.start[0];
@@ -1187,7 +1207,7 @@ __global__ void __launch_bounds__(NT, WPE) k_nb_query(GridView g, const int32_t*
           c[u] = g.sp[pos[u]];
         }
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
+        for (int u = 0; u < UL; ++u) {
           const int e = e0 + NT * u;
           if (e < kk) {
             const float d2 = flann_d2(q.x, q.y, q.z, c[u].x, c[u].y, c[u].z);
@@ -1199,22 +1219,22 @@ __global__ void __launch_bounds__(NT, WPE) k_nb_query(GridView g, const int32_t*
         }
       }
     }
-    for (int t0 = 0; !from_list && t0 < R.pref[9]; t0 += 4 * NT) {  // 4 candidates per thread in flight
-      float4 c[4];
-      int32_t pos[4];
+    for (int t0 = 0; !from_list && t0 < R.pref[9]; t0 += UL * NT) {  // UL candidates per thread in flight
+      float4 c[UL];
+      int32_t pos[UL];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+      for (int u = 0; u < UL; ++u) {
         const int t = t0 + u * NT + tid;
         pos[u] = t < R.pref[9] ? run_pos(R, t) : -1;
         c[u] = g.sp[pos[u] < 0 ? 0 : pos[u]];
       }
       // one slot reservation per wave and round (the four ballots' total) instead of one per
       // ballot, and the sort's bucket counts taken here instead of in a pass over the hits
-      float d2[4];
-      uint64_t m[4];
+      float d2[UL];
+      uint64_t m[UL];
       int tot = 0;
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+      for (int u = 0; u < UL; ++u) {
         d2[u] = flann_d2(q.x, q.y, q.z, c[u].x, c[u].y, c[u].z);
         m[u] = __ballot(pos[u] >= 0 && d2[u] < rr);
         tot += __popcll(m[u]);
@@ -1223,7 +1243,7 @@ __global__ void __launch_bounds__(NT, WPE) k_nb_query(GridView g, const int32_t*
       if (lane == 0 && tot) base = atomicAdd(&s_count, tot);
       base = __shfl(base, 0);
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+      for (int u = 0; u < UL; ++u) {
         if ((m[u] >> lane) & 1) {
           const int slot = base + __popcll(m[u] & lanemask_lt());
           if (slot < CAP) {
@@ -1302,8 +1322,10 @@ __global__ void __launch_bounds__(NT, WPE) k_nb_query(GridView g, const int32_t*
       return b < NB ? b : NB - 1;
     };
     if (sorted && k > 1) {  // (the bucket counts were taken with the hits)
-      bucket_scan<NB, NT>(bcount, bpos, wsum);
+      bucket_scan<NB, NT>(bcount, GLOBAL ? bcount : bpos, wsum);
       __syncthreads();
+      TPROF_T(q1s);
+      if (!GLOBAL && CAP == kCapQuery) { TPROF_ADD(24, q1, q1s); TPROF_ADD(27, 0, (long long)from_list); }
       if constexpr (!GLOBAL) {
         // bucket scatter in place through registers (8 B of LDS per entry)
         constexpr int PT = CAP / NT;
@@ -1325,6 +1347,8 @@ __global__ void __launch_bounds__(NT, WPE) k_nb_query(GridView g, const int32_t*
         }
         commit();
         __syncthreads();
+        TPROF_T(q1c);
+        if (CAP == kCapQuery) { TPROF_ADD(25, q1s, q1c); }
         const int64_t off = (int64_t)s_base;
         // (a compact list occupies (k + 1) / 2 words: the words its slot reservation counted)
         const bool fits = (unsigned long long)(off + (c16 ? (k + 1) / 2 : k)) <= out.cap;
@@ -1343,22 +1367,26 @@ __global__ void __launch_bounds__(NT, WPE) k_nb_query(GridView g, const int32_t*
         }
         __syncthreads();
         TPROF_T(q2);
-        if (CAP == kCapQuery) { TPROF_ADD(21, q1, q2); TPROF_ADD(22, 0, (long long)k); TPROF_ADD(23, 0, (long long)R.pref[9]); }
+        if (CAP == kCapQuery) {
+          TPROF_ADD(21, q1, q2); TPROF_ADD(22, 0, (long long)k); TPROF_ADD(23, 0, (long long)R.pref[9]);
+          TPROF_ADD(26, q1c, q2);
+        }
         continue;
       } else {
-        // scatter to bucket order (scratch), four entries per thread in flight
-        for (int e0 = tid; e0 < k; e0 += 4 * NT) {
-          uint32_t dd[4], pp[4];
+        // scatter to bucket order (scratch), UL entries per thread in flight; bcount holds the
+        // bucket starts, advanced to the ends
+        for (int e0 = tid; e0 < k; e0 += UL * NT) {
+          uint32_t dd[UL], pp[UL];
 #pragma unroll
-          for (int u = 0; u < 4; ++u) {
+          for (int u = 0; u < UL; ++u) {
             const int e = min(e0 + u * NT, k - 1);
             dd[u] = hd[e];
             pp[u] = hits[e];
           }
 #pragma unroll
-          for (int u = 0; u < 4; ++u) {
+          for (int u = 0; u < UL; ++u) {
             if (e0 + u * NT < k) {
-              const int slot = atomicAdd(&bpos[bucket_of(dd[u])], 1);
+              const int slot = atomicAdd(&bcount[bucket_of(dd[u])], 1);
               sdv[slot] = dd[u];
               spv[slot] = pp[u];
             }
@@ -1384,7 +1412,7 @@ __global__ void __launch_bounds__(NT, WPE) k_nb_query(GridView g, const int32_t*
             const uint32_t p = spv[s];
             const uint32_t d = wd[s - w0];
             const int b = bucket_of(d);
-            const int en = bpos[b], st = en - bcount[b];
+            const int en = bcount[b], st = b ? bcount[b - 1] : 0;
             int rank = 0;
             bool tie = false;
             if (st >= w0 && en <= w0 + wn) {
@@ -1568,7 +1596,7 @@ void build_lists(pfx_ctx* ctx, const Grid& G, const uint8_t* mask, double radius
     check_launch("nblist tiles");
   }
   const size_t lds_q = sizeof(uint32_t) * 2 * kCapQuery;
-  PFX_HIP(hipFuncSetAttribute((const void*)k_nb_query<kCapQuery, kBucketsQuery, false, kNtQuery, kNtQuery / 64>,
+  PFX_HIP(hipFuncSetAttribute((const void*)k_nb_query<kCapQuery, kBucketsQuery, false, kNtQuery, PFX_Q_WPE>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_q));
   const size_t lds_m8 = sizeof(uint32_t) * 2 * kCapMid8;
   PFX_HIP(hipFuncSetAttribute((const void*)k_nb_query<kCapMid8, kBucketsMid8, false, kNtMid8, kNtMid8 / 128>,
@@ -1673,7 +1701,7 @@ void build_lists(pfx_ctx* ctx, const Grid& G, const uint8_t* mask, double radius
       }
       {
         TimeScope t3(ctx, std::string(tag) + "_lists_query");
-        k_nb_query<kCapQuery, kBucketsQuery, false, kNtQuery, kNtQuery / 64><<<256 * 4, kNtQuery, lds_q, st>>>(
+        k_nb_query<kCapQuery, kBucketsQuery, false, kNtQuery, PFX_Q_WPE><<<256 * 4, kNtQuery, lds_q, st>>>(
             g, single, counters + 2, rr, (float)kBucketsQuery / rr, isort, lo, tq_dev, counters + 4, nullptr,
             counters + 8);
         // lists of 4k-8k entries (dense clouds: ~14 % of the 10M-pt room's queries, 31 % of its
@@ -1773,7 +1801,7 @@ void build_lists(pfx_ctx* ctx, const Grid& G, const uint8_t* mask, double radius
     ctx->stats[std::string(tag) + "_mid8"] = h_cnt[14];
 #ifdef PFX_SHOT_PROFILE
     {
-      unsigned long long pr[24];
+      unsigned long long pr[28];
       PFX_HIP(hipMemcpyFromSymbol(pr, HIP_SYMBOL(g_tile_prof), sizeof(pr)));
       fprintf(stderr, "%s wave_sort cycles (wave 0): count %llu scan %llu scatter %llu rank %llu\n", tag, pr[8],
               pr[9], pr[10], pr[11]);
@@ -1782,6 +1810,8 @@ void build_lists(pfx_ctx* ctx, const Grid& G, const uint8_t* mask, double radius
               pr[3], pr[4], pr[5], pr[6], pr[7], pr[16], pr[17], pr[18], pr[19]);
       fprintf(stderr, "%s query cycles: test %llu sort+write %llu | entries %llu candidates %llu\n", tag, pr[20],
               pr[21], pr[22], pr[23]);
+      fprintf(stderr, "%s query 4k-tier phases: scan %llu scatter %llu rank+write %llu | list-mode items %llu\n", tag,
+              pr[24], pr[25], pr[26], pr[27]);
       unsigned long long pw[12];
       PFX_HIP(hipMemcpyFromSymbol(pw, HIP_SYMBOL(g_tile_prof2), sizeof(pw)));
       fprintf(stderr, "%s wave cycles (sum over waves): small sort %llu sortwait %llu staging %llu listwrite %llu | "
