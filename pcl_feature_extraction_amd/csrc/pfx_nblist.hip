@@ -49,7 +49,7 @@ constexpr int kCapHuge = 1 << 18, kBucketsHuge = 4096, kHugeBlocks = PFX_HUGE_BL
 #define PFX_Q_PF 1
 #endif
 #ifndef PFX_Q_WPE  // waves per SIMD the 4k tier's registers are held to
-#define PFX_Q_WPE 8
+#define PFX_Q_WPE 6
 #endif
 constexpr int kNtQuery = PFX_NT_QUERY, kNtMid8 = PFX_NT_MID8, kNtMid = PFX_NT_MID, kNtHuge = 256;
 constexpr int kNCounters = 20;
@@ -1525,6 +1525,8 @@ bool build_lists_check(pfx_ctx* ctx, const Grid& G, NbLists& out, const char* ta
   ctx->stats[std::string(tag) + "_huge"] = h_cnt[3];
   ctx->stats[std::string(tag) + "_mid"] = h_cnt[12];
   ctx->stats[std::string(tag) + "_wide"] = h_cnt[16];
+  ctx->stats[std::string(tag) + "_slots"] = (int64_t)h_cur[0];
+  ctx->stats[std::string(tag) + "_list_words"] = (int64_t)(lb.bytes / sizeof(uint32_t));
   return true;
 }
 
@@ -1605,7 +1607,13 @@ void build_lists(pfx_ctx* ctx, const Grid& G, const uint8_t* mask, double radius
   PFX_HIP(hipFuncSetAttribute((const void*)k_nb_query<kCapMid, kBucketsMid, false, kNtMid, kNtMid / 256>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_m));
   DevBuf& lb = B("list");
-  if (!lb.ptr) lb.get(sizeof(uint32_t) * 64 * (size_t)(n + 1));
+  if (!lb.ptr) {
+    // (PFX_LIST_WORDS: the first buffer's size in 32-bit words, for tests of the capacity guards
+    // and the regrow path; the buffer grows as needed either way)
+    size_t words = 64 * (size_t)(n + 1);
+    if (const char* e = std::getenv("PFX_LIST_WORDS")) words = std::max<size_t>(256, std::strtoull(e, nullptr, 10));
+    lb.get(sizeof(uint32_t) * words);
+  }
   const int isort = sorted ? 1 : 0;
   // tiles per queue fetch, per class: many cheap small tiles amortise the queue atomic over 4,
   // the heavy sparse / dense tiles balance better with 2 / 1 at ~1M queries (sweep S/P/D on the
@@ -1799,6 +1807,8 @@ void build_lists(pfx_ctx* ctx, const Grid& G, const uint8_t* mask, double radius
     ctx->stats[std::string(tag) + "_mid"] = h_cnt[12];
     ctx->stats[std::string(tag) + "_wide"] = h_cnt[16];
     ctx->stats[std::string(tag) + "_mid8"] = h_cnt[14];
+    ctx->stats[std::string(tag) + "_slots"] = (int64_t)h_cur[0];  // list words reserved (entries + padding + arena tails)
+    ctx->stats[std::string(tag) + "_list_words"] = (int64_t)lo.cap;
 #ifdef PFX_SHOT_PROFILE
     {
       unsigned long long pr[28];

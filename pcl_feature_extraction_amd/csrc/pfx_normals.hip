@@ -480,13 +480,22 @@ __global__ void __launch_bounds__(256, 1) k_normals_chain_big(GridView g, NbList
 // (four steps per ds_read_b128): one latency per 32 steps instead of per 16.
 // Persistent waves (grid-stride over groups of seven queries): the queue length is only known
 // on the device, and a grid sized for the worst case spends its time dispatching empty waves.
-constexpr int kPerWave = 7, kLB = 32;
+#ifndef PFX_LONG_LB
+#define PFX_LONG_LB 64
+#endif
+// steps per batch (round 6: 64, two 32-step halves per lane -- a batch's gathers are one latency
+// on the wave's chain, so twice the steps per batch halves that exposure; 32 before)
+constexpr int kPerWave = 7, kLB = PFX_LONG_LB, kLR = kLB / 32;
+static_assert(kLB % 32 == 0, "whole 32-step halves");
+// workgroups of k_normals_long resident per CU (its launch is sized to them: a persistent grid,
+// workgroups beyond them would run as a second round): 124 VGPRs at 32 steps, 154 at 64
+constexpr int kLongWgPerCu = kLB <= 32 ? 4 : 3;
 // rows padded by one float4 (a 144-B stride): the 21 rows a chain step reads (7 queries x 3
 // planes, one ds_read_b128 per lane at the same step) spread over the LDS banks instead of
 // piling onto two bank groups (a 128-B stride: 9.4 conflict cycles per LDS instruction, r03 PMC)
 constexpr int kLBPad = kLB + 4;
 struct LongLds {
-  float c[2][3][kPerWave][kLBPad];  // double-buffered x | y | z per query and step (6 KB)
+  float c[2][3][kPerWave][kLBPad];  // double-buffered x | y | z per query and step (11 KB)
   int32_t rtab[kPerWave * 9];
 };
 
@@ -593,8 +602,8 @@ __global__ void __launch_bounds__(256) k_normals_long(GridView g, NbLists L, con
       return ok ? g.sp[S.rtab[9 * qq + entry_run(e)] + (int32_t)entry_off(e)] : make_float4(0.f, 0.f, 0.f, 0.f);
     };
     constexpr int NS = (kPerWave + 1) / 2;  // slots per lane
-    uint32_t e1[NS], e2[NS];
-    float4 cv[NS];
+    uint32_t e1[NS * kLR], e2[NS * kLR];
+    float4 cv[NS * kLR];
     // staged steps past a list's end are exact zeros (acc is never -0: + 0.0f is the identity),
     // so every lane runs whole batches without bounds checks
     auto put = [&](int buf, int m0) {
@@ -602,19 +611,23 @@ __global__ void __launch_bounds__(256) k_normals_long(GridView g, NbLists L, con
       for (int i = 0; i < NS; ++i) {
         const int qq = 2 * i + half;
         if (qq < kPerWave) {
-          const bool in = m0 + st < pick(kq, qq);
-          S.c[buf][0][qq][st] = in ? cv[i].x : 0.f;
-          S.c[buf][1][qq][st] = in ? cv[i].y : 0.f;
-          S.c[buf][2][qq][st] = in ? cv[i].z : 0.f;
+#pragma unroll
+          for (int h = 0; h < kLR; ++h) {
+            const int step = st + 32 * h;
+            const bool in = m0 + step < pick(kq, qq);
+            S.c[buf][0][qq][step] = in ? cv[i * kLR + h].x : 0.f;
+            S.c[buf][1][qq][step] = in ? cv[i * kLR + h].y : 0.f;
+            S.c[buf][2][qq][step] = in ? cv[i * kLR + h].z : 0.f;
+          }
         }
       }
     };
 #pragma unroll
-    for (int i = 0; i < NS; ++i) e1[i] = entry(i, st);
+    for (int i = 0; i < NS * kLR; ++i) e1[i] = entry(i / kLR, st + 32 * (i % kLR));
 #pragma unroll
-    for (int i = 0; i < NS; ++i) cv[i] = coord(i, e1[i]);
+    for (int i = 0; i < NS * kLR; ++i) cv[i] = coord(i / kLR, e1[i]);
 #pragma unroll
-    for (int i = 0; i < NS; ++i) e1[i] = entry(i, kLB + st);
+    for (int i = 0; i < NS * kLR; ++i) e1[i] = entry(i / kLR, kLB + st + 32 * (i % kLR));
     put(0, 0);
     wsync();
     // chain term a = u * v over the coordinate planes: x*x x*y x*z y*y y*z z*z x y z
@@ -627,9 +640,9 @@ __global__ void __launch_bounds__(256) k_normals_long(GridView g, NbLists L, con
       const bool more = m0 + kLB < kmax;
       if (more) {
 #pragma unroll
-        for (int i = 0; i < NS; ++i) cv[i] = coord(i, e1[i]);  // batch m0 + kLB
+        for (int i = 0; i < NS * kLR; ++i) cv[i] = coord(i / kLR, e1[i]);  // batch m0 + kLB
 #pragma unroll
-        for (int i = 0; i < NS; ++i) e2[i] = entry(i, m0 + 2 * kLB + st);
+        for (int i = 0; i < NS * kLR; ++i) e2[i] = entry(i / kLR, m0 + 2 * kLB + st + 32 * (i % kLR));
       }
       const float4* bu = reinterpret_cast<const float4*>(&S.c[buf][pu][q7][0]);
       const float4* bv = reinterpret_cast<const float4*>(&S.c[buf][pv][q7][0]);
@@ -649,7 +662,7 @@ __global__ void __launch_bounds__(256) k_normals_long(GridView g, NbLists L, con
       if (more) {
         put(buf ^ 1, m0 + kLB);
 #pragma unroll
-        for (int i = 0; i < NS; ++i) e1[i] = e2[i];
+        for (int i = 0; i < NS * kLR; ++i) e1[i] = e2[i];
       }
       wsync();
     }
@@ -743,7 +756,7 @@ void normals_chains_dev(pfx_ctx* ctx, pfx_ctx* owner, const uint8_t* mask, int w
   k_long_lists<<<(unsigned)nb, 256, 0, st>>>(view(G), L, mask, want, lane_max, longq, n_long);
   check_launch("k_long_lists");
   // (sized to what is resident at once: waves beyond it would wait for a second round)
-  const int64_t lb = std::min<int64_t>(ceil_div(L.nq, 7 * 4), 256 * 4);
+  const int64_t lb = std::min<int64_t>(ceil_div(L.nq, 7 * 4), 256 * kLongWgPerCu);
   if (fork) {
     ctx->ensure_side();
     PFX_HIP(hipEventRecord(ctx->fork_ev[0], st));
