@@ -11,3 +11,5 @@ cp gpurun_out/pmc_$T/summary.txt profiles/${T}_pmc_summary.txt
 cp gpurun_out/pmc_$T/pmc_normals_stage.json profiles/pmc_normals_stage.json
 cp gpurun_out/pmc_$T/pmc_normals_chain.json profiles/pmc_normals_chain.json
 cp gpurun_out/t_$T.log profiles/${T}_pytest_gpu.log
+[ -f gpurun_out/prof_dense_$T/run_kernel_stats.csv ] && cp gpurun_out/prof_dense_$T/run_kernel_stats.csv profiles/${T}_dense_normals_kernel_stats.csv
+[ -f gpurun_out/prof_dense_$T.log ] && grep -E "^(dense)" gpurun_out/prof_dense_$T.log > profiles/${T}_dense_normals_only.txt

@@ -17,4 +17,7 @@ cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof_$TAG -o run -- python3 $R/bench.py --steps 5 --warmup 2 --no-cpu-baseline > $R/gpurun_out/prof_$TAG.log 2>&1 || { tail -20 $R/gpurun_out/prof_$TAG.log; exit 1; }
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof_iss_$TAG -o run -- python3 $R/bench.py --workload iss --steps 5 --warmup 2 --no-cpu-baseline > $R/gpurun_out/prof_iss_$TAG.log 2>&1 || { tail -20 $R/gpurun_out/prof_iss_$TAG.log; exit 1; }
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof_match_$TAG -o run -- python3 $R/bench.py --workload match --steps 20 --warmup 3 --no-cpu-baseline > $R/gpurun_out/prof_match_$TAG.log 2>&1 || { tail -20 $R/gpurun_out/prof_match_$TAG.log; exit 1; }
-cd $R && bash scripts/gpu_pmc.sh $TAG
+cd $R && bash scripts/gpu_pmc.sh $TAG || exit 1
+# the dense variant's normal estimation alone, per kernel (round 6)
+cd /tmp && PFX_NO_SCENES=dense PFX_NO_STEPS=2 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof_dense_$TAG -o run -- python3 $R/scripts/normals_only.py > $R/gpurun_out/prof_dense_$TAG.log 2>&1 || { tail -20 $R/gpurun_out/prof_dense_$TAG.log; exit 1; }
+echo round evidence done
