@@ -1353,15 +1353,31 @@ __global__ void __launch_bounds__(NT, WPE) k_nb_query(GridView g, const int32_t*
         // (a compact list occupies (k + 1) / 2 words: the words its slot reservation counted)
         const bool fits = (unsigned long long)(off + (c16 ? (k + 1) / 2 : k)) <= out.cap;
         // exact (d2, caller index) rank inside the bucket, written straight to the list
+        // (round 6: the bucket's first four entries read together -- buckets hold ~2-4 -- the rest
+        // one by one; it read every mate in turn, one dependent LDS round trip each)
         for (int s = tid; s < k; s += NT) {
           const uint32_t d = hd[s], p = hits[s];
           const int b = bucket_of(d);
           const int en = bpos[b], st = en - bcount[b];
+          uint32_t dv[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) dv[j] = st + j < en ? hd[st + j] : 0xffffffffu;  // (never < or == d)
           int rank = 0;
-          for (int v = st; v < en; ++v) {
-            const uint32_t dv = hd[v];
-            if (dv < d) ++rank;
-            else if (dv == d && v != s && g.perm[hits[v]] < g.perm[p]) ++rank;
+          bool tie = false;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            rank += dv[j] < d ? 1 : 0;
+            tie |= dv[j] == d && st + j != s;
+          }
+          for (int v = st + 4; v < en; ++v) {
+            const uint32_t x = hd[v];
+            rank += x < d ? 1 : 0;
+            tie |= x == d && v != s;
+          }
+          if (tie) {  // equal d2: the caller index decides (FLANN); rare
+            const int32_t mine = g.perm[p];
+            for (int v = st; v < en; ++v)
+              if (v != s && hd[v] == d && g.perm[hits[v]] < mine) ++rank;
           }
           if (fits) put(off, st + rank, p);
         }
@@ -1416,10 +1432,18 @@ __global__ void __launch_bounds__(NT, WPE) k_nb_query(GridView g, const int32_t*
             int rank = 0;
             bool tie = false;
             if (st >= w0 && en <= w0 + wn) {
-              for (int v = st; v < en; ++v) {
-                const uint32_t dv = wd[v - w0];
-                rank += dv < d ? 1 : 0;
-                tie |= dv == d && v != s;
+              uint32_t dv[4];
+#pragma unroll
+              for (int j = 0; j < 4; ++j) dv[j] = st + j < en ? wd[st + j - w0] : 0xffffffffu;
+#pragma unroll
+              for (int j = 0; j < 4; ++j) {
+                rank += dv[j] < d ? 1 : 0;
+                tie |= dv[j] == d && st + j != s;
+              }
+              for (int v = st + 4; v < en; ++v) {
+                const uint32_t x = wd[v - w0];
+                rank += x < d ? 1 : 0;
+                tie |= x == d && v != s;
               }
             } else {
               for (int v = st; v < en; ++v) {

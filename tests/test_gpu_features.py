@@ -361,6 +361,35 @@ def test_fpfh_weighting_beyond_lds_capacity(ctx):
     assert _nan_aware_equal(g, o)
 
 
+def _disc(n, radius, seed, centre=(0.2, -0.1, 1.2)):
+    """n points spread over a slightly rough disc (their distances to the centre spread evenly in
+    d2, as a surface neighbourhood's) plus jittered upward normals."""
+    rng = np.random.default_rng(seed)
+    ang = rng.uniform(0.0, 2.0 * np.pi, n)
+    rad = radius * np.sqrt(rng.uniform(0.0, 1.0, n))
+    p = np.stack([centre[0] + rad * np.cos(ang), centre[1] + rad * np.sin(ang),
+                  centre[2] + 1e-3 * rng.standard_normal(n)], axis=1).astype(np.float32)
+    v = np.stack([0.05 * rng.standard_normal(n), 0.05 * rng.standard_normal(n), np.ones(n)], axis=1)
+    v /= np.linalg.norm(v, axis=1, keepdims=True)
+    v = v.astype(np.float32)
+    return p[:, 0].copy(), p[:, 1].copy(), p[:, 2].copy(), v[:, 0].copy(), v[:, 1].copy(), v[:, 2].copy()
+
+
+def test_fpfh_weighting_global_pass_spread(ctx):
+    """A keypoint whose neighbourhood outgrows the weighting kernel's LDS (8,192) with its
+    distances spread evenly in d2, as a surface's (the shell test's centre has them all equal): a
+    disc whose 20,000 points all neighbour its centre, weighted by the global-scratch pass, gives
+    the restatement's descriptor bits."""
+    x, y, z, nx, ny, nz = _disc(20_000, 0.04, 21)
+    qx = np.array([0.2, x[5], 0.2 + 0.02], np.float32)
+    qy = np.array([-0.1, y[5], -0.1], np.float32)
+    qz = np.array([1.2, z[5], 1.2], np.float32)
+    o = O.fpfh(x, y, z, nx, ny, nz, qx, qy, qz, 0.05, threads=8)
+    g = ctx.fpfh(x, y, z, nx, ny, nz, qx, qy, qz, 0.05)
+    assert ctx.stat("fpfh_weight_global") >= 1
+    assert _nan_aware_equal(g, o)
+
+
 def test_fpfh_same_as_surface_dev_reuses_normal_lists():
     """Device API, Features::compute's sequence (features.h:187-195): normals then FPFH
     (pfx_fpfh_after_normals_dev) on the same device cloud at the same radius reuse the normals'
