@@ -1,0 +1,17 @@
+#!/bin/bash
+# round 6: two queries per wave in the all-points FPFH weighting -- FPFH / facade GPU tests, then
+# the configs[1] line (full-size bit-exact parity against the CPU restatement) for the new kernel
+# and the one-query kernel (wl1)
+set -o pipefail
+mkdir -p gpurun_out
+timeout -k 10 300 python -u -m pytest tests/test_gpu_features.py tests/test_facade.py -x -q -m gpu --timeout 120 --timeout-method thread > gpurun_out/t_r06w.log 2>&1; rc=$?
+tail -1 gpurun_out/t_r06w.log
+[ $rc -eq 0 ] || { grep -E "FAIL|Error|assert" gpurun_out/t_r06w.log | head -30; exit 1; }
+for r in 1 2; do
+for L in "" wl1; do
+  lib=pcl_feature_extraction_amd/libpfx${L:+_$L}.so
+  if [ $r = 1 ] && [ "$L" = "" ]; then extra=""; else extra="--no-cpu-baseline"; fi
+  PFX_LIB=$PWD/$lib timeout -k 10 400 python bench.py --workload config1 $extra > gpurun_out/bench_c1_ab.json 2> gpurun_out/bench_c1_ab.err || { tail -20 gpurun_out/bench_c1_ab.err; exit 1; }
+  python -c "import json; d=json.load(open('gpurun_out/bench_c1_ab.json')); r=d['roofline']; print('$L', d['value'], d['ms_per_step'], r['avg_ms'], d.get('stages_ms_per_scan'), (d.get('cpu_baseline') or {}).get('parity'))"
+done
+done
