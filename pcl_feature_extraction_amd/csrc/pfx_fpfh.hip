@@ -817,6 +817,9 @@ __global__ void __launch_bounds__(kWT) k_fpfh_weight(GridView g, const float* __
 #ifndef PFX_WL_PIPE
 #define PFX_WL_PIPE 2
 #endif
+#ifndef PFX_WL_GRID  // workgroups per CU launched for the all-points weighting (static query stride)
+#define PFX_WL_GRID 32
+#endif
 __device__ __forceinline__ int32_t entry_pos(uint32_t e, const int32_t (&rs)[9]) {
   const int r = entry_run(e);
   int32_t s = rs[0];
@@ -1254,7 +1257,7 @@ void fpfh_dev(pfx_ctx* ctx, const float* sx, const float* sy, const float* sz, c
     k_nan_rows_nonfinite<<<(unsigned)ceil_div(ns * kDesc, 256), 256, 0, st>>>(sx, sy, sz, ns, out);
     if (L.nq > 0)
     {
-      const unsigned bl = (unsigned)std::min<int64_t>(ceil_div(L.nq, 4), 256 * 8);
+      const unsigned bl = (unsigned)std::min<int64_t>(ceil_div(L.nq, 4), 256 * PFX_WL_GRID);
       const GridView gv = reuse ? view(ctx->grid_a) : g;
       const bool buf = ns * kDesc * 4 < ((int64_t)1 << 31);
       if (buf)

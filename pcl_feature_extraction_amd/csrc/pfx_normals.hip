@@ -490,6 +490,9 @@ static_assert(kLB % 32 == 0, "whole 32-step halves");
 // workgroups of k_normals_long resident per CU (its launch is sized to them: a persistent grid,
 // workgroups beyond them would run as a second round): 124 VGPRs at 32 steps, 154 at 64
 constexpr int kLongWgPerCu = kLB <= 32 ? 4 : 3;
+#ifndef PFX_LONG_GRID_MUL  // (A/B: workgroups launched per resident one)
+#define PFX_LONG_GRID_MUL 1
+#endif
 // rows padded by one float4 (a 144-B stride): the 21 rows a chain step reads (7 queries x 3
 // planes, one ds_read_b128 per lane at the same step) spread over the LDS banks instead of
 // piling onto two bank groups (a 128-B stride: 9.4 conflict cycles per LDS instruction, r03 PMC)
@@ -756,7 +759,7 @@ void normals_chains_dev(pfx_ctx* ctx, pfx_ctx* owner, const uint8_t* mask, int w
   k_long_lists<<<(unsigned)nb, 256, 0, st>>>(view(G), L, mask, want, lane_max, longq, n_long);
   check_launch("k_long_lists");
   // (sized to what is resident at once: waves beyond it would wait for a second round)
-  const int64_t lb = std::min<int64_t>(ceil_div(L.nq, 7 * 4), 256 * kLongWgPerCu);
+  const int64_t lb = std::min<int64_t>(ceil_div(L.nq, 7 * 4), 256 * kLongWgPerCu * PFX_LONG_GRID_MUL);
   if (fork) {
     ctx->ensure_side();
     PFX_HIP(hipEventRecord(ctx->fork_ev[0], st));

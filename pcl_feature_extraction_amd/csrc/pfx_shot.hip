@@ -33,6 +33,9 @@ __device__ unsigned long long g_shot_prof[16];
 #define SPROF_ADD(i, a, b)
 #endif
 
+#ifndef PFX_SHOT_GRID_MUL  // (A/B: the split kernels' grids, x this)
+#define PFX_SHOT_GRID_MUL 1
+#endif
 constexpr int kCapSmall = 2048;  // sorted-neighbour capacity of the first pass (LDS keys, 5 WG/CU)
 constexpr int kCap = 16384;      // second pass for the longer lists (1 WG/CU)
 constexpr int kChunk = 256;   // neighbours staged per chunk
@@ -990,13 +993,14 @@ void shot_dev(pfx_ctx* ctx, const float* sx, const float* sy, const float* sz, c
       for (int64_t q0 = 0; q0 < nq; q0 += kSplitBatch) {
         const int64_t m = std::min<int64_t>(kSplitBatch, nq - q0);
         // (a multiple of 8: k_shot_lrf's per-XCD ranges)
-        const unsigned bl = (unsigned)(ceil_div(std::min<int64_t>(m, 256 * 10), 8) * 8);
+        const unsigned bl = (unsigned)(ceil_div(std::min<int64_t>(m, 256 * 10 * PFX_SHOT_GRID_MUL), 8) * 8);
         k_shot_lrf<<<bl, 256, lds_s, st>>>(g, qx, qy, qz, q0, m, over, n_over, r, desc, rf, grec, sq, ipos, snp, nbr,
                                            order);
         k_shot_eigen<<<(unsigned)ceil_div(m, 64), 64, 0, st>>>(sq, m);
-        k_shot_frame<<<(unsigned)std::min<int64_t>(m, 256 * 16), 256, 0, st>>>(q0, m, r, desc, rf, grec, sq, upd,
-                                                                                order);
-        k_shot_accum<<<(unsigned)std::min<int64_t>(m, 256 * 16), 256, 0, st>>>(q0, m, desc, upd, sq, order);
+        k_shot_frame<<<(unsigned)std::min<int64_t>(m, 256 * 16 * PFX_SHOT_GRID_MUL), 256, 0, st>>>(q0, m, r, desc, rf,
+                                                                                                  grec, sq, upd, order);
+        k_shot_accum<<<(unsigned)std::min<int64_t>(m, 256 * 16 * PFX_SHOT_GRID_MUL), 256, 0, st>>>(q0, m, desc, upd, sq,
+                                                                                                  order);
       }
     }
     // longer lists: grid sized for the worst case, the count stays on the device
