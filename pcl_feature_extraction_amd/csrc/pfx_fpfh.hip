@@ -817,6 +817,9 @@ __global__ void __launch_bounds__(kWT) k_fpfh_weight(GridView g, const float* __
 #ifndef PFX_WL_PIPE
 #define PFX_WL_PIPE 2
 #endif
+#ifndef PFX_W_BLOCKS  // workgroups launched for the keypoint weighting (static query stride, one per CU resident)
+#define PFX_W_BLOCKS 512
+#endif
 #ifndef PFX_WL_GRID  // workgroups per CU launched for the all-points weighting (static query stride)
 #define PFX_WL_GRID 32
 #endif
@@ -1271,7 +1274,7 @@ void fpfh_dev(pfx_ctx* ctx, const float* sx, const float* sy, const float* sz, c
     TimeScope ts(ctx, "fpfh_weight", true);
     const size_t lds = sizeof(uint64_t) * 2 * kCapW;
     PFX_HIP(hipFuncSetAttribute((const void*)k_fpfh_weight<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    const unsigned blocks = (unsigned)std::min<int64_t>(nq, 256 * 2);
+    const unsigned blocks = (unsigned)std::min<int64_t>(nq, PFX_W_BLOCKS);
     k_fpfh_weight<false><<<blocks, kWT, lds, st>>>(g, qx, qy, qz, nq, rr, spfh, out, err, ovf, err + 8, nullptr, 0);
     if (overflow_pass)
       k_fpfh_weight<true><<<kWOvfBlocks, kWT, 0, st>>>(g, qx, qy, qz, nq, rr, spfh, out, err, ovf, err + 8, wscratch,

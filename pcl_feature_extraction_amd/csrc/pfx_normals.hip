@@ -490,6 +490,9 @@ static_assert(kLB % 32 == 0, "whole 32-step halves");
 // workgroups of k_normals_long resident per CU (its launch is sized to them: a persistent grid,
 // workgroups beyond them would run as a second round): 124 VGPRs at 32 steps, 154 at 64
 constexpr int kLongWgPerCu = kLB <= 32 ? 4 : 3;
+#ifndef PFX_BIG_GRID  // workgroups of k_normals_chain_big (static stride over the deferred groups, one per CU resident)
+#define PFX_BIG_GRID 256
+#endif
 #ifndef PFX_LONG_GRID_MUL  // (A/B: workgroups launched per resident one)
 #define PFX_LONG_GRID_MUL 1
 #endif
@@ -787,7 +790,7 @@ void normals_chains_dev(pfx_ctx* ctx, pfx_ctx* owner, const uint8_t* mask, int w
     });
     PFX_HIP(attr_err);
     TimeScope tb(ctx, "normals_chain_big");
-    k_normals_chain_big<<<256, 256, sizeof(ChainLds<kStageBig>), st>>>(view(G), L, vp[0], vp[1], vp[2], nx, ny, nz,
+    k_normals_chain_big<<<PFX_BIG_GRID, 256, sizeof(ChainLds<kStageBig>), st>>>(view(G), L, vp[0], vp[1], vp[2], nx, ny, nz,
                                                                          curv, longq, n_long, n_long + 1, deferq,
                                                                          mask, want, lane_max);
     check_launch("k_normals_chain_big");

@@ -34,7 +34,7 @@ __device__ unsigned long long g_shot_prof[16];
 #endif
 
 #ifndef PFX_SHOT_GRID_MUL  // (A/B: the split kernels' grids, x this)
-#define PFX_SHOT_GRID_MUL 1
+#define PFX_SHOT_GRID_MUL 4
 #endif
 constexpr int kCapSmall = 2048;  // sorted-neighbour capacity of the first pass (LDS keys, 5 WG/CU)
 constexpr int kCap = 16384;      // second pass for the longer lists (1 WG/CU)

@@ -13,3 +13,11 @@ for L in "" s2 s4; do
   python -c "import json; d=json.load(open('gpurun_out/bench_shot_ab.json')); r=d['roofline']; print('shot $L', d['value'], d['ms_per_step'], r['avg_ms'], d.get('stages_ms_per_scan'))"
 done
 done
+# the keypoint weighting's grid: 512 (shipped) / 2048 (w2k) / 256 (w256) workgroups (headline)
+for r in 1 2; do
+for L in "" w2k w256; do
+  lib=pcl_feature_extraction_amd/libpfx${L:+_$L}.so
+  PFX_LIB=$PWD/$lib timeout -k 10 300 python bench.py --no-cpu-baseline --no-e2e > gpurun_out/bench_head_ab.json 2> gpurun_out/bench_head_ab.err || { tail -20 gpurun_out/bench_head_ab.err; exit 1; }
+  python -c "import json; d=json.load(open('gpurun_out/bench_head_ab.json')); r=d['roofline']; print('head $L', d['value'], d['ms_per_step'], r['avg_ms'], d.get('stages_ms_per_scan'))"
+done
+done
