@@ -13,10 +13,13 @@
 //      strictly ordered float chains in registers, eigen33 + viewpoint flip, output scattered to
 //      the caller's order; lists longer than kLaneMax (2048) go to k_normals_long (nine lanes per
 //      query, one per chain).
+#include <cstring>
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <mutex>
+
+#include <rocprim/rocprim.hpp>
 
 #include "pfx_nblist.h"
 #include "pfx_neighbors.h"
@@ -493,6 +496,9 @@ constexpr int kLongWgPerCu = kLB <= 32 ? 4 : 3;
 #ifndef PFX_BIG_GRID  // workgroups of k_normals_chain_big (static stride over the deferred groups, one per CU resident)
 #define PFX_BIG_GRID 256
 #endif
+#ifndef PFX_LONG_ORDERED  // (A/B: 0 = the pushed long-list queue in the dense schedule too)
+#define PFX_LONG_ORDERED 1
+#endif
 #ifndef PFX_LONG_GRID_MUL  // (A/B: workgroups launched per resident one)
 #define PFX_LONG_GRID_MUL 1
 #endif
@@ -526,10 +532,12 @@ __global__ void k_nan_fill4_masked(float* __restrict__ a, float* __restrict__ b,
   }
 }
 
-// the lists longer than kLaneMax of this pass (mask[caller] == want), for k_normals_long
+// the lists longer than kLaneMax of this pass (mask[caller] == want), for k_normals_long: pushed
+// to longq, or (flags non-null) flagged for an order-preserving compaction
 __global__ void __launch_bounds__(256) k_long_lists(GridView g, NbLists L, const uint8_t* __restrict__ mask, int want,
                                                     int lane_max,
-                                                    int32_t* __restrict__ longq, int* __restrict__ n_long) {
+                                                    int32_t* __restrict__ longq, int* __restrict__ n_long,
+                                                    uint8_t* __restrict__ flags) {
   const int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   bool push = false;
   if (want >= 2 && mask) {  // workgroup partition (blocks of 256 queries, as k_normals_chain's)
@@ -539,7 +547,11 @@ __global__ void __launch_bounds__(256) k_long_lists(GridView g, NbLists L, const
   } else if (j < nq_of(L) && L.cnt[j] > lane_max) {
     push = !mask || ((mask[g.perm[L.qpos[j]]] != 0) == (want != 0));
   }
-  if (push) longq[wave_push_slot(n_long)] = (int32_t)j;
+  if (flags) {
+    flags[j] = push ? 1 : 0;  // (every slot of the grid: a deferred build's count is an upper bound on the host)
+  } else if (push) {
+    longq[wave_push_slot(n_long)] = (int32_t)j;
+  }
 }
 
 __global__ void __launch_bounds__(256) k_normals_long(GridView g, NbLists L, const int32_t* __restrict__ longq,
@@ -759,8 +771,24 @@ void normals_chains_dev(pfx_ctx* ctx, pfx_ctx* owner, const uint8_t* mask, int w
   const bool fork = L.nq_dev ? ctx->normals_fork_hint : L.long_nq * 8 <= L.nq;
   if (!L.nq_dev) ctx->normals_fork_hint = fork;
   const int lane_max = fork ? kLaneMax : kLaneMaxDense;
-  k_long_lists<<<(unsigned)nb, 256, 0, st>>>(view(G), L, mask, want, lane_max, longq, n_long);
-  check_launch("k_long_lists");
+  if (fork || !PFX_LONG_ORDERED) {
+    k_long_lists<<<(unsigned)nb, 256, 0, st>>>(view(G), L, mask, want, lane_max, longq, n_long, nullptr);
+    check_launch("k_long_lists");
+  } else {
+    // many long lists (dense clouds): the queue keeps the cell order, so the groups k_normals_long
+    // runs at once gather from one compact region (the pushed queue's order is the order the
+    // resident workgroups of k_long_lists happened to reach their atomics: its L2 hit rate was
+    // 0.745 on the dense variant)
+    uint8_t* flags = ctx->buf("normals_longflag").as<uint8_t>(nb * 256);
+    k_long_lists<<<(unsigned)nb, 256, 0, st>>>(view(G), L, mask, want, lane_max, longq, n_long, flags);
+    check_launch("k_long_lists");
+    size_t tb = 0;
+    PFX_HIP(rocprim::select(nullptr, tb, rocprim::counting_iterator<int32_t>(0), flags, longq, n_long,
+                            (size_t)L.nq, st));
+    void* tmp = ctx->buf("normals_longsel").get(tb + 16);
+    PFX_HIP(rocprim::select(tmp, tb, rocprim::counting_iterator<int32_t>(0), flags, longq, n_long, (size_t)L.nq,
+                            st));
+  }
   // (sized to what is resident at once: waves beyond it would wait for a second round)
   const int64_t lb = std::min<int64_t>(ceil_div(L.nq, 7 * 4), 256 * kLongWgPerCu * PFX_LONG_GRID_MUL);
   if (fork) {
